@@ -1,0 +1,477 @@
+// api.hip — the C-ABI of libdeltagpu (include/deltagpu.h): engine lifecycle,
+// argument validation, scratch management and kernel sequencing.  Errors follow
+// the header's conventions; nothing here falls back to a CPU path.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/deltagpu.h"
+#include "dg_launch.h"
+
+using namespace dg;
+
+struct dg_engine {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  // decoupled look-back scratch
+  u64* state = nullptr;
+  u64 state_cap = 0;
+  u32* ticket = nullptr;  // [0] ticket, [1] error bits, [2] store_check flag
+  u32 epoch = 0;
+  // small device counters + pinned host mirror
+  u64* d_counts = nullptr;  // 8 entries
+  u64* h_counts = nullptr;  // pinned, 8 entries
+  // general scratch
+  void* tmp = nullptr;
+  size_t tmp_cap = 0;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                    \
+  do {                                                                                   \
+    hipError_t _e = (expr);                                                              \
+    if (_e != hipSuccess)                                                                \
+      return fail(DG_E_DEVICE, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e),   \
+                  __FILE__, __LINE__);                                                   \
+  } while (0)
+
+int set_device(dg_engine* e) {
+  HIP_TRY(hipSetDevice(e->device));
+  return DG_OK;
+}
+
+int ensure_state(dg_engine* e, u64 tiles) {
+  if (tiles <= e->state_cap) return DG_OK;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (e->state) HIP_TRY(hipFree(e->state));
+  e->state = nullptr;
+  u64 cap = std::max<u64>(tiles, 1024);
+  if (hipMalloc(&e->state, cap * sizeof(u64)) != hipSuccess)
+    return fail(DG_E_NOMEM, "hipMalloc of %llu look-back granules failed", cap);
+  HIP_TRY(hipMemset(e->state, 0, cap * sizeof(u64)));
+  e->state_cap = cap;
+  e->epoch = 0;
+  return DG_OK;
+}
+
+int ensure_tmp(dg_engine* e, size_t bytes) {
+  if (bytes <= e->tmp_cap) return DG_OK;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (e->tmp) HIP_TRY(hipFree(e->tmp));
+  e->tmp = nullptr;
+  size_t cap = std::max<size_t>(bytes, 1 << 20);
+  if (hipMalloc(&e->tmp, cap) != hipSuccess)
+    return fail(DG_E_NOMEM, "hipMalloc of %zu scratch bytes failed", cap);
+  e->tmp_cap = cap;
+  return DG_OK;
+}
+
+// A fresh epoch per look-back launch; granules of older epochs read as "not ready".
+int next_scan(dg_engine* e, Scan* s) {
+  if (++e->epoch >= (1u << 20)) {
+    HIP_TRY(hipMemsetAsync(e->state, 0, e->state_cap * sizeof(u64), e->stream));
+    e->epoch = 1;
+  }
+  s->state = e->state;
+  s->ticket = e->ticket;
+  s->err = e->ticket + 1;
+  s->epoch = e->epoch;
+  return DG_OK;
+}
+
+int read_counts(dg_engine* e, int n) {
+  HIP_TRY(hipMemcpyAsync(e->h_counts, e->d_counts, n * sizeof(u64), hipMemcpyDeviceToHost,
+                         e->stream));
+  u32 err = 0;
+  HIP_TRY(hipMemcpyAsync(&e->h_counts[7], e->ticket + 1, sizeof(u32), hipMemcpyDeviceToHost,
+                         e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  memcpy(&err, &e->h_counts[7], sizeof(u32));
+  if (err) {
+    HIP_TRY(hipMemset(e->ticket, 0, 4 * sizeof(u32)));
+    return fail(DG_E_DEVICE, "look-back timeout inside a kernel (error bits 0x%x)", err);
+  }
+  return DG_OK;
+}
+
+Rows rows_of(const dg_store* s) {
+  Rows r;
+  r.key = s->key;
+  r.val = s->val;
+  r.ts = s->ts;
+  r.node = s->node;
+  r.cnt = s->cnt;
+  r.n = s->n;
+  return r;
+}
+
+RowsOut rows_out_of(dg_store* s) {
+  RowsOut r;
+  r.key = s->key;
+  r.val = s->val;
+  r.ts = s->ts;
+  r.node = s->node;
+  r.cnt = s->cnt;
+  return r;
+}
+
+Ctx ctx_of(const dg_context* c) {
+  Ctx x;
+  x.node = c->node;
+  x.cnt = c->cnt;
+  x.n = c->n;
+  x.kind = c->kind;
+  return x;
+}
+
+int check_store(const dg_store* s, const char* what) {
+  if (!s) return fail(DG_E_INVAL, "%s: null store", what);
+  if (s->n && (!s->key || !s->val || !s->ts || !s->node || !s->cnt))
+    return fail(DG_E_INVAL, "%s: null column with n=%llu", what, (unsigned long long)s->n);
+  return DG_OK;
+}
+
+int check_ctx(const dg_context* c, const char* what) {
+  if (!c) return fail(DG_E_INVAL, "%s: null context", what);
+  if (c->kind != DG_CTX_VV && c->kind != DG_CTX_DOTS)
+    return fail(DG_E_INVAL, "%s: bad context kind %d", what, c->kind);
+  if (c->n && (!c->node || !c->cnt)) return fail(DG_E_INVAL, "%s: null context column", what);
+  return DG_OK;
+}
+
+#define TRY(x)              \
+  do {                      \
+    int _r = (x);           \
+    if (_r != DG_OK) return _r; \
+  } while (0)
+
+int join2_enqueue(dg_engine* e, const dg_store* a, const dg_context* ca, const dg_store* b,
+                  const dg_context* cb, const uint64_t* keys, uint64_t n_keys, dg_store* out,
+                  dg_context* out_ctx, uint64_t* d_counts) {
+  TRY(check_store(a, "dg_join2 a"));
+  TRY(check_store(b, "dg_join2 b"));
+  TRY(check_ctx(ca, "dg_join2 ca"));
+  TRY(check_ctx(cb, "dg_join2 cb"));
+  if (!out || !out_ctx || !d_counts) return fail(DG_E_INVAL, "dg_join2: null output");
+  if (keys == nullptr && n_keys != 0) return fail(DG_E_INVAL, "dg_join2: keys NULL with n_keys>0");
+  if (out->cap < a->n + b->n)
+    return fail(DG_E_CAPACITY, "dg_join2: out cap %llu < %llu rows in", (unsigned long long)out->cap,
+                (unsigned long long)(a->n + b->n));
+  if (out_ctx->cap < ca->n + cb->n)
+    return fail(DG_E_CAPACITY, "dg_join2: out_ctx cap %llu < %llu", (unsigned long long)out_ctx->cap,
+                (unsigned long long)(ca->n + cb->n));
+  if (a->n + b->n && (!out->key || !out->val || !out->ts || !out->node || !out->cnt))
+    return fail(DG_E_INVAL, "dg_join2: null output column");
+  TRY(set_device(e));
+  TRY(ensure_state(e, join2_tiles(a->n, b->n)));
+  TRY(ensure_tmp(e, ctx_union_tmp_bytes(ca->n, cb->n)));
+  Scan sc;
+  TRY(next_scan(e, &sc));
+  HIP_TRY(launch_ctx_union(ctx_of(ca), ctx_of(cb), out_ctx->node, out_ctx->cnt, d_counts + 1,
+                           e->tmp, e->stream));
+  HIP_TRY(launch_join2_rows(rows_of(a), ctx_of(ca), rows_of(b), ctx_of(cb), keys,
+                            keys ? n_keys : 0, rows_out_of(out), sc, d_counts, e->stream));
+  out_ctx->kind = (ca->kind == DG_CTX_DOTS && cb->kind == DG_CTX_DOTS) ? DG_CTX_DOTS : DG_CTX_VV;
+  return DG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dg_abi_version(void) { return DG_ABI_VERSION; }
+
+const char* dg_last_error(void) { return g_err.c_str(); }
+
+int dg_engine_create(int device, void* hip_stream, dg_engine** out) {
+  if (!out) return fail(DG_E_INVAL, "dg_engine_create: null out");
+  *out = nullptr;
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev)
+    return fail(DG_E_INVAL, "dg_engine_create: device %d of %d", device, ndev);
+  dg_engine* e = new dg_engine();
+  e->device = device;
+  int rc = set_device(e);
+  if (rc != DG_OK) {
+    delete e;
+    return rc;
+  }
+  if (hip_stream) {
+    e->stream = (hipStream_t)hip_stream;
+  } else {
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+      delete e;
+      return fail(DG_E_DEVICE, "hipStreamCreate failed");
+    }
+    e->own_stream = true;
+  }
+  if (hipMalloc(&e->ticket, 16 * sizeof(u32)) != hipSuccess ||
+      hipMalloc(&e->d_counts, 8 * sizeof(u64)) != hipSuccess ||
+      hipHostMalloc(&e->h_counts, 8 * sizeof(u64), 0) != hipSuccess) {
+    dg_engine_destroy(e);
+    return fail(DG_E_NOMEM, "dg_engine_create: allocation failed");
+  }
+  hipMemset(e->ticket, 0, 16 * sizeof(u32));
+  hipMemset(e->d_counts, 0, 8 * sizeof(u64));
+  rc = ensure_state(e, 4096);
+  if (rc != DG_OK) {
+    dg_engine_destroy(e);
+    return rc;
+  }
+  *out = e;
+  return DG_OK;
+}
+
+int dg_engine_destroy(dg_engine* e) {
+  if (!e) return DG_OK;
+  hipSetDevice(e->device);
+  if (e->stream) hipStreamSynchronize(e->stream);
+  if (e->state) hipFree(e->state);
+  if (e->ticket) hipFree(e->ticket);
+  if (e->d_counts) hipFree(e->d_counts);
+  if (e->h_counts) hipHostFree(e->h_counts);
+  if (e->tmp) hipFree(e->tmp);
+  if (e->own_stream && e->stream) hipStreamDestroy(e->stream);
+  delete e;
+  return DG_OK;
+}
+
+void* dg_engine_stream(dg_engine* e) { return e ? (void*)e->stream : nullptr; }
+
+int dg_engine_sync(dg_engine* e) {
+  if (!e) return fail(DG_E_INVAL, "null engine");
+  TRY(set_device(e));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  u32 err = 0;
+  HIP_TRY(hipMemcpy(&err, e->ticket + 1, sizeof(u32), hipMemcpyDeviceToHost));
+  if (err) {
+    HIP_TRY(hipMemset(e->ticket, 0, 4 * sizeof(u32)));
+    return fail(DG_E_DEVICE, "look-back timeout inside a kernel (error bits 0x%x)", err);
+  }
+  return DG_OK;
+}
+
+int dg_store_check(dg_engine* e, const dg_store* s) {
+  if (!e) return fail(DG_E_INVAL, "null engine");
+  TRY(check_store(s, "dg_store_check"));
+  TRY(set_device(e));
+  HIP_TRY(hipMemsetAsync(e->ticket + 2, 0, sizeof(u32), e->stream));
+  HIP_TRY(launch_store_check(rows_of(s), e->ticket + 2, e->stream));
+  u32 bad = 0;
+  HIP_TRY(hipMemcpyAsync(&e->h_counts[6], e->ticket + 2, sizeof(u32), hipMemcpyDeviceToHost,
+                         e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  memcpy(&bad, &e->h_counts[6], sizeof(u32));
+  if (bad) return fail(DG_E_ORDER, "store rows are not strictly ascending");
+  return DG_OK;
+}
+
+int dg_join2_async(dg_engine* e, const dg_store* a, const dg_context* ca, const dg_store* b,
+                   const dg_context* cb, const uint64_t* keys, uint64_t n_keys, dg_store* out,
+                   dg_context* out_ctx, uint64_t* d_counts) {
+  if (!e) return fail(DG_E_INVAL, "null engine");
+  return join2_enqueue(e, a, ca, b, cb, keys, n_keys, out, out_ctx, d_counts);
+}
+
+int dg_join2(dg_engine* e, const dg_store* a, const dg_context* ca, const dg_store* b,
+             const dg_context* cb, const uint64_t* keys, uint64_t n_keys, dg_store* out,
+             dg_context* out_ctx) {
+  if (!e) return fail(DG_E_INVAL, "null engine");
+  TRY(join2_enqueue(e, a, ca, b, cb, keys, n_keys, out, out_ctx, e->d_counts));
+  TRY(read_counts(e, 2));
+  out->n = e->h_counts[0];
+  out_ctx->n = e->h_counts[1];
+  return DG_OK;
+}
+
+int dg_joink(dg_engine* e, int k, const dg_store* stores, const dg_context* ctxs, dg_store* out,
+             dg_context* out_ctx) {
+  if (!e) return fail(DG_E_INVAL, "null engine");
+  if (k <= 0 || !stores || !ctxs || !out || !out_ctx) return fail(DG_E_INVAL, "dg_joink: bad args");
+  u64 total = 0, total_ctx = 0;
+  for (int s = 0; s < k; s++) {
+    TRY(check_store(&stores[s], "dg_joink store"));
+    TRY(check_ctx(&ctxs[s], "dg_joink ctx"));
+    total += stores[s].n;
+    total_ctx += ctxs[s].n;
+  }
+  if (out->cap < total || out_ctx->cap < total_ctx)
+    return fail(DG_E_CAPACITY, "dg_joink: output capacity too small");
+  TRY(set_device(e));
+  // Left fold through two ping-pong row buffers in device scratch.
+  const size_t row_bytes = 36;
+  const size_t ctx_bytes = 12;
+  const size_t half = total * row_bytes + total_ctx * ctx_bytes + 256;
+  void* fold = nullptr;
+  if (k > 2) {
+    if (hipMalloc(&fold, 2 * half) != hipSuccess)
+      return fail(DG_E_NOMEM, "dg_joink: scratch allocation failed");
+  }
+  auto carve = [&](int which, dg_store* st, dg_context* cx) {
+    char* p = (char*)fold + which * half;
+    st->key = (uint64_t*)p;
+    p += total * 8;
+    st->val = (uint64_t*)p;
+    p += total * 8;
+    st->ts = (int64_t*)p;
+    p += total * 8;
+    st->cnt = (uint64_t*)p;
+    p += total * 8;
+    cx->cnt = (uint64_t*)p;
+    p += total_ctx * 8;
+    st->node = (uint32_t*)p;
+    p += total * 4;
+    cx->node = (uint32_t*)p;
+    st->cap = total;
+    cx->cap = total_ctx;
+    st->n = 0;
+    cx->n = 0;
+  };
+  dg_store acc = stores[0];
+  dg_context acc_ctx = ctxs[0];
+  dg_store buf[2];
+  dg_context bufc[2];
+  if (k > 2) {
+    carve(0, &buf[0], &bufc[0]);
+    carve(1, &buf[1], &bufc[1]);
+  }
+  int rc = DG_OK;
+  if (k == 1) {
+    // join of a single store is the store itself
+    HIP_TRY(hipMemcpyAsync(out->key, acc.key, acc.n * 8, hipMemcpyDeviceToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(out->val, acc.val, acc.n * 8, hipMemcpyDeviceToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(out->ts, acc.ts, acc.n * 8, hipMemcpyDeviceToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(out->node, acc.node, acc.n * 4, hipMemcpyDeviceToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(out->cnt, acc.cnt, acc.n * 8, hipMemcpyDeviceToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(out_ctx->node, acc_ctx.node, acc_ctx.n * 4, hipMemcpyDeviceToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(out_ctx->cnt, acc_ctx.cnt, acc_ctx.n * 8, hipMemcpyDeviceToDevice, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    out->n = acc.n;
+    out_ctx->n = acc_ctx.n;
+    out_ctx->kind = acc_ctx.kind;
+    return DG_OK;
+  }
+  for (int s = 1; s < k && rc == DG_OK; s++) {
+    dg_store* dst = (s == k - 1) ? out : &buf[s & 1];
+    dg_context* dstc = (s == k - 1) ? out_ctx : &bufc[s & 1];
+    dst->n = 0;
+    rc = dg_join2(e, &acc, &acc_ctx, &stores[s], &ctxs[s], nullptr, 0, dst, dstc);
+    acc = *dst;
+    acc_ctx = *dstc;
+  }
+  if (fold) hipFree(fold);
+  return rc;
+}
+
+int dg_context_union(dg_engine* e, const dg_context* a, const dg_context* b, dg_context* out) {
+  if (!e) return fail(DG_E_INVAL, "null engine");
+  TRY(check_ctx(a, "dg_context_union a"));
+  TRY(check_ctx(b, "dg_context_union b"));
+  if (!out) return fail(DG_E_INVAL, "dg_context_union: null out");
+  if (out->cap < a->n + b->n) return fail(DG_E_CAPACITY, "dg_context_union: out cap too small");
+  TRY(set_device(e));
+  TRY(ensure_tmp(e, ctx_union_tmp_bytes(a->n, b->n)));
+  HIP_TRY(launch_ctx_union(ctx_of(a), ctx_of(b), out->node, out->cnt, e->d_counts + 1, e->tmp,
+                           e->stream));
+  TRY(read_counts(e, 2));
+  out->n = e->h_counts[1];
+  out->kind = (a->kind == DG_CTX_DOTS && b->kind == DG_CTX_DOTS) ? DG_CTX_DOTS : DG_CTX_VV;
+  return DG_OK;
+}
+
+int dg_compress_dots(dg_engine* e, const dg_context* dots, dg_context* out_vv) {
+  if (!e) return fail(DG_E_INVAL, "null engine");
+  TRY(check_ctx(dots, "dg_compress_dots"));
+  if (dots->kind != DG_CTX_DOTS)
+    return fail(DG_E_CLAUSE,
+                "no function clause matching in DeltaCrdt.AWLWWMap.Dots.compress/1 "
+                "(context is already a version vector; aw_lww_map.ex:13)");
+  dg_context empty;
+  memset(&empty, 0, sizeof empty);
+  empty.kind = DG_CTX_VV;
+  return dg_context_union(e, &empty, dots, out_vv);
+}
+
+int dg_read_lww(dg_engine* e, const dg_store* s, const uint64_t* keys, uint64_t n_keys,
+                uint64_t* out_key, uint64_t* out_val, uint64_t cap, uint64_t* n_out) {
+  if (!e) return fail(DG_E_INVAL, "null engine");
+  TRY(check_store(s, "dg_read_lww"));
+  if (!n_out || (s->n && (!out_key || !out_val))) return fail(DG_E_INVAL, "dg_read_lww: null output");
+  if (keys == nullptr && n_keys != 0) return fail(DG_E_INVAL, "dg_read_lww: keys NULL with n_keys>0");
+  u64 need = keys ? std::min<u64>(n_keys, s->n) : s->n;
+  if (cap < need)
+    return fail(DG_E_CAPACITY, "dg_read_lww: cap %llu < %llu", (unsigned long long)cap,
+                (unsigned long long)need);
+  TRY(set_device(e));
+  TRY(ensure_state(e, seg_tiles(s->n)));
+  Scan sc;
+  TRY(next_scan(e, &sc));
+  HIP_TRY(launch_read_lww(rows_of(s), keys, keys ? n_keys : 0, out_key, out_val, sc, e->d_counts,
+                          e->stream));
+  TRY(read_counts(e, 1));
+  *n_out = e->h_counts[0];
+  return DG_OK;
+}
+
+int dg_merkle_build(dg_engine* e, const dg_store* s, dg_merkle* t) {
+  if (!e) return fail(DG_E_INVAL, "null engine");
+  TRY(check_store(s, "dg_merkle_build"));
+  if (!t || !t->nodes || !t->bucket_off || (s->n && (!t->leaf_key || !t->leaf_hash)))
+    return fail(DG_E_INVAL, "dg_merkle_build: null tree array");
+  if (t->depth < 1 || t->depth > 26) return fail(DG_E_INVAL, "dg_merkle_build: depth %u", t->depth);
+  if (t->cap_keys < s->n) return fail(DG_E_CAPACITY, "dg_merkle_build: cap_keys < rows");
+  TRY(set_device(e));
+  TRY(ensure_state(e, seg_tiles(s->n)));
+  Scan sc;
+  TRY(next_scan(e, &sc));
+  HIP_TRY(launch_merkle_leaves(rows_of(s), t->depth, t->leaf_key, t->leaf_hash, t->bucket_off, sc,
+                               e->d_counts, e->stream));
+  HIP_TRY(launch_merkle_levels(t->depth, t->leaf_hash, t->bucket_off, t->nodes, e->stream));
+  TRY(read_counts(e, 1));
+  t->n_keys = e->h_counts[0];
+  return DG_OK;
+}
+
+int dg_merkle_diff(dg_engine* e, const dg_merkle* a, const dg_merkle* b, uint64_t* out_keys,
+                   uint64_t cap, uint64_t* n_out) {
+  if (!e) return fail(DG_E_INVAL, "null engine");
+  if (!a || !b || !n_out) return fail(DG_E_INVAL, "dg_merkle_diff: null argument");
+  if (a->depth != b->depth) return fail(DG_E_INVAL, "dg_merkle_diff: depth %u != %u", a->depth, b->depth);
+  if (a->depth < 1 || a->depth > 26) return fail(DG_E_INVAL, "dg_merkle_diff: depth %u", a->depth);
+  if (cap && !out_keys) return fail(DG_E_INVAL, "dg_merkle_diff: null out_keys");
+  TRY(set_device(e));
+  TRY(ensure_state(e, diff_tiles(a->depth)));
+  Scan sc;
+  TRY(next_scan(e, &sc));
+  HIP_TRY(launch_merkle_diff(a->depth, a->nodes, a->leaf_key, a->leaf_hash, a->bucket_off, b->nodes,
+                             b->leaf_key, b->leaf_hash, b->bucket_off, out_keys, cap, sc,
+                             e->d_counts, e->stream));
+  TRY(read_counts(e, 1));
+  *n_out = e->h_counts[0];
+  if (*n_out > cap)
+    return fail(DG_E_CAPACITY, "dg_merkle_diff: %llu differing keys > cap %llu",
+                (unsigned long long)*n_out, (unsigned long long)cap);
+  return DG_OK;
+}
+
+}  // extern "C"

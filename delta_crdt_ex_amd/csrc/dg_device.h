@@ -1,0 +1,219 @@
+// dg_device.h — device-side building blocks shared by the libdeltagpu kernels
+// (gfx950 / CDNA4, wave64).
+//
+//  * Row views over the SoA dot store (include/deltagpu.h) and the full-tuple
+//    order (key, val, ts[signed], node, cnt) every store is sorted by.
+//  * Causal-context membership: Dots.member?/2 (reference aw_lww_map.ex:67-73).
+//  * Wave/block exclusive scans (64-wide shuffles; never 32-wide warp idioms).
+//  * The decoupled look-back used for single-pass stream compaction: every tile
+//    publishes one 64-bit granule {epoch:20 | flag:2 | value:42} with a relaxed
+//    agent-scope atomic store (an `sc1` store) and predecessors poll it with
+//    relaxed agent-scope atomic loads.  Data and flag live in the same naturally
+//    aligned 8-byte word, so no release/acquire fence is needed (MI355X microarch
+//    guide, "Valid forms", R2 granule).  Tiles are numbered by an atomic ticket in
+//    launch order, so a tile only waits on tiles that are already resident.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dg {
+
+typedef uint64_t u64;
+typedef int64_t i64;
+typedef uint32_t u32;
+
+constexpr int WAVE = 64;
+
+struct Rows {
+  const u64* key;
+  const u64* val;
+  const i64* ts;
+  const u32* node;
+  const u64* cnt;
+  u64 n;
+};
+
+struct RowsOut {
+  u64* key;
+  u64* val;
+  i64* ts;
+  u32* node;
+  u64* cnt;
+};
+
+struct Ctx {
+  const u32* node;
+  const u64* cnt;
+  u64 n;
+  int kind;  // 0 = VV, 1 = explicit dot set
+};
+
+struct Row {
+  u64 key, val, cnt;
+  i64 ts;
+  u32 node;
+};
+
+__device__ __forceinline__ Row load_row(const Rows& r, u64 i) {
+  Row x;
+  x.key = r.key[i];
+  x.val = r.val[i];
+  x.ts = r.ts[i];
+  x.node = r.node[i];
+  x.cnt = r.cnt[i];
+  return x;
+}
+
+// -1 / 0 / 1 on the full tuple.
+__device__ __forceinline__ int row_cmp(const Row& a, const Row& b) {
+  if (a.key != b.key) return a.key < b.key ? -1 : 1;
+  if (a.val != b.val) return a.val < b.val ? -1 : 1;
+  if (a.ts != b.ts) return a.ts < b.ts ? -1 : 1;
+  if (a.node != b.node) return a.node < b.node ? -1 : 1;
+  if (a.cnt != b.cnt) return a.cnt < b.cnt ? -1 : 1;
+  return 0;
+}
+
+__device__ __forceinline__ bool row_le(const Row& a, const Row& b) { return row_cmp(a, b) <= 0; }
+__device__ __forceinline__ bool row_eq(const Row& a, const Row& b) {
+  return a.key == b.key && a.val == b.val && a.ts == b.ts && a.node == b.node && a.cnt == b.cnt;
+}
+
+// Dots.member?/2 (aw_lww_map.ex:67-73).  VV: Map.get(vv, node, 0) >= cnt.
+// Dot set: exact (node, cnt) membership.  `node`/`cnt` may point at LDS or global
+// memory (flat addressing).
+__device__ __forceinline__ bool ctx_covers(const u32* node, const u64* cnt, u64 n, int kind,
+                                           u32 dn, u64 dc) {
+  u64 lo = 0, hi = n;
+  if (kind == 0) {
+    while (lo < hi) {
+      u64 mid = (lo + hi) >> 1;
+      if (node[mid] < dn)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    u64 have = (lo < n && node[lo] == dn) ? cnt[lo] : 0ull;
+    return have >= dc;
+  }
+  while (lo < hi) {
+    u64 mid = (lo + hi) >> 1;
+    u32 mn = node[mid];
+    if (mn < dn || (mn == dn && cnt[mid] < dc))
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo < n && node[lo] == dn && cnt[lo] == dc;
+}
+
+__device__ __forceinline__ bool keyset_has(const u64* keys, u64 n, u64 k) {
+  u64 lo = 0, hi = n;
+  while (lo < hi) {
+    u64 mid = (lo + hi) >> 1;
+    if (keys[mid] < k)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo < n && keys[lo] == k;
+}
+
+// Inclusive scan of a 32-bit value across the 64 lanes of a wave.
+__device__ __forceinline__ u32 wave_incl_scan(u32 v) {
+  const int lane = threadIdx.x & (WAVE - 1);
+#pragma unroll
+  for (int d = 1; d < WAVE; d <<= 1) {
+    u32 t = __shfl_up(v, d, WAVE);
+    if (lane >= d) v += t;
+  }
+  return v;
+}
+
+// Exclusive block scan; returns the exclusive prefix of `v` and the block total in
+// *total.  `s_wave` must hold BLOCK/64 + 1 words of LDS.
+template <int BLOCK>
+__device__ __forceinline__ u32 block_excl_scan(u32 v, u32* s_wave, u32* total) {
+  constexpr int NW = BLOCK / WAVE;
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int w = threadIdx.x / WAVE;
+  u32 inc = wave_incl_scan(v);
+  if (lane == WAVE - 1) s_wave[w] = inc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u32 run = 0;
+#pragma unroll
+    for (int i = 0; i < NW; i++) {
+      u32 t = s_wave[i];
+      s_wave[i] = run;
+      run += t;
+    }
+    s_wave[NW] = run;
+  }
+  __syncthreads();
+  *total = s_wave[NW];
+  return s_wave[w] + inc - v;
+}
+
+// ---------------------------------------------------------------- look-back
+constexpr u64 LB_VALUE_MASK = (1ull << 42) - 1;
+constexpr u32 LB_AGG = 1, LB_INC = 2;
+
+__device__ __forceinline__ u64 lb_pack(u32 epoch, u32 flag, u64 value) {
+  return ((u64)epoch << 44) | ((u64)flag << 42) | (value & LB_VALUE_MASK);
+}
+
+__device__ __forceinline__ void lb_publish(u64* state, u64 tile, u32 epoch, u32 flag, u64 value) {
+  __hip_atomic_store(state + tile, lb_pack(epoch, flag, value), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Called by ONE full wave of the tile (tile > 0) after it published its aggregate.
+// Returns the exclusive prefix of tile `tile` (same value in every lane).  Spins are
+// bounded: on timeout *err gets bit 0 set and the partial prefix is returned.
+__device__ __forceinline__ u64 lb_lookback(u64* state, u64 tile, u32 epoch, u32* err) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  u64 prefix = 0;
+  i64 base = (i64)tile - 1;
+  u32 spins = 0;
+  while (true) {
+    i64 idx = base - lane;
+    u32 flag;
+    u64 value;
+    if (idx >= 0) {
+      u64 w = __hip_atomic_load(state + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      bool cur = (u32)(w >> 44) == epoch;
+      flag = cur ? (u32)((w >> 42) & 3) : 0u;
+      value = w & LB_VALUE_MASK;
+    } else {
+      flag = LB_INC;
+      value = 0;
+    }
+    u64 inc_mask = __ballot(flag == LB_INC);
+    u64 zero_mask = __ballot(flag == 0);
+    if (inc_mask) {
+      int first = __ffsll((long long)inc_mask) - 1;  // nearest inclusive predecessor
+      u64 upto = (first == 63) ? ~0ull : ((2ull << first) - 1);
+      if ((zero_mask & upto) == 0) {
+        u64 contrib = (lane <= first) ? value : 0;
+#pragma unroll
+        for (int d = WAVE / 2; d >= 1; d >>= 1) contrib += __shfl_xor(contrib, d, WAVE);
+        return prefix + contrib;
+      }
+    } else if (zero_mask == 0) {
+      u64 contrib = value;
+#pragma unroll
+      for (int d = WAVE / 2; d >= 1; d >>= 1) contrib += __shfl_xor(contrib, d, WAVE);
+      prefix += contrib;
+      base -= WAVE;
+      continue;
+    }
+    if (++spins > (1u << 24)) {
+      if (lane == 0) atomicOr(err, 1u);
+      return prefix;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+}  // namespace dg

@@ -1,0 +1,61 @@
+// dg_launch.h — host-side launchers exported by each kernel translation unit to the
+// C-ABI layer (api.hip).  Plain structs only; no torch types anywhere in libdeltagpu.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dg_device.h"
+
+namespace dg {
+
+// Per-launch scratch for single-pass compaction kernels (decoupled look-back).
+struct Scan {
+  u64* state;   // one granule per tile (device)
+  u32* ticket;  // tile ticket counter, left at 0 by every launch (device)
+  u32* err;     // error bits (device): 1 = look-back timeout
+  u32 epoch;    // granules of other epochs are ignored
+};
+
+// ---- join.hip
+constexpr int JOIN_BLOCK = 256;
+constexpr int JOIN_ITEMS = 4;
+constexpr int JOIN_TILE = JOIN_BLOCK * JOIN_ITEMS;
+
+inline u64 join2_tiles(u64 na, u64 nb) { return (na + nb + JOIN_TILE - 1) / JOIN_TILE; }
+// Rows of join/3.  Writes the output row count to d_count[0].
+hipError_t launch_join2_rows(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& cb,
+                             const u64* keys, u64 n_keys, const RowsOut& out, const Scan& scan,
+                             u64* d_count, hipStream_t st);
+// Dots.union/2 of two contexts; out kind: DOTS iff both DOTS.  Writes |out| to *d_count.
+// tmp: (a.n + b.n) u32 + (a.n + b.n) u64 + (a.n + b.n + 1) u32 of device scratch.
+hipError_t launch_ctx_union(const Ctx& a, const Ctx& b, u32* out_node, u64* out_cnt,
+                            u64* d_count, void* tmp, hipStream_t st);
+inline size_t ctx_union_tmp_bytes(u64 na, u64 nb) {
+  return (size_t)(na + nb) * 4 + (size_t)(na + nb) * 8 + (size_t)(na + nb + 1) * 4 + 64;
+}
+
+// ---- segred.hip (segmented reductions over key runs)
+constexpr int SEG_BLOCK = 256;
+constexpr int SEG_ITEMS = 4;
+constexpr int SEG_TILE = SEG_BLOCK * SEG_ITEMS;
+inline u64 seg_tiles(u64 n) { return (n + SEG_TILE - 1) / SEG_TILE; }
+hipError_t launch_read_lww(const Rows& s, const u64* keys, u64 n_keys, u64* out_key, u64* out_val,
+                           const Scan& scan, u64* d_count, hipStream_t st);
+// Merkle leaves: (key, Σ row hashes) per key + bucket_off[b] = first leaf of bucket >= b.
+hipError_t launch_merkle_leaves(const Rows& s, u32 depth, u64* leaf_key, u64* leaf_hash,
+                                u64* bucket_off, const Scan& scan, u64* d_count, hipStream_t st);
+// Sortedness check: sets *d_bad to nonzero if rows are not strictly ascending.
+hipError_t launch_store_check(const Rows& s, u32* d_bad, hipStream_t st);
+
+// ---- merkle.hip
+hipError_t launch_merkle_levels(u32 depth, const u64* leaf_hash, const u64* bucket_off,
+                                u64* nodes, hipStream_t st);
+constexpr int DIFF_BLOCK = 256;
+inline u64 diff_tiles(u32 depth) { return depth >= 8 ? (1ull << (depth - 8)) : 1ull; }
+hipError_t launch_merkle_diff(u32 depth, const u64* nodes_a, const u64* leaf_key_a,
+                              const u64* leaf_hash_a, const u64* off_a, const u64* nodes_b,
+                              const u64* leaf_key_b, const u64* leaf_hash_b, const u64* off_b,
+                              u64* out_keys, u64 cap, const Scan& scan, u64* d_count,
+                              hipStream_t st);
+
+}  // namespace dg

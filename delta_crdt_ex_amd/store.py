@@ -1,0 +1,335 @@
+"""Device-resident dot stores and causal contexts, and the Engine that drives
+libdeltagpu on them.
+
+PyTorch is plumbing here: it owns HBM allocations and the stream.  Columns are
+int64/int32 tensors holding the bits of the u64/i64/u32 columns of
+include/deltagpu.h (u64 ids are reinterpreted, never compared in torch).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _abi
+from ._abi import DG_CTX_DOTS, DG_CTX_VV, check
+
+_I64 = torch.int64
+_I32 = torch.int32
+
+
+def _ptr(t: torch.Tensor | None, ctype):
+    if t is None or t.numel() == 0:
+        return C.cast(C.c_void_p(t.data_ptr() if t is not None and t.numel() else 0), ctype)
+    return C.cast(C.c_void_p(t.data_ptr()), ctype)
+
+
+def _np_to_dev(a: np.ndarray, dtype_view, device) -> torch.Tensor:
+    a = np.ascontiguousarray(a).view(dtype_view)
+    return torch.from_numpy(a.copy()).to(device, non_blocking=False)
+
+
+@dataclass
+class Store:
+    """SoA dot rows on the device: key u64, val u64, ts i64, node u32, cnt u64."""
+
+    key: torch.Tensor
+    val: torch.Tensor
+    ts: torch.Tensor
+    node: torch.Tensor
+    cnt: torch.Tensor
+    n: int
+
+    @property
+    def cap(self) -> int:
+        return int(self.key.numel())
+
+    @property
+    def device(self):
+        return self.key.device
+
+    @staticmethod
+    def empty(cap: int, device) -> "Store":
+        cap = max(int(cap), 1)
+        return Store(
+            torch.empty(cap, dtype=_I64, device=device),
+            torch.empty(cap, dtype=_I64, device=device),
+            torch.empty(cap, dtype=_I64, device=device),
+            torch.empty(cap, dtype=_I32, device=device),
+            torch.empty(cap, dtype=_I64, device=device),
+            0,
+        )
+
+    @staticmethod
+    def from_numpy(key, val, ts, node, cnt, device) -> "Store":
+        n = len(key)
+        if n == 0:
+            return Store.empty(1, device)
+        return Store(
+            _np_to_dev(np.asarray(key, dtype=np.uint64), np.int64, device),
+            _np_to_dev(np.asarray(val, dtype=np.uint64), np.int64, device),
+            _np_to_dev(np.asarray(ts, dtype=np.int64), np.int64, device),
+            _np_to_dev(np.asarray(node, dtype=np.uint32), np.int32, device),
+            _np_to_dev(np.asarray(cnt, dtype=np.uint64), np.int64, device),
+            n,
+        )
+
+    def to_numpy(self):
+        n = self.n
+        return (
+            self.key[:n].cpu().numpy().view(np.uint64),
+            self.val[:n].cpu().numpy().view(np.uint64),
+            self.ts[:n].cpu().numpy().view(np.int64),
+            self.node[:n].cpu().numpy().view(np.uint32),
+            self.cnt[:n].cpu().numpy().view(np.uint64),
+        )
+
+    def abi(self) -> _abi.dg_store:
+        s = _abi.dg_store()
+        s.key = _ptr(self.key, _abi.P64)
+        s.val = _ptr(self.val, _abi.P64)
+        s.ts = _ptr(self.ts, _abi.PI64)
+        s.node = _ptr(self.node, _abi.P32)
+        s.cnt = _ptr(self.cnt, _abi.P64)
+        s.n = self.n
+        s.cap = self.cap
+        return s
+
+
+@dataclass
+class Context:
+    """A causal context: DG_CTX_VV (version vector) or DG_CTX_DOTS (dot set)."""
+
+    kind: int
+    node: torch.Tensor
+    cnt: torch.Tensor
+    n: int
+
+    @property
+    def cap(self) -> int:
+        return int(self.node.numel())
+
+    @staticmethod
+    def empty(kind: int, cap: int, device) -> "Context":
+        cap = max(int(cap), 1)
+        return Context(kind, torch.empty(cap, dtype=_I32, device=device),
+                       torch.empty(cap, dtype=_I64, device=device), 0)
+
+    @staticmethod
+    def from_numpy(kind, node, cnt, device) -> "Context":
+        n = len(node)
+        if n == 0:
+            return Context.empty(kind, 1, device)
+        return Context(kind, _np_to_dev(np.asarray(node, dtype=np.uint32), np.int32, device),
+                       _np_to_dev(np.asarray(cnt, dtype=np.uint64), np.int64, device), n)
+
+    def to_numpy(self):
+        return (self.node[: self.n].cpu().numpy().view(np.uint32),
+                self.cnt[: self.n].cpu().numpy().view(np.uint64))
+
+    def abi(self) -> _abi.dg_context:
+        c = _abi.dg_context()
+        c.kind = self.kind
+        c.node = _ptr(self.node, _abi.P32)
+        c.cnt = _ptr(self.cnt, _abi.P64)
+        c.n = self.n
+        c.cap = self.cap
+        return c
+
+
+@dataclass
+class MerkleTree:
+    depth: int
+    nodes: torch.Tensor
+    bucket_off: torch.Tensor
+    leaf_key: torch.Tensor
+    leaf_hash: torch.Tensor
+    n_keys: int
+
+    @staticmethod
+    def empty(depth: int, cap_keys: int, device) -> "MerkleTree":
+        nb = 1 << depth
+        cap_keys = max(int(cap_keys), 1)
+        return MerkleTree(depth, torch.empty(2 * nb - 1, dtype=_I64, device=device),
+                          torch.empty(nb + 1, dtype=_I64, device=device),
+                          torch.empty(cap_keys, dtype=_I64, device=device),
+                          torch.empty(cap_keys, dtype=_I64, device=device), 0)
+
+    def abi(self) -> _abi.dg_merkle:
+        t = _abi.dg_merkle()
+        t.depth = self.depth
+        t.nodes = _ptr(self.nodes, _abi.P64)
+        t.bucket_off = _ptr(self.bucket_off, _abi.P64)
+        t.leaf_key = _ptr(self.leaf_key, _abi.P64)
+        t.leaf_hash = _ptr(self.leaf_hash, _abi.P64)
+        t.n_keys = self.n_keys
+        t.cap_keys = int(self.leaf_key.numel())
+        return t
+
+    def root(self) -> int:
+        return int(self.nodes[0].item()) & ((1 << 64) - 1)
+
+
+class Engine:
+    """One libdeltagpu engine (one HIP stream) on one device."""
+
+    def __init__(self, device=None, stream=None):
+        if not torch.cuda.is_available():
+            raise RuntimeError("libdeltagpu needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.lib = _abi.load()
+        dev = torch.device("cuda", torch.cuda.current_device() if device is None else
+                           torch.device(device).index or 0)
+        self.device = dev
+        if stream is None:
+            # a dedicated stream: the legacy null stream (handle 0) would be ambiguous
+            # at the C-ABI, where NULL means "create one"
+            stream = torch.cuda.Stream(device=dev)
+        self.stream = stream
+        h = C.c_void_p()
+        check(self.lib.dg_engine_create(dev.index, C.c_void_p(stream.cuda_stream), C.byref(h)))
+        self.h = h
+        self._d_counts = torch.zeros(8, dtype=_I64, device=dev)
+
+    def _order(self):
+        """Make the engine stream wait for work already queued on torch's current stream
+        (uploads of the inputs), so a call never reads half-written tensors."""
+        cur = torch.cuda.current_stream(self.device)
+        if cur.cuda_stream != self.stream.cuda_stream:
+            self.stream.wait_stream(cur)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.dg_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync(self):
+        check(self.lib.dg_engine_sync(self.h))
+
+    # ---------------------------------------------------------------- join
+    def join2(self, a: Store, ca: Context, b: Store, cb: Context, keys: torch.Tensor | None = None,
+              out: Store | None = None, out_ctx: Context | None = None):
+        self._order()
+        if out is None:
+            out = Store.empty(a.n + b.n, self.device)
+        if out_ctx is None:
+            out_ctx = Context.empty(DG_CTX_VV, ca.n + cb.n, self.device)
+        so, co = out.abi(), out_ctx.abi()
+        sa, sb, xa, xb = a.abi(), b.abi(), ca.abi(), cb.abi()
+        kp = _ptr(keys, _abi.P64) if keys is not None else None
+        nk = int(keys.numel()) if keys is not None else 0
+        check(self.lib.dg_join2(self.h, C.byref(sa), C.byref(xa), C.byref(sb), C.byref(xb),
+                                kp, nk, C.byref(so), C.byref(co)))
+        out.n = int(so.n)
+        out_ctx.n = int(co.n)
+        out_ctx.kind = int(co.kind)
+        return out, out_ctx
+
+    def join2_async(self, a: Store, ca: Context, b: Store, cb: Context, out: Store,
+                    out_ctx: Context, keys: torch.Tensor | None = None, d_counts=None):
+        """Enqueue the join; counts land in d_counts[0:2] (device)."""
+        self._order()
+        if d_counts is None:
+            d_counts = self._d_counts
+        so, co = out.abi(), out_ctx.abi()
+        sa, sb, xa, xb = a.abi(), b.abi(), ca.abi(), cb.abi()
+        kp = _ptr(keys, _abi.P64) if keys is not None else None
+        nk = int(keys.numel()) if keys is not None else 0
+        check(self.lib.dg_join2_async(self.h, C.byref(sa), C.byref(xa), C.byref(sb), C.byref(xb),
+                                      kp, nk, C.byref(so), C.byref(co), _ptr(d_counts, _abi.P64)))
+        out_ctx.kind = int(co.kind)
+        return d_counts
+
+    def joink(self, stores, ctxs, out: Store | None = None, out_ctx: Context | None = None):
+        self._order()
+        k = len(stores)
+        arr_s = (_abi.dg_store * k)(*[s.abi() for s in stores])
+        arr_c = (_abi.dg_context * k)(*[c.abi() for c in ctxs])
+        if out is None:
+            out = Store.empty(sum(s.n for s in stores), self.device)
+        if out_ctx is None:
+            out_ctx = Context.empty(DG_CTX_VV, sum(c.n for c in ctxs), self.device)
+        so, co = out.abi(), out_ctx.abi()
+        check(self.lib.dg_joink(self.h, k, arr_s, arr_c, C.byref(so), C.byref(co)))
+        out.n = int(so.n)
+        out_ctx.n = int(co.n)
+        out_ctx.kind = int(co.kind)
+        return out, out_ctx
+
+    # ---------------------------------------------------------------- contexts
+    def context_union(self, a: Context, b: Context, out: Context | None = None) -> Context:
+        self._order()
+        if out is None:
+            out = Context.empty(DG_CTX_VV, a.n + b.n, self.device)
+        xa, xb, xo = a.abi(), b.abi(), out.abi()
+        check(self.lib.dg_context_union(self.h, C.byref(xa), C.byref(xb), C.byref(xo)))
+        out.n = int(xo.n)
+        out.kind = int(xo.kind)
+        return out
+
+    def compress_dots(self, dots: Context, out: Context | None = None) -> Context:
+        self._order()
+        if out is None:
+            out = Context.empty(DG_CTX_VV, dots.n, self.device)
+        xa, xo = dots.abi(), out.abi()
+        check(self.lib.dg_compress_dots(self.h, C.byref(xa), C.byref(xo)))
+        out.n = int(xo.n)
+        out.kind = int(xo.kind)
+        return out
+
+    # ---------------------------------------------------------------- read
+    def read_lww(self, s: Store, keys: torch.Tensor | None = None):
+        self._order()
+        cap = max(s.n, 1)
+        ok = torch.empty(cap, dtype=_I64, device=self.device)
+        ov = torch.empty(cap, dtype=_I64, device=self.device)
+        n = C.c_uint64()
+        ss = s.abi()
+        kp = _ptr(keys, _abi.P64) if keys is not None else None
+        nk = int(keys.numel()) if keys is not None else 0
+        check(self.lib.dg_read_lww(self.h, C.byref(ss), kp, nk, _ptr(ok, _abi.P64),
+                                   _ptr(ov, _abi.P64), cap, C.byref(n)))
+        return ok[: n.value], ov[: n.value]
+
+    # ---------------------------------------------------------------- merkle
+    def merkle_build(self, s: Store, depth: int, tree: MerkleTree | None = None) -> MerkleTree:
+        self._order()
+        if tree is None or tree.depth != depth or tree.leaf_key.numel() < s.n:
+            tree = MerkleTree.empty(depth, s.n, self.device)
+        t = tree.abi()
+        ss = s.abi()
+        check(self.lib.dg_merkle_build(self.h, C.byref(ss), C.byref(t)))
+        tree.n_keys = int(t.n_keys)
+        return tree
+
+    def merkle_diff(self, a: MerkleTree, b: MerkleTree, cap: int | None = None) -> torch.Tensor:
+        self._order()
+        if cap is None:
+            cap = a.n_keys + b.n_keys
+        cap = max(int(cap), 1)
+        out = torch.empty(cap, dtype=_I64, device=self.device)
+        n = C.c_uint64()
+        ta, tb = a.abi(), b.abi()
+        check(self.lib.dg_merkle_diff(self.h, C.byref(ta), C.byref(tb), _ptr(out, _abi.P64), cap,
+                                      C.byref(n)))
+        return out[: n.value]
+
+    def store_check(self, s: Store):
+        self._order()
+        ss = s.abi()
+        check(self.lib.dg_store_check(self.h, C.byref(ss)))
+
+
+def u64(t: torch.Tensor) -> np.ndarray:
+    """Device int64 tensor holding u64 bits -> numpy uint64."""
+    return t.cpu().numpy().view(np.uint64)
+
+
+__all__ = ["Store", "Context", "MerkleTree", "Engine", "u64", "DG_CTX_VV", "DG_CTX_DOTS"]

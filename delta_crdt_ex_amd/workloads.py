@@ -1,0 +1,205 @@
+"""Seeded synthetic replicas for BASELINE.json's configs.
+
+Every generator builds exactly the state the reference's mutators would reach
+(`AWLWWMap.add/4` :99-112 and `remove/3` :133-146 applied through
+`join(state, delta, [key])` as CausalCrdt does, causal_crdt.ex:337-342,383-384),
+but vectorised with numpy: keys/values are integers (as in
+bench/basic_operations.exs:4), key ids are splitmix64(k), value ids the
+order-preserving integer encoding, node ids u32, ts i64.  tests/ check the
+generators against the term-level oracle replaying the same operations.
+
+A replica is a dict: {"rows": (key, val, ts, node, cnt) sorted, "ctx": (kind, node, cnt)}.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .interning import encode_int_value, splitmix64_np
+
+VV, DOTS = 0, 1
+
+
+def sort_rows(k, v, t, n, c):
+    order = np.lexsort((c, n, t, v, k))
+    return (np.ascontiguousarray(k[order], np.uint64), np.ascontiguousarray(v[order], np.uint64),
+            np.ascontiguousarray(t[order], np.int64), np.ascontiguousarray(n[order], np.uint32),
+            np.ascontiguousarray(c[order], np.uint64))
+
+
+def vv(d: dict):
+    items = sorted(d.items())
+    return (VV, np.array([a for a, _ in items], np.uint32), np.array([b for _, b in items], np.uint64))
+
+
+def config1(n_keys: int = 10_000):
+    """Config 1 (bench/basic_operations.exs-style, CPU plumbing): node 1 adds
+    k => k for k = 1..n; B := A; A removes k % 10 == 0; B (node 2) re-adds
+    k % 10 == 5 with v = k + 1.  Returns (A, B)."""
+    k = np.arange(1, n_keys + 1, dtype=np.uint64)
+    key = splitmix64_np(k)
+    val = encode_int_value(k.astype(np.int64))
+    ts = k.astype(np.int64) * 1000
+    node = np.full(n_keys, 1, np.uint32)
+    cnt = k.copy()
+    # A: removes k % 10 == 0 (remove/3 ctx = the removed dots; the VV absorbs them)
+    keep_a = (k % 10) != 0
+    A = {"rows": sort_rows(key[keep_a], val[keep_a], ts[keep_a], node[keep_a], cnt[keep_a]),
+         "ctx": vv({1: n_keys})}
+    # B: re-adds k % 10 == 5 with v = k + 1 as node 2, counters 1.. in key order
+    re = (k % 10) == 5
+    nre = int(re.sum())
+    val_b = val.copy()
+    ts_b = ts.copy()
+    node_b = node.copy()
+    cnt_b = cnt.copy()
+    val_b[re] = encode_int_value(k[re].astype(np.int64) + 1)
+    ts_b[re] = n_keys * 1000 + k[re].astype(np.int64)
+    node_b[re] = 2
+    cnt_b[re] = np.arange(1, nre + 1, dtype=np.uint64)
+    B = {"rows": sort_rows(key, val_b, ts_b, node_b, cnt_b), "ctx": vv({1: n_keys, 2: nre})}
+    return A, B
+
+
+def config2(n_keys: int = 1_000_000, seed: int = 2, key_lo: int = 1, keys=None):
+    """Config 2: base node 0 writes k = key_lo..key_lo+n-1 (counter = k,
+    ts = k * 1000); replicas A (node 1) and B (node 2) both overwrite the ~10 % of
+    keys with splitmix64(k ^ seed) % 10 == 0 with fresh random values, ts = base +
+    U[0, 1e9).  `keys` (uint64 array of k) overrides the key range (sharding).
+    Returns (A, B); N_in ~= 2 n, N_out ~= 1.1 n."""
+    if keys is None:
+        k = np.arange(key_lo, key_lo + n_keys, dtype=np.uint64)
+    else:
+        k = np.asarray(keys, np.uint64)
+    n = len(k)
+    key = splitmix64_np(k)
+    val = encode_int_value(k.astype(np.int64))
+    ts = k.astype(np.int64) * 1000
+    cnt0 = k.copy()  # node 0 wrote key k as its k-th add
+    conflict = (splitmix64_np(k ^ np.uint64(seed)) % np.uint64(10)) == 0
+    nc = int(conflict.sum())
+    rng = np.random.default_rng(seed)
+    ts_base = int(ts.max()) + 1000 if n else 0
+    out = []
+    for node_id in (1, 2):
+        v_new = rng.integers(0, 1 << 62, nc, dtype=np.int64)
+        t_new = ts_base + rng.integers(0, 1_000_000_000, nc, dtype=np.int64)
+        val_r = val.copy()
+        ts_r = ts.copy()
+        node_r = np.zeros(n, np.uint32)
+        cnt_r = cnt0.copy()
+        val_r[conflict] = encode_int_value(v_new)
+        ts_r[conflict] = t_new
+        node_r[conflict] = node_id
+        cnt_r[conflict] = np.arange(1, nc + 1, dtype=np.uint64)
+        out.append({"rows": sort_rows(key, val_r, ts_r, node_r, cnt_r),
+                    "ctx": vv({0: int(k.max()) if n else 0, node_id: nc})})
+    return out[0], out[1]
+
+
+def shard_of(key_ids: np.ndarray, n_shards: int) -> np.ndarray:
+    """Key-hash range sharding: shard = floor(key_id * n_shards / 2^64)."""
+    hi = (key_ids >> np.uint64(32)).astype(np.uint64)
+    lo = (key_ids & np.uint64(0xFFFFFFFF)).astype(np.uint64)
+    s = np.uint64(n_shards)
+    # (hi * 2^32 + lo) * s >> 64 = (hi * s + ((lo * s) >> 32)) >> 32
+    return ((hi * s + ((lo * s) >> np.uint64(32))) >> np.uint64(32)).astype(np.int64)
+
+
+def config2_shard(rank: int, world: int, keys_per_rank: int = 1_000_000, seed: int = 2):
+    """Config 2 at weak scaling: the global key space 1..world*keys_per_rank is
+    range-sharded by key hash and rank `rank` builds its shard of A and B."""
+    k = np.arange(1, world * keys_per_rank + 1, dtype=np.uint64)
+    mine = shard_of(splitmix64_np(k), world) == rank
+    return config2(seed=seed, keys=k[mine])
+
+
+def merkle_pair(n_keys: int = 1_000_000, diff_frac: float = 0.01, seed: int = 4, keys=None):
+    """Config-4-shaped pair: two replicas of the same base that differ on ~diff_frac
+    of the keys (one side re-added them as node 2).  Returns (A, B)."""
+    if keys is None:
+        k = np.arange(1, n_keys + 1, dtype=np.uint64)
+    else:
+        k = np.asarray(keys, np.uint64)
+    n = len(k)
+    key = splitmix64_np(k)
+    val = encode_int_value(k.astype(np.int64))
+    ts = k.astype(np.int64) * 1000
+    node = np.zeros(n, np.uint32)
+    cnt = np.arange(1, n + 1, dtype=np.uint64)
+    A = {"rows": sort_rows(key, val, ts, node, cnt), "ctx": vv({0: n})}
+    rng = np.random.default_rng(seed)
+    d = rng.random(n) < diff_frac
+    nd = int(d.sum())
+    val_b, ts_b, node_b, cnt_b = val.copy(), ts.copy(), node.copy(), cnt.copy()
+    val_b[d] = encode_int_value(rng.integers(0, 1 << 62, nd, dtype=np.int64))
+    ts_b[d] = int(ts.max() if n else 0) + 1000 + rng.integers(0, 1_000_000_000, nd, dtype=np.int64)
+    node_b[d] = 2
+    cnt_b[d] = np.arange(1, nd + 1, dtype=np.uint64)
+    B = {"rows": sort_rows(key, val_b, ts_b, node_b, cnt_b), "ctx": vv({0: n, 2: nd})}
+    return A, B
+
+
+def random_pair(rng: np.random.Generator, n_keys: int, n_nodes: int = 4, max_entries: int = 3,
+                p_remove: float = 0.3, ts_range: int = 1 << 40, dense_ctx: bool = True,
+                ctx_kind: int = VV):
+    """Two replicas of one key space that evolved independently from a common base,
+    with concurrent adds, removes, LWW ties (small ts_range) and — unless dense_ctx —
+    stores that are NOT covered by their own VV (the sync path's
+    VV-snapshot + current-values shape).  Used by the randomized parity tests."""
+    keys = splitmix64_np(rng.choice(1 << 40, n_keys, replace=False).astype(np.uint64))
+    reps = []
+    for r in range(2):
+        ks, vs, ts, ns, cs = [], [], [], [], []
+        counters = {}
+        for kid in keys:
+            if rng.random() < p_remove:
+                continue
+            for _ in range(int(rng.integers(1, max_entries + 1))):
+                nd = int(rng.integers(0, n_nodes))
+                c = counters.get(nd, 0) + 1 + int(rng.integers(0, 3))
+                counters[nd] = c
+                ks.append(kid)
+                vs.append(int(rng.integers(0, 8)) + (1 << 62))
+                ts.append(int(rng.integers(-ts_range, ts_range)))
+                ns.append(nd)
+                cs.append(c)
+        rows = (np.array(ks, np.uint64), np.array(vs, np.uint64), np.array(ts, np.int64),
+                np.array(ns, np.uint32), np.array(cs, np.uint64))
+        rows = sort_rows(*rows)
+        # dedupe identical rows (a store is a set)
+        if len(rows[0]):
+            m = np.ones(len(rows[0]), bool)
+            m[1:] = ~((rows[0][1:] == rows[0][:-1]) & (rows[1][1:] == rows[1][:-1]) &
+                      (rows[2][1:] == rows[2][:-1]) & (rows[3][1:] == rows[3][:-1]) &
+                      (rows[4][1:] == rows[4][:-1]))
+            rows = tuple(c[m] for c in rows)
+        if ctx_kind == VV:
+            vvd = {}
+            for nd in range(n_nodes):
+                top = counters.get(nd, 0)
+                vvd[nd] = top if dense_ctx else int(rng.integers(0, top + 2))
+            ctx = vv(vvd)
+        else:
+            dots = set()
+            for nd in range(n_nodes):
+                top = counters.get(nd, 0)
+                for c in range(1, top + 1):
+                    if dense_ctx or rng.random() < 0.5:
+                        dots.add((nd, c))
+            dots = sorted(dots)
+            ctx = (DOTS, np.array([d[0] for d in dots], np.uint32),
+                   np.array([d[1] for d in dots], np.uint64))
+        reps.append({"rows": rows, "ctx": ctx})
+    # shared rows: copy a slice of A into B so that "in both" happens
+    a, b = reps
+    if len(a["rows"][0]):
+        take = rng.random(len(a["rows"][0])) < 0.4
+        merged = tuple(np.concatenate([b["rows"][i], a["rows"][i][take]]) for i in range(5))
+        merged = sort_rows(*merged)
+        m = np.ones(len(merged[0]), bool)
+        if len(merged[0]) > 1:
+            m[1:] = ~((merged[0][1:] == merged[0][:-1]) & (merged[1][1:] == merged[1][:-1]) &
+                      (merged[2][1:] == merged[2][:-1]) & (merged[3][1:] == merged[3][:-1]) &
+                      (merged[4][1:] == merged[4][:-1]))
+        b["rows"] = tuple(c[m] for c in merged)
+    return a, b

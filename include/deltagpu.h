@@ -1,0 +1,169 @@
+/*
+ * deltagpu.h — C-ABI of libdeltagpu, the MI355X-native batched delta-join and
+ * anti-entropy engine for DeltaCrdt.AWLWWMap (reference: burmajam/delta_crdt_ex 0.5.10).
+ *
+ * This header is the drop-in boundary.  Each entry point names the reference
+ * function it replaces (path:line relative to the reference repository).  A
+ * caller (the Erlang NIF sketched in INTEGRATION.md, or the Python host mirror in
+ * delta_crdt_ex_amd/aw_lww_map.py via ctypes) marshals `%AWLWWMap{}` terms into
+ * the SoA dot rows below and back.
+ *
+ * Data model.  A state `%AWLWWMap{dots: c, value: %{key =>
+ * %{{v, ts} => MapSet[{node, counter}]}}}` is flattened to one ROW per dot:
+ *
+ *     key  u64   interned key id (a 64-bit hash of the key; exact interning on the host)
+ *     val  u64   order-preserving id of the value (Erlang term order), see H2
+ *     ts   i64   System.monotonic_time(:nanosecond) of the add (signed)
+ *     node u32   interned node id of the dot
+ *     cnt  u64   dot counter
+ *
+ * Rows are stored column-wise (SoA, device memory), sorted ascending by the tuple
+ * (key, val, ts [signed], node, cnt) and free of duplicates.  Every entry point
+ * that consumes a store assumes this; `dg_store_check` verifies it.
+ *
+ * A causal context is either a version vector (DG_CTX_VV: node[i] ascending and
+ * unique, cnt[i] = max counter, as produced by `Dots.compress/1`) or an explicit
+ * dot set (DG_CTX_DOTS: (node, cnt) ascending and unique, a `MapSet` of dots).
+ *
+ * Conventions: every function returns DG_OK (0) or a negative DG_E_* code and sets
+ * a thread-local message readable with dg_last_error().  Input pointers are
+ * caller-owned device pointers (a context's arrays may also be host pointers where
+ * noted).  Output stores/contexts are caller-allocated with `cap` set; on return
+ * `n` holds the produced count; DG_E_CAPACITY if `cap` is too small (nothing
+ * else is touched).  One dg_engine owns one HIP stream; engines are independent
+ * and may be used from different threads; a single engine is not re-entrant.
+ */
+#ifndef DELTAGPU_H
+#define DELTAGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DG_ABI_VERSION 1
+
+enum dg_status {
+  DG_OK = 0,
+  DG_E_INVAL = -1,     /* bad argument (null pointer, mixed context kinds where forbidden, ...) */
+  DG_E_CAPACITY = -2,  /* output capacity too small */
+  DG_E_DEVICE = -3,    /* HIP runtime error */
+  DG_E_NOMEM = -4,     /* device allocation failed */
+  DG_E_ORDER = -5,     /* input store/context not sorted+unique (dg_store_check) */
+  DG_E_CLAUSE = -6     /* the reference would raise FunctionClauseError / RuntimeError */
+};
+
+enum dg_context_kind { DG_CTX_VV = 0, DG_CTX_DOTS = 1 };
+
+typedef struct dg_store {
+  uint64_t* key;
+  uint64_t* val;
+  int64_t* ts;
+  uint32_t* node;
+  uint64_t* cnt;
+  uint64_t n;   /* rows present */
+  uint64_t cap; /* rows allocated (outputs only) */
+} dg_store;
+
+typedef struct dg_context {
+  int32_t kind; /* enum dg_context_kind */
+  int32_t reserved;
+  uint32_t* node;
+  uint64_t* cnt;
+  uint64_t n;
+  uint64_t cap;
+} dg_context;
+
+/* Merkle index over a store (the MerkleMap role, causal_crdt.ex:21,94,96,254,255,392-393).
+ * Leaves: one (key, hash) per distinct key, ascending by key.  Buckets: 2^depth,
+ * bucket(key) = key >> (64 - depth).  `nodes` is a heap in level order: level l
+ * (root l = 0) occupies [2^l - 1, 2^(l+1) - 1); the buckets are level `depth`. */
+typedef struct dg_merkle {
+  uint32_t depth;       /* 1..26 */
+  uint32_t reserved;
+  uint64_t* nodes;      /* 2^(depth+1) - 1 entries (caller-allocated) */
+  uint64_t* bucket_off; /* 2^depth + 1 entries: first leaf index of each bucket */
+  uint64_t* leaf_key;   /* cap_keys entries */
+  uint64_t* leaf_hash;
+  uint64_t n_keys;
+  uint64_t cap_keys;    /* must be >= the indexed store's row count */
+} dg_merkle;
+
+typedef struct dg_engine dg_engine;
+
+/* ---- lifecycle ------------------------------------------------------------ */
+int dg_abi_version(void);
+const char* dg_last_error(void);
+/* `hip_stream` NULL: the engine creates its own stream; otherwise it launches on the
+ * given hipStream_t (e.g. torch.cuda.current_stream().cuda_stream) and never
+ * destroys it. */
+int dg_engine_create(int device, void* hip_stream, dg_engine** out);
+int dg_engine_destroy(dg_engine* e);
+void* dg_engine_stream(dg_engine* e);
+int dg_engine_sync(dg_engine* e);
+
+/* Verify the sorted+unique precondition of a store (DG_E_ORDER if violated). */
+int dg_store_check(dg_engine* e, const dg_store* s);
+
+/* ---- the join (hot path) --------------------------------------------------- */
+/* AWLWWMap.join/3 (lib/delta_crdt/aw_lww_map.ex:153-158) with join_or_maps/4
+ * (:161-193) and join_dot_sets/4 (:196-209):
+ *   per (key, {v, ts}) entry:  s1 ∩ s2  ∪  s1 \ c2  ∪  s2 \ c1      (Dots.difference :54-65,
+ *                                                                     Dots.member? :67-73)
+ *   empty entries and keys dropped (:177-181); out_ctx = Dots.union(c1, c2) (:39-52).
+ * `keys` (device, ascending unique, n_keys entries) is the reference's `keys`
+ * argument; NULL means "every key of a and b" (a full-state join).  Keys of a or b
+ * outside `keys` are not joined but carried over right-biased, as
+ * Map.merge(Map.drop(d1, keys), Map.drop(d2, keys)) does (:185-188).
+ * out->cap must be >= a->n + b->n; out_ctx->cap >= ca->n + cb->n.  Synchronous. */
+int dg_join2(dg_engine* e, const dg_store* a, const dg_context* ca, const dg_store* b,
+             const dg_context* cb, const uint64_t* keys, uint64_t n_keys, dg_store* out,
+             dg_context* out_ctx);
+
+/* Same, asynchronous on the engine stream: the output row count is written to
+ * d_counts[0] and the output context size to d_counts[1] (device memory); out->n
+ * and out_ctx->n are NOT updated and out_ctx->kind is set on the host. */
+int dg_join2_async(dg_engine* e, const dg_store* a, const dg_context* ca, const dg_store* b,
+                   const dg_context* cb, const uint64_t* keys, uint64_t n_keys,
+                   dg_store* out, dg_context* out_ctx, uint64_t* d_counts);
+
+/* Fold of join/3 over k stores (how CausalCrdt applies k deltas in a row,
+ * causal_crdt.ex:86-89,383-384): out = join(...join(join(s0, s1), s2)..., s_{k-1})
+ * over all keys.  A row survives iff for every input i it is present in s_i or its
+ * dot is not covered by c_i.  out->cap >= Σ n_i. */
+int dg_joink(dg_engine* e, int k, const dg_store* stores, const dg_context* ctxs, dg_store* out,
+             dg_context* out_ctx);
+
+/* ---- causal-context algebra ----------------------------------------------- */
+/* Dots.union/2 (aw_lww_map.ex:39-52): VV ⊔ VV = per-node max; VV ⊔ DOTS folds the
+ * dots into the VV; DOTS ⊔ DOTS = set union. */
+int dg_context_union(dg_engine* e, const dg_context* a, const dg_context* b, dg_context* out);
+/* Dots.compress/1 + compress_dots/1 (aw_lww_map.ex:13-20,115-117).  DG_E_CLAUSE if
+ * `dots` is already a VV (the reference raises FunctionClauseError there). */
+int dg_compress_dots(dg_engine* e, const dg_context* dots, dg_context* out_vv);
+
+/* ---- read (LWW) ------------------------------------------------------------ */
+/* AWLWWMap.read/1,2 (aw_lww_map.ex:211-224): per key, the value of the entry with
+ * the greatest ts; a tie goes to the smallest {val, ts} (the first entry in flatmap
+ * order).  `keys` NULL: every key; otherwise only those keys
+ * (Map.take).  Output ascending by key. */
+int dg_read_lww(dg_engine* e, const dg_store* s, const uint64_t* keys, uint64_t n_keys,
+                uint64_t* out_key, uint64_t* out_val, uint64_t cap, uint64_t* n_out);
+
+/* ---- Merkle anti-entropy (MerkleMap role) --------------------------------- */
+/* Build leaves + level-wise bucket hashes for `s` (MerkleMap.put/update_hashes,
+ * causal_crdt.ex:94,254,390-394).  t->depth and capacities set by the caller. */
+int dg_merkle_build(dg_engine* e, const dg_store* s, dg_merkle* t);
+/* Keys whose raw value maps differ between the two indexed stores (present in one
+ * only, or with different rows), ascending — the role of
+ * MerkleMap.prepare_partial_diff/continue_partial_diff (causal_crdt.ex:96,255).
+ * Both trees must have the same depth. */
+int dg_merkle_diff(dg_engine* e, const dg_merkle* a, const dg_merkle* b, uint64_t* out_keys,
+                   uint64_t cap, uint64_t* n_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DELTAGPU_H */

@@ -1,0 +1,243 @@
+"""ctypes wrapper around oracle/_build/libdeltaref.so (the C restatement) over
+numpy arrays.  TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
+
+Rows are a tuple of five numpy arrays ``(key u64, val u64, ts i64, node u32, cnt u64)``
+sorted by the full tuple; a context is ``(kind, node u32, cnt u64)``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from delta_crdt_ex_amd import _abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_build", "libdeltaref.so")
+
+VV, DOTS = _abi.DG_CTX_VV, _abi.DG_CTX_DOTS
+
+_lib = None
+
+
+def build():
+    r = subprocess.run(["make", "-s", "-C", HERE], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("oracle build failed:\n" + r.stdout + r.stderr)
+    return LIB
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = C.CDLL(LIB)
+        S, X, M = C.POINTER(_abi.dg_store), C.POINTER(_abi.dg_context), C.POINTER(_abi.dg_merkle)
+        L.ref_join2.argtypes = [S, X, S, X, _abi.P64, C.c_uint64, S, X]
+        L.ref_joink.argtypes = [C.c_int, S, X, S, X]
+        L.ref_context_union.argtypes = [X, X, X]
+        L.ref_compress_dots.argtypes = [X, X]
+        L.ref_read_lww.argtypes = [S, _abi.P64, C.c_uint64, _abi.P64, _abi.P64, C.c_uint64,
+                                   _abi.P64]
+        L.ref_merkle_build.argtypes = [S, M]
+        L.ref_merkle_diff.argtypes = [M, M, _abi.P64, C.c_uint64, _abi.P64]
+        L.ref_store_diff.argtypes = [S, S, _abi.P64, C.c_uint64, _abi.P64]
+        L.ref_store_check.argtypes = [S]
+        L.ref_row_hash.argtypes = [C.c_uint64, C.c_uint64, C.c_int64, C.c_uint32, C.c_uint64]
+        L.ref_row_hash.restype = C.c_uint64
+        L.ref_node_hash.argtypes = [C.c_uint64, C.c_uint64]
+        L.ref_node_hash.restype = C.c_uint64
+        _lib = L
+    return _lib
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+def empty_rows(n=0):
+    return (np.zeros(n, np.uint64), np.zeros(n, np.uint64), np.zeros(n, np.int64),
+            np.zeros(n, np.uint32), np.zeros(n, np.uint64))
+
+
+def as_rows(rows):
+    k, v, t, nd, c = rows
+    return (np.ascontiguousarray(k, np.uint64), np.ascontiguousarray(v, np.uint64),
+            np.ascontiguousarray(t, np.int64), np.ascontiguousarray(nd, np.uint32),
+            np.ascontiguousarray(c, np.uint64))
+
+
+def _store(rows, cap=None):
+    rows = as_rows(rows)
+    s = _abi.dg_store()
+    s.key = _p(rows[0], _abi.P64)
+    s.val = _p(rows[1], _abi.P64)
+    s.ts = _p(rows[2], _abi.PI64)
+    s.node = _p(rows[3], _abi.P32)
+    s.cnt = _p(rows[4], _abi.P64)
+    s.n = len(rows[0])
+    s.cap = len(rows[0]) if cap is None else cap
+    return s, rows
+
+
+def _ctx(ctx):
+    kind, node, cnt = ctx
+    node = np.ascontiguousarray(node, np.uint32)
+    cnt = np.ascontiguousarray(cnt, np.uint64)
+    c = _abi.dg_context()
+    c.kind = kind
+    c.node = _p(node, _abi.P32)
+    c.cnt = _p(cnt, _abi.P64)
+    c.n = len(node)
+    c.cap = len(node)
+    return c, (kind, node, cnt)
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with {rc}")
+
+
+def join2(a, ca, b, cb, keys=None):
+    """AWLWWMap.join/3 over SoA rows (aw_lww_map.ex:153-209)."""
+    sa, a = _store(a)
+    sb, b = _store(b)
+    xa, ca = _ctx(ca)
+    xb, cb = _ctx(cb)
+    n = len(a[0]) + len(b[0])
+    out = empty_rows(n + 1)
+    so, _ = _store(out, cap=n)
+    so.n = 0
+    nc = len(ca[1]) + len(cb[1])
+    onode, ocnt = np.zeros(nc + 1, np.uint32), np.zeros(nc + 1, np.uint64)
+    xo, _ = _ctx((VV, onode, ocnt))
+    xo.cap = nc
+    if keys is not None:
+        keys = np.ascontiguousarray(np.unique(np.asarray(keys, np.uint64)))
+        kp, nk = _p(keys, _abi.P64), len(keys)
+    else:
+        kp, nk = None, 0
+    _check(lib().ref_join2(C.byref(sa), C.byref(xa), C.byref(sb), C.byref(xb), kp, nk,
+                           C.byref(so), C.byref(xo)), "ref_join2")
+    m = so.n
+    return tuple(col[:m] for col in out), (xo.kind, onode[: xo.n], ocnt[: xo.n])
+
+
+def joink(stores, ctxs):
+    k = len(stores)
+    keep = []
+    S = (_abi.dg_store * k)()
+    X = (_abi.dg_context * k)()
+    for i in range(k):
+        S[i], r = _store(stores[i])
+        X[i], c = _ctx(ctxs[i])
+        keep.append((r, c))
+    n = sum(len(s[0]) for s in stores)
+    nc = sum(len(c[1]) for c in ctxs)
+    out = empty_rows(n + 1)
+    so, _ = _store(out, cap=n)
+    so.n = 0
+    onode, ocnt = np.zeros(nc + 1, np.uint32), np.zeros(nc + 1, np.uint64)
+    xo, _ = _ctx((VV, onode, ocnt))
+    xo.cap = nc
+    _check(lib().ref_joink(k, S, X, C.byref(so), C.byref(xo)), "ref_joink")
+    return tuple(col[: so.n] for col in out), (xo.kind, onode[: xo.n], ocnt[: xo.n])
+
+
+def context_union(ca, cb):
+    xa, ca = _ctx(ca)
+    xb, cb = _ctx(cb)
+    nc = len(ca[1]) + len(cb[1])
+    onode, ocnt = np.zeros(nc + 1, np.uint32), np.zeros(nc + 1, np.uint64)
+    xo, _ = _ctx((VV, onode, ocnt))
+    xo.cap = nc
+    _check(lib().ref_context_union(C.byref(xa), C.byref(xb), C.byref(xo)), "ref_context_union")
+    return (xo.kind, onode[: xo.n], ocnt[: xo.n])
+
+
+def compress_dots(c):
+    xa, c = _ctx(c)
+    onode, ocnt = np.zeros(len(c[1]) + 1, np.uint32), np.zeros(len(c[1]) + 1, np.uint64)
+    xo, _ = _ctx((VV, onode, ocnt))
+    xo.cap = len(c[1])
+    rc = lib().ref_compress_dots(C.byref(xa), C.byref(xo))
+    if rc == _abi.DG_E_CLAUSE:
+        raise _abi.FunctionClauseError(rc, "compress/1 on a VV")
+    _check(rc, "ref_compress_dots")
+    return (xo.kind, onode[: xo.n], ocnt[: xo.n])
+
+
+def read_lww(rows, keys=None):
+    s, rows = _store(rows)
+    n = len(rows[0])
+    ok, ov = np.zeros(n + 1, np.uint64), np.zeros(n + 1, np.uint64)
+    cnt = np.zeros(1, np.uint64)
+    if keys is not None:
+        keys = np.ascontiguousarray(np.unique(np.asarray(keys, np.uint64)))
+        kp, nk = _p(keys, _abi.P64), len(keys)
+    else:
+        kp, nk = None, 0
+    _check(lib().ref_read_lww(C.byref(s), kp, nk, _p(ok, _abi.P64), _p(ov, _abi.P64), n,
+                              _p(cnt, _abi.P64)), "ref_read_lww")
+    m = int(cnt[0])
+    return ok[:m], ov[:m]
+
+
+class Tree:
+    def __init__(self, depth, cap):
+        nb = 1 << depth
+        self.depth = depth
+        self.nodes = np.zeros(2 * nb - 1, np.uint64)
+        self.bucket_off = np.zeros(nb + 1, np.uint64)
+        self.leaf_key = np.zeros(max(cap, 1), np.uint64)
+        self.leaf_hash = np.zeros(max(cap, 1), np.uint64)
+        self.n_keys = 0
+
+    def abi(self):
+        t = _abi.dg_merkle()
+        t.depth = self.depth
+        t.nodes = _p(self.nodes, _abi.P64)
+        t.bucket_off = _p(self.bucket_off, _abi.P64)
+        t.leaf_key = _p(self.leaf_key, _abi.P64)
+        t.leaf_hash = _p(self.leaf_hash, _abi.P64)
+        t.n_keys = self.n_keys
+        t.cap_keys = len(self.leaf_key)
+        return t
+
+
+def merkle_build(rows, depth):
+    s, rows = _store(rows)
+    t = Tree(depth, len(rows[0]))
+    ta = t.abi()
+    _check(lib().ref_merkle_build(C.byref(s), C.byref(ta)), "ref_merkle_build")
+    t.n_keys = ta.n_keys
+    return t
+
+
+def merkle_diff(ta: Tree, tb: Tree):
+    cap = ta.n_keys + tb.n_keys + 1
+    out = np.zeros(cap, np.uint64)
+    n = np.zeros(1, np.uint64)
+    a, b = ta.abi(), tb.abi()
+    _check(lib().ref_merkle_diff(C.byref(a), C.byref(b), _p(out, _abi.P64), cap, _p(n, _abi.P64)),
+           "ref_merkle_diff")
+    return out[: int(n[0])]
+
+
+def store_diff(ra, rb):
+    sa, ra = _store(ra)
+    sb, rb = _store(rb)
+    cap = len(ra[0]) + len(rb[0]) + 1
+    out = np.zeros(cap, np.uint64)
+    n = np.zeros(1, np.uint64)
+    _check(lib().ref_store_diff(C.byref(sa), C.byref(sb), _p(out, _abi.P64), cap, _p(n, _abi.P64)),
+           "ref_store_diff")
+    return out[: int(n[0])]
+
+
+def store_check(rows) -> bool:
+    s, _ = _store(rows)
+    return lib().ref_store_check(C.byref(s)) == 0

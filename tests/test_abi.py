@@ -1,0 +1,93 @@
+"""The C-ABI boundary (include/deltagpu.h) without a GPU: the library builds and
+loads, exports every function the header declares, the ctypes mirror matches the
+header's struct layouts, and the product fails loudly (no CPU fallback) when no
+device is present."""
+import ctypes as C
+import os
+import subprocess
+import tempfile
+
+import pytest
+
+from delta_crdt_ex_amd import _abi
+from delta_crdt_ex_amd.build import build
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    build()
+    return _abi.load()
+
+
+def test_every_header_function_is_exported(lib):
+    names = _abi.header_functions()
+    assert len(names) >= 15
+    for name in names:
+        assert hasattr(lib, name), name
+        assert name in _abi._SIGS, f"ctypes signature missing for {name}"
+
+
+def test_abi_version(lib):
+    assert lib.dg_abi_version() == 1
+
+
+LAYOUT_C = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "deltagpu.h"
+#define F(T, f) printf(#T "." #f " %zu\n", offsetof(T, f));
+int main(void) {
+  printf("dg_store %zu\n", sizeof(dg_store));
+  F(dg_store, key) F(dg_store, val) F(dg_store, ts) F(dg_store, node) F(dg_store, cnt)
+  F(dg_store, n) F(dg_store, cap)
+  printf("dg_context %zu\n", sizeof(dg_context));
+  F(dg_context, kind) F(dg_context, node) F(dg_context, cnt) F(dg_context, n) F(dg_context, cap)
+  printf("dg_merkle %zu\n", sizeof(dg_merkle));
+  F(dg_merkle, depth) F(dg_merkle, nodes) F(dg_merkle, bucket_off) F(dg_merkle, leaf_key)
+  F(dg_merkle, leaf_hash) F(dg_merkle, n_keys) F(dg_merkle, cap_keys)
+  return 0;
+}
+"""
+
+
+def test_struct_layout_matches_header():
+    with tempfile.TemporaryDirectory() as d:
+        src = os.path.join(d, "layout.c")
+        exe = os.path.join(d, "layout")
+        open(src, "w").write(LAYOUT_C)
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), src, "-o", exe], check=True)
+        out = subprocess.run([exe], capture_output=True, text=True, check=True).stdout
+    want = {}
+    for line in out.strip().splitlines():
+        name, v = line.split()
+        want[name] = int(v)
+    for cls in (_abi.dg_store, _abi.dg_context, _abi.dg_merkle):
+        assert C.sizeof(cls) == want[cls.__name__]
+        for fname, _ in cls._fields_:
+            key = f"{cls.__name__}.{fname}"
+            if key in want:
+                assert getattr(cls, fname).offset == want[key], key
+
+
+def test_no_device_fails_loudly(lib):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    h = C.c_void_p()
+    rc = lib.dg_engine_create(0, None, C.byref(h))
+    assert rc == _abi.DG_E_DEVICE
+    assert b"hipGetDeviceCount" in lib.dg_last_error()
+    from delta_crdt_ex_amd.store import Engine
+    with pytest.raises(RuntimeError):
+        Engine(0)
+
+
+def test_null_arguments_are_rejected(lib):
+    # argument validation happens before any device call
+    s = _abi.dg_store()
+    x = _abi.dg_context()
+    assert lib.dg_join2(None, C.byref(s), C.byref(x), C.byref(s), C.byref(x), None, 0,
+                        C.byref(s), C.byref(x)) == _abi.DG_E_INVAL
+    assert lib.dg_read_lww(None, C.byref(s), None, 0, None, None, 0, None) == _abi.DG_E_INVAL

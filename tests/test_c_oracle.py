@@ -1,0 +1,200 @@
+"""The C oracle (oracle/deltaref.c, the SoA restatement and the timed CPU baseline)
+against the term-level oracle (oracle/awlww_term.py, pinned by the reference's own
+tests in test_oracle_reference_tests.py), and the synthetic generators against the
+term oracle replaying the same operations."""
+import numpy as np
+import pytest
+
+from delta_crdt_ex_amd import workloads as W
+from delta_crdt_ex_amd.interning import Universe, splitmix64
+from oracle import awlww_term as T
+from oracle import convert as CV
+from oracle import ref as R
+
+
+def soa_to_term(rows, ctx):
+    """Raw-id term state (keys/values/nodes are their integer ids)."""
+    k, v, t, n, c = rows
+    value = {}
+    for i in range(len(k)):
+        value.setdefault(int(k[i]), {}).setdefault((int(v[i]), int(t[i])), set()).add(
+            (int(n[i]), int(c[i])))
+    value = {key: {e: frozenset(d) for e, d in ents.items()} for key, ents in value.items()}
+    kind, node, cnt = ctx
+    if kind == R.DOTS:
+        dots = frozenset((int(a), int(b)) for a, b in zip(node, cnt))
+    else:
+        dots = {int(a): int(b) for a, b in zip(node, cnt)}
+    return T.AW(dots, value)
+
+
+def term_to_soa_raw(state):
+    ks, vs, ts, ns, cs = [], [], [], [], []
+    for key, ents in state.value.items():
+        for (val, t), dots in ents.items():
+            for (nd, c) in dots:
+                ks.append(key)
+                vs.append(val)
+                ts.append(t)
+                ns.append(nd)
+                cs.append(c)
+    rows = CV.sort_rows(ks, vs, ts, ns, cs)
+    d = state.dots
+    if isinstance(d, frozenset):
+        pairs = sorted(d)
+        ctx = (R.DOTS, np.array([p[0] for p in pairs], np.uint32), np.array([p[1] for p in pairs], np.uint64))
+    else:
+        pairs = sorted(d.items())
+        ctx = (R.VV, np.array([p[0] for p in pairs], np.uint32), np.array([p[1] for p in pairs], np.uint64))
+    return rows, ctx
+
+
+def rows_equal(a, b):
+    return len(a[0]) == len(b[0]) and all(np.array_equal(x, y) for x, y in zip(a, b))
+
+
+def ctx_equal(a, b):
+    return a[0] == b[0] and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
+
+
+CASES = [
+    dict(n_keys=40, ts_range=1 << 40, dense_ctx=True, ctx_kind=W.VV),
+    dict(n_keys=40, ts_range=2, dense_ctx=True, ctx_kind=W.VV),        # LWW ties
+    dict(n_keys=40, ts_range=1 << 40, dense_ctx=False, ctx_kind=W.VV),  # store not covered by own VV (H5)
+    dict(n_keys=30, ts_range=4, dense_ctx=False, ctx_kind=W.DOTS),
+    dict(n_keys=30, ts_range=4, dense_ctx=True, ctx_kind=W.DOTS),
+    dict(n_keys=0, ts_range=4, dense_ctx=True, ctx_kind=W.VV),          # empty
+]
+
+
+@pytest.mark.parametrize("case", range(len(CASES)))
+@pytest.mark.parametrize("seed", range(12))
+def test_join2_matches_term_oracle(case, seed):
+    rng = np.random.default_rng(1000 * case + seed)
+    a, b = W.random_pair(rng, **CASES[case])
+    ta, tb = soa_to_term(a["rows"], a["ctx"]), soa_to_term(b["rows"], b["ctx"])
+    all_keys = sorted(set(ta.value) | set(tb.value))
+    keysets = [None, all_keys, all_keys[: len(all_keys) // 2],
+               [x for x in all_keys if x % 3 == 0] + [12345]]
+    for ks in keysets:
+        rows, ctx = R.join2(a["rows"], a["ctx"], b["rows"], b["ctx"], keys=ks)
+        want = T.join(ta, tb, all_keys if ks is None else ks)
+        wrows, wctx = term_to_soa_raw(want)
+        assert rows_equal(rows, wrows), f"keys={ks is None}"
+        assert ctx_equal(ctx, wctx)
+        assert R.store_check(rows)
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_read_and_contexts_match_term_oracle(seed):
+    rng = np.random.default_rng(seed)
+    a, b = W.random_pair(rng, n_keys=50, ts_range=3, ctx_kind=W.DOTS if seed % 2 else W.VV)
+    ta = soa_to_term(a["rows"], a["ctx"])
+    ok, ov = R.read_lww(a["rows"])
+    want = T.read(ta)
+    assert dict(zip(map(int, ok), map(int, ov))) == want
+    assert list(map(int, ok)) == sorted(want)
+    sub = sorted(want)[::3]
+    ok2, ov2 = R.read_lww(a["rows"], keys=sub)
+    assert dict(zip(map(int, ok2), map(int, ov2))) == T.read(ta, list(sub))
+    # Dots.union / compress
+    u = R.context_union(a["ctx"], b["ctx"])
+    tu = T.dots_union(soa_to_term(a["rows"], a["ctx"]).dots, soa_to_term(b["rows"], b["ctx"]).dots)
+    assert ctx_equal(u, term_to_soa_raw(T.AW(tu, {}))[1])
+    if a["ctx"][0] == R.DOTS:
+        cc = R.compress_dots(a["ctx"])
+        tc = T.dots_compress(ta.dots)
+        assert ctx_equal(cc, term_to_soa_raw(T.AW(tc, {}))[1])
+    else:
+        with pytest.raises(Exception):
+            R.compress_dots(a["ctx"])
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_joink_is_left_fold(seed):
+    rng = np.random.default_rng(77 + seed)
+    reps = []
+    for _ in range(3):
+        a, b = W.random_pair(rng, n_keys=25, ts_range=8, dense_ctx=bool(seed % 2))
+        reps += [a, b]
+    rows, ctx = R.joink([r["rows"] for r in reps], [r["ctx"] for r in reps])
+    acc_r, acc_c = reps[0]["rows"], reps[0]["ctx"]
+    for r in reps[1:]:
+        acc_r, acc_c = R.join2(acc_r, acc_c, r["rows"], r["ctx"])
+    assert rows_equal(rows, acc_r) and ctx_equal(ctx, acc_c)
+    terms = [soa_to_term(r["rows"], r["ctx"]) for r in reps]
+    keys = sorted(set().union(*[set(t.value) for t in terms]))
+    want = T.join_k(terms, keys)
+    wr, wc = term_to_soa_raw(want)
+    assert rows_equal(rows, wr) and ctx_equal(ctx, wc)
+
+
+@pytest.mark.parametrize("seed", range(5))
+def test_merkle_diff_is_exact_store_diff(seed):
+    rng = np.random.default_rng(seed)
+    a, b = W.random_pair(rng, n_keys=300, ts_range=1 << 30)
+    for depth in (1, 3, 8, 12):
+        ta, tb = R.merkle_build(a["rows"], depth), R.merkle_build(b["rows"], depth)
+        d = R.merkle_diff(ta, tb)
+        assert np.array_equal(d, R.store_diff(a["rows"], b["rows"]))
+        same = R.merkle_diff(ta, R.merkle_build(a["rows"], depth))
+        assert len(same) == 0
+        # roots differ iff the stores differ
+        assert (ta.nodes[0] != tb.nodes[0]) == (len(d) > 0)
+
+
+# ------------------------------------------------------------- generators vs term replay
+
+def test_config1_generator_matches_term_replay():
+    n = 200
+    U = Universe()
+    clock = iter(range(10**9))
+    # node 1 adds k => k with ts = k * 1000
+    A = T.compress_dots(T.new())
+    for k in range(1, n + 1):
+        A = T.join(A, T.add(k, k, 1, A, k * 1000), [k])
+    B = A
+    for k in range(1, n + 1):
+        if k % 10 == 0:
+            A = T.join(A, T.remove(k, 1, A), [k])
+    for k in range(1, n + 1):
+        if k % 10 == 5:
+            B = T.join(B, T.add(k, k + 1, 2, B, n * 1000 + k), [k])
+    ga, gb = W.config1(n)
+    for term_state, gen in ((A, ga), (B, gb)):
+        rows, ctx = CV.state_to_soa(term_state, U)
+        assert rows_equal(rows, gen["rows"])
+        assert ctx_equal(ctx, gen["ctx"])
+    # and the config-1 join (CPU path) agrees across the two oracles
+    rows, ctx = R.join2(ga["rows"], ga["ctx"], gb["rows"], gb["ctx"])
+    want = T.join(A, B, sorted(set(A.value) | set(B.value)))
+    wrows, wctx = CV.state_to_soa(want, U)
+    assert rows_equal(rows, wrows) and ctx_equal(ctx, wctx)
+    ok, ov = R.read_lww(rows)
+    got = {U.key_term(int(k)): U.value_term(int(v)) for k, v in zip(ok, ov)}
+    assert got == T.read(want)
+    del clock
+
+
+def test_config2_generator_matches_term_replay():
+    n = 300
+    U = Universe()
+    ga, gb = W.config2(n_keys=n, seed=5)
+    base = T.compress_dots(T.new())
+    for k in range(1, n + 1):
+        base = T.join(base, T.add(k, k, 0, base, k * 1000), [k])
+    # recover the generator's choices (which keys, which values/ts) from its rows
+    for node_id, gen in ((1, ga), (2, gb)):
+        k, v, t, nd, c = gen["rows"]
+        mine = nd == node_id
+        order = np.argsort(c[mine])
+        st = base
+        for kid, vid, ts in zip(k[mine][order], v[mine][order], t[mine][order]):
+            key = U.key_term(int(kid)) if int(kid) in U._key_term else None
+            if key is None:
+                key = next(x for x in range(1, n + 1) if splitmix64(x) == int(kid))
+            val = int(vid) - (1 << 62)
+            st = T.join(st, T.add(key, val, node_id, st, int(ts)), [key])
+        rows, ctx = CV.state_to_soa(st, U)
+        assert rows_equal(rows, gen["rows"])
+        assert ctx_equal(ctx, gen["ctx"])

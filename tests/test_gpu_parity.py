@@ -1,0 +1,247 @@
+"""GPU parity: libdeltagpu (through its C-ABI, on cuda:0) against the C oracle and
+the golden fixtures.  Integer work => bit-exact equality everywhere."""
+import numpy as np
+import pytest
+import torch
+
+from delta_crdt_ex_amd import workloads as W
+from delta_crdt_ex_amd._abi import CapacityError, FunctionClauseError
+from delta_crdt_ex_amd.store import Context, Store, u64
+from oracle import ref as R
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def up(rep):
+    rows, ctx = rep["rows"], rep["ctx"]
+    return Store.from_numpy(*rows, device=DEV), Context.from_numpy(ctx[0], ctx[1], ctx[2], DEV)
+
+
+def rows_eq(got: Store, want):
+    g = got.to_numpy()
+    assert got.n == len(want[0]), (got.n, len(want[0]))
+    for i, (x, y) in enumerate(zip(g, want)):
+        assert np.array_equal(x, y), f"column {i} differs"
+
+
+def ctx_eq(got: Context, want):
+    assert got.kind == want[0]
+    node, cnt = got.to_numpy()
+    assert np.array_equal(node, want[1]) and np.array_equal(cnt, want[2])
+
+
+def check_join(engine, a, b, keys=None):
+    sa, ca = up(a)
+    sb, cb = up(b)
+    kt = None
+    if keys is not None:
+        ku = np.unique(np.asarray(keys, np.uint64))
+        kt = torch.from_numpy(ku.view(np.int64)).to(DEV)
+    out, octx = engine.join2(sa, ca, sb, cb, keys=kt)
+    wrows, wctx = R.join2(a["rows"], a["ctx"], b["rows"], b["ctx"], keys=keys)
+    rows_eq(out, wrows)
+    ctx_eq(octx, wctx)
+    return out, octx
+
+
+CASES = [
+    dict(n_keys=40, ts_range=1 << 40, dense_ctx=True, ctx_kind=W.VV),
+    dict(n_keys=40, ts_range=2, dense_ctx=True, ctx_kind=W.VV),
+    dict(n_keys=40, ts_range=1 << 40, dense_ctx=False, ctx_kind=W.VV),
+    dict(n_keys=30, ts_range=4, dense_ctx=False, ctx_kind=W.DOTS),
+    dict(n_keys=30, ts_range=4, dense_ctx=True, ctx_kind=W.DOTS),
+    dict(n_keys=0, ts_range=4, dense_ctx=True, ctx_kind=W.VV),
+    dict(n_keys=3000, ts_range=1 << 20, dense_ctx=False, ctx_kind=W.VV),   # multi-tile
+    dict(n_keys=2000, ts_range=3, dense_ctx=False, ctx_kind=W.DOTS),       # multi-tile, ties
+]
+
+
+@pytest.mark.parametrize("case", range(len(CASES)))
+@pytest.mark.parametrize("seed", range(4))
+def test_join2_random(engine, case, seed):
+    rng = np.random.default_rng(1000 * case + seed)
+    a, b = W.random_pair(rng, **CASES[case])
+    check_join(engine, a, b)
+    check_join(engine, b, a)
+    keys = np.unique(np.concatenate([a["rows"][0], b["rows"][0]]))
+    if len(keys):
+        check_join(engine, a, b, keys=keys[::2])
+        check_join(engine, a, b, keys=np.concatenate([keys[1::3], np.array([12345], np.uint64)]))
+
+
+def test_join2_identical_and_subset(engine):
+    """Every row duplicated across the stores: dedup at every tile seam."""
+    a, b = W.config2(n_keys=20000, seed=9)
+    check_join(engine, a, a)
+    # b's store as a subset of a's, contexts equal
+    sub = {"rows": tuple(c[::3] for c in a["rows"]), "ctx": a["ctx"]}
+    check_join(engine, a, sub)
+    check_join(engine, sub, a)
+
+
+def test_join2_empty_sides(engine):
+    a, b = W.config2(n_keys=5000, seed=3)
+    empty = {"rows": R.empty_rows(0), "ctx": W.vv({})}
+    check_join(engine, a, empty)
+    check_join(engine, empty, b)
+    check_join(engine, empty, empty)
+
+
+def test_join2_config2_full_size(engine):
+    """BASELINE config 2 at its full size (1M keys, 2M rows in)."""
+    a, b = W.config2()
+    out, octx = check_join(engine, a, b)
+    assert 1_050_000 < out.n < 1_150_000
+    engine.store_check(out)
+
+
+def test_join2_properties_full_size(engine):
+    """Size-independent CRDT laws at config-2 size: commutativity, idempotence."""
+    a, b = W.config2(seed=11)
+    sa, ca = up(a)
+    sb, cb = up(b)
+    ab, cab = engine.join2(sa, ca, sb, cb)
+    ba, cba = engine.join2(sb, cb, sa, ca)
+    for x, y in zip(ab.to_numpy(), ba.to_numpy()):
+        assert np.array_equal(x, y)
+    aa, caa = engine.join2(ab, cab, ab, cab)
+    for x, y in zip(aa.to_numpy(), ab.to_numpy()):
+        assert np.array_equal(x, y)
+
+
+def test_join2_capacity_error(engine):
+    a, b = W.config2(n_keys=1000, seed=1)
+    sa, ca = up(a)
+    sb, cb = up(b)
+    small = Store.empty(10, DEV)
+    with pytest.raises(CapacityError):
+        engine.join2(sa, ca, sb, cb, out=small)
+
+
+def test_join2_async_counts(engine):
+    a, b = W.config2(n_keys=50000, seed=4)
+    sa, ca = up(a)
+    sb, cb = up(b)
+    out = Store.empty(sa.n + sb.n, DEV)
+    octx = Context.empty(0, ca.n + cb.n, DEV)
+    d = torch.zeros(8, dtype=torch.int64, device=DEV)
+    for _ in range(3):
+        engine.join2_async(sa, ca, sb, cb, out, octx, d_counts=d)
+    engine.sync()
+    out.n, octx.n = int(d[0]), int(d[1])
+    wrows, wctx = R.join2(a["rows"], a["ctx"], b["rows"], b["ctx"])
+    rows_eq(out, wrows)
+    ctx_eq(octx, wctx)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_read_lww(engine, seed):
+    rng = np.random.default_rng(seed)
+    a, _ = W.random_pair(rng, n_keys=3000 if seed % 2 else 50, ts_range=3)
+    s, _c = up(a)
+    ok, ov = engine.read_lww(s)
+    wk, wv = R.read_lww(a["rows"])
+    assert np.array_equal(u64(ok), wk) and np.array_equal(u64(ov), wv)
+    sub = wk[::3]
+    kt = torch.from_numpy(np.ascontiguousarray(sub).view(np.int64)).to(DEV)
+    ok, ov = engine.read_lww(s, keys=kt)
+    wk, wv = R.read_lww(a["rows"], keys=sub)
+    assert np.array_equal(u64(ok), wk) and np.array_equal(u64(ov), wv)
+
+
+def test_read_lww_config2(engine):
+    a, b = W.config2()
+    rows, _ = R.join2(a["rows"], a["ctx"], b["rows"], b["ctx"])
+    s = Store.from_numpy(*rows, device=DEV)
+    ok, ov = engine.read_lww(s)
+    wk, wv = R.read_lww(rows)
+    assert np.array_equal(u64(ok), wk) and np.array_equal(u64(ov), wv)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_context_union_and_compress(engine, seed):
+    rng = np.random.default_rng(seed)
+    kinds = [(W.VV, W.VV), (W.DOTS, W.DOTS), (W.VV, W.DOTS)][seed % 3]
+    a, _ = W.random_pair(rng, n_keys=200, ctx_kind=kinds[0], dense_ctx=False)
+    b, _ = W.random_pair(rng, n_keys=200, ctx_kind=kinds[1], dense_ctx=False)
+    _, ca = up(a)
+    _, cb = up(b)
+    ctx_eq(engine.context_union(ca, cb), R.context_union(a["ctx"], b["ctx"]))
+    ctx_eq(engine.context_union(cb, ca), R.context_union(b["ctx"], a["ctx"]))
+    if a["ctx"][0] == W.DOTS:
+        ctx_eq(engine.compress_dots(ca), R.compress_dots(a["ctx"]))
+    else:
+        with pytest.raises(FunctionClauseError):
+            engine.compress_dots(ca)
+
+
+def test_large_dot_set_union(engine):
+    n = 20000
+    rng = np.random.default_rng(5)
+    def dots():
+        nd = np.sort(rng.integers(0, 50, n).astype(np.uint32))
+        c = rng.integers(1, 10**6, n).astype(np.uint64)
+        o = np.lexsort((c, nd))
+        pairs = np.unique(np.stack([nd[o].astype(np.uint64), c[o]], 1), axis=0)
+        return (W.DOTS, pairs[:, 0].astype(np.uint32), pairs[:, 1].astype(np.uint64))
+    x, y = dots(), dots()
+    cx = Context.from_numpy(*x, DEV)
+    cy = Context.from_numpy(*y, DEV)
+    ctx_eq(engine.context_union(cx, cy), R.context_union(x, y))
+    ctx_eq(engine.compress_dots(cx), R.compress_dots(x))
+
+
+@pytest.mark.parametrize("depth", [1, 5, 8, 12, 16])
+def test_merkle_build_and_diff(engine, depth):
+    a, b = W.merkle_pair(n_keys=20000, diff_frac=0.01, seed=depth)
+    sa, _ = up(a)
+    sb, _ = up(b)
+    ta, tb = engine.merkle_build(sa, depth), engine.merkle_build(sb, depth)
+    ra, rb = R.merkle_build(a["rows"], depth), R.merkle_build(b["rows"], depth)
+    for t, r in ((ta, ra), (tb, rb)):
+        assert t.n_keys == r.n_keys
+        assert np.array_equal(u64(t.leaf_key[: t.n_keys]), r.leaf_key[: r.n_keys])
+        assert np.array_equal(u64(t.leaf_hash[: t.n_keys]), r.leaf_hash[: r.n_keys])
+        assert np.array_equal(u64(t.bucket_off), r.bucket_off)
+        assert np.array_equal(u64(t.nodes), r.nodes)
+    d = engine.merkle_diff(ta, tb)
+    assert np.array_equal(u64(d), R.merkle_diff(ra, rb))
+    assert np.array_equal(u64(d), R.store_diff(a["rows"], b["rows"]))
+    assert engine.merkle_diff(ta, ta).numel() == 0
+
+
+def test_merkle_diff_capacity(engine):
+    a, b = W.merkle_pair(n_keys=5000, diff_frac=0.1, seed=1)
+    sa, _ = up(a)
+    sb, _ = up(b)
+    ta, tb = engine.merkle_build(sa, 10), engine.merkle_build(sb, 10)
+    with pytest.raises(CapacityError):
+        engine.merkle_diff(ta, tb, cap=5)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_joink(engine, seed):
+    rng = np.random.default_rng(50 + seed)
+    reps = []
+    for _ in range(3):
+        a, b = W.random_pair(rng, n_keys=400, ts_range=8, dense_ctx=bool(seed % 2))
+        reps += [a, b]
+    stores, ctxs = zip(*[up(r) for r in reps])
+    out, octx = engine.joink(list(stores), list(ctxs))
+    wr, wc = R.joink([r["rows"] for r in reps], [r["ctx"] for r in reps])
+    rows_eq(out, wr)
+    ctx_eq(octx, wc)
+
+
+def test_store_check_detects_unsorted(engine):
+    a, _ = W.config2(n_keys=3000, seed=2)
+    rows = list(a["rows"])
+    s = Store.from_numpy(*rows, device=DEV)
+    engine.store_check(s)
+    rows = [c.copy() for c in rows]
+    rows[0][[10, 11]] = rows[0][[11, 10]]
+    bad = Store.from_numpy(*rows, device=DEV)
+    with pytest.raises(Exception):
+        engine.store_check(bad)
