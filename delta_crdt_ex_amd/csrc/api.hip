@@ -186,10 +186,9 @@ int join2_enqueue(dg_engine* e, const dg_store* a, const dg_context* ca, const d
   TRY(ensure_tmp(e, ctx_union_tmp_bytes(ca->n, cb->n)));
   Scan sc;
   TRY(next_scan(e, &sc));
-  HIP_TRY(launch_ctx_union(ctx_of(ca), ctx_of(cb), out_ctx->node, out_ctx->cnt, d_counts + 1,
-                           e->tmp, e->stream));
-  HIP_TRY(launch_join2_rows(rows_of(a), ctx_of(ca), rows_of(b), ctx_of(cb), keys,
-                            keys ? n_keys : 0, rows_out_of(out), sc, d_counts, e->stream));
+  HIP_TRY(launch_join2(rows_of(a), ctx_of(ca), rows_of(b), ctx_of(cb), keys, keys ? n_keys : 0,
+                       rows_out_of(out), out_ctx->node, out_ctx->cnt, e->tmp, sc, d_counts,
+                       e->stream));
   out_ctx->kind = (ca->kind == DG_CTX_DOTS && cb->kind == DG_CTX_DOTS) ? DG_CTX_DOTS : DG_CTX_VV;
   return DG_OK;
 }

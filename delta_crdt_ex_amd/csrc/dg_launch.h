@@ -22,10 +22,13 @@ constexpr int JOIN_ITEMS = 4;
 constexpr int JOIN_TILE = JOIN_BLOCK * JOIN_ITEMS;
 
 inline u64 join2_tiles(u64 na, u64 nb) { return (na + nb + JOIN_TILE - 1) / JOIN_TILE; }
-// Rows of join/3.  Writes the output row count to d_count[0].
-hipError_t launch_join2_rows(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& cb,
-                             const u64* keys, u64 n_keys, const RowsOut& out, const Scan& scan,
-                             u64* d_count, hipStream_t st);
+// join/3 in ONE launch: rows (d_counts[0] = output rows) and, in an extra workgroup,
+// the context union (d_counts[1] = output context entries).  ctx_tmp: see
+// ctx_union_tmp_bytes.
+hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& cb,
+                        const u64* keys, u64 n_keys, const RowsOut& out, u32* out_ctx_node,
+                        u64* out_ctx_cnt, void* ctx_tmp, const Scan& scan, u64* d_counts,
+                        hipStream_t st);
 // Dots.union/2 of two contexts; out kind: DOTS iff both DOTS.  Writes |out| to *d_count.
 // tmp: (a.n + b.n) u32 + (a.n + b.n) u64 + (a.n + b.n + 1) u32 of device scratch.
 hipError_t launch_ctx_union(const Ctx& a, const Ctx& b, u32* out_node, u64* out_cnt,

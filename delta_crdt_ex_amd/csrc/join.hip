@@ -34,6 +34,160 @@ constexpr int JT = JOIN_TILE;
 constexpr int JS = JT + 4;  // LDS row slots: tile rows + one neighbour on each side per store
 constexpr int CTX_LDS = 256;
 
+// ------------------------------------------------------------- context union
+// Dots.union/2 (aw_lww_map.ex:39-52) in one 1024-thread workgroup: contexts are
+// version vectors of at most a few hundred nodes in practice (one entry per
+// replica) or the explicit dot sets of mutation deltas.
+
+constexpr int CB = 1024;  // threads of the standalone context-union kernel
+
+struct CtxUnionArgs {
+  Ctx a, b;
+  u32* out_node;
+  u64* out_cnt;
+  u64* d_count;
+  u32* tmp_node;  // a.n + b.n
+  u64* tmp_cnt;   // a.n + b.n
+  u32* rank;      // b.n + 1 (after compression)
+};
+
+// Chunked exclusive block scan of flags produced by `flag(i)` for i < n; writes the
+// running exclusive count to out[i] (and the total to out[n]).  Returns the total.
+template <int NT, class F>
+__device__ u32 block_scan_flags(u64 n, F flag, u32* out, u32* s_wave) {
+  u32 carry = 0;
+  for (u64 base = 0; base < n; base += NT) {
+    u64 i = base + threadIdx.x;
+    u32 f = i < n ? (flag(i) ? 1u : 0u) : 0u;
+    u32 tot;
+    u32 ex = block_excl_scan<NT>(f, s_wave, &tot);
+    if (i < n) out[i] = carry + ex;
+    carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[n] = carry;
+  __syncthreads();
+  return carry;
+}
+
+// Compress a dot set (sorted by (node, cnt)) into a VV: the last dot of every node
+// run carries the node's max counter (Dots.compress/1, aw_lww_map.ex:13-20).
+template <int NT>
+__device__ u64 compress_into(const Ctx& c, u32* onode, u64* ocnt, u32* scratch, u32* s_wave) {
+  auto tail = [&](u64 i) { return i + 1 == c.n || c.node[i + 1] != c.node[i]; };
+  u32 total = block_scan_flags<NT>(c.n, tail, scratch, s_wave);
+  for (u64 i = threadIdx.x; i < c.n; i += NT)
+    if (tail(i)) {
+      onode[scratch[i]] = c.node[i];
+      ocnt[scratch[i]] = c.cnt[i];
+    }
+  __syncthreads();
+  return total;
+}
+
+// Dots.union/2 by one workgroup of NT threads; `s_wave` holds NT/64 + 1 words of LDS.
+template <int NT>
+__device__ void ctx_union_block(const CtxUnionArgs& p, u32* s_wave) {
+  const int tid = threadIdx.x;
+  if (p.a.kind == 1 && p.b.kind == 1) {
+    // MapSet.union: sorted set union on (node, cnt)
+    const Ctx &X = p.a, &Y = p.b;
+    auto lbX = [&](u32 n, u64 c) {
+      u64 lo = 0, hi = X.n;
+      while (lo < hi) {
+        u64 m = (lo + hi) >> 1;
+        if (X.node[m] < n || (X.node[m] == n && X.cnt[m] < c))
+          lo = m + 1;
+        else
+          hi = m;
+      }
+      return lo;
+    };
+    auto lbY = [&](u32 n, u64 c) {
+      u64 lo = 0, hi = Y.n;
+      while (lo < hi) {
+        u64 m = (lo + hi) >> 1;
+        if (Y.node[m] < n || (Y.node[m] == n && Y.cnt[m] < c))
+          lo = m + 1;
+        else
+          hi = m;
+      }
+      return lo;
+    };
+    auto ynew = [&](u64 j) {
+      u64 q = lbX(Y.node[j], Y.cnt[j]);
+      return !(q < X.n && X.node[q] == Y.node[j] && X.cnt[q] == Y.cnt[j]);
+    };
+    u32 ny = block_scan_flags<NT>(Y.n, ynew, p.rank, s_wave);
+    for (u64 i = tid; i < X.n; i += NT) {
+      u64 q = lbY(X.node[i], X.cnt[i]);
+      u64 o = i + p.rank[q];
+      p.out_node[o] = X.node[i];
+      p.out_cnt[o] = X.cnt[i];
+    }
+    for (u64 j = tid; j < Y.n; j += NT)
+      if (ynew(j)) {
+        u64 o = p.rank[j] + lbX(Y.node[j], Y.cnt[j]);
+        p.out_node[o] = Y.node[j];
+        p.out_cnt[o] = Y.cnt[j];
+      }
+    if (tid == 0) *p.d_count = X.n + ny;
+    return;
+  }
+  // At least one VV: fold dot sets into VVs first (union(set, map) = union(map, set)).
+  Ctx X = p.a, Y = p.b;
+  if (X.kind == 1) {
+    u64 n = compress_into<NT>(X, p.tmp_node, p.tmp_cnt, p.rank, s_wave);
+    X.node = p.tmp_node;
+    X.cnt = p.tmp_cnt;
+    X.n = n;
+    X.kind = 0;
+  }
+  if (Y.kind == 1) {
+    u64 n = compress_into<NT>(Y, p.tmp_node + p.a.n, p.tmp_cnt + p.a.n, p.rank, s_wave);
+    Y.node = p.tmp_node + p.a.n;
+    Y.cnt = p.tmp_cnt + p.a.n;
+    Y.n = n;
+    Y.kind = 0;
+  }
+  auto lb = [](const Ctx& c, u32 n) {
+    u64 lo = 0, hi = c.n;
+    while (lo < hi) {
+      u64 m = (lo + hi) >> 1;
+      if (c.node[m] < n)
+        lo = m + 1;
+      else
+        hi = m;
+    }
+    return lo;
+  };
+  auto ynew = [&](u64 j) {
+    u64 q = lb(X, Y.node[j]);
+    return !(q < X.n && X.node[q] == Y.node[j]);
+  };
+  u32 ny = block_scan_flags<NT>(Y.n, ynew, p.rank, s_wave);
+  for (u64 i = tid; i < X.n; i += NT) {
+    u64 q = lb(Y, X.node[i]);
+    u64 c = X.cnt[i];
+    if (q < Y.n && Y.node[q] == X.node[i] && Y.cnt[q] > c) c = Y.cnt[q];  // Map.update max
+    u64 o = i + p.rank[q];
+    p.out_node[o] = X.node[i];
+    p.out_cnt[o] = c;
+  }
+  for (u64 j = tid; j < Y.n; j += NT)
+    if (ynew(j)) {
+      u64 o = p.rank[j] + lb(X, Y.node[j]);
+      p.out_node[o] = Y.node[j];
+      p.out_cnt[o] = Y.cnt[j];
+    }
+  if (tid == 0) *p.d_count = X.n + ny;
+}
+
+__global__ __launch_bounds__(CB) void ctx_union_kernel(CtxUnionArgs p) {
+  __shared__ u32 s_wave[CB / WAVE + 1];
+  ctx_union_block<CB>(p, s_wave);
+}
+
 struct JoinArgs {
   Rows a, b;
   Ctx ca, cb;
@@ -43,6 +197,7 @@ struct JoinArgs {
   Scan scan;
   u64 ntiles;
   u64* d_count;
+  CtxUnionArgs cu;  // the context union, run by the grid's extra last workgroup
 };
 
 // Merge-path predicate on diagonal `diag`: A[i] <= B[diag-1-i] (ties go to A).
@@ -82,6 +237,10 @@ __global__ __launch_bounds__(JB) void join2_rows_kernel(JoinArgs p) {
   __shared__ Lds s;
   const int tid = threadIdx.x;
   const u64 na = p.a.n, nb = p.b.n, total = na + nb;
+  if (blockIdx.x == p.ntiles) {  // extra workgroup: Dots.union(c1, c2) (aw_lww_map.ex:155)
+    ctx_union_block<JB>(p.cu, s.wave);
+    return;
+  }
 
   // ---- ticket (tile id in launch order) + context staging
   if (tid == 0) {
@@ -278,176 +437,10 @@ __global__ __launch_bounds__(JB) void join2_rows_kernel(JoinArgs p) {
   }
 }
 
-// ------------------------------------------------------------- context union
-// Dots.union/2 (aw_lww_map.ex:39-52) in one 1024-thread workgroup: contexts are
-// version vectors of at most a few hundred nodes in practice (one entry per
-// replica) or the explicit dot sets of mutation deltas.
-
-constexpr int CB = 1024;
-
-struct CtxUnionArgs {
-  Ctx a, b;
-  u32* out_node;
-  u64* out_cnt;
-  u64* d_count;
-  u32* tmp_node;  // a.n + b.n
-  u64* tmp_cnt;   // a.n + b.n
-  u32* rank;      // b.n + 1 (after compression)
-};
-
-// Chunked exclusive block scan of flags produced by `flag(i)` for i < n; writes the
-// running exclusive count to out[i] (and the total to out[n]).  Returns the total.
-template <class F>
-__device__ u32 block_scan_flags(u64 n, F flag, u32* out, u32* s_wave) {
-  u32 carry = 0;
-  for (u64 base = 0; base < n; base += CB) {
-    u64 i = base + threadIdx.x;
-    u32 f = i < n ? (flag(i) ? 1u : 0u) : 0u;
-    u32 tot;
-    u32 ex = block_excl_scan<CB>(f, s_wave, &tot);
-    if (i < n) out[i] = carry + ex;
-    carry += tot;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) out[n] = carry;
-  __syncthreads();
-  return carry;
-}
-
-// Compress a dot set (sorted by (node, cnt)) into a VV: the last dot of every node
-// run carries the node's max counter (Dots.compress/1, aw_lww_map.ex:13-20).
-__device__ u64 compress_into(const Ctx& c, u32* onode, u64* ocnt, u32* scratch, u32* s_wave) {
-  auto tail = [&](u64 i) { return i + 1 == c.n || c.node[i + 1] != c.node[i]; };
-  u32 total = block_scan_flags(c.n, tail, scratch, s_wave);
-  for (u64 i = threadIdx.x; i < c.n; i += CB)
-    if (tail(i)) {
-      onode[scratch[i]] = c.node[i];
-      ocnt[scratch[i]] = c.cnt[i];
-    }
-  __syncthreads();
-  return total;
-}
-
-__global__ __launch_bounds__(CB) void ctx_union_kernel(CtxUnionArgs p) {
-  __shared__ u32 s_wave[CB / WAVE + 1];
-  const int tid = threadIdx.x;
-  if (p.a.kind == 1 && p.b.kind == 1) {
-    // MapSet.union: sorted set union on (node, cnt)
-    const Ctx &X = p.a, &Y = p.b;
-    auto lbX = [&](u32 n, u64 c) {
-      u64 lo = 0, hi = X.n;
-      while (lo < hi) {
-        u64 m = (lo + hi) >> 1;
-        if (X.node[m] < n || (X.node[m] == n && X.cnt[m] < c))
-          lo = m + 1;
-        else
-          hi = m;
-      }
-      return lo;
-    };
-    auto lbY = [&](u32 n, u64 c) {
-      u64 lo = 0, hi = Y.n;
-      while (lo < hi) {
-        u64 m = (lo + hi) >> 1;
-        if (Y.node[m] < n || (Y.node[m] == n && Y.cnt[m] < c))
-          lo = m + 1;
-        else
-          hi = m;
-      }
-      return lo;
-    };
-    auto ynew = [&](u64 j) {
-      u64 q = lbX(Y.node[j], Y.cnt[j]);
-      return !(q < X.n && X.node[q] == Y.node[j] && X.cnt[q] == Y.cnt[j]);
-    };
-    u32 ny = block_scan_flags(Y.n, ynew, p.rank, s_wave);
-    for (u64 i = tid; i < X.n; i += CB) {
-      u64 q = lbY(X.node[i], X.cnt[i]);
-      u64 o = i + p.rank[q];
-      p.out_node[o] = X.node[i];
-      p.out_cnt[o] = X.cnt[i];
-    }
-    for (u64 j = tid; j < Y.n; j += CB)
-      if (ynew(j)) {
-        u64 o = p.rank[j] + lbX(Y.node[j], Y.cnt[j]);
-        p.out_node[o] = Y.node[j];
-        p.out_cnt[o] = Y.cnt[j];
-      }
-    if (tid == 0) *p.d_count = X.n + ny;
-    return;
-  }
-  // At least one VV: fold dot sets into VVs first (union(set, map) = union(map, set)).
-  Ctx X = p.a, Y = p.b;
-  if (X.kind == 1) {
-    u64 n = compress_into(X, p.tmp_node, p.tmp_cnt, p.rank, s_wave);
-    X.node = p.tmp_node;
-    X.cnt = p.tmp_cnt;
-    X.n = n;
-    X.kind = 0;
-  }
-  if (Y.kind == 1) {
-    u64 n = compress_into(Y, p.tmp_node + p.a.n, p.tmp_cnt + p.a.n, p.rank, s_wave);
-    Y.node = p.tmp_node + p.a.n;
-    Y.cnt = p.tmp_cnt + p.a.n;
-    Y.n = n;
-    Y.kind = 0;
-  }
-  auto lb = [](const Ctx& c, u32 n) {
-    u64 lo = 0, hi = c.n;
-    while (lo < hi) {
-      u64 m = (lo + hi) >> 1;
-      if (c.node[m] < n)
-        lo = m + 1;
-      else
-        hi = m;
-    }
-    return lo;
-  };
-  auto ynew = [&](u64 j) {
-    u64 q = lb(X, Y.node[j]);
-    return !(q < X.n && X.node[q] == Y.node[j]);
-  };
-  u32 ny = block_scan_flags(Y.n, ynew, p.rank, s_wave);
-  for (u64 i = tid; i < X.n; i += CB) {
-    u64 q = lb(Y, X.node[i]);
-    u64 c = X.cnt[i];
-    if (q < Y.n && Y.node[q] == X.node[i] && Y.cnt[q] > c) c = Y.cnt[q];  // Map.update max
-    u64 o = i + p.rank[q];
-    p.out_node[o] = X.node[i];
-    p.out_cnt[o] = c;
-  }
-  for (u64 j = tid; j < Y.n; j += CB)
-    if (ynew(j)) {
-      u64 o = p.rank[j] + lb(X, Y.node[j]);
-      p.out_node[o] = Y.node[j];
-      p.out_cnt[o] = Y.cnt[j];
-    }
-  if (tid == 0) *p.d_count = X.n + ny;
-}
-
 }  // namespace
 
-hipError_t launch_join2_rows(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& cb,
-                             const u64* keys, u64 n_keys, const RowsOut& out, const Scan& scan,
-                             u64* d_count, hipStream_t st) {
-  JoinArgs p;
-  p.a = a;
-  p.b = b;
-  p.ca = ca;
-  p.cb = cb;
-  p.keys = keys;
-  p.n_keys = n_keys;
-  p.out = out;
-  p.scan = scan;
-  p.ntiles = join2_tiles(a.n, b.n);
-  p.d_count = d_count;
-  if (p.ntiles == 0) return hipMemsetAsync(d_count, 0, sizeof(u64), st);
-  hipLaunchKernelGGL(join2_rows_kernel, dim3((unsigned)p.ntiles), dim3(JB), 0, st, p);
-  return hipGetLastError();
-}
-
-hipError_t launch_ctx_union(const Ctx& a, const Ctx& b, u32* out_node, u64* out_cnt,
-                            u64* d_count, void* tmp, hipStream_t st) {
+static CtxUnionArgs make_cu(const Ctx& a, const Ctx& b, u32* out_node, u64* out_cnt,
+                            u64* d_count, void* tmp) {
   CtxUnionArgs p;
   p.a = a;
   p.b = b;
@@ -460,6 +453,37 @@ hipError_t launch_ctx_union(const Ctx& a, const Ctx& b, u32* out_node, u64* out_
   p.tmp_node = (u32*)t;
   t += (a.n + b.n) * 4;
   p.rank = (u32*)t;
+  return p;
+}
+
+hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& cb,
+                        const u64* keys, u64 n_keys, const RowsOut& out, u32* out_ctx_node,
+                        u64* out_ctx_cnt, void* ctx_tmp, const Scan& scan, u64* d_counts,
+                        hipStream_t st) {
+  JoinArgs p;
+  p.a = a;
+  p.b = b;
+  p.ca = ca;
+  p.cb = cb;
+  p.keys = keys;
+  p.n_keys = n_keys;
+  p.out = out;
+  p.scan = scan;
+  p.ntiles = join2_tiles(a.n, b.n);
+  p.d_count = d_counts;
+  p.cu = make_cu(ca, cb, out_ctx_node, out_ctx_cnt, d_counts + 1, ctx_tmp);
+  if (p.ntiles == 0) {
+    hipError_t e = hipMemsetAsync(d_counts, 0, sizeof(u64), st);
+    if (e != hipSuccess) return e;
+  }
+  // one workgroup per tile + one for the context union
+  hipLaunchKernelGGL(join2_rows_kernel, dim3((unsigned)p.ntiles + 1), dim3(JB), 0, st, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_ctx_union(const Ctx& a, const Ctx& b, u32* out_node, u64* out_cnt,
+                            u64* d_count, void* tmp, hipStream_t st) {
+  CtxUnionArgs p = make_cu(a, b, out_node, out_cnt, d_count, tmp);
   hipLaunchKernelGGL(ctx_union_kernel, dim3(1), dim3(CB), 0, st, p);
   return hipGetLastError();
 }

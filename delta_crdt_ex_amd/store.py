@@ -247,6 +247,23 @@ class Engine:
         out_ctx.kind = int(co.kind)
         return d_counts
 
+    def prepare_join2(self, a: Store, ca: Context, b: Store, cb: Context, out: Store,
+                      out_ctx: Context, d_counts: torch.Tensor, keys: torch.Tensor | None = None):
+        """Pre-marshal one join for repeated asynchronous launches (benchmark loops):
+        returns a zero-argument callable that enqueues dg_join2_async."""
+        args = [a.abi(), ca.abi(), b.abi(), cb.abi(), out.abi(), out_ctx.abi()]
+        refs = [C.byref(x) for x in args]
+        kp = _ptr(keys, _abi.P64) if keys is not None else None
+        nk = int(keys.numel()) if keys is not None else 0
+        dp = _ptr(d_counts, _abi.P64)
+        f, h = self.lib.dg_join2_async, self.h
+
+        def launch():
+            check(f(h, refs[0], refs[1], refs[2], refs[3], kp, nk, refs[4], refs[5], dp))
+
+        launch._keep = (args, keys, d_counts)
+        return launch
+
     def joink(self, stores, ctxs, out: Store | None = None, out_ctx: Context | None = None):
         self._order()
         k = len(stores)
