@@ -198,7 +198,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "join2_rows_kernel (1 launch/step)",
+                "kernel": "join2 = join2_partition_kernel + join2_rows_kernel (events bracket both)",
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_launch_us": avg_launch_s * 1e6,
             },

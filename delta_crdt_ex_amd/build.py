@@ -15,8 +15,9 @@ from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-OBJ = os.path.join(HERE, "_build")
-LIB = os.path.join(HERE, "libdeltagpu.so")
+STAMPS = os.environ.get("DG_STAMPS") == "1"  # diagnostic build with in-kernel phase stamps
+OBJ = os.path.join(HERE, "_build_stamps" if STAMPS else "_build")
+LIB = os.path.join(HERE, "libdeltagpu_stamps.so" if STAMPS else "libdeltagpu.so")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 SOURCES = ["join.hip", "segred.hip", "merkle.hip", "api.hip"]
 ARCH = os.environ.get("DG_OFFLOAD_ARCH", "gfx950")
@@ -46,7 +47,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     hipcc = _hipcc()
     deps = _deps()
     flags = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall",
-             "-Wno-unused-result", "-I" + INCLUDE]
+             "-Wno-unused-result", "-I" + INCLUDE] + (["-DDG_STAMPS"] if STAMPS else [])
     jobs = []
     objs = []
     for src in SOURCES:

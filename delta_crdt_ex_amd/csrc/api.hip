@@ -182,7 +182,7 @@ int join2_enqueue(dg_engine* e, const dg_store* a, const dg_context* ca, const d
   if (a->n + b->n && (!out->key || !out->val || !out->ts || !out->node || !out->cnt))
     return fail(DG_E_INVAL, "dg_join2: null output column");
   TRY(set_device(e));
-  TRY(ensure_state(e, join2_tiles(a->n, b->n)));
+  TRY(ensure_state(e, 2 * join2_tiles(a->n, b->n) + 2));
   TRY(ensure_tmp(e, ctx_union_tmp_bytes(ca->n, cb->n)));
   Scan sc;
   TRY(next_scan(e, &sc));

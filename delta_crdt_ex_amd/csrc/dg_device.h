@@ -216,4 +216,90 @@ __device__ __forceinline__ u64 lb_lookback(u64* state, u64 tile, u32 epoch, u32*
   }
 }
 
+// Block-wide decoupled look-back: EVERY thread of the NT-thread block calls it after
+// the block published its aggregate (tile > 0).  Thread t reads predecessors
+// base - (t*Q + q), q < Q, so one round reaches NT*Q tiles back: when all tiles of a
+// launch round progress in lockstep (no inclusive prefix published yet), a tile still
+// resolves its prefix in one or two round trips instead of tile/64.  `s_lb` is LDS
+// scratch of 3 * NT/64 + 2 u64.  Spins are bounded (err bit 0 on timeout).
+template <int NT, int Q>
+__device__ __forceinline__ u64 lb_lookback_block(u64* state, u64 tile, u32 epoch, u32* err,
+                                                 u64* s_lb) {
+  constexpr int NW = NT / WAVE;
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
+  u64 prefix = 0;
+  i64 base = (i64)tile - 1;
+  u32 spins = 0;
+  while (true) {
+    u32 fl[Q];
+    u64 vl[Q];
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+      const i64 idx = base - ((i64)tid * Q + q);
+      if (idx >= 0) {
+        const u64 g = __hip_atomic_load(state + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        fl[q] = ((u32)(g >> 44) == epoch) ? (u32)((g >> 42) & 3) : 0u;
+        vl[q] = g & LB_VALUE_MASK;
+      } else {
+        fl[q] = LB_INC;
+        vl[q] = 0;
+      }
+    }
+    int qi = Q;
+#pragma unroll
+    for (int q = Q - 1; q >= 0; q--)
+      if (fl[q] == LB_INC) qi = q;
+    bool zb = false;
+    u64 part = 0;
+#pragma unroll
+    for (int q = 0; q < Q; q++)
+      if (q <= qi) {
+        zb |= fl[q] == 0;
+        part += vl[q];
+      }
+    const u64 im = __ballot(qi < Q), bm = __ballot(zb);
+    const int first = im ? __ffsll((long long)im) - 1 : WAVE;
+    const u64 upto = first >= WAVE - 1 ? ~0ull : ((2ull << first) - 1);
+    u64 c = lane <= first ? part : 0;
+#pragma unroll
+    for (int d = WAVE / 2; d >= 1; d >>= 1) c += __shfl_xor(c, d, WAVE);
+    if (lane == 0) {
+      s_lb[w] = c;
+      s_lb[NW + w] = im != 0;
+      s_lb[2 * NW + w] = (bm & upto) == 0;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      u64 acc = 0, st = 2;  // 2: all ready, no inclusive prefix yet -> go further back
+      for (int ww = 0; ww < NW; ww++) {
+        if (!s_lb[2 * NW + ww]) {
+          st = 0;  // a granule before the nearest inclusive prefix is not ready
+          break;
+        }
+        acc += s_lb[ww];
+        if (s_lb[NW + ww]) {
+          st = 1;
+          break;
+        }
+      }
+      s_lb[3 * NW] = st;
+      s_lb[3 * NW + 1] = acc;
+    }
+    __syncthreads();
+    const u64 st = s_lb[3 * NW], acc = s_lb[3 * NW + 1];
+    __syncthreads();
+    if (st == 1) return prefix + acc;
+    if (st == 2) {
+      prefix += acc;
+      base -= (i64)NT * Q;
+      continue;
+    }
+    if (++spins > (1u << 22)) {
+      if (tid == 0) atomicOr(err, 1u);
+      return prefix;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
 }  // namespace dg

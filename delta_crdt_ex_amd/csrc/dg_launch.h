@@ -17,8 +17,8 @@ struct Scan {
 };
 
 // ---- join.hip
-constexpr int JOIN_BLOCK = 256;
-constexpr int JOIN_ITEMS = 4;
+constexpr int JOIN_BLOCK = 512;
+constexpr int JOIN_ITEMS = 2;
 constexpr int JOIN_TILE = JOIN_BLOCK * JOIN_ITEMS;
 
 inline u64 join2_tiles(u64 na, u64 nb) { return (na + nb + JOIN_TILE - 1) / JOIN_TILE; }

@@ -1,0 +1,58 @@
+"""Phase breakdown of the join kernel from the DG_STAMPS diagnostic build.
+
+    DG_STAMPS=1 python -m delta_crdt_ex_amd.build   # on the CPU host
+    python tools/join_stamps.py                        # on the GPU box
+
+Stamps are s_memrealtime (100 MHz) taken by lane 0 of every tile at:
+0 tile start (after the ticket)  1 after the merge-path search  2 after LDS staging
+3 after the per-thread merge     4 after the block scan          5 after the look-back
+6 after the output write.  Only SHARES are meaningful (stamps add fences).
+"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from delta_crdt_ex_amd import _abi  # noqa: E402
+
+_abi.LIB_PATH = os.path.join(ROOT, "delta_crdt_ex_amd", "libdeltagpu_stamps.so")
+
+
+def main():
+    import torch
+    from delta_crdt_ex_amd import workloads as W
+    from delta_crdt_ex_amd.store import Context, Engine, Store
+    lib = _abi.load(_abi.LIB_PATH)
+    dev = "cuda:0"
+    a, b = W.config2()
+    eng = Engine(0)
+    sa, sb = Store.from_numpy(*a["rows"], device=dev), Store.from_numpy(*b["rows"], device=dev)
+    ca, cb = Context.from_numpy(*a["ctx"], dev), Context.from_numpy(*b["ctx"], dev)
+    out = Store.empty(sa.n + sb.n, dev)
+    octx = Context.empty(0, 8, dev)
+    for _ in range(5):
+        eng.join2(sa, ca, sb, cb, out=out, out_ctx=octx)
+    ntiles = (sa.n + sb.n + 1023) // 1024
+    buf = np.zeros(65536 * 8, np.uint64)
+    lib.dg_debug_join_stamps.argtypes = [C.c_void_p, C.c_size_t]
+    assert lib.dg_debug_join_stamps(buf.ctypes.data, len(buf)) == 0
+    st = buf[: ntiles * 8].reshape(ntiles, 8).astype(np.int64)
+    t0 = st[:, 0].min()
+    names = ["search", "stage", "merge", "scan", "lookback", "write"]
+    d = np.diff(st[:, :7], axis=1) * 10 / 1000.0  # us
+    print(f"tiles={ntiles} kernel span={(st[:, 6].max() - t0) * 10 / 1000:.1f} us")
+    for i, nm in enumerate(names):
+        print(f"{nm:9s} median {np.median(d[:, i]):6.2f} us  p90 {np.percentile(d[:, i], 90):6.2f}"
+              f"  mean {d[:, i].mean():6.2f}")
+    tot = (st[:, 6] - st[:, 0]) * 10 / 1000
+    print(f"per-tile total median {np.median(tot):.2f} us  mean {tot.mean():.2f}")
+    starts = (st[:, 0] - t0) * 10 / 1000
+    print("tile start times (us) at deciles:", np.percentile(starts, np.arange(0, 101, 10)).round(1))
+
+
+if __name__ == "__main__":
+    main()
