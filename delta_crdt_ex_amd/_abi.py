@@ -11,7 +11,7 @@ import os
 import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libdeltagpu.so")
+LIB_PATH = os.environ.get("DG_LIB_PATH") or os.path.join(HERE, "libdeltagpu.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "deltagpu.h")
 
 DG_OK = 0

@@ -16,8 +16,10 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 STAMPS = os.environ.get("DG_STAMPS") == "1"  # diagnostic build with in-kernel phase stamps
-OBJ = os.path.join(HERE, "_build_stamps" if STAMPS else "_build")
-LIB = os.path.join(HERE, "libdeltagpu_stamps.so" if STAMPS else "libdeltagpu.so")
+VARIANT = os.environ.get("DG_VARIANT", "")     # experiment builds: extra -D flags, own .so
+_SUFFIX = ("_stamps" if STAMPS else "") + (("_" + VARIANT.replace("=", "").replace("-D", "").replace(" ", "_")) if VARIANT else "")
+OBJ = os.path.join(HERE, "_build" + _SUFFIX)
+LIB = os.path.join(HERE, "libdeltagpu" + _SUFFIX + ".so")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 SOURCES = ["join.hip", "segred.hip", "merkle.hip", "api.hip"]
 ARCH = os.environ.get("DG_OFFLOAD_ARCH", "gfx950")
@@ -47,7 +49,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     hipcc = _hipcc()
     deps = _deps()
     flags = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall",
-             "-Wno-unused-result", "-I" + INCLUDE] + (["-DDG_STAMPS"] if STAMPS else [])
+             "-Wno-unused-result", "-I" + INCLUDE] + (["-DDG_STAMPS"] if STAMPS else []) + VARIANT.split()
     jobs = []
     objs = []
     for src in SOURCES:

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -30,6 +31,8 @@ struct dg_engine {
   // general scratch
   void* tmp = nullptr;
   size_t tmp_cap = 0;
+  int join_workers = 1024;  // persistent join tile workgroups (single-pass mode)
+  int join_mode = JOIN_TWO_PASS;  // DG_JOIN_MODE=1: single-pass persistent look-back kernel
 };
 
 namespace {
@@ -182,12 +185,15 @@ int join2_enqueue(dg_engine* e, const dg_store* a, const dg_context* ca, const d
   if (a->n + b->n && (!out->key || !out->val || !out->ts || !out->node || !out->cnt))
     return fail(DG_E_INVAL, "dg_join2: null output column");
   TRY(set_device(e));
-  TRY(ensure_state(e, 2 * join2_tiles(a->n, b->n) + 2));
-  TRY(ensure_tmp(e, ctx_union_tmp_bytes(ca->n, cb->n)));
+  TRY(ensure_state(e, 2 * join2_tiles(a->n, b->n) + 2));  // granules + tile splits
+  const size_t ctx_bytes = (ctx_union_tmp_bytes(ca->n, cb->n) + 255) / 256 * 256;
+  const size_t pass_bytes = e->join_mode == JOIN_TWO_PASS ? join2_pass_tmp_bytes(a->n, b->n) : 0;
+  TRY(ensure_tmp(e, ctx_bytes + pass_bytes));
   Scan sc;
   TRY(next_scan(e, &sc));
   HIP_TRY(launch_join2(rows_of(a), ctx_of(ca), rows_of(b), ctx_of(cb), keys, keys ? n_keys : 0,
-                       rows_out_of(out), out_ctx->node, out_ctx->cnt, e->tmp, sc, d_counts,
+                       rows_out_of(out), out_ctx->node, out_ctx->cnt, e->tmp,
+                       (char*)e->tmp + ctx_bytes, e->join_mode, sc, e->join_workers, d_counts,
                        e->stream));
   out_ctx->kind = (ca->kind == DG_CTX_DOTS && cb->kind == DG_CTX_DOTS) ? DG_CTX_DOTS : DG_CTX_VV;
   return DG_OK;
@@ -210,6 +216,16 @@ int dg_engine_create(int device, void* hip_stream, dg_engine** out) {
     return fail(DG_E_INVAL, "dg_engine_create: device %d of %d", device, ndev);
   dg_engine* e = new dg_engine();
   e->device = device;
+  {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
+        cus > 0)
+      e->join_workers = 2 * cus;  // 2 resident join workgroups per CU (VGPR-bound)
+    const char* v = getenv("DG_JOIN_WORKERS");
+    if (v && atoi(v) > 0) e->join_workers = atoi(v);
+    const char* m = getenv("DG_JOIN_MODE");
+    if (m && m[0] == '1') e->join_mode = JOIN_SINGLE_PASS;
+  }
   int rc = set_device(e);
   if (rc != DG_OK) {
     delete e;

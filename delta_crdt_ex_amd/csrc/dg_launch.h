@@ -17,18 +17,30 @@ struct Scan {
 };
 
 // ---- join.hip
-constexpr int JOIN_BLOCK = 512;
-constexpr int JOIN_ITEMS = 2;
+#ifndef DG_JOIN_BLOCK
+#define DG_JOIN_BLOCK 512
+#endif
+#ifndef DG_JOIN_ITEMS
+#define DG_JOIN_ITEMS 2
+#endif
+constexpr int JOIN_BLOCK = DG_JOIN_BLOCK;  // threads per join tile (one wave per SIMD)
+constexpr int JOIN_ITEMS = DG_JOIN_ITEMS;  // merged positions per thread
 constexpr int JOIN_TILE = JOIN_BLOCK * JOIN_ITEMS;
 
 inline u64 join2_tiles(u64 na, u64 nb) { return (na + nb + JOIN_TILE - 1) / JOIN_TILE; }
-// join/3 in ONE launch: rows (d_counts[0] = output rows) and, in an extra workgroup,
-// the context union (d_counts[1] = output context entries).  ctx_tmp: see
-// ctx_union_tmp_bytes.
+// join/3: a merge-path partition pass (its extra workgroup computes the context union,
+// d_counts[1] = its size), then persistent tile workers that merge each tile, publish
+// its aggregate, and write the previous tile's rows once its prefix is resolved
+// (d_counts[0] = output rows).  Uses scan.state[0, 2 * ntiles + 2).
+enum { JOIN_SINGLE_PASS = 0, JOIN_TWO_PASS = 1 };
 hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& cb,
                         const u64* keys, u64 n_keys, const RowsOut& out, u32* out_ctx_node,
-                        u64* out_ctx_cnt, void* ctx_tmp, const Scan& scan, u64* d_counts,
-                        hipStream_t st);
+                        u64* out_ctx_cnt, void* ctx_tmp, void* pass_tmp, int mode,
+                        const Scan& scan, int workers, u64* d_counts, hipStream_t st);
+inline size_t join2_pass_tmp_bytes(u64 na, u64 nb) {
+  const u64 t = join2_tiles(na, nb);
+  return ((t * 4 + 255) / 256) * 256 + t * (u64)JOIN_TILE * 36 + 256;
+}
 // Dots.union/2 of two contexts; out kind: DOTS iff both DOTS.  Writes |out| to *d_count.
 // tmp: (a.n + b.n) u32 + (a.n + b.n) u64 + (a.n + b.n + 1) u32 of device scratch.
 hipError_t launch_ctx_union(const Ctx& a, const Ctx& b, u32* out_node, u64* out_cnt,

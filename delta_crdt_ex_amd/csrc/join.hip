@@ -23,6 +23,8 @@
 //   * each thread merges 4 positions serially from LDS and decides keep/drop;
 //   * block scan of keep counts -> block-wide look-back (1024 predecessors per
 //     round) -> compacted rows written coalesced.
+#include <algorithm>
+
 #include "dg_launch.h"
 
 namespace dg {
@@ -33,7 +35,6 @@ constexpr int JB = JOIN_BLOCK;
 constexpr int JI = JOIN_ITEMS;
 constexpr int JT = JOIN_TILE;
 constexpr int JS = JT + 4;  // LDS row slots: tile rows + one neighbour on each side per store
-constexpr int CTX_LDS = 64;  // VVs up to 64 nodes are staged in LDS (else read from L2)
 
 #ifdef DG_STAMPS
 // Diagnostic build only (DG_STAMPS=1): per-tile phase timestamps (s_memrealtime,
@@ -212,49 +213,38 @@ struct JoinArgs {
   Ctx ca, cb;
   const u64* keys;
   u64 n_keys;
-  RowsOut out;
-  Scan scan;
-  u64* splits;  // per-tile merge-path split granules {epoch:20 | a_index:44}
+  u64* splits;  // merge-path split (a index) of every tile boundary, from the partition pass
   u64 ntiles;
+  RowsOut out;
+  Scan scan;        // look-back granules + tile tickets
   u64* d_count;
-  CtxUnionArgs cu;  // the context union, run by the grid's extra last workgroup
 };
 
-struct Lds {
+constexpr int SMALL_VV = 8;  // VVs up to this many nodes are probed from LDS
+
+// One staged tile: its rows (+ neighbours) and, after the merge, its compaction list.
+struct Buf {
   u64 key[JS];
   u64 val[JS];
   u64 cnt[JS];
   i64 ts[JS];
   u32 node[JS];
-  union {  // the contexts are dead once the merge is done; the compaction list reuses them
-    struct {
-      u64 ctx_cnt[2][CTX_LDS];
-      u32 ctx_node[2][CTX_LDS];
-    };
-    unsigned short comp[JT];
-  };
-  u32 wave[JB / WAVE + 1];
-  u64 lb[3 * (JB / WAVE) + 2];
-  u64 bcast[4];
+  unsigned short comp[JT];
 };
 
-// Full-tuple compare of two LDS slots, key first (the only load for distinct keys).
-__device__ __forceinline__ bool slot_le(const Lds& s, int x, int y) {
-  u64 kx = s.key[x], ky = s.key[y];
-  if (kx != ky) return kx < ky;
-  u64 vx = s.val[x], vy = s.val[y];
-  if (vx != vy) return vx < vy;
-  i64 tx = s.ts[x], ty = s.ts[y];
-  if (tx != ty) return tx < ty;
-  u32 nx = s.node[x], ny = s.node[y];
-  if (nx != ny) return nx < ny;
-  return s.cnt[x] <= s.cnt[y];
-}
+// Two tiles live per workgroup: the one being merged and the previous one, whose
+// output offset is resolved (look-back) and whose rows are written one iteration later.
+struct Lds {
+  Buf buf[2];
+  unsigned short posinfo[JT];  // merge of the current tile: slot of each position | keep << 15
+  u64 vv_cnt[2][SMALL_VV];     // small version vectors (c_a, c_b), staged once
+  u32 vv_node[2][SMALL_VV];
+  u32 wave[JB / WAVE + 1];
+  u64 lb[3 * (JB / WAVE) + 2];
+  u64 bcast[8];
+};
 
-__device__ __forceinline__ bool slot_eq(const Lds& s, int x, int y) {
-  return s.key[x] == s.key[y] && s.val[x] == s.val[y] && s.ts[x] == s.ts[y] &&
-         s.node[x] == s.node[y] && s.cnt[x] == s.cnt[y];
-}
+
 
 // Merge-path predicate on diagonal `diag` over global memory: A[i] <= B[diag-1-i].
 __device__ __forceinline__ bool mp_pred(const Rows A, const Rows B, u64 diag, u64 i) {
@@ -265,11 +255,6 @@ __device__ __forceinline__ bool mp_pred(const Rows A, const Rows B, u64 diag, u6
 }
 
 // Dots.member? against a context staged in LDS or read from global memory.
-template <bool LDS>
-__device__ __forceinline__ bool covers(const Lds& s, int which, const Ctx c, u32 dn, u64 dc) {
-  if (LDS) return ctx_covers(s.ctx_node[which], s.ctx_cnt[which], c.n, c.kind, dn, dc);
-  return ctx_covers(c.node, c.cnt, c.n, c.kind, dn, dc);
-}
 
 // Merge-path partition: one wave per tile boundary q (diagonal min(q * JT, na + nb))
 // finds the boundary's split with a 128-ary search (two samples per lane per round).
@@ -280,7 +265,12 @@ __device__ __forceinline__ bool covers(const Lds& s, int which, const Ctx c, u32
 constexpr int PB = 256;  // threads per partition block = 4 boundaries
 
 __global__ __launch_bounds__(PB) void join2_partition_kernel(Rows A, Rows B, u64 ntiles,
-                                                             u64* splits) {
+                                                             u64* splits, CtxUnionArgs cu) {
+  if (blockIdx.x == gridDim.x - 1) {  // extra workgroup: Dots.union(c1, c2) (aw_lww_map.ex:155)
+    __shared__ u32 s_wave[PB / WAVE + 1];
+    ctx_union_block<PB>(cu, s_wave);
+    return;
+  }
   const int lane = threadIdx.x & (WAVE - 1);
   const u64 q = (u64)blockIdx.x * (PB / WAVE) + (threadIdx.x >> 6);
   if (q > ntiles) return;
@@ -336,185 +326,437 @@ __global__ __launch_bounds__(PB) void join2_partition_kernel(Rows A, Rows B, u64
   if (lane == 0) splits[q] = lo;
 }
 
-template <bool CA_LDS, bool CB_LDS>
-__device__ __forceinline__ void merge_items(const Ctx ca, const Ctx cb, const u64* keys,
-                                            const u64 n_keys, const u64 nb, const Lds& s,
+// Version vectors of at most SMALL_VV nodes (one entry per replica: the common case)
+// are held in wave-uniform registers and probed with unrolled compares; anything else
+// (bigger VVs, explicit dot sets) is binary-searched in global memory (L1/L2-resident).
+
+// A small VV staged in LDS (uniform addresses: every probe is a broadcast read).
+struct SmallVV {
+  const u32* node;
+  const u64* cnt;
+  u32 n;
+};
+
+// Dots.member?(vv, {dn, dc}): Map.get(vv, dn, 0) >= dc  (aw_lww_map.ex:71-73)
+__device__ __forceinline__ bool small_vv_covers(const SmallVV& v, u32 dn, u64 dc) {
+  u64 have = 0;
+#pragma unroll
+  for (int q = 0; q < SMALL_VV; q++)
+    if ((u32)q < v.n && v.node[q] == dn) have = v.cnt[q];
+  return have >= dc;
+}
+
+__device__ __forceinline__ Row lds_row(const Buf& s, int x) {
+  Row r;
+  r.key = s.key[x];
+  r.val = s.val[x];
+  r.ts = s.ts[x];
+  r.node = s.node[x];
+  r.cnt = s.cnt[x];
+  return r;
+}
+
+// Merge JI consecutive positions of the tile and decide keep/drop for each (the body
+// of join_dot_sets/4 per row, see the file header).  Rows are read from LDS whole (all
+// five columns in parallel) so every merge step costs one LDS round trip.
+template <bool SMALL, bool KEYS>
+__device__ __forceinline__ void merge_items(const Ctx ca, const Ctx cb, const SmallVV& va,
+                                            const SmallVV& vb, const u64* keys,
+                                            const u64 n_keys, const u64 nb, const Buf& s,
                                             int nat, int nbt, u64 a0, u64 b0, u32& keep,
-                                            unsigned short (&src)[JI]) {
+                                            unsigned short (&src)[JI], u64 t_stamp) {
   const int tid = threadIdx.x;
   const int offB = nat + 2;
   const int tt = nat + nbt;
   const int diag = min(tid * JI, tt);
   const int dend = min(diag + JI, tt);
-  int lo = diag > nbt ? diag - nbt : 0, hi = min(diag, nat);
+  // Merge-path split of this thread's diagonal: first i with NOT(a[i] <= b[diag-1-i]).
+  // (1) key-only binary search for iq = first i with a[i].key > b[diag-1-i].key (two
+  //     LDS words per probe); the exact split lies in (iq - r, iq] where r counts the
+  //     positions whose keys tie; (2) full-tuple gallop down from iq to find it.
+  const int lo0 = diag > nbt ? diag - nbt : 0, hi0 = min(diag, nat);
+  int lo = lo0, hi = hi0;
   while (lo < hi) {
-    int mid = (lo + hi) >> 1;
-    if (slot_le(s, 1 + mid, offB + 1 + (diag - 1 - mid)))
+    const int mid = (lo + hi) >> 1;
+    if (s.key[1 + mid] <= s.key[offB + 1 + (diag - 1 - mid)])
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  // P(i) = a[i] <= b[diag-1-i] is monotone and P(i) implies key <=, so split <= iq = lo.
+  int hiP = lo, loP = lo0, step = 1;
+  while (hiP > loP) {  // gallop: find a point where P holds
+    const int x = max(hiP - step, loP);
+    if (row_le(lds_row(s, 1 + x), lds_row(s, offB + 1 + (diag - 1 - x)))) {
+      loP = x + 1;
+      break;
+    }
+    hiP = x;
+    step <<= 1;
+  }
+  lo = loP;
+  hi = hiP;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (row_le(lds_row(s, 1 + mid), lds_row(s, offB + 1 + (diag - 1 - mid))))
       lo = mid + 1;
     else
       hi = mid;
   }
   int i = lo, j = diag - lo;
+  JSTAMP(t_stamp, 5);
+  // ra = a[i], rb = b[j] (possibly the neighbour past the tile), pa = a[i-1]
+  Row ra = lds_row(s, 1 + i), rb = lds_row(s, offB + 1 + j), pa = lds_row(s, i);
   keep = 0;
 #pragma unroll
   for (int k = 0; k < JI; k++) {
     src[k] = 0;
     if (diag + k < dend) {
-      const int sa = 1 + i, sb = offB + 1 + j;
-      const bool bvalid = (b0 + (u64)j) < nb;  // b[j] exists (may be the b1 neighbour)
-      const bool takeA = i < nat && (j >= nbt || slot_le(s, sa, sb));
+      const bool bvalid = (b0 + (u64)j) < nb;  // b[j] exists globally
+      const bool takeA = i < nat && (j >= nbt || row_le(ra, rb));
       bool kp;
       if (takeA) {
-        const u64 key = s.key[sa];
-        const bool joined = keys == nullptr || keyset_has(keys, n_keys, key);
+        const bool joined = !KEYS || keys == nullptr || keyset_has(keys, n_keys, ra.key);
         if (joined) {
-          const bool inB = bvalid && slot_eq(s, sa, sb);
-          kp = inB || !covers<CB_LDS>(s, 1, cb, s.node[sa], s.cnt[sa]);
+          const bool inB = bvalid && row_eq(ra, rb);
+          const bool cov = SMALL ? small_vv_covers(vb, ra.node, ra.cnt)
+                                 : ctx_covers(cb.node, cb.cnt, cb.n, cb.kind, ra.node, ra.cnt);
+          kp = inB || !cov;
         } else {
           // Map.merge(Map.drop(a), Map.drop(b)): a's rows survive iff b lacks the key
-          const bool bprev = (b0 + (u64)j) >= 1 && s.key[sb - 1] == key;
-          const bool bnext = bvalid && s.key[sb] == key;
+          const bool bprev = (b0 + (u64)j) >= 1 && s.key[offB + j] == ra.key;
+          const bool bnext = bvalid && rb.key == ra.key;
           kp = !(bprev || bnext);
         }
-        src[k] = (unsigned short)sa;
+        src[k] = (unsigned short)(1 + i);
         i++;
+        pa = ra;
+        if (k + 1 < JI) ra = lds_row(s, 1 + i);
       } else {
-        const bool joined = keys == nullptr || keyset_has(keys, n_keys, s.key[sb]);
+        const bool joined = !KEYS || keys == nullptr || keyset_has(keys, n_keys, rb.key);
         if (joined) {
-          const bool dupA = (a0 + (u64)i) >= 1 && slot_eq(s, sa - 1, sb);  // slot sa-1 = a[i-1]
-          kp = !dupA && !covers<CA_LDS>(s, 0, ca, s.node[sb], s.cnt[sb]);
+          const bool dupA = (a0 + (u64)i) >= 1 && row_eq(pa, rb);
+          const bool cov = SMALL ? small_vv_covers(va, rb.node, rb.cnt)
+                                 : ctx_covers(ca.node, ca.cnt, ca.n, ca.kind, rb.node, rb.cnt);
+          kp = !dupA && !cov;
         } else {
           kp = true;
         }
-        src[k] = (unsigned short)sb;
+        src[k] = (unsigned short)(offB + 1 + j);
         j++;
+        if (k + 1 < JI) rb = lds_row(s, offB + 1 + j);
       }
       if (kp) keep |= 1u << k;
     }
   }
 }
 
-__global__ __launch_bounds__(JB, 8) void join2_rows_kernel(JoinArgs p) {
+// Rows of a tile (plus one neighbour on each side of each store) as staged in LDS:
+// slot x < nat + 2 is a[a0 - 1 + x], slot x >= nat + 2 is b[b0 - 1 + (x - nat - 2)].
+// A thread owns slots tid, tid + JB, ... (SLOTS of them); their rows are prefetched
+// into registers one tile ahead so that HBM reads of tile k+1 overlap the merge of k.
+constexpr int SLOTS = (JS + JB - 1) / JB;
+
+struct Prefetch {
+  u64 key[SLOTS], val[SLOTS], cnt[SLOTS];
+  i64 ts[SLOTS];
+  u32 node[SLOTS];
+};
+
+// Global row index of staging slot x, or -1 if the slot is outside the stores.
+__device__ __forceinline__ i64 slot_row(int x, int nat, u64 a0, u64 b0, u64 na, u64 nb,
+                                        bool* from_b) {
+  if (x < nat + 2) {
+    const i64 g = (i64)a0 - 1 + x;
+    *from_b = false;
+    return (g >= 0 && (u64)g < na) ? g : -1;
+  }
+  const i64 g = (i64)b0 - 1 + (x - (nat + 2));
+  *from_b = true;
+  return (g >= 0 && (u64)g < nb) ? g : -1;
+}
+
+// FAST: full-state join (no key list) of two version vectors of <= SMALL_VV nodes —
+// the anti-entropy shape; everything else takes the general instantiation.
+template <bool FAST>
+__global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 4))) void join2_tiles_kernel(JoinArgs p) {
   __shared__ Lds s;
   const int tid = threadIdx.x;
+  const u64 na = p.a.n, nb = p.b.n, total = na + nb, ntiles = p.ntiles;
+  const u64 G = gridDim.x;  // persistent tile workers
+  if (FAST && tid < SMALL_VV) {
+    s.vv_node[0][tid] = (u64)tid < p.ca.n ? p.ca.node[tid] : 0u;
+    s.vv_cnt[0][tid] = (u64)tid < p.ca.n ? p.ca.cnt[tid] : 0ull;
+    s.vv_node[1][tid] = (u64)tid < p.cb.n ? p.cb.node[tid] : 0u;
+    s.vv_cnt[1][tid] = (u64)tid < p.cb.n ? p.cb.cnt[tid] : 0ull;
+  }
+  const SmallVV va{s.vv_node[0], s.vv_cnt[0], (u32)p.ca.n};
+  const SmallVV vb{s.vv_node[1], s.vv_cnt[1], (u32)p.cb.n};
+  // Tiles are handed out by an atomic ticket (launch order), so a tile's look-back only
+  // ever waits on tiles already held by running workgroups.  Every workgroup takes
+  // exactly one ticket >= ntiles (its stop signal): ntiles + G tickets in all, and the
+  // taker of the last one resets the counter for the next launch.
+  auto take_ticket = [&]() -> u64 {
+    const u32 tk = atomicAdd(p.scan.ticket, 1u);
+    if ((u64)tk == ntiles + G - 1) atomicExch(p.scan.ticket, 0u);
+    return tk;
+  };
+  if (tid == 0) {
+    const u64 t0 = take_ticket();
+    s.bcast[0] = t0;
+    if (t0 < ntiles) {
+      s.bcast[1] = p.splits[t0];
+      s.bcast[2] = p.splits[t0 + 1];
+      const u64 t1 = take_ticket();
+      s.bcast[3] = t1;
+      if (t1 < ntiles) {
+        s.bcast[4] = p.splits[t1];
+        s.bcast[5] = p.splits[t1 + 1];
+      }
+    }
+  }
+  __syncthreads();
+  u64 t = s.bcast[0];
+  if (t >= ntiles) return;
+  u64 a0 = s.bcast[1], a1 = s.bcast[2];
+  u64 tn = s.bcast[3], a0n = s.bcast[4], a1n = s.bcast[5];
+
+  Prefetch R;
+  auto prefetch = [&](u64 tt, u64 x0, u64 x1) {
+    const u64 d0 = tt * JT, d1 = min(d0 + (u64)JT, total);
+    const int nat = (int)(x1 - x0), nbt = (int)((d1 - x1) - (d0 - x0));
+    const u64 y0 = d0 - x0;
+#pragma unroll
+    for (int k = 0; k < SLOTS; k++) {
+      const int x = tid + k * JB;
+      bool fb;
+      const i64 g = x < nat + nbt + 4 ? slot_row(x, nat, x0, y0, na, nb, &fb) : -1;
+      if (g >= 0) {
+        const Rows& src = fb ? p.b : p.a;
+        R.key[k] = src.key[g];
+        R.val[k] = src.val[g];
+        R.ts[k] = src.ts[g];
+        R.node[k] = src.node[g];
+        R.cnt[k] = src.cnt[g];
+      }
+    }
+  };
+  prefetch(t, a0, a1);
+
+  // the previous tile, kept in the other buffer until its output offset is known
+  bool pending = false;
+  u64 tp = 0;
+  u32 np = 0;
+  int pbuf = 0;
+
+  // resolve the pending tile's prefix (look-back), publish its inclusive prefix and
+  // write its compacted rows to the output
+  auto flush = [&](int pb) {
+    u64 prefix = 0;
+    if (tp > 0) prefix = lb_lookback_block<JB, 2>(p.scan.state, tp, p.scan.epoch, p.scan.err, s.lb);
+    if (tid == 0) {
+      if (tp > 0) lb_publish(p.scan.state, tp, p.scan.epoch, LB_INC, prefix + np);
+      if (tp == ntiles - 1) p.d_count[0] = prefix + np;
+    }
+    const Buf& b = s.buf[pb];
+    for (u32 q = tid; q < np; q += JB) {
+      const int slot = b.comp[q];
+      const u64 o = prefix + q;
+      p.out.key[o] = b.key[slot];
+      p.out.val[o] = b.val[slot];
+      p.out.ts[o] = b.ts[slot];
+      p.out.node[o] = b.node[slot];
+      p.out.cnt[o] = b.cnt[slot];
+    }
+  };
+
+  for (int k = 0;; k++) {
+    const int cb_ = k & 1;
+    Buf& cur = s.buf[cb_];
+    const u64 d0 = t * JT, d1 = min(d0 + (u64)JT, total);
+    const int nat = (int)(a1 - a0), nbt = (int)((d1 - a1) - (d0 - a0));
+    const u64 b0 = d0 - a0;
+    JSTAMP(t, 0);
+    u64 t2 = 0;  // ticket after next: issued now, consumed after the merge
+    if (tid == 0 && tn < ntiles) t2 = take_ticket();
+    // ---- commit the prefetched rows of tile t to LDS
+#pragma unroll
+    for (int q = 0; q < SLOTS; q++) {
+      const int x = tid + q * JB;
+      bool fb;
+      const i64 g = x < nat + nbt + 4 ? slot_row(x, nat, a0, b0, na, nb, &fb) : -1;
+      if (g >= 0) {
+        cur.key[x] = R.key[q];
+        cur.val[x] = R.val[q];
+        cur.ts[x] = R.ts[q];
+        cur.node[x] = R.node[q];
+        cur.cnt[x] = R.cnt[q];
+      }
+    }
+    __syncthreads();
+    JSTAMP(t, 2);
+    // ---- prefetch the next tile while this one is merged
+    if (tn < ntiles) prefetch(tn, a0n, a1n);
+
+    // ---- per-thread merge of JI positions
+    u32 keep;
+    unsigned short src[JI];
+    merge_items<FAST, !FAST>(p.ca, p.cb, va, vb, p.keys, p.n_keys, nb, cur, nat, nbt, a0, b0, keep,
+                             src, t);
+    JSTAMP(t, 3);
+
+    // ---- compaction list + aggregate of tile t
+    u32 tile_total;
+    u32 pos = block_excl_scan<JB>(__popc(keep), s.wave, &tile_total);
+#pragma unroll
+    for (int q = 0; q < JI; q++)
+      if (keep & (1u << q)) cur.comp[pos++] = src[q];
+    if (tid == 0) {
+      lb_publish(p.scan.state, t, p.scan.epoch, t == 0 ? LB_INC : LB_AGG, tile_total);
+      if (tn < ntiles) {  // the ticket after next (taken at the top of this iteration)
+        s.bcast[3] = t2;
+        if (t2 < ntiles) {
+          s.bcast[4] = p.splits[t2];
+          s.bcast[5] = p.splits[t2 + 1];
+        }
+      }
+    }
+    __syncthreads();
+    JSTAMP(t, 4);
+    // ---- the previous tile: its predecessors' aggregates are out by now
+    if (pending) flush(pbuf);
+    pending = true;
+    tp = t;
+    np = tile_total;
+    pbuf = cb_;
+    JSTAMP(t, 6);
+    if (tn >= ntiles) break;
+    t = tn;
+    a0 = a0n;
+    a1 = a1n;
+    __syncthreads();  // flushed buffer free; next ticket visible
+    tn = s.bcast[3];
+    a0n = s.bcast[4];
+    a1n = s.bcast[5];
+  }
+  __syncthreads();
+  flush(pbuf);
+}
+
+// ---------------------------------------------------------------- two-pass join
+// Pass 1: one workgroup per tile (no inter-workgroup dependency at all): stage, merge,
+// and write the tile's compacted rows to its own slot of a scratch store + its count.
+// Pass 2: each workgroup sums the counts before its tile and moves the slot's rows to
+// the output.  (The persistent single-pass kernel above trades the extra pass for a
+// decoupled look-back; DG_JOIN_MODE selects between them.)
+struct SlotLds {
+  Buf buf;
+  u32 wave[JB / WAVE + 1];
+  u64 vv_cnt[2][SMALL_VV];
+  u32 vv_node[2][SMALL_VV];
+};
+
+struct SlotArgs {
+  Rows a, b;
+  Ctx ca, cb;
+  const u64* keys;
+  u64 n_keys;
+  const u64* splits;
+  RowsOut tmp;
+  u32* counts;
+};
+
+template <bool FAST>
+__global__ __launch_bounds__(JB) void join2_slot_kernel(SlotArgs p) {
+  __shared__ SlotLds s;
+  const int tid = threadIdx.x;
   const u64 na = p.a.n, nb = p.b.n, total = na + nb;
-  if (blockIdx.x == p.ntiles) {  // extra workgroup: Dots.union(c1, c2) (aw_lww_map.ex:155)
-    ctx_union_block<JB>(p.cu, s.wave);
-    return;
+  const u64 t = blockIdx.x;
+  if (FAST && tid < SMALL_VV) {
+    s.vv_node[0][tid] = (u64)tid < p.ca.n ? p.ca.node[tid] : 0u;
+    s.vv_cnt[0][tid] = (u64)tid < p.ca.n ? p.ca.cnt[tid] : 0ull;
+    s.vv_node[1][tid] = (u64)tid < p.cb.n ? p.cb.node[tid] : 0u;
+    s.vv_cnt[1][tid] = (u64)tid < p.cb.n ? p.cb.cnt[tid] : 0ull;
   }
-
-  // ---- ticket (tile id in launch order) + context staging
-  if (tid == 0) {
-    u32 t = atomicAdd(p.scan.ticket, 1u);
-    if ((u64)t == p.ntiles - 1) atomicExch(p.scan.ticket, 0u);  // every tile has its ticket
-    s.bcast[0] = t;
-  }
-  const bool ca_lds = p.ca.n <= CTX_LDS, cb_lds = p.cb.n <= CTX_LDS;
-  if (ca_lds)
-    for (u64 x = tid; x < p.ca.n; x += JB) {
-      s.ctx_node[0][x] = p.ca.node[x];
-      s.ctx_cnt[0][x] = p.ca.cnt[x];
-    }
-  if (cb_lds)
-    for (u64 x = tid; x < p.cb.n; x += JB) {
-      s.ctx_node[1][x] = p.cb.node[x];
-      s.ctx_cnt[1][x] = p.cb.cnt[x];
-    }
-  __syncthreads();
-  const u64 tile = s.bcast[0];
-  JSTAMP(tile, 0);
-  const u64 d0 = tile * JT;
-  const u64 d1 = min(d0 + (u64)JT, total);
-
-  // ---- merge-path split from the partition pass
-  if (tid == 0) {
-    s.bcast[2] = p.splits[tile];
-    s.bcast[3] = p.splits[tile + 1];
-  }
-  __syncthreads();
-  JSTAMP(tile, 1);
-  const u64 a0 = s.bcast[2], a1 = s.bcast[3];
-  const u64 b0 = d0 - a0, b1 = d1 - a1;
-  const int nat = (int)(a1 - a0), nbt = (int)(b1 - b0);
-  const int offB = nat + 2;
-
-  // ---- stage rows a[a0-1 .. a1] and b[b0-1 .. b1] in LDS
-  for (int x = tid; x < nat + 2; x += JB) {
-    i64 g = (i64)a0 - 1 + x;
-    if (g >= 0 && (u64)g < na) {
-      s.key[x] = p.a.key[g];
-      s.val[x] = p.a.val[g];
-      s.ts[x] = p.a.ts[g];
-      s.node[x] = p.a.node[g];
-      s.cnt[x] = p.a.cnt[g];
-    }
-  }
-  for (int x = tid; x < nbt + 2; x += JB) {
-    i64 g = (i64)b0 - 1 + x;
-    if (g >= 0 && (u64)g < nb) {
-      s.key[offB + x] = p.b.key[g];
-      s.val[offB + x] = p.b.val[g];
-      s.ts[offB + x] = p.b.ts[g];
-      s.node[offB + x] = p.b.node[g];
-      s.cnt[offB + x] = p.b.cnt[g];
+  const SmallVV va{s.vv_node[0], s.vv_cnt[0], (u32)p.ca.n};
+  const SmallVV vb{s.vv_node[1], s.vv_cnt[1], (u32)p.cb.n};
+  const u64 a0 = p.splits[t], a1 = p.splits[t + 1];
+  const u64 d0 = t * JT, d1 = min(d0 + (u64)JT, total);
+  const int nat = (int)(a1 - a0), nbt = (int)((d1 - a1) - (d0 - a0));
+  const u64 b0 = d0 - a0;
+  Buf& cur = s.buf;
+  JSTAMP(t, 0);
+  // ---- stage a[a0-1 .. a1] and b[b0-1 .. b1] in LDS
+  for (int x = tid; x < nat + nbt + 4; x += JB) {
+    bool fb;
+    const i64 g = slot_row(x, nat, a0, b0, na, nb, &fb);
+    if (g >= 0) {
+      const Rows& src = fb ? p.b : p.a;
+      cur.key[x] = src.key[g];
+      cur.val[x] = src.val[g];
+      cur.ts[x] = src.ts[g];
+      cur.node[x] = src.node[g];
+      cur.cnt[x] = src.cnt[g];
     }
   }
   __syncthreads();
-  JSTAMP(tile, 2);
-
-  // ---- per-thread merge of JI positions
+  JSTAMP(t, 2);
   u32 keep;
   unsigned short src[JI];
-  if (ca_lds && cb_lds)
-    merge_items<true, true>(p.ca, p.cb, p.keys, p.n_keys, nb, s, nat, nbt, a0, b0, keep, src);
-  else if (ca_lds)
-    merge_items<true, false>(p.ca, p.cb, p.keys, p.n_keys, nb, s, nat, nbt, a0, b0, keep, src);
-  else if (cb_lds)
-    merge_items<false, true>(p.ca, p.cb, p.keys, p.n_keys, nb, s, nat, nbt, a0, b0, keep, src);
-  else
-    merge_items<false, false>(p.ca, p.cb, p.keys, p.n_keys, nb, s, nat, nbt, a0, b0, keep, src);
-
-  // ---- tile compaction
-  JSTAMP(tile, 3);
+  merge_items<FAST, !FAST>(p.ca, p.cb, va, vb, p.keys, p.n_keys, nb, cur, nat, nbt, a0, b0, keep,
+                           src, t);
+  JSTAMP(t, 3);
   u32 tile_total;
-  const u32 cnt = __popc(keep);
-  u32 pos = block_excl_scan<JB>(cnt, s.wave, &tile_total);
+  u32 pos = block_excl_scan<JB>(__popc(keep), s.wave, &tile_total);
 #pragma unroll
-  for (int k = 0; k < JI; k++)
-    if (keep & (1u << k)) s.comp[pos++] = src[k];
-
-  // ---- decoupled look-back for the tile's output offset
-  JSTAMP(tile, 4);
-  u64 prefix = 0;
-  if (tile == 0) {
-    if (tid == 0) lb_publish(p.scan.state, 0, p.scan.epoch, LB_INC, tile_total);
-  } else {
-    if (tid == 0) lb_publish(p.scan.state, tile, p.scan.epoch, LB_AGG, tile_total);
-    prefix = lb_lookback_block<JB, 2>(p.scan.state, tile, p.scan.epoch, p.scan.err, s.lb);
-    if (tid == 0) lb_publish(p.scan.state, tile, p.scan.epoch, LB_INC, prefix + tile_total);
-  }
-  if (tid == 0) {
-    s.bcast[1] = prefix;
-    if (tile == p.ntiles - 1) p.d_count[0] = prefix + tile_total;
-  }
+  for (int q = 0; q < JI; q++)
+    if (keep & (1u << q)) cur.comp[pos++] = src[q];
+  if (tid == 0) p.counts[t] = tile_total;
   __syncthreads();
-  const u64 base = s.bcast[1];
-  JSTAMP(tile, 5);
-
-  // ---- coalesced write of the kept rows
+  JSTAMP(t, 4);
   for (u32 q = tid; q < tile_total; q += JB) {
-    const int slot = s.comp[q];
-    const u64 o = base + q;
-    p.out.key[o] = s.key[slot];
-    p.out.val[o] = s.val[slot];
-    p.out.ts[o] = s.ts[slot];
-    p.out.node[o] = s.node[slot];
-    p.out.cnt[o] = s.cnt[slot];
+    const int slot = cur.comp[q];
+    const u64 o = t * JT + q;
+    p.tmp.key[o] = cur.key[slot];
+    p.tmp.val[o] = cur.val[slot];
+    p.tmp.ts[o] = cur.ts[slot];
+    p.tmp.node[o] = cur.node[slot];
+    p.tmp.cnt[o] = cur.cnt[slot];
   }
 #ifdef DG_STAMPS
-  __syncthreads();
-  JSTAMP(tile, 6);
+  JSTAMP(t, 6);
 #endif
+}
+
+constexpr int CPB = 256;
+
+__global__ __launch_bounds__(CPB) void join2_compact_kernel(RowsOut tmp, const u32* counts,
+                                                            u64 ntiles, RowsOut out,
+                                                            u64* d_count) {
+  __shared__ u32 s_wave[CPB / WAVE + 1];
+  __shared__ u64 s_pre;
+  const u64 tile = blockIdx.x;
+  u64 part = 0;
+  for (u64 i = threadIdx.x; i < tile; i += CPB) part += counts[i];
+#pragma unroll
+  for (int d = WAVE / 2; d >= 1; d >>= 1) part += __shfl_xor(part, d, WAVE);
+  if ((threadIdx.x & (WAVE - 1)) == 0) s_wave[threadIdx.x / WAVE] = (u32)part;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u64 acc = 0;
+    for (int w = 0; w < CPB / WAVE; w++) acc += s_wave[w];
+    s_pre = acc;
+    if (tile == ntiles - 1) d_count[0] = acc + counts[tile];
+  }
+  __syncthreads();
+  const u64 base = s_pre, n = counts[tile], src = tile * JT;
+  for (u64 q = threadIdx.x; q < n; q += CPB) {
+    out.key[base + q] = tmp.key[src + q];
+    out.val[base + q] = tmp.val[src + q];
+    out.ts[base + q] = tmp.ts[src + q];
+    out.node[base + q] = tmp.node[src + q];
+    out.cnt[base + q] = tmp.cnt[src + q];
+  }
 }
 
 }  // namespace
@@ -538,8 +780,8 @@ static CtxUnionArgs make_cu(const Ctx& a, const Ctx& b, u32* out_node, u64* out_
 
 hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& cb,
                         const u64* keys, u64 n_keys, const RowsOut& out, u32* out_ctx_node,
-                        u64* out_ctx_cnt, void* ctx_tmp, const Scan& scan, u64* d_counts,
-                        hipStream_t st) {
+                        u64* out_ctx_cnt, void* ctx_tmp, void* pass_tmp, int mode,
+                        const Scan& scan, int workers, u64* d_counts, hipStream_t st) {
   JoinArgs p;
   p.a = a;
   p.b = b;
@@ -547,23 +789,61 @@ hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& 
   p.cb = cb;
   p.keys = keys;
   p.n_keys = n_keys;
+  p.ntiles = join2_tiles(a.n, b.n);
+  p.splits = scan.state + p.ntiles;  // look-back granules first, then the splits
+  const CtxUnionArgs cu = make_cu(ca, cb, out_ctx_node, out_ctx_cnt, d_counts + 1, ctx_tmp);
   p.out = out;
   p.scan = scan;
-  p.ntiles = join2_tiles(a.n, b.n);
-  p.splits = scan.state + p.ntiles;  // the engine reserves 2 granules per tile + 2
   p.d_count = d_counts;
-  p.cu = make_cu(ca, cb, out_ctx_node, out_ctx_cnt, d_counts + 1, ctx_tmp);
   if (p.ntiles == 0) {
+    // no rows: only the context union runs
     hipError_t e = hipMemsetAsync(d_counts, 0, sizeof(u64), st);
     if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(ctx_union_kernel, dim3(1), dim3(CB), 0, st, cu);
+    return hipGetLastError();
   }
-  if (p.ntiles > 0) {
-    const u64 nb_part = (p.ntiles + 1 + (PB / WAVE) - 1) / (PB / WAVE);
-    hipLaunchKernelGGL(join2_partition_kernel, dim3((unsigned)nb_part), dim3(PB), 0, st, a, b,
-                       p.ntiles, p.splits);
+  // 1) merge-path partition (+1 workgroup for the context union), 2) persistent tile
+  // workers: merge, decoupled look-back one tile late, direct output writes
+  const u64 nb_part = (p.ntiles + 1 + (PB / WAVE) - 1) / (PB / WAVE);
+  hipLaunchKernelGGL(join2_partition_kernel, dim3((unsigned)nb_part + 1), dim3(PB), 0, st, a, b,
+                     p.ntiles, p.splits, cu);
+  const bool fast = keys == nullptr && ca.kind == 0 && cb.kind == 0 && ca.n <= (u64)SMALL_VV &&
+                    cb.n <= (u64)SMALL_VV;
+  if (mode == JOIN_TWO_PASS) {
+    SlotArgs q;
+    q.a = a;
+    q.b = b;
+    q.ca = ca;
+    q.cb = cb;
+    q.keys = keys;
+    q.n_keys = n_keys;
+    q.splits = p.splits;
+    char* t = (char*)pass_tmp;
+    const u64 cap = p.ntiles * (u64)JT;
+    q.counts = (u32*)t;
+    t += ((p.ntiles * 4 + 255) / 256) * 256;
+    q.tmp.key = (u64*)t;
+    t += cap * 8;
+    q.tmp.val = (u64*)t;
+    t += cap * 8;
+    q.tmp.ts = (i64*)t;
+    t += cap * 8;
+    q.tmp.cnt = (u64*)t;
+    t += cap * 8;
+    q.tmp.node = (u32*)t;
+    if (fast)
+      hipLaunchKernelGGL(join2_slot_kernel<true>, dim3((unsigned)p.ntiles), dim3(JB), 0, st, q);
+    else
+      hipLaunchKernelGGL(join2_slot_kernel<false>, dim3((unsigned)p.ntiles), dim3(JB), 0, st, q);
+    hipLaunchKernelGGL(join2_compact_kernel, dim3((unsigned)p.ntiles), dim3(CPB), 0, st, q.tmp,
+                       q.counts, p.ntiles, out, d_counts);
+    return hipGetLastError();
   }
-  // one workgroup per tile + one for the context union
-  hipLaunchKernelGGL(join2_rows_kernel, dim3((unsigned)p.ntiles + 1), dim3(JB), 0, st, p);
+  const u64 g = std::min<u64>(p.ntiles, (u64)(workers > 0 ? workers : 512));
+  if (fast)
+    hipLaunchKernelGGL(join2_tiles_kernel<true>, dim3((unsigned)g), dim3(JB), 0, st, p);
+  else
+    hipLaunchKernelGGL(join2_tiles_kernel<false>, dim3((unsigned)g), dim3(JB), 0, st, p);
   return hipGetLastError();
 }
 

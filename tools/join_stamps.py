@@ -42,13 +42,16 @@ def main():
     assert lib.dg_debug_join_stamps(buf.ctypes.data, len(buf)) == 0
     st = buf[: ntiles * 8].reshape(ntiles, 8).astype(np.int64)
     t0 = st[:, 0].min()
-    names = ["search", "stage", "merge", "scan", "lookback", "write"]
-    d = np.diff(st[:, :7], axis=1) * 10 / 1000.0  # us
+    # persistent kernel: 0 tile start, 2 rows committed to LDS, 5 merge-path search
+    # done, 3 merge done, 4 aggregate published, 6 previous tile flushed (look-back+write)
+    order = [0, 2, 5, 3, 4, 6]
+    names = ["stage", "search", "merge", "scan", "write"]
+    d = np.diff(st[:, order], axis=1) * 10 / 1000.0  # us
     print(f"tiles={ntiles} kernel span={(st[:, 6].max() - t0) * 10 / 1000:.1f} us")
     for i, nm in enumerate(names):
         print(f"{nm:9s} median {np.median(d[:, i]):6.2f} us  p90 {np.percentile(d[:, i], 90):6.2f}"
               f"  mean {d[:, i].mean():6.2f}")
-    tot = (st[:, 6] - st[:, 0]) * 10 / 1000
+    tot = (st[:, 6] - st[:, 0]) * 10 / 1000  # 0 -> 6
     print(f"per-tile total median {np.median(tot):.2f} us  mean {tot.mean():.2f}")
     starts = (st[:, 0] - t0) * 10 / 1000
     print("tile start times (us) at deciles:", np.percentile(starts, np.arange(0, 101, 10)).round(1))
