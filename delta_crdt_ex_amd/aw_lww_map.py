@@ -1,0 +1,188 @@
+"""Host mirror of `DeltaCrdt.AWLWWMap` (reference lib/delta_crdt/aw_lww_map.ex) on top
+of libdeltagpu: the same functions, argument meaning and error behaviour, with the
+state kept device-resident as SoA dot rows.
+
+    from delta_crdt_ex_amd import aw_lww_map as AWLWWMap
+    s = AWLWWMap.compress_dots(AWLWWMap.new())
+    s = AWLWWMap.join(s, AWLWWMap.add("k", "v", node_id, s), ["k"])
+    AWLWWMap.read(s)                       # => {"k": "v"}
+
+Terms (keys, values, node ids) are interned exactly through a `Universe`
+(interning.py); a state remembers its universe.  `join/3` and `read/1,2` run on the
+GPU (dg_join2 / dg_read_lww); `compress_dots/1` too (dg_compress_dots).  The mutators
+`add/4` and `remove/3` build per-op deltas on the host from the state's rows for one
+key, exactly as the reference does (:99-146) — a handful of rows, not the hot path.
+There is no CPU fallback: without a GPU the Engine raises.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import torch
+
+from . import interning
+from ._abi import DG_CTX_DOTS, DG_CTX_VV, FunctionClauseError
+from .store import Context, Engine, Store, u64
+
+_ENGINE: Engine | None = None
+
+
+def engine() -> Engine:
+    global _ENGINE
+    if _ENGINE is None:
+        _ENGINE = Engine(0)
+    return _ENGINE
+
+
+def _dev():
+    return engine().device
+
+
+class AWLWWMap:
+    """`%DeltaCrdt.AWLWWMap{dots, value}` (aw_lww_map.ex:2-3), device-resident."""
+
+    __slots__ = ("rows", "ctx", "universe", "_host")
+
+    def __init__(self, rows: Store, ctx: Context, universe: interning.Universe):
+        self.rows = rows
+        self.ctx = ctx
+        self.universe = universe
+        self._host = None
+
+    # -- host views (small states / single keys only)
+    def _host_rows(self):
+        if self._host is None:
+            self._host = self.rows.to_numpy()
+        return self._host
+
+    def _rows_of_key(self, kid: int):
+        k, v, t, n, c = self._host_rows()
+        lo = int(np.searchsorted(k, np.uint64(kid), side="left"))
+        hi = int(np.searchsorted(k, np.uint64(kid), side="right"))
+        return v[lo:hi], t[lo:hi], n[lo:hi], c[lo:hi]
+
+    @property
+    def dots(self):
+        """The causal context as terms: a frozenset of dots or a {node: max} dict."""
+        node, cnt = self.ctx.to_numpy()
+        U = self.universe
+        if self.ctx.kind == DG_CTX_DOTS:
+            return frozenset((U.node_term(int(a)), int(b)) for a, b in zip(node, cnt))
+        return {U.node_term(int(a)): int(b) for a, b in zip(node, cnt)}
+
+    @property
+    def value(self):
+        """The value map as terms: {key: {(value, ts): frozenset(dots)}}."""
+        U = self.universe
+        k, v, t, n, c = self._host_rows()
+        out: dict = {}
+        for i in range(len(k)):
+            ent = out.setdefault(U.key_term(int(k[i])), {})
+            ent.setdefault((U.value_term(int(v[i])), int(t[i])), set()).add(
+                (U.node_term(int(n[i])), int(c[i])))
+        return {key: {e: frozenset(d) for e, d in ents.items()} for key, ents in out.items()}
+
+
+def _ctx_from_pairs(kind, pairs) -> Context:
+    pairs = sorted(set(pairs))
+    return Context.from_numpy(kind, np.array([p[0] for p in pairs], np.uint32),
+                              np.array([p[1] for p in pairs], np.uint64), _dev())
+
+
+def _empty_rows() -> Store:
+    return Store.empty(1, _dev())
+
+
+def new(universe: interning.Universe | None = None) -> AWLWWMap:
+    """aw_lww_map.ex:8 — empty value, empty MapSet context."""
+    return AWLWWMap(_empty_rows(), Context.empty(DG_CTX_DOTS, 1, _dev()),
+                    universe or interning.DEFAULT)
+
+
+def compress_dots(state: AWLWWMap) -> AWLWWMap:
+    """aw_lww_map.ex:115-117 (FunctionClauseError on an already compressed state)."""
+    if state.ctx.kind != DG_CTX_DOTS:
+        raise FunctionClauseError(-6, "no function clause matching in Dots.compress/1")
+    return AWLWWMap(state.rows, engine().compress_dots(state.ctx), state.universe)
+
+
+def _next_dot(nid: int, ctx: Context):
+    """Dots.next_dot/2 (aw_lww_map.ex:30-37)."""
+    node, cnt = ctx.to_numpy()
+    if ctx.kind == DG_CTX_DOTS:  # compress (the reference logs "inefficient next_dot")
+        m = cnt[node == nid]
+        top = int(m.max()) if len(m) else 0
+    else:
+        m = cnt[node == nid]
+        top = int(m[0]) if len(m) else 0
+    return nid, top + 1
+
+
+def remove(key, node_id, state: AWLWWMap) -> AWLWWMap:
+    """aw_lww_map.ex:133-146: a delta whose context holds the key's current dots."""
+    U = state.universe
+    kid = U.key(key)
+    _v, _t, n, c = state._rows_of_key(kid)
+    return AWLWWMap(_empty_rows(), _ctx_from_pairs(DG_CTX_DOTS, zip(n.tolist(), c.tolist())), U)
+
+
+def add(key, value, node_id, state: AWLWWMap, ts: int | None = None) -> AWLWWMap:
+    """aw_lww_map.ex:99-112.  `ts` defaults to time.monotonic_ns() (the reference's
+    System.monotonic_time(:nanosecond))."""
+    U = state.universe
+    if ts is None:
+        ts = time.monotonic_ns()
+    kid, vid, nid = U.key(key), U.value(value), U.node(node_id)
+    rem = remove(key, node_id, state)
+    d_node, d_cnt = _next_dot(nid, state.ctx)
+    # aw_set_add (:119-122): the new dot plus any dots of an identical {value, ts} entry
+    v, t, n, c = state._rows_of_key(kid)
+    same = (v == np.uint64(vid)) & (t == np.int64(ts))
+    ctx_pairs = [(d_node, d_cnt)] + list(zip(n[same].tolist(), c[same].tolist()))
+    rows = Store.from_numpy(np.array([kid], np.uint64), np.array([vid], np.uint64),
+                            np.array([ts], np.int64), np.array([d_node], np.uint32),
+                            np.array([d_cnt], np.uint64), _dev())
+    addd = AWLWWMap(rows, _ctx_from_pairs(DG_CTX_DOTS, ctx_pairs), U)
+    if rem.ctx.n == 0:
+        return addd
+    return join(rem, addd, [key])
+
+
+def clear(_node_id, state: AWLWWMap) -> AWLWWMap:
+    """aw_lww_map.ex:148-150."""
+    return AWLWWMap(_empty_rows(), state.ctx, state.universe)
+
+
+def join(delta1: AWLWWMap, delta2: AWLWWMap, keys) -> AWLWWMap:
+    """aw_lww_map.ex:153-158 on the GPU (dg_join2)."""
+    U = delta1.universe
+    kids = np.unique(np.array([U.key(k) for k in keys], dtype=np.uint64))
+    kt = torch.from_numpy(np.ascontiguousarray(kids).view(np.int64)).to(_dev())
+    out, octx = engine().join2(delta1.rows, delta1.ctx, delta2.rows, delta2.ctx, keys=kt)
+    return AWLWWMap(out, octx, U)
+
+
+def join_all(delta1: AWLWWMap, delta2: AWLWWMap) -> AWLWWMap:
+    """join/3 over every key of both states (the full-state anti-entropy join)."""
+    out, octx = engine().join2(delta1.rows, delta1.ctx, delta2.rows, delta2.ctx)
+    return AWLWWMap(out, octx, delta1.universe)
+
+
+def read(state: AWLWWMap, keys=None) -> dict:
+    """aw_lww_map.ex:211-224 (read/1, read/2 with a list, read/3 with one key)."""
+    U = state.universe
+    kt = None
+    if keys is not None:
+        if not isinstance(keys, list):
+            keys = [keys]
+        kids = np.unique(np.array([U.key(k) for k in keys], dtype=np.uint64))
+        kt = torch.from_numpy(np.ascontiguousarray(kids).view(np.int64)).to(_dev())
+    if state.rows.n == 0:
+        return {}
+    ok, ov = engine().read_lww(state.rows, keys=kt)
+    return {U.key_term(int(k)): U.value_term(int(v)) for k, v in zip(u64(ok), u64(ov))}
+
+
+__all__ = ["AWLWWMap", "new", "compress_dots", "add", "remove", "clear", "join", "join_all", "read",
+           "DG_CTX_VV", "DG_CTX_DOTS"]

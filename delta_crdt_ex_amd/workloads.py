@@ -15,6 +15,7 @@ from __future__ import annotations
 import numpy as np
 
 from .interning import encode_int_value, splitmix64_np
+from .sharding import shard_of
 
 VV, DOTS = 0, 1
 
@@ -94,15 +95,6 @@ def config2(n_keys: int = 1_000_000, seed: int = 2, key_lo: int = 1, keys=None):
         out.append({"rows": sort_rows(key, val_r, ts_r, node_r, cnt_r),
                     "ctx": vv({0: int(k.max()) if n else 0, node_id: nc})})
     return out[0], out[1]
-
-
-def shard_of(key_ids: np.ndarray, n_shards: int) -> np.ndarray:
-    """Key-hash range sharding: shard = floor(key_id * n_shards / 2^64)."""
-    hi = (key_ids >> np.uint64(32)).astype(np.uint64)
-    lo = (key_ids & np.uint64(0xFFFFFFFF)).astype(np.uint64)
-    s = np.uint64(n_shards)
-    # (hi * 2^32 + lo) * s >> 64 = (hi * s + ((lo * s) >> 32)) >> 32
-    return ((hi * s + ((lo * s) >> np.uint64(32))) >> np.uint64(32)).astype(np.int64)
 
 
 def config2_shard(rank: int, world: int, keys_per_rank: int = 1_000_000, seed: int = 2):

@@ -1,0 +1,103 @@
+"""Key-hash range sharding with world_size-2 torch.distributed/gloo
+on the CPU: per-shard joins reassemble the unsharded join exactly, the VV all-reduce
+yields the global context union, and Merkle shard roots localise the diff.  The
+per-shard compute here is the C oracle (the GPU box runs libdeltagpu per rank)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from delta_crdt_ex_amd import sharding as S
+from delta_crdt_ex_amd import workloads as W
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_shard_of_matches_bounds():
+    rng = np.random.default_rng(0)
+    keys = np.sort(rng.integers(0, 1 << 63, 5000, dtype=np.int64).astype(np.uint64) * np.uint64(2))
+    for n in (1, 2, 3, 8):
+        sh = S.shard_of(keys, n)
+        assert np.all(np.diff(sh) >= 0) and sh.min() >= 0 and sh.max() < n
+        for s in range(n):
+            lb = S.shard_lower_bound(s, n)
+            assert np.all(keys[sh == s] >= np.uint64(lb)) if lb < (1 << 64) else True
+            if s > 0:
+                assert np.all(keys[sh == s - 1] < np.uint64(lb))
+        parts = S.split_rows((keys, keys, keys.view(np.int64), keys.astype(np.uint32), keys), n)
+        assert sum(len(p[0]) for p in parts) == len(keys)
+        for s, p in enumerate(parts):
+            assert np.all(S.shard_of(p[0], n) == s)
+
+
+def test_fold_roots_matches_c_tree():
+    from oracle import ref as R
+    # a depth-3 tree over 8 "shard roots" equals fold_roots over the level-3 nodes
+    a, _ = W.merkle_pair(n_keys=3000, seed=3)
+    t = R.merkle_build(a["rows"], 3)
+    lvl3 = t.nodes[7:15]
+    assert S.fold_roots(lvl3.tolist()) == int(t.nodes[0])
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    from oracle import ref as R
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                                world_size=world)
+        rng = np.random.default_rng(7)
+        a, b = W.random_pair(rng, n_keys=400, ts_range=5, dense_ctx=False)
+        a2, b2 = W.config2(n_keys=6000, seed=3)
+        for A, B in ((a, b), (a2, b2)):
+            mine_a = S.split_rows(A["rows"], world)[rank]
+            mine_b = S.split_rows(B["rows"], world)[rank]
+            rows, ctx = R.join2(mine_a, A["ctx"], mine_b, B["ctx"])
+            # every shard computed the same (replicated) context union
+            node, cnt = S.vv_allreduce_max(ctx[1], ctx[2])
+            want_rows, want_ctx = R.join2(A["rows"], A["ctx"], B["rows"], B["ctx"])
+            assert np.array_equal(node, want_ctx[1]) and np.array_equal(cnt, want_ctx[2])
+            # the shard's output is exactly the unsharded output's slice
+            want_mine = S.split_rows(want_rows, world)[rank]
+            for x, y in zip(rows, want_mine):
+                assert np.array_equal(x, y)
+            # Merkle: shard roots, replica root, and the diff restricted to differing shards
+            depth = 8
+            ta, tb = R.merkle_build(mine_a, depth), R.merkle_build(mine_b, depth)
+            ra, root_a = S.merkle_roots(int(ta.nodes[0]))
+            rb, root_b = S.merkle_roots(int(tb.nodes[0]))
+            diff_local = R.merkle_diff(ta, tb)
+            full = R.store_diff(A["rows"], B["rows"])
+            assert np.array_equal(diff_local, S.split_rows((full,) * 5, world)[rank][0])
+            assert (root_a != root_b) == (len(full) > 0)
+            if rank not in S.differing_shards(ra, rb):
+                assert len(diff_local) == 0
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, "".join(traceback.format_exception(e))))
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_gloo_sharded_join_and_merkle():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, msg in sorted(res):
+        assert msg == "ok", f"rank {rank}: {msg}"
