@@ -34,16 +34,30 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 KEYS_PER_GPU = 1_000_000
 
 
+def kernel_source_digest():
+    """sha256 over the HIP sources of libdeltagpu: ties a PMC summary to the kernels
+    it measured."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    for f in sorted(glob.glob(os.path.join(ROOT, "delta_crdt_ex_amd", "csrc", "*"))):
+        h.update(os.path.basename(f).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
 def _traffic_from_profiles(n_in, n_out):
-    """HBM bytes per launch of the join kernel from the committed PMC summary, if one
-    exists for this exact workload (profiles/join2_pmc.json, written by
-    tools/pmc_traffic.py); else None."""
+    """HBM bytes per launch of the join from the committed PMC summary, if one exists
+    for this exact workload and these exact kernel sources (profiles/join2_pmc.json,
+    written by tools/pmc_traffic.py); else None."""
     p = os.path.join(ROOT, "profiles", "join2_pmc.json")
     try:
         d = json.load(open(p))
     except Exception:
         return None
     if d.get("rows_in") != n_in or d.get("rows_out") != n_out:
+        return None
+    if d.get("kernel_sources") != kernel_source_digest():
         return None
     return d.get("hbm_bytes_per_launch")
 
@@ -101,6 +115,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-merkle", action="store_true")
+    ap.add_argument("--rotate", type=int, default=4,
+                    help="distinct replica pairs joined round-robin (defeats cache residency)")
+    ap.add_argument("--calibrate", action="store_true",
+                    help="after timing, run dg_store_check once over every input store: a "
+                         "read of exactly 36 B/row that tools/pmc_traffic.py uses to "
+                         "calibrate FETCH_SIZE for 8-B/lane loads")
     args = ap.parse_args()
 
     import torch
@@ -120,33 +140,43 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    a, b = W.config2_shard(rank, world, KEYS_PER_GPU)
-    n_in = len(a["rows"][0]) + len(b["rows"][0])
+    # `--rotate R` distinct replica pairs (different seeds), joined round-robin: R x 112 MB
+    # of inputs+outputs exceeds the 256 MB Infinity Cache, so every step streams its
+    # inputs from HBM instead of re-reading the previous step's cache-resident copy.
     eng = Engine(local)
     stream = eng.stream
-    sa = Store.from_numpy(*a["rows"], device=dev)
-    sb = Store.from_numpy(*b["rows"], device=dev)
-    ca = Context.from_numpy(*a["ctx"], dev)
-    cb = Context.from_numpy(*b["ctx"], dev)
-    out = Store.empty(sa.n + sb.n, dev)
-    octx = Context.empty(0, ca.n + cb.n, dev)
-    d_counts = torch.zeros(8, dtype=torch.int64, device=dev)
+    pairs = []
+    for r in range(args.rotate):
+        a, b = W.config2_shard(rank, world, KEYS_PER_GPU, seed=2 + r)
+        sa = Store.from_numpy(*a["rows"], device=dev)
+        sb = Store.from_numpy(*b["rows"], device=dev)
+        ca = Context.from_numpy(*a["ctx"], dev)
+        cb = Context.from_numpy(*b["ctx"], dev)
+        out = Store.empty(sa.n + sb.n, dev)
+        octx = Context.empty(0, ca.n + cb.n, dev)
+        d_counts = torch.zeros(8, dtype=torch.int64, device=dev)
+        pairs.append(dict(a=a, b=b, sa=sa, sb=sb, ca=ca, cb=cb, out=out, octx=octx, d=d_counts,
+                          launch=eng.prepare_join2(sa, ca, sb, cb, out, octx, d_counts)))
     torch.cuda.synchronize()
+    launches = [pr["launch"] for pr in pairs]
+    R = len(launches)
+    a, b, ca, cb = pairs[0]["a"], pairs[0]["b"], pairs[0]["ca"], pairs[0]["cb"]
+    n_in = len(a["rows"][0]) + len(b["rows"][0])
+    n_in_all = [len(pr["a"]["rows"][0]) + len(pr["b"]["rows"][0]) for pr in pairs]
 
-    launch = eng.prepare_join2(sa, ca, sb, cb, out, octx, d_counts)
-    for _ in range(args.warmup):
-        launch()
+    for i in range(args.warmup):
+        launches[i % R]()
     eng.sync()
-    n_out = int(d_counts[0].item())
-    n_ctx_out = int(d_counts[1].item())
+    n_out = int(pairs[0]["d"][0].item())
+    n_ctx_out = int(pairs[0]["d"][1].item())
 
     # timed region: K back-to-back joins, barrier + sync on both sides
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        launch()
+    for i in range(args.steps):
+        launches[i % R]()
     eng.sync()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
@@ -160,15 +190,24 @@ def main():
     with torch.cuda.stream(stream):
         for i in range(nev):
             ev[i].record(stream)
-            launch()
+            launches[i % R]()
         ev[nev].record(stream)
     eng.sync()
     torch.cuda.synchronize()
     launch_ms = [ev[i].elapsed_time(ev[i + 1]) for i in range(nev)]
     avg_launch_s = float(np.median(launch_ms)) / 1e3
 
+    calib_rows = 0
+    if args.calibrate:
+        for pr in pairs:
+            for st_ in (pr["sa"], pr["sb"]):
+                eng.store_check(st_)
+                calib_rows += st_.n
+        eng.sync()
+
+    rows_done = sum(n_in_all[i % R] for i in range(args.steps))  # input rows merged by K steps
     el_t = torch.tensor([el], dtype=torch.float64, device=dev)
-    tot = torch.tensor([float(n_in)], dtype=torch.float64, device=dev)
+    tot = torch.tensor([float(rows_done)], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
@@ -181,7 +220,7 @@ def main():
         traffic = _traffic_from_profiles(n_in, n_out)
         res = {
             "metric": "merged dots/sec for AWLWWMap delta join + Merkle diff keys/sec at 1\u20138 GPUs",
-            "value": total_rows * args.steps / el_max,
+            "value": total_rows / el_max,
             "unit": "merged dots/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -199,7 +238,9 @@ def main():
                 "rows_in_per_gpu": n_in,
                 "rows_out_per_gpu": n_out,
                 "parallelism": f"key-hash shards x{world}",
+                "rotate": R,
             },
+            **({"calib_rows": calib_rows} if args.calibrate else {}),
             "roofline": {
                 "bound": "hbm",
                 "achieved": achieved,
@@ -207,7 +248,8 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "join2 = join2_partition_kernel + join2_rows_kernel (events bracket both)",
+                "kernel": "join2 = join2_partition_kernel + join2_slot_kernel + join2_compact_kernel "
+                          "(events bracket all three)",
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_launch_us": avg_launch_s * 1e6,
                 "launch_timing": "median of per-step HIP event pairs on the engine stream",

@@ -39,7 +39,7 @@ hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& 
                         const Scan& scan, int workers, u64* d_counts, hipStream_t st);
 inline size_t join2_pass_tmp_bytes(u64 na, u64 nb) {
   const u64 t = join2_tiles(na, nb);
-  return ((t * 4 + 255) / 256) * 256 + t * (u64)JOIN_TILE * 36 + 256;
+  return ((t * 4 + 255) / 256) * 256 + t * (u64)JOIN_TILE * 2 + 256;
 }
 // Dots.union/2 of two contexts; out kind: DOTS iff both DOTS.  Writes |out| to *d_count.
 // tmp: (a.n + b.n) u32 + (a.n + b.n) u64 + (a.n + b.n + 1) u32 of device scratch.

@@ -662,8 +662,8 @@ struct SlotArgs {
   const u64* keys;
   u64 n_keys;
   const u64* splits;
-  RowsOut tmp;
-  u32* counts;
+  unsigned short* lists;  // tile t's compaction list (staging slots) at lists[t * JT ...]
+  u32* counts;            // kept rows per tile
 };
 
 template <bool FAST>
@@ -714,15 +714,7 @@ __global__ __launch_bounds__(JB) void join2_slot_kernel(SlotArgs p) {
   if (tid == 0) p.counts[t] = tile_total;
   __syncthreads();
   JSTAMP(t, 4);
-  for (u32 q = tid; q < tile_total; q += JB) {
-    const int slot = cur.comp[q];
-    const u64 o = t * JT + q;
-    p.tmp.key[o] = cur.key[slot];
-    p.tmp.val[o] = cur.val[slot];
-    p.tmp.ts[o] = cur.ts[slot];
-    p.tmp.node[o] = cur.node[slot];
-    p.tmp.cnt[o] = cur.cnt[slot];
-  }
+  for (u32 q = tid; q < tile_total; q += JB) p.lists[t * JT + q] = cur.comp[q];
 #ifdef DG_STAMPS
   JSTAMP(t, 6);
 #endif
@@ -730,9 +722,15 @@ __global__ __launch_bounds__(JB) void join2_slot_kernel(SlotArgs p) {
 
 constexpr int CPB = 256;
 
-__global__ __launch_bounds__(CPB) void join2_compact_kernel(RowsOut tmp, const u32* counts,
-                                                            u64 ntiles, RowsOut out,
-                                                            u64* d_count) {
+// Pass 2: tile t's prefix = Σ counts before it (summed by the workgroup itself), then
+// every kept row is gathered from a or b through the tile's compaction list (slots of
+// the pass-1 staging: slot x < nat + 2 is a[a0 - 1 + x], else b[b0 - 1 + x - nat - 2])
+// and written to the output.  The rows were read by pass 1 just before, so the gathers
+// mostly hit the Infinity Cache; the list is 2 bytes per kept row.
+__global__ __launch_bounds__(CPB) void join2_compact_kernel(Rows a, Rows b, const u64* splits,
+                                                            const unsigned short* lists,
+                                                            const u32* counts, u64 ntiles,
+                                                            RowsOut out, u64* d_count) {
   __shared__ u32 s_wave[CPB / WAVE + 1];
   __shared__ u64 s_pre;
   const u64 tile = blockIdx.x;
@@ -749,13 +747,23 @@ __global__ __launch_bounds__(CPB) void join2_compact_kernel(RowsOut tmp, const u
     if (tile == ntiles - 1) d_count[0] = acc + counts[tile];
   }
   __syncthreads();
-  const u64 base = s_pre, n = counts[tile], src = tile * JT;
+  const u64 total = a.n + b.n;
+  const u64 a0 = splits[tile], a1 = splits[tile + 1];
+  const u64 d0 = tile * JT;
+  const int nat = (int)(a1 - a0);
+  const u64 b0 = d0 - a0;
+  const u64 base = s_pre, n = counts[tile];
+  (void)total;
   for (u64 q = threadIdx.x; q < n; q += CPB) {
-    out.key[base + q] = tmp.key[src + q];
-    out.val[base + q] = tmp.val[src + q];
-    out.ts[base + q] = tmp.ts[src + q];
-    out.node[base + q] = tmp.node[src + q];
-    out.cnt[base + q] = tmp.cnt[src + q];
+    const int x = lists[tile * JT + q];
+    const bool fb = x >= nat + 2;
+    const u64 g = fb ? b0 - 1 + (u64)(x - nat - 2) : a0 - 1 + (u64)x;
+    const Rows& src = fb ? b : a;
+    out.key[base + q] = src.key[g];
+    out.val[base + q] = src.val[g];
+    out.ts[base + q] = src.ts[g];
+    out.node[base + q] = src.node[g];
+    out.cnt[base + q] = src.cnt[g];
   }
 }
 
@@ -819,24 +827,15 @@ hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& 
     q.n_keys = n_keys;
     q.splits = p.splits;
     char* t = (char*)pass_tmp;
-    const u64 cap = p.ntiles * (u64)JT;
     q.counts = (u32*)t;
     t += ((p.ntiles * 4 + 255) / 256) * 256;
-    q.tmp.key = (u64*)t;
-    t += cap * 8;
-    q.tmp.val = (u64*)t;
-    t += cap * 8;
-    q.tmp.ts = (i64*)t;
-    t += cap * 8;
-    q.tmp.cnt = (u64*)t;
-    t += cap * 8;
-    q.tmp.node = (u32*)t;
+    q.lists = (unsigned short*)t;
     if (fast)
       hipLaunchKernelGGL(join2_slot_kernel<true>, dim3((unsigned)p.ntiles), dim3(JB), 0, st, q);
     else
       hipLaunchKernelGGL(join2_slot_kernel<false>, dim3((unsigned)p.ntiles), dim3(JB), 0, st, q);
-    hipLaunchKernelGGL(join2_compact_kernel, dim3((unsigned)p.ntiles), dim3(CPB), 0, st, q.tmp,
-                       q.counts, p.ntiles, out, d_counts);
+    hipLaunchKernelGGL(join2_compact_kernel, dim3((unsigned)p.ntiles), dim3(CPB), 0, st, a, b,
+                       q.splits, q.lists, q.counts, p.ntiles, out, d_counts);
     return hipGetLastError();
   }
   const u64 g = std::min<u64>(p.ntiles, (u64)(workers > 0 ? workers : 512));
