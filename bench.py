@@ -119,8 +119,8 @@ def main():
                     help="distinct replica pairs joined round-robin (defeats cache residency)")
     ap.add_argument("--calibrate", action="store_true",
                     help="after timing, run dg_store_check once over every input store: a "
-                         "read of exactly 36 B/row that tools/pmc_traffic.py uses to "
-                         "calibrate FETCH_SIZE for 8-B/lane loads")
+                         "read of exactly the key column (8 B/row on config-2 stores) that "
+                         "tools/pmc_traffic.py uses to calibrate FETCH_SIZE for 8-B/lane loads")
     args = ap.parse_args()
 
     import torch
