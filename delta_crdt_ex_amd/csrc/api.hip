@@ -31,8 +31,8 @@ struct dg_engine {
   // general scratch
   void* tmp = nullptr;
   size_t tmp_cap = 0;
-  int join_workers = 1024;  // persistent join tile workgroups (single-pass mode)
-  int join_mode = JOIN_TWO_PASS;  // DG_JOIN_MODE=1: single-pass persistent look-back kernel
+  int join_mode = JOIN_TWO_PASS;  // DG_JOIN_MODE=1: single-pass look-back variant
+  int join_workers = 0;           // persistent pass-1 workgroups (0: all resident ones)
 };
 
 namespace {
@@ -217,10 +217,6 @@ int dg_engine_create(int device, void* hip_stream, dg_engine** out) {
   dg_engine* e = new dg_engine();
   e->device = device;
   {
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
-        cus > 0)
-      e->join_workers = 2 * cus;  // 2 resident join workgroups per CU (VGPR-bound)
     const char* v = getenv("DG_JOIN_WORKERS");
     if (v && atoi(v) > 0) e->join_workers = atoi(v);
     const char* m = getenv("DG_JOIN_MODE");

@@ -64,6 +64,32 @@ __device__ __forceinline__ Row load_row(const Rows& r, u64 i) {
   return x;
 }
 
+// A pointer value the optimizer cannot trace back to the memory it was loaded from.
+template <class T>
+__device__ __forceinline__ T* opaque_ptr(T* p) {
+  asm("" : "+s"(p));
+  return p;
+}
+
+// Row g of B if fb else of A.  The per-lane choice is a select between opaque pointer
+// VALUES: a select between two loads of struct fields (`fb ? B.key : A.key`) is
+// rewritten by the compiler into a load through a selected struct address, which
+// spills the kernel's arguments to scratch and turns the row loads into flat loads.
+template <class T>
+__device__ __forceinline__ T gload(const T* p, u64 g) {  // a global_load, not a flat_load
+  return ((const __attribute__((address_space(1))) T*)p)[g];
+}
+
+__device__ __forceinline__ Row load_row_sel(const Rows& A, const Rows& B, bool fb, u64 g) {
+  Row x;
+  x.key = gload(fb ? opaque_ptr(B.key) : opaque_ptr(A.key), g);
+  x.val = gload(fb ? opaque_ptr(B.val) : opaque_ptr(A.val), g);
+  x.ts = gload(fb ? opaque_ptr(B.ts) : opaque_ptr(A.ts), g);
+  x.node = gload(fb ? opaque_ptr(B.node) : opaque_ptr(A.node), g);
+  x.cnt = gload(fb ? opaque_ptr(B.cnt) : opaque_ptr(A.cnt), g);
+  return x;
+}
+
 // -1 / 0 / 1 on the full tuple.
 __device__ __forceinline__ int row_cmp(const Row& a, const Row& b) {
   if (a.key != b.key) return a.key < b.key ? -1 : 1;

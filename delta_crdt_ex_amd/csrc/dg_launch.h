@@ -29,9 +29,11 @@ constexpr int JOIN_TILE = JOIN_BLOCK * JOIN_ITEMS;
 
 inline u64 join2_tiles(u64 na, u64 nb) { return (na + nb + JOIN_TILE - 1) / JOIN_TILE; }
 // join/3: a merge-path partition pass (its extra workgroup computes the context union,
-// d_counts[1] = its size), then persistent tile workers that merge each tile, publish
-// its aggregate, and write the previous tile's rows once its prefix is resolved
-// (d_counts[0] = output rows).  Uses scan.state[0, 2 * ntiles + 2).
+// d_counts[1] = its size), then one workgroup per tile that merges it, resolves its
+// output offset by decoupled look-back and writes its kept rows (d_counts[0] = output
+// rows).  Uses scan.state[0, 2 * ntiles + 2).  JOIN_TWO_PASS replaces the look-back by
+// a count/compact pass pair (pass_tmp: join2_pass_tmp_bytes) whose first pass runs
+// `workers` persistent workgroups.
 enum { JOIN_SINGLE_PASS = 0, JOIN_TWO_PASS = 1 };
 hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& cb,
                         const u64* keys, u64 n_keys, const RowsOut& out, u32* out_ctx_node,

@@ -4,9 +4,10 @@
     python tools/join_stamps.py                        # on the GPU box
 
 Stamps are s_memrealtime (100 MHz) taken by lane 0 of every tile at:
-0 tile start (after the ticket)  1 after the merge-path search  2 after LDS staging
-3 after the per-thread merge     4 after the block scan          5 after the look-back
-6 after the output write.  Only SHARES are meaningful (stamps add fences).
+0 tile start (after the ticket)  1 VV tables filled  2 rows staged in LDS
+3 per-thread merge done          4 block scan + compaction list done
+5 look-back done (single pass) / count written (two pass)   6 output written.
+Only SHARES are meaningful (stamps add barriers).
 """
 import ctypes as C
 import os
@@ -42,10 +43,8 @@ def main():
     assert lib.dg_debug_join_stamps(buf.ctypes.data, len(buf)) == 0
     st = buf[: ntiles * 8].reshape(ntiles, 8).astype(np.int64)
     t0 = st[:, 0].min()
-    # persistent kernel: 0 tile start, 2 rows committed to LDS, 5 merge-path search
-    # done, 3 merge done, 4 aggregate published, 6 previous tile flushed (look-back+write)
-    order = [0, 2, 5, 3, 4, 6]
-    names = ["stage", "search", "merge", "scan", "write"]
+    order = [0, 1, 2, 3, 4, 5, 6]
+    names = ["tables", "stage", "merge", "scan", "lookback", "write"]
     d = np.diff(st[:, order], axis=1) * 10 / 1000.0  # us
     print(f"tiles={ntiles} kernel span={(st[:, 6].max() - t0) * 10 / 1000:.1f} us")
     for i, nm in enumerate(names):
