@@ -24,6 +24,8 @@ struct dg_engine {
   u64* state = nullptr;
   u64 state_cap = 0;
   u32* ticket = nullptr;  // [0] ticket, [1] error bits, [2] store_check flag
+  u32* counts = nullptr;  // single-pass join tile-count granules
+  u64 counts_cap = 0;
   u32 epoch = 0;
   // small device counters + pinned host mirror
   u64* d_counts = nullptr;  // 8 entries
@@ -31,7 +33,7 @@ struct dg_engine {
   // general scratch
   void* tmp = nullptr;
   size_t tmp_cap = 0;
-  int join_mode = JOIN_TWO_PASS;  // DG_JOIN_MODE=1: single-pass look-back variant
+  int join_mode = JOIN_SINGLE_PASS;  // DG_JOIN_MODE=2: two-pass count/compact variant
   int join_workers = 0;           // persistent pass-1 workgroups (0: all resident ones)
 };
 
@@ -88,12 +90,27 @@ int ensure_tmp(dg_engine* e, size_t bytes) {
   return DG_OK;
 }
 
+int ensure_counts(dg_engine* e, u64 tiles) {
+  if (tiles <= e->counts_cap) return DG_OK;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (e->counts) HIP_TRY(hipFree(e->counts));
+  e->counts = nullptr;
+  u64 cap = std::max<u64>(tiles, 4096);
+  if (hipMalloc(&e->counts, cap * sizeof(u32)) != hipSuccess)
+    return fail(DG_E_NOMEM, "hipMalloc of %llu tile-count granules failed", cap);
+  HIP_TRY(hipMemset(e->counts, 0, cap * sizeof(u32)));  // epoch 0 is never current
+  e->counts_cap = cap;
+  return DG_OK;
+}
+
 // A fresh epoch per look-back launch; granules of older epochs read as "not ready".
 int next_scan(dg_engine* e, Scan* s) {
   if (++e->epoch >= (1u << 20)) {
     HIP_TRY(hipMemsetAsync(e->state, 0, e->state_cap * sizeof(u64), e->stream));
+    if (e->counts) HIP_TRY(hipMemsetAsync(e->counts, 0, e->counts_cap * sizeof(u32), e->stream));
     e->epoch = 1;
   }
+  s->counts = e->counts;
   s->state = e->state;
   s->ticket = e->ticket;
   s->err = e->ticket + 1;
@@ -186,6 +203,7 @@ int join2_enqueue(dg_engine* e, const dg_store* a, const dg_context* ca, const d
     return fail(DG_E_INVAL, "dg_join2: null output column");
   TRY(set_device(e));
   TRY(ensure_state(e, 2 * join2_tiles(a->n, b->n) + 2));  // granules + tile splits
+  if (e->join_mode == JOIN_SINGLE_PASS) TRY(ensure_counts(e, join2_tiles(a->n, b->n)));
   const size_t ctx_bytes = (ctx_union_tmp_bytes(ca->n, cb->n) + 255) / 256 * 256;
   const size_t pass_bytes = e->join_mode == JOIN_TWO_PASS ? join2_pass_tmp_bytes(a->n, b->n) : 0;
   TRY(ensure_tmp(e, ctx_bytes + pass_bytes));
@@ -220,7 +238,7 @@ int dg_engine_create(int device, void* hip_stream, dg_engine** out) {
     const char* v = getenv("DG_JOIN_WORKERS");
     if (v && atoi(v) > 0) e->join_workers = atoi(v);
     const char* m = getenv("DG_JOIN_MODE");
-    if (m && m[0] == '1') e->join_mode = JOIN_SINGLE_PASS;
+    if (m && m[0] == '2') e->join_mode = JOIN_TWO_PASS;
   }
   int rc = set_device(e);
   if (rc != DG_OK) {
@@ -262,6 +280,7 @@ int dg_engine_destroy(dg_engine* e) {
   if (e->d_counts) hipFree(e->d_counts);
   if (e->h_counts) hipHostFree(e->h_counts);
   if (e->tmp) hipFree(e->tmp);
+  if (e->counts) hipFree(e->counts);
   if (e->own_stream && e->stream) hipStreamDestroy(e->stream);
   delete e;
   return DG_OK;

@@ -71,6 +71,12 @@ __device__ __forceinline__ T* opaque_ptr(T* p) {
   return p;
 }
 
+template <class T>
+__device__ __forceinline__ T opaque_val(T v) {
+  asm("" : "+s"(v));
+  return v;
+}
+
 // Row g of B if fb else of A.  The per-lane choice is a select between opaque pointer
 // VALUES: a select between two loads of struct fields (`fb ? B.key : A.key`) is
 // rewritten by the compiler into a load through a selected struct address, which
@@ -88,6 +94,18 @@ __device__ __forceinline__ Row load_row_sel(const Rows& A, const Rows& B, bool f
   x.node = gload(fb ? opaque_ptr(B.node) : opaque_ptr(A.node), g);
   x.cnt = gload(fb ? opaque_ptr(B.cnt) : opaque_ptr(A.cnt), g);
   return x;
+}
+
+// c ? x : y field by field (a conditional on two Row objects selects an ADDRESS and
+// copies through it, which keeps both rows in scratch memory).
+__device__ __forceinline__ Row row_sel(bool c, const Row& x, const Row& y) {
+  Row r;
+  r.key = c ? x.key : y.key;
+  r.val = c ? x.val : y.val;
+  r.ts = c ? x.ts : y.ts;
+  r.node = c ? x.node : y.node;
+  r.cnt = c ? x.cnt : y.cnt;
+  return r;
 }
 
 // -1 / 0 / 1 on the full tuple.

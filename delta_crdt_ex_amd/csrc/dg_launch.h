@@ -14,6 +14,8 @@ struct Scan {
   u32* ticket;  // tile ticket counter, left at 0 by every launch (device)
   u32* err;     // error bits (device): 1 = look-back timeout
   u32 epoch;    // granules of other epochs are ignored
+  u32* counts;  // per-tile count granules {epoch:20 | count:12} of the single-pass join
+                // (written only by that kernel, zeroed when allocated)
 };
 
 // ---- join.hip
@@ -25,7 +27,9 @@ struct Scan {
 #endif
 constexpr int JOIN_BLOCK = DG_JOIN_BLOCK;  // threads per join tile (one wave per SIMD)
 constexpr int JOIN_ITEMS = DG_JOIN_ITEMS;  // merged positions per thread
-constexpr int JOIN_TILE = JOIN_BLOCK * JOIN_ITEMS;
+// merged positions per tile: JOIN_BLOCK * JOIN_ITEMS less 8, so the staged rows (tile +
+// 2 neighbours per store + 1 look-ahead) fit JOIN_ITEMS register slots per thread
+constexpr int JOIN_TILE = JOIN_BLOCK * JOIN_ITEMS - 8;
 
 inline u64 join2_tiles(u64 na, u64 nb) { return (na + nb + JOIN_TILE - 1) / JOIN_TILE; }
 // join/3: a merge-path partition pass (its extra workgroup computes the context union,
@@ -41,7 +45,7 @@ hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& 
                         const Scan& scan, int workers, u64* d_counts, hipStream_t st);
 inline size_t join2_pass_tmp_bytes(u64 na, u64 nb) {
   const u64 t = join2_tiles(na, nb);
-  return ((t * 4 + 255) / 256) * 256 + t * (u64)JOIN_TILE * 2 + 256;
+  return ((t * 4 + 255) / 256) * 256 + t * (u64)JOIN_TILE * 2 + 256;  // counts + slot lists
 }
 // Dots.union/2 of two contexts; out kind: DOTS iff both DOTS.  Writes |out| to *d_count.
 // tmp: (a.n + b.n) u32 + (a.n + b.n) u64 + (a.n + b.n + 1) u32 of device scratch.

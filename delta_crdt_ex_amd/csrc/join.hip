@@ -47,11 +47,7 @@ constexpr int JI = JOIN_ITEMS;
 constexpr int JT = JOIN_TILE;
 constexpr int JS = JT + 5;  // LDS row slots: tile rows + one neighbour on each side per store
                             // (+1: the merge's look-ahead read past the last B slot)
-#ifndef DG_JOIN_PIPE
-#define DG_JOIN_PIPE 0
-#endif
-constexpr bool JOIN_PIPE = DG_JOIN_PIPE;  // pass 1: persistent, next tile prefetched in registers
-constexpr int VT = 128;     // VV table: node ids below this are looked up directly in LDS
+constexpr int VT = 64;      // VV table: node ids below this are looked up directly in LDS
 
 #ifdef DG_STAMPS
 // Diagnostic build only (DG_STAMPS=1): per-tile phase timestamps (s_memrealtime,
@@ -361,37 +357,38 @@ __device__ __forceinline__ bool covers(const u64* tab, const Ctx& c, u32 dn, u64
   return ctx_covers(c.node, c.cnt, c.n, c.kind, dn, dc);
 }
 
-// Map.get(vv, want, 0) by binary search of a VV in global memory.
-__device__ __noinline__ u64 vv_get(const u32* node, const u64* cnt, u64 n, u32 want) {
-  u64 lo = 0, hi = n;
-  while (lo < hi) {
-    const u64 m = (lo + hi) >> 1;
-    if (node[m] < want)
-      lo = m + 1;
-    else
-      hi = m;
-  }
-  return (lo < n && node[lo] == want) ? cnt[lo] : 0ull;
-}
-
-// Fill the two VV tables (threads of the block; tables zeroed by the caller and a
-// barrier in between).
+// VV tables: tab_a[node] / tab_b[node] = the VV's counter for node ids < VT (coalesced
+// loads; the tables must have been zeroed behind a barrier).
 __device__ __forceinline__ void fill_vv_tables(const Ctx& ca, const Ctx& cb, u64* tab_a, u64* tab_b) {
-  for (u64 i = threadIdx.x; i < ca.n; i += blockDim.x)
-    if (ca.node[i] < (u32)VT) tab_a[ca.node[i]] = ca.cnt[i];
-  for (u64 i = threadIdx.x; i < cb.n; i += blockDim.x)
-    if (cb.node[i] < (u32)VT) tab_b[cb.node[i]] = cb.cnt[i];
+  for (u64 i = threadIdx.x; i < ca.n; i += JB) {
+    const u32 nd = ca.node[i];
+    if (nd < (u32)VT) tab_a[nd] = ca.cnt[i];
+  }
+  for (u64 i = threadIdx.x; i < cb.n; i += JB) {
+    const u32 nd = cb.node[i];
+    if (nd < (u32)VT) tab_b[nd] = cb.cnt[i];
+  }
 }
 
 // ------------------------------------------------------------------- staging
-// One staged tile: its rows (+ one neighbour on each side of each store).
+// One staged tile: its rows (+ one neighbour on each side of each store), as 16-byte
+// {key, val} and {ts, cnt} pairs plus the node column: a whole row is 3 LDS accesses
+// (2 x ds_read_b128 + ds_read_b32) instead of 5, and the key-only search reads the
+// low half of kv.
 struct Buf {
-  u64 key[JS];
-  u64 val[JS];
-  u64 cnt[JS];
-  i64 ts[JS];
+  alignas(16) u64 kv[JS][2];
+  alignas(16) u64 tc[JS][2];
   u32 node[JS];
 };
+
+__device__ __forceinline__ u64 buf_key(const Buf& s, int x) { return s.kv[x][0]; }
+
+__device__ __forceinline__ void buf_put(Buf& s, int x, u64 key, u64 val, i64 ts, u32 node, u64 cnt) {
+  typedef u64 v2u64 __attribute__((ext_vector_type(2)));
+  *(v2u64*)s.kv[x] = v2u64{key, val};
+  *(v2u64*)s.tc[x] = v2u64{(u64)ts, cnt};
+  s.node[x] = node;
+}
 
 // Global row index of staging slot x, or -1 if the slot is outside the stores:
 // slot x < nat + 2 is a[a0 - 1 + x], slot x >= nat + 2 is b[b0 - 1 + (x - nat - 2)].
@@ -409,56 +406,28 @@ __device__ __forceinline__ i64 slot_row(int x, int nat, u64 a0, u64 b0, u64 na, 
 
 constexpr int SLOTS = (JS + JB - 1) / JB;
 
-// Stage the tile's rows in LDS.  Every lane issues the loads of all its slots before
-// the first LDS write, so the whole tile is in flight at once (one HBM round trip).
-__device__ __forceinline__ void stage_tile(const Rows& A, const Rows& B, int nat, int nbt, u64 a0,
-                                           u64 b0, Buf& s) {
-  const int tid = threadIdx.x;
-  u64 rk[SLOTS], rv[SLOTS], rc[SLOTS];
-  i64 rt[SLOTS];
-  u32 rn[SLOTS];
-  bool ok[SLOTS];
-#pragma unroll
-  for (int k = 0; k < SLOTS; k++) {
-    const int x = tid + k * JB;
-    bool fb = false;
-    const i64 g = x < nat + nbt + 4 ? slot_row(x, nat, a0, b0, A.n, B.n, &fb) : -1;
-    ok[k] = g >= 0;
-    if (ok[k]) {
-      const Row x = load_row_sel(A, B, fb, (u64)g);
-      rk[k] = x.key;
-      rv[k] = x.val;
-      rt[k] = x.ts;
-      rn[k] = x.node;
-      rc[k] = x.cnt;
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < SLOTS; k++) {
-    const int x = tid + k * JB;
-    if (ok[k]) {
-      s.key[x] = rk[k];
-      s.val[x] = rv[k];
-      s.ts[x] = rt[k];
-      s.node[x] = rn[k];
-      s.cnt[x] = rc[k];
-    }
-  }
-}
-
 __device__ __forceinline__ Row lds_row(const Buf& s, int x) {
+  typedef u64 v2u64 __attribute__((ext_vector_type(2)));
+  const v2u64 kv = *(const v2u64*)s.kv[x];
+  const v2u64 tc = *(const v2u64*)s.tc[x];
   Row r;
-  r.key = s.key[x];
-  r.val = s.val[x];
-  r.ts = s.ts[x];
+  r.key = kv.x;
+  r.val = kv.y;
+  r.ts = (i64)tc.x;
+  r.cnt = tc.y;
   r.node = s.node[x];
-  r.cnt = s.cnt[x];
   return r;
 }
 
+// Highest power of two <= JT: the first step of the binary-lifting search.
+constexpr int search_top(int n) { return n <= 1 ? 1 : 2 * search_top(n / 2); }
+constexpr int STOP = search_top(JT);
+
 // Merge JI consecutive positions of the tile and decide keep/drop for each (the body
-// of join_dot_sets/4 per row, see the file header).  Rows are read from LDS whole (all
-// five columns in parallel) so every merge step costs one LDS round trip.
+// of join_dot_sets/4 per row, see the file header).  Branch-free where it matters:
+// the key search runs a fixed number of binary-lifting steps and each merge step
+// selects between the a and b candidates instead of branching (divergent branches
+// cost exec-mask SALU work on every path).
 template <bool FAST>
 __device__ __forceinline__ void merge_items(const Ctx& ca, const Ctx& cb, const u64* tab_a,
                                             const u64* tab_b, const u64* keys, const u64 n_keys,
@@ -470,82 +439,85 @@ __device__ __forceinline__ void merge_items(const Ctx& ca, const Ctx& cb, const 
   const int diag = min(tid * JI, tt);
   const int dend = min(diag + JI, tt);
   // Merge-path split of this thread's diagonal: first i with NOT(a[i] <= b[diag-1-i]).
-  // (1) key-only binary search for iq = first i with a[i].key > b[diag-1-i].key (two
-  //     LDS words per probe); the exact split lies in (iq - r, iq] where r counts the
-  //     positions whose keys tie; (2) full-tuple gallop down from iq to find it.
+  // (1) key-only: iq = first i in [lo0, hi0] with a[i].key > b[diag-1-i].key, by binary
+  //     lifting (lo grows while a[m-1].key <= b[diag-m].key); slot of a[x] is 1 + x,
+  //     of b[y] is offB + 1 + y.
   const int lo0 = diag > nbt ? diag - nbt : 0, hi0 = min(diag, nat);
-  int lo = lo0, hi = hi0;
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (s.key[1 + mid] <= s.key[offB + 1 + (diag - 1 - mid)])
-      lo = mid + 1;
-    else
-      hi = mid;
+  int lo = lo0;
+#pragma unroll
+  for (int step = STOP; step >= 1; step >>= 1) {
+    const int m = lo + step;
+    const int mc = min(m, hi0);
+    const bool c = m <= hi0 && buf_key(s, mc) <= buf_key(s, offB + 1 + diag - mc);
+    lo = c ? m : lo;
   }
-  // P(i) = a[i] <= b[diag-1-i] is monotone and P(i) implies key <=, so split <= iq = lo.
-  int hiP = lo, loP = lo0, step = 1;
-  while (hiP > loP) {  // gallop: find a point where P holds
-    const int x = max(hiP - step, loP);
-    if (row_le(lds_row(s, 1 + x), lds_row(s, offB + 1 + (diag - 1 - x)))) {
-      loP = x + 1;
-      break;
-    }
-    hiP = x;
-    step <<= 1;
-  }
-  lo = loP;
-  hi = hiP;
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (row_le(lds_row(s, 1 + mid), lds_row(s, offB + 1 + (diag - 1 - mid))))
-      lo = mid + 1;
-    else
-      hi = mid;
-  }
-  int i = lo, j = diag - lo;
-  // ra = a[i], rb = b[j] (possibly the neighbour past the tile), pa = a[i-1]; xa / xb are
-  // the rows after them, read one step ahead so no merge step waits on LDS.  (Reads past
-  // a side's end land in other slots of the buffer and are never used.)
-  Row ra = lds_row(s, 1 + i), rb = lds_row(s, offB + 1 + j), pa = lds_row(s, i);
+  // (2) P(i) implies key <=, so the split is <= iq; step down while the full tuples of
+  //     a[i-1] and b[diag-i] (equal keys) say a > b.  Runs of tied keys are short.
+  int i = lo;
+  while (i > lo0 && !row_le(lds_row(s, i), lds_row(s, offB + 1 + diag - i))) i--;
+  int j = diag - i;
+  // ra = a[i], rb = b[j] (possibly the neighbour past the tile); xa / xb are the rows
+  // after them, read one step ahead so no merge step waits on LDS.  (Reads past a side's
+  // end land in other slots of the buffer and are never used.)  dup: the current b row
+  // equals the last a row merged before it -- ties go to a, so an a row and its equal b
+  // row are adjacent and the b row is the MapSet duplicate.
+  Row ra = lds_row(s, 1 + i), rb = lds_row(s, offB + 1 + j);
+  bool dup = (a0 + (u64)i) >= 1 && row_eq(lds_row(s, i), rb);
   Row xa = lds_row(s, 2 + i), xb = lds_row(s, offB + 2 + j);
   keep = 0;
 #pragma unroll
   for (int k = 0; k < JI; k++) {
-    src[k] = 0;
-    if (diag + k < dend) {
-      const bool bvalid = (b0 + (u64)j) < nb;  // b[j] exists globally
-      const bool takeA = i < nat && (j >= nbt || row_le(ra, rb));
-      bool kp;
-      if (takeA) {
-        const bool joined = FAST || keys == nullptr || keyset_has(keys, n_keys, ra.key);
-        if (joined) {
-          const bool inB = bvalid && row_eq(ra, rb);
-          kp = inB || !covers<FAST>(tab_b, cb, ra.node, ra.cnt);
-        } else {
-          // Map.merge(Map.drop(a), Map.drop(b)): a's rows survive iff b lacks the key
-          const bool bprev = (b0 + (u64)j) >= 1 && s.key[offB + j] == ra.key;
-          const bool bnext = bvalid && rb.key == ra.key;
-          kp = !(bprev || bnext);
-        }
-        src[k] = (unsigned short)(1 + i);
-        i++;
-        pa = ra;
-        ra = xa;
-        if (k + 1 < JI) xa = lds_row(s, 2 + i);
+    const bool valid = diag + k < dend;
+    const bool bvalid = (b0 + (u64)j) < nb;  // b[j] exists globally
+    const int c = row_cmp(ra, rb);
+    const bool takeA = i < nat && (j >= nbt || c <= 0);
+    const bool inB = bvalid && c == 0;
+    bool kp;
+    if (FAST) {
+      // Dots.member?(c_other, dot of the taken row): one LDS table read
+      const u32 dn = takeA ? ra.node : rb.node;
+      const u64 dc = takeA ? ra.cnt : rb.cnt;
+      // (the other side's VV by field VALUES: a select between the two Ctx structs
+      // would make them addressable and spill them to scratch)
+      bool cov;
+      if (dn < (u32)VT) {
+        cov = (takeA ? tab_b : tab_a)[dn] >= dc;
       } else {
-        const bool joined = FAST || keys == nullptr || keyset_has(keys, n_keys, rb.key);
-        if (joined) {
-          const bool dupA = (a0 + (u64)i) >= 1 && row_eq(pa, rb);
-          kp = !dupA && !covers<FAST>(tab_a, ca, rb.node, rb.cnt);
-        } else {
-          kp = true;
-        }
-        src[k] = (unsigned short)(offB + 1 + j);
-        j++;
-        rb = xb;
-        if (k + 1 < JI) xb = lds_row(s, offB + 2 + j);
+        const u32* vn = takeA ? opaque_ptr(cb.node) : opaque_ptr(ca.node);
+        const u64* vc = takeA ? opaque_ptr(cb.cnt) : opaque_ptr(ca.cnt);
+        const u64 vnn = takeA ? opaque_val(cb.n) : opaque_val(ca.n);
+        cov = ctx_covers(vn, vc, vnn, 0, dn, dc);
       }
-      if (kp) keep |= 1u << k;
+      kp = takeA ? (inB || !cov) : (!dup && !cov);
+    } else if (takeA) {
+      if (keys == nullptr || keyset_has(keys, n_keys, ra.key)) {
+        kp = inB || !covers<FAST>(tab_b, cb, ra.node, ra.cnt);
+      } else {
+        // Map.merge(Map.drop(a), Map.drop(b)): a's rows survive iff b lacks the key
+        const bool bprev = (b0 + (u64)j) >= 1 && buf_key(s, offB + j) == ra.key;
+        const bool bnext = bvalid && rb.key == ra.key;
+        kp = !(bprev || bnext);
+      }
+    } else {
+      if (keys == nullptr || keyset_has(keys, n_keys, rb.key))
+        kp = !dup && !covers<FAST>(tab_a, ca, rb.node, rb.cnt);
+      else
+        kp = true;
+    }
+    src[k] = valid ? (unsigned short)(takeA ? 1 + i : offB + 1 + j) : (unsigned short)0;
+    if (valid && kp) keep |= 1u << k;
+    // advance the taken side; the next row after it is read one step ahead
+    // (b rows are unique and larger than every a row merged so far, so a taken b row
+    // clears dup; a taken a row passes its inB on to the b row it tied with)
+    dup = takeA ? inB : false;
+    i += takeA ? 1 : 0;
+    j += takeA ? 0 : 1;
+    ra = row_sel(takeA, xa, ra);
+    rb = row_sel(takeA, rb, xb);
+    if (k + 1 < JI) {
+      const Row nx = lds_row(s, takeA ? 2 + i : offB + 2 + j);
+      xa = row_sel(takeA, nx, xa);
+      xb = row_sel(takeA, xb, nx);
     }
   }
 }
@@ -564,95 +536,9 @@ struct TileLds {
   u64 bcast[4];
 };
 
-// Common front half of a tile: stage, merge, block scan -> compaction list in LDS.
-// Returns the tile's kept-row count.
-template <bool FAST>
-__device__ __forceinline__ u32 tile_merge(const JoinArgs& p, TileLds& s, u64 t, u64 a0, u64 a1) {
-  const int tid = threadIdx.x;
-  const u64 na = p.a.n, nb = p.b.n, total = na + nb;
-  const u64 d0 = t * JT, d1 = min(d0 + (u64)JT, total);
-  const int nat = (int)(a1 - a0), nbt = (int)((d1 - a1) - (d0 - a0));
-  const u64 b0 = d0 - a0;
-  if (FAST) fill_vv_tables(p.ca, p.cb, s.u.tab[0], s.u.tab[1]);
-  JSTAMP(t, 1);
-  stage_tile(p.a, p.b, nat, nbt, a0, b0, s.buf);
-  __syncthreads();
-  JSTAMP(t, 2);
-  u32 keep;
-  unsigned short src[JI];
-  merge_items<FAST>(p.ca, p.cb, s.u.tab[0], s.u.tab[1], p.keys, p.n_keys, nb, s.buf, nat, nbt, a0,
-                    b0, keep, src);
-  JSTAMP(t, 3);
-  u32 tile_total;
-  u32 pos = block_excl_scan<JB>(__popc(keep), s.wave, &tile_total);  // barriers: tables dead
-#pragma unroll
-  for (int q = 0; q < JI; q++)
-    if (keep & (1u << q)) s.u.comp[pos++] = src[q];
-  __syncthreads();
-  JSTAMP(t, 4);
-  return tile_total;
-}
-
-// Single-pass join: one workgroup per tile (see the file header).
-template <bool FAST>
-__global__ __launch_bounds__(JB) void join2_main_kernel(JoinArgs p) {
-  __shared__ TileLds s;
-  const int tid = threadIdx.x;
-  const u64 ntiles = p.ntiles;
-  if (FAST)
-    for (int x = tid; x < 2 * VT; x += JB) (&s.u.tab[0][0])[x] = 0;
-  if (tid == 0) {
-    // The ticket numbers tiles in dispatch order; the splits of tile blockIdx.x are
-    // loaded speculatively beside it (the ticket almost always equals blockIdx.x).
-    const u64 tk = atomicAdd(p.scan.ticket, 1u);
-    const u64 g = blockIdx.x;
-    u64 s0 = p.splits[g], s1 = p.splits[g + 1];
-    if (tk == ntiles - 1) atomicExch(p.scan.ticket, 0u);
-    if (tk != g) {
-      s0 = p.splits[tk];
-      s1 = p.splits[tk + 1];
-    }
-    s.bcast[0] = tk;
-    s.bcast[1] = s0;
-    s.bcast[2] = s1;
-  }
-  __syncthreads();
-  const u64 t = s.bcast[0], a0 = s.bcast[1], a1 = s.bcast[2];
-  JSTAMP(t, 0);
-  const u32 n = tile_merge<FAST>(p, s, t, a0, a1);
-  u64 prefix = 0;
-  if (t == 0) {
-    if (tid == 0) lb_publish(p.scan.state, 0, p.scan.epoch, LB_INC, n);
-  } else {
-    if (tid == 0) lb_publish(p.scan.state, t, p.scan.epoch, LB_AGG, n);
-    prefix = lb_lookback_block<JB, 2>(p.scan.state, t, p.scan.epoch, p.scan.err, s.lb);
-    if (tid == 0) lb_publish(p.scan.state, t, p.scan.epoch, LB_INC, prefix + n);
-  }
-  if (tid == 0 && t == ntiles - 1) p.d_count[0] = prefix + n;
-  JSTAMP(t, 5);
-  const Buf& b = s.buf;
-  for (u32 q = tid; q < n; q += JB) {
-    const int slot = s.u.comp[q];
-    const u64 o = prefix + q;
-    p.out.key[o] = b.key[slot];
-    p.out.val[o] = b.val[slot];
-    p.out.ts[o] = b.ts[slot];
-    p.out.node[o] = b.node[slot];
-    p.out.cnt[o] = b.cnt[slot];
-  }
-  JSTAMP(t, 6);
-}
-
-// ---------------------------------------------------------------- two-pass join
-// Pass 1 (join2_slot_kernel): persistent workgroups, each merging tiles blockIdx.x,
-// blockIdx.x + gridDim.x, ...  While tile t is merged from LDS, the rows of the next
-// tile are already in flight into registers (issued right after t was committed to
-// LDS), so HBM streams through the merge instead of stalling each tile on its own
-// loads.  The VV tables are loaded once per workgroup and kept in registers.  Output
-// per tile: its kept-row count and its compaction list (LDS slot numbers, u16).
-// Pass 2 (join2_compact_kernel): each workgroup sums the counts before its tile and
-// gathers the kept rows from a/b into the output.  No inter-workgroup dependency in
-// either pass.
+// Register staging of a tile: every lane issues the loads of all its slots (issue_tile)
+// long before it writes them to LDS (commit_tile), so a whole tile streams in while the
+// previous one is merged.
 struct Staged {  // one thread's share of a staged tile, in registers
   u64 k[SLOTS], v[SLOTS], c[SLOTS];
   i64 t[SLOTS];
@@ -693,88 +579,257 @@ __device__ __forceinline__ void commit_tile(const Staged& r, Buf& s) {
 #pragma unroll
   for (int k = 0; k < SLOTS; k++) {
     const int x = tid + k * JB;
-    if (r.ok[k]) {
-      s.key[x] = r.k[k];
-      s.val[x] = r.v[k];
-      s.ts[x] = r.t[k];
-      s.node[x] = r.n[k];
-      s.cnt[x] = r.c[k];
+    if (r.ok[k]) buf_put(s, x, r.k[k], r.v[k], r.t[k], r.n[k], r.c[k]);
+  }
+}
+
+// ------------------------------------------------------------- single-pass join
+// join2_stream_kernel: persistent workgroups (the whole grid is co-resident: it is
+// sized from the occupancy query); workgroup w merges tiles w, w + G, w + 2G, ...
+// so iteration k of every workgroup together covers the stripe of tiles [kG, (k+1)G).
+// Two LDS tile buffers alternate.  Iteration k of workgroup w (tile t = w + kG):
+//   1. commit tile t's rows (prefetched into registers) to buffer k%2;
+//   2. issue the loads of tile t + G into registers, and the loads of stripe k-1's
+//      G tile counts (they stream during the merge);
+//   3. merge tile t, block-scan its keep bits: count n_t and compaction list;
+//      publish n_t (an epoch-tagged 32-bit granule, written once);
+//   4. offsets of stripe k-1, computed redundantly by every workgroup from its G
+//      counts: tile (w + (k-1)G) starts at base_{k-1} + Σ_{w' < w} n, and
+//      base_k = base_{k-1} + Σ_{all w'} n;
+//   5. write tile t - G's kept rows (still in buffer (k-1)%2), coalesced, at that
+//      offset.
+// No look-back chain and no ticket: a stripe's counts were all published one merge
+// earlier, so step 4 rarely waits; its cost is one G-word read per iteration, issued
+// before the merge.  Spins stay bounded (scan.err bit 0 on timeout).
+struct StreamLds {
+  Buf buf[2];
+  unsigned short comp[2][JT];
+  u64 tab[2][VT];
+  u32 wave[JB / WAVE + 1];
+  u64 red[2 * (JB / WAVE)];
+};
+
+constexpr u32 CNT_BITS = 12;  // count field of a tile-count granule (JT < 4096)
+static_assert(JT < (1 << CNT_BITS), "tile count must fit the granule's count field");
+constexpr int CQ = (1024 + JB - 1) / JB;  // stripe counts per thread (grid <= CQ * JB)
+
+__device__ __forceinline__ void publish_count(u32* cs, u64 t, u32 epoch, u32 n) {
+  __hip_atomic_store(cs + t, (epoch << CNT_BITS) | n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Stripe counts of tiles [base_t, base_t + G) ∩ [0, ntiles), CQ per thread: issued
+// early (stripe_load), consumed after the merge (stripe_sums), which re-polls the ones
+// not yet published and returns (Σ over workgroups w' < w, Σ over all).
+struct StripeCounts {
+  u32 v[CQ];
+  bool ready;
+};
+
+__device__ __forceinline__ void stripe_load(const u32* cs, u64 base_t, u64 G, u64 ntiles, u32 epoch,
+                                            StripeCounts& c) {
+  c.ready = true;
+#pragma unroll
+  for (int q = 0; q < CQ; q++) {
+    const u64 x = (u64)threadIdx.x + (u64)q * JB;  // workgroup index within the stripe
+    c.v[q] = epoch << CNT_BITS;                     // absent tiles count 0
+    if (x < G && base_t + x < ntiles)
+      c.v[q] = __hip_atomic_load(cs + base_t + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__device__ __forceinline__ void stripe_sums(const u32* cs, u64 base_t, u64 G, u64 ntiles, u32 epoch,
+                                            u64 w, u32* err, StripeCounts& c, u64* s_red,
+                                            u64* below, u64* all) {
+  const int tid = threadIdx.x;
+  for (u32 spins = 0;; spins++) {  // (rare) wait for counts not yet published
+    bool ready = true;
+#pragma unroll
+    for (int q = 0; q < CQ; q++) ready &= (c.v[q] >> CNT_BITS) == epoch;
+    if (ready) break;
+    if (spins > (1u << 22)) {
+      atomicOr(err, 1u);
+      break;
     }
+    __builtin_amdgcn_s_sleep(2);
+#pragma unroll
+    for (int q = 0; q < CQ; q++) {
+      const u64 x = (u64)tid + (u64)q * JB;
+      if ((c.v[q] >> CNT_BITS) != epoch)
+        c.v[q] = __hip_atomic_load(cs + base_t + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  u64 lo = 0, tot = 0;
+#pragma unroll
+  for (int q = 0; q < CQ; q++) {
+    const u64 x = (u64)tid + (u64)q * JB;
+    const u64 n = c.v[q] & ((1u << CNT_BITS) - 1);
+    tot += n;
+    lo += x < w ? n : 0;
+  }
+#pragma unroll
+  for (int d = WAVE / 2; d >= 1; d >>= 1) {
+    lo += __shfl_xor(lo, d, WAVE);
+    tot += __shfl_xor(tot, d, WAVE);
+  }
+  constexpr int NW = JB / WAVE;
+  if ((tid & (WAVE - 1)) == 0) {
+    s_red[tid / WAVE] = lo;
+    s_red[NW + tid / WAVE] = tot;
+  }
+  __syncthreads();
+  lo = 0;
+  tot = 0;
+#pragma unroll
+  for (int i = 0; i < NW; i++) {
+    lo += s_red[i];
+    tot += s_red[NW + i];
+  }
+  *below = lo;
+  *all = tot;
+}
+
+__device__ __forceinline__ void write_tile(const JoinArgs& p, const StreamLds& s, int bi, u64 o0,
+                                           u32 n) {
+  const Buf& b = s.buf[bi];
+  for (u32 q = threadIdx.x; q < n; q += JB) {
+    const Row x = lds_row(b, s.comp[bi][q]);
+    const u64 o = o0 + q;
+    p.out.key[o] = x.key;
+    p.out.val[o] = x.val;
+    p.out.ts[o] = x.ts;
+    p.out.node[o] = x.node;
+    p.out.cnt[o] = x.cnt;
   }
 }
 
 template <bool FAST>
-__global__ __launch_bounds__(JB) void join2_slot_kernel(JoinArgs p) {
-  __shared__ TileLds s;
+__global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void join2_stream_kernel(JoinArgs p) {
+  __shared__ StreamLds s;
   const int tid = threadIdx.x;
-  const u64 total = p.a.n + p.b.n, ntiles = p.ntiles, G = gridDim.x;
-  // this thread's VV-table entries x = tid + q*JB < 2*VT: Map.get(vv, x % VT, 0)
-  constexpr int TQ = (2 * VT + JB - 1) / JB;
-  u64 tab_entry[TQ];
-#pragma unroll
-  for (int q = 0; q < TQ; q++) {
-    const int x = tid + q * JB;
-    tab_entry[q] = 0;
-    if (FAST) {
-      if (x < VT)
-        tab_entry[q] = vv_get(p.ca.node, p.ca.cnt, p.ca.n, (u32)x);
-      else if (x < 2 * VT)
-        tab_entry[q] = vv_get(p.cb.node, p.cb.cnt, p.cb.n, (u32)(x - VT));
-    }
-  }
+  const u64 total = p.a.n + p.b.n, ntiles = p.ntiles, G = gridDim.x, w = blockIdx.x;
+  u32* cs = p.scan.counts;  // tile-count granules
+  const u32 epoch = p.scan.epoch;
   const Rows& A = p.a;
   const Rows& B = p.b;
-  u64 t = blockIdx.x;
+  if (FAST)
+    for (int x = tid; x < 2 * VT; x += JB) (&s.tab[0][0])[x] = 0;
+  u64 t = w;
   u64 a0 = p.splits[t], a1 = p.splits[t + 1];
   int nat, nbt;
   u64 b0;
   tile_geom(t, a0, a1, total, &nat, &nbt, &b0);
   Staged r;
   issue_tile(A, B, nat, nbt, a0, b0, r);
-  while (true) {
+  __syncthreads();  // zeroed tables visible
+  if (FAST) fill_vv_tables(p.ca, p.cb, s.tab[0], s.tab[1]);  // once per workgroup
+  u64 base = 0;  // output offset of the first tile of the current stripe
+  u32 np = 0;    // kept rows of this workgroup's tile of the previous stripe
+  for (int k = 0;; k++) {
+    const int bi = k & 1;
     JSTAMP(t, 0);
     JSTAMP(t, 1);
-    commit_tile(r, s.buf);
-#pragma unroll
-    for (int q = 0; q < TQ; q++)
-      if (FAST && tid + q * JB < 2 * VT) (&s.u.tab[0][0])[tid + q * JB] = tab_entry[q];
+    commit_tile(r, s.buf[bi]);
     __syncthreads();
     JSTAMP(t, 2);
-    // prefetch the next tile while this one is merged
-    const u64 tn = JOIN_PIPE ? t + G : ntiles;
+    const u64 tn = t + G;
     u64 a0n = 0, a1n = 0, b0n = 0;
     int natn = 0, nbtn = 0;
-    if (JOIN_PIPE && tn < ntiles) {
+    if (tn < ntiles) {
       a0n = p.splits[tn];
       a1n = p.splits[tn + 1];
       tile_geom(tn, a0n, a1n, total, &natn, &nbtn, &b0n);
       issue_tile(A, B, natn, nbtn, a0n, b0n, r);
     }
+    StripeCounts sc;  // stripe k-1's counts, in flight during the merge
+    if (k > 0) stripe_load(cs, t - G - w, G, ntiles, epoch, sc);
     u32 keep;
     unsigned short src[JI];
-    merge_items<FAST>(p.ca, p.cb, s.u.tab[0], s.u.tab[1], p.keys, p.n_keys, p.b.n, s.buf, nat,
-                      nbt, a0, b0, keep, src);
+    merge_items<FAST>(p.ca, p.cb, s.tab[0], s.tab[1], p.keys, p.n_keys, B.n, s.buf[bi], nat, nbt,
+                      a0, b0, keep, src);
     JSTAMP(t, 3);
     u32 n;
-    u32 pos = block_excl_scan<JB>(__popc(keep), s.wave, &n);  // barriers: tables dead
+    u32 pos = block_excl_scan<JB>(__popc(keep), s.wave, &n);
 #pragma unroll
     for (int q = 0; q < JI; q++)
-      if (keep & (1u << q)) s.u.comp[pos++] = src[q];
+      if (keep & (1u << q)) s.comp[bi][pos++] = src[q];
+    if (tid == 0) publish_count(cs, t, epoch, n);
     __syncthreads();
     JSTAMP(t, 4);
+    if (k > 0) {  // stripe k-1: this workgroup's tile t - G
+      u64 below, all;
+      stripe_sums(cs, t - G - w, G, ntiles, epoch, w, p.scan.err, sc, s.red, &below, &all);
+      write_tile(p, s, bi ^ 1, base + below, np);
+      base += all;
+    }
     JSTAMP(t, 5);
-    if (tid == 0) p.counts[t] = n;
-    for (u32 q = tid; q < n; q += JB) p.lists[t * JT + q] = s.u.comp[q];
     JSTAMP(t, 6);
-    if (tn >= ntiles) break;
-    __syncthreads();  // LDS tile and list free for the next commit
+    np = n;
+    if (tn >= ntiles) {
+      u64 below, all;
+      StripeCounts last;
+      stripe_load(cs, t - w, G, ntiles, epoch, last);
+      stripe_sums(cs, t - w, G, ntiles, epoch, w, p.scan.err, last, s.red, &below, &all);
+      write_tile(p, s, bi, base + below, np);
+      if (tid == 0 && t == ntiles - 1) p.d_count[0] = base + below + np;
+      break;
+    }
     t = tn;
     a0 = a0n;
     a1 = a1n;
     nat = natn;
     nbt = nbtn;
     b0 = b0n;
+    __syncthreads();  // buffer bi^1 written out: free for the next commit
   }
+}
+
+// ---------------------------------------------------------------- two-pass join
+// Pass 1 (join2_slot_kernel): persistent workgroups, each merging tiles blockIdx.x,
+// blockIdx.x + gridDim.x, ...  While tile t is merged from LDS, the rows of the next
+// tile are already in flight into registers (issued right after t was committed to
+// LDS), so HBM streams through the merge instead of stalling each tile on its own
+// loads.  The VV tables are loaded once per workgroup and kept in registers.  Output
+// per tile: its kept-row count and its compaction list (LDS slot numbers, u16).
+// Pass 2 (join2_compact_kernel): each workgroup sums the counts before its tile and
+// gathers the kept rows from a/b into the output.  No inter-workgroup dependency in
+// either pass.
+template <bool FAST>
+__global__ __launch_bounds__(JB) void join2_slot_kernel(JoinArgs p) {
+  __shared__ TileLds s;
+  const int tid = threadIdx.x;
+  const u64 total = p.a.n + p.b.n;
+  if (FAST)
+    for (int x = tid; x < 2 * VT; x += JB) (&s.u.tab[0][0])[x] = 0;
+  const u64 t = blockIdx.x;
+  const u64 a0 = p.splits[t], a1 = p.splits[t + 1];
+  int nat, nbt;
+  u64 b0;
+  tile_geom(t, a0, a1, total, &nat, &nbt, &b0);
+  Staged r;
+  issue_tile(p.a, p.b, nat, nbt, a0, b0, r);
+  __syncthreads();  // zeroed tables visible
+  if (FAST) fill_vv_tables(p.ca, p.cb, s.u.tab[0], s.u.tab[1]);
+  JSTAMP(t, 0);
+  JSTAMP(t, 1);
+  commit_tile(r, s.buf);
+  __syncthreads();
+  JSTAMP(t, 2);
+  u32 keep;
+  unsigned short src[JI];
+  merge_items<FAST>(p.ca, p.cb, s.u.tab[0], s.u.tab[1], p.keys, p.n_keys, p.b.n, s.buf, nat, nbt,
+                    a0, b0, keep, src);
+  JSTAMP(t, 3);
+  u32 n;
+  u32 pos = block_excl_scan<JB>(__popc(keep), s.wave, &n);  // barriers: tables dead
+#pragma unroll
+  for (int q = 0; q < JI; q++)
+    if (keep & (1u << q)) s.u.comp[pos++] = src[q];
+  __syncthreads();
+  JSTAMP(t, 4);
+  JSTAMP(t, 5);
+  if (tid == 0) p.counts[t] = n;
+  for (u32 q = tid; q < n; q += JB) p.lists[t * JT + q] = s.u.comp[q];
+  JSTAMP(t, 6);
 }
 
 constexpr int CPB = 256;
@@ -810,11 +865,11 @@ __global__ __launch_bounds__(CPB) void join2_compact_kernel(Rows a, Rows b, cons
     if (tile == ntiles - 1) d_count[0] = acc + counts[tile];
   }
   __syncthreads();
+  const u64 base = s_pre, n = counts[tile];
   const u64 a0 = splits[tile], a1 = splits[tile + 1];
   const u64 d0 = tile * JT;
   const int nat = (int)(a1 - a0);
   const u64 b0 = d0 - a0;
-  const u64 base = s_pre, n = counts[tile];
   for (u64 q = threadIdx.x; q < n; q += CPB) {
     const int x = lists[tile * JT + q];
     const bool fb = x >= nat + 2;
@@ -829,6 +884,18 @@ __global__ __launch_bounds__(CPB) void join2_compact_kernel(Rows a, Rows b, cons
 }
 
 }  // namespace
+
+// Workgroups of kernel `k` (JB threads) resident at once on the current device: the
+// grid of a persistent kernel whose workgroups wait on each other.
+static u64 resident_grid(const void* k) {
+  int per_cu = 0, dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, JB, 0) != hipSuccess || per_cu <= 0 ||
+      cus <= 0)
+    return 256;
+  return (u64)per_cu * (u64)cus;
+}
 
 static CtxUnionArgs make_cu(const Ctx& a, const Ctx& b, u32* out_node, u64* out_cnt,
                             u64* d_count, void* tmp) {
@@ -884,29 +951,17 @@ hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& 
     p.counts = (u32*)t;
     t += ((p.ntiles * 4 + 255) / 256) * 256;
     p.lists = (unsigned short*)t;
-    // persistent pass 1: as many workgroups as are resident at once (registers and
-    // LDS per tile decide it), unless the caller fixed the count (workers > 0)
     auto kern = fast ? join2_slot_kernel<true> : join2_slot_kernel<false>;
-    u64 g = workers > 0 ? (u64)workers : (JOIN_PIPE ? 0 : p.ntiles);
-    if (!g) {
-      int per_cu = 0, dev = 0, cus = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, JB, 0) != hipSuccess ||
-          per_cu <= 0 || cus <= 0)
-        per_cu = 1, cus = 256;
-      g = (u64)per_cu * (u64)cus;
-    }
-    g = std::min<u64>(p.ntiles, g);
-    hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(JB), 0, st, p);
+    hipLaunchKernelGGL(kern, dim3((unsigned)p.ntiles), dim3(JB), 0, st, p);
     hipLaunchKernelGGL(join2_compact_kernel, dim3((unsigned)p.ntiles), dim3(CPB), 0, st, a, b,
                        p.splits, p.lists, p.counts, p.ntiles, out, d_counts);
     return hipGetLastError();
   }
-  if (fast)
-    hipLaunchKernelGGL(join2_main_kernel<true>, dim3((unsigned)p.ntiles), dim3(JB), 0, st, p);
-  else
-    hipLaunchKernelGGL(join2_main_kernel<false>, dim3((unsigned)p.ntiles), dim3(JB), 0, st, p);
+  auto kern = fast ? join2_stream_kernel<true> : join2_stream_kernel<false>;
+  u64 g = workers > 0 ? (u64)workers : 0;
+  if (!g) g = resident_grid((const void*)kern);
+  g = std::min<u64>(std::min<u64>(p.ntiles, g), (u64)CQ * JB);  // stripe counts: CQ per thread
+  hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(JB), 0, st, p);
   return hipGetLastError();
 }
 

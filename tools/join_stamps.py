@@ -37,11 +37,12 @@ def main():
     octx = Context.empty(0, 8, dev)
     for _ in range(5):
         eng.join2(sa, ca, sb, cb, out=out, out_ctx=octx)
-    ntiles = (sa.n + sb.n + 1023) // 1024
     buf = np.zeros(65536 * 8, np.uint64)
     lib.dg_debug_join_stamps.argtypes = [C.c_void_p, C.c_size_t]
     assert lib.dg_debug_join_stamps(buf.ctypes.data, len(buf)) == 0
-    st = buf[: ntiles * 8].reshape(ntiles, 8).astype(np.int64)
+    st = buf.reshape(65536, 8).astype(np.int64)
+    ntiles = int(np.nonzero(st[:, 0])[0].max()) + 1  # tiles of the last launch stamp slot 0
+    st = st[:ntiles]
     t0 = st[:, 0].min()
     order = [0, 1, 2, 3, 4, 5, 6]
     names = ["tables", "stage", "merge", "scan", "lookback", "write"]

@@ -15,7 +15,9 @@ for f in sorted(glob.glob("gpurun_out/pmc/pass*_counter_collection.csv")):
         k = r["Kernel_Name"]
         if "join2" not in k:
             continue
-        name = k.split("(")[0].split("::")[-1][:40]
+        import re
+        m = re.search(r"(join2_\w+)", k)
+        name = m.group(1) if m else k[:40]
         agg[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in agg.items():
     print(k)
