@@ -638,13 +638,17 @@ __device__ __forceinline__ void stripe_load(const u32* cs, u64 base_t, u64 G, u6
 }
 
 __device__ __forceinline__ void stripe_sums(const u32* cs, u64 base_t, u64 G, u64 ntiles, u32 epoch,
-                                            u64 w, u32* err, StripeCounts& c, u64* s_red,
-                                            u64* below, u64* all) {
+                                            u64 w, bool need_all, u32* err, StripeCounts& c,
+                                            u64* s_red, u64* below, u64* all) {
   const int tid = threadIdx.x;
+  // counts this workgroup needs: all of the stripe's (for the next stripe's base), or
+  // only those of the workgroups below it (its last tile: no next stripe)
+  const u64 need = need_all ? G : w;
   for (u32 spins = 0;; spins++) {  // (rare) wait for counts not yet published
     bool ready = true;
 #pragma unroll
-    for (int q = 0; q < CQ; q++) ready &= (c.v[q] >> CNT_BITS) == epoch;
+    for (int q = 0; q < CQ; q++)
+      ready &= (u64)tid + (u64)q * JB >= need || (c.v[q] >> CNT_BITS) == epoch;
     if (ready) break;
     if (spins > (1u << 22)) {
       atomicOr(err, 1u);
@@ -654,7 +658,7 @@ __device__ __forceinline__ void stripe_sums(const u32* cs, u64 base_t, u64 G, u6
 #pragma unroll
     for (int q = 0; q < CQ; q++) {
       const u64 x = (u64)tid + (u64)q * JB;
-      if ((c.v[q] >> CNT_BITS) != epoch)
+      if (x < need && (c.v[q] >> CNT_BITS) != epoch)
         c.v[q] = __hip_atomic_load(cs + base_t + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -757,7 +761,7 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     JSTAMP(t, 4);
     if (k > 0) {  // stripe k-1: this workgroup's tile t - G
       u64 below, all;
-      stripe_sums(cs, t - G - w, G, ntiles, epoch, w, p.scan.err, sc, s.red, &below, &all);
+      stripe_sums(cs, t - G - w, G, ntiles, epoch, w, true, p.scan.err, sc, s.red, &below, &all);
       write_tile(p, s, bi ^ 1, base + below, np);
       base += all;
     }
@@ -768,7 +772,7 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       u64 below, all;
       StripeCounts last;
       stripe_load(cs, t - w, G, ntiles, epoch, last);
-      stripe_sums(cs, t - w, G, ntiles, epoch, w, p.scan.err, last, s.red, &below, &all);
+      stripe_sums(cs, t - w, G, ntiles, epoch, w, false, p.scan.err, last, s.red, &below, &all);
       write_tile(p, s, bi, base + below, np);
       if (tid == 0 && t == ntiles - 1) p.d_count[0] = base + below + np;
       break;
