@@ -96,6 +96,10 @@ _SIGS = {
                                  C.POINTER(dg_store), C.POINTER(dg_context), P64]),
     "dg_joink": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(dg_store), C.POINTER(dg_context),
                            C.POINTER(dg_store), C.POINTER(dg_context)]),
+    "dg_apply_deltas": (C.c_int, [C.c_void_p, C.POINTER(dg_store), C.POINTER(dg_context), C.c_int,
+                                  C.POINTER(dg_store), C.POINTER(dg_context),
+                                  C.POINTER(C.c_void_p), P64, C.POINTER(dg_store),
+                                  C.POINTER(dg_context)]),
     "dg_context_union": (C.c_int, [C.c_void_p, C.POINTER(dg_context), C.POINTER(dg_context),
                                    C.POINTER(dg_context)]),
     "dg_compress_dots": (C.c_int, [C.c_void_p, C.POINTER(dg_context), C.POINTER(dg_context)]),

@@ -26,6 +26,9 @@ struct dg_engine {
   u32* ticket = nullptr;  // [0] ticket, [1] error bits, [2] store_check flag
   u32* counts = nullptr;  // single-pass join tile-count granules
   u64 counts_cap = 0;
+  // ping-pong intermediate states of dg_joink / dg_apply_deltas
+  void* fold = nullptr;
+  size_t fold_cap = 0;
   u32 epoch = 0;
   // small device counters + pinned host mirror
   u64* d_counts = nullptr;  // 8 entries
@@ -72,9 +75,13 @@ int ensure_state(dg_engine* e, u64 tiles) {
   u64 cap = std::max<u64>(tiles, 1024);
   if (hipMalloc(&e->state, cap * sizeof(u64)) != hipSuccess)
     return fail(DG_E_NOMEM, "hipMalloc of %llu look-back granules failed", cap);
-  HIP_TRY(hipMemset(e->state, 0, cap * sizeof(u64)));
+  // zeroed ON the engine stream: a plain hipMemset runs on the null stream, which is not
+  // ordered with a non-blocking engine stream, and could land after the next kernel
+  // has already written this array
+  HIP_TRY(hipMemsetAsync(e->state, 0, cap * sizeof(u64), e->stream));
   e->state_cap = cap;
-  e->epoch = 0;
+  // the epoch stays monotonic: the tile-count granules (e->counts) outlive this array,
+  // and a restarted epoch would make their stale values read as current
   return DG_OK;
 }
 
@@ -98,7 +105,7 @@ int ensure_counts(dg_engine* e, u64 tiles) {
   u64 cap = std::max<u64>(tiles, 4096);
   if (hipMalloc(&e->counts, cap * sizeof(u32)) != hipSuccess)
     return fail(DG_E_NOMEM, "hipMalloc of %llu tile-count granules failed", cap);
-  HIP_TRY(hipMemset(e->counts, 0, cap * sizeof(u32)));  // epoch 0 is never current
+  HIP_TRY(hipMemsetAsync(e->counts, 0, cap * sizeof(u32), e->stream));  // epoch 0: never current
   e->counts_cap = cap;
   return DG_OK;
 }
@@ -127,7 +134,8 @@ int read_counts(dg_engine* e, int n) {
   HIP_TRY(hipStreamSynchronize(e->stream));
   memcpy(&err, &e->h_counts[7], sizeof(u32));
   if (err) {
-    HIP_TRY(hipMemset(e->ticket, 0, 4 * sizeof(u32)));
+    HIP_TRY(hipMemsetAsync(e->ticket, 0, 4 * sizeof(u32), e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
     return fail(DG_E_DEVICE, "look-back timeout inside a kernel (error bits 0x%x)", err);
   }
   return DG_OK;
@@ -260,8 +268,11 @@ int dg_engine_create(int device, void* hip_stream, dg_engine** out) {
     dg_engine_destroy(e);
     return fail(DG_E_NOMEM, "dg_engine_create: allocation failed");
   }
-  hipMemset(e->ticket, 0, 16 * sizeof(u32));
-  hipMemset(e->d_counts, 0, 8 * sizeof(u64));
+  if (hipMemsetAsync(e->ticket, 0, 16 * sizeof(u32), e->stream) != hipSuccess ||
+      hipMemsetAsync(e->d_counts, 0, 8 * sizeof(u64), e->stream) != hipSuccess) {
+    dg_engine_destroy(e);
+    return fail(DG_E_DEVICE, "dg_engine_create: hipMemsetAsync failed");
+  }
   rc = ensure_state(e, 4096);
   if (rc != DG_OK) {
     dg_engine_destroy(e);
@@ -281,6 +292,7 @@ int dg_engine_destroy(dg_engine* e) {
   if (e->h_counts) hipHostFree(e->h_counts);
   if (e->tmp) hipFree(e->tmp);
   if (e->counts) hipFree(e->counts);
+  if (e->fold) hipFree(e->fold);
   if (e->own_stream && e->stream) hipStreamDestroy(e->stream);
   delete e;
   return DG_OK;
@@ -291,11 +303,14 @@ void* dg_engine_stream(dg_engine* e) { return e ? (void*)e->stream : nullptr; }
 int dg_engine_sync(dg_engine* e) {
   if (!e) return fail(DG_E_INVAL, "null engine");
   TRY(set_device(e));
-  HIP_TRY(hipStreamSynchronize(e->stream));
   u32 err = 0;
-  HIP_TRY(hipMemcpy(&err, e->ticket + 1, sizeof(u32), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpyAsync(&e->h_counts[7], e->ticket + 1, sizeof(u32), hipMemcpyDeviceToHost,
+                         e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  memcpy(&err, &e->h_counts[7], sizeof(u32));
   if (err) {
-    HIP_TRY(hipMemset(e->ticket, 0, 4 * sizeof(u32)));
+    HIP_TRY(hipMemsetAsync(e->ticket, 0, 4 * sizeof(u32), e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
     return fail(DG_E_DEVICE, "look-back timeout inside a kernel (error bits 0x%x)", err);
   }
   return DG_OK;
@@ -334,83 +349,129 @@ int dg_join2(dg_engine* e, const dg_store* a, const dg_context* ca, const dg_sto
   return DG_OK;
 }
 
-int dg_joink(dg_engine* e, int k, const dg_store* stores, const dg_context* ctxs, dg_store* out,
-             dg_context* out_ctx) {
-  if (!e) return fail(DG_E_INVAL, "null engine");
-  if (k <= 0 || !stores || !ctxs || !out || !out_ctx) return fail(DG_E_INVAL, "dg_joink: bad args");
-  u64 total = 0, total_ctx = 0;
+}  // extern "C"
+
+namespace {
+
+// Two intermediate states (rows + context) for a fold over at most `rows` rows and
+// `ctx` context entries, carved from engine scratch that persists across calls.
+int fold_buffers(dg_engine* e, u64 rows, u64 ctx, dg_store* st, dg_context* cx) {
+  const size_t half = ((rows * 36 + ctx * 12 + 1024) + 255) / 256 * 256;
+  if (2 * half > e->fold_cap) {
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    if (e->fold) HIP_TRY(hipFree(e->fold));
+    e->fold = nullptr;
+    e->fold_cap = 0;
+    if (hipMalloc(&e->fold, 2 * half) != hipSuccess)
+      return fail(DG_E_NOMEM, "hipMalloc of %zu fold scratch bytes failed", 2 * half);
+    e->fold_cap = 2 * half;
+  }
+  for (int w = 0; w < 2; w++) {
+    char* p = (char*)e->fold + w * half;
+    st[w].key = (uint64_t*)p;
+    p += rows * 8;
+    st[w].val = (uint64_t*)p;
+    p += rows * 8;
+    st[w].ts = (int64_t*)p;
+    p += rows * 8;
+    st[w].cnt = (uint64_t*)p;
+    p += rows * 8;
+    cx[w].cnt = (uint64_t*)p;
+    p += ctx * 8;
+    st[w].node = (uint32_t*)p;
+    p += rows * 4;
+    cx[w].node = (uint32_t*)p;
+    st[w].cap = rows;
+    cx[w].cap = ctx;
+    st[w].n = 0;
+    cx[w].n = 0;
+    cx[w].kind = DG_CTX_VV;
+  }
+  return DG_OK;
+}
+
+int copy_state(dg_engine* e, const dg_store* s, const dg_context* c, dg_store* out,
+               dg_context* out_ctx) {
+  if (out->cap < s->n || out_ctx->cap < c->n) return fail(DG_E_CAPACITY, "output capacity too small");
+  if (s->n) {
+    HIP_TRY(hipMemcpyAsync(out->key, s->key, s->n * 8, hipMemcpyDeviceToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(out->val, s->val, s->n * 8, hipMemcpyDeviceToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(out->ts, s->ts, s->n * 8, hipMemcpyDeviceToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(out->node, s->node, s->n * 4, hipMemcpyDeviceToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(out->cnt, s->cnt, s->n * 8, hipMemcpyDeviceToDevice, e->stream));
+  }
+  if (c->n) {
+    HIP_TRY(hipMemcpyAsync(out_ctx->node, c->node, c->n * 4, hipMemcpyDeviceToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(out_ctx->cnt, c->cnt, c->n * 8, hipMemcpyDeviceToDevice, e->stream));
+  }
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  out->n = s->n;
+  out_ctx->n = c->n;
+  out_ctx->kind = c->kind;
+  return DG_OK;
+}
+
+// acc <- join(acc, s_i, keys_i) for i = 0..k-1 (acc starts as (state, ctx)); the last
+// step writes into out.
+int fold_join(dg_engine* e, const dg_store* state, const dg_context* ctx, int k,
+              const dg_store* stores, const dg_context* ctxs, const uint64_t* const* keys,
+              const uint64_t* n_keys, dg_store* out, dg_context* out_ctx, const char* what) {
+  u64 total = state->n, total_ctx = ctx->n;
   for (int s = 0; s < k; s++) {
-    TRY(check_store(&stores[s], "dg_joink store"));
-    TRY(check_ctx(&ctxs[s], "dg_joink ctx"));
+    TRY(check_store(&stores[s], what));
+    TRY(check_ctx(&ctxs[s], what));
     total += stores[s].n;
     total_ctx += ctxs[s].n;
   }
   if (out->cap < total || out_ctx->cap < total_ctx)
-    return fail(DG_E_CAPACITY, "dg_joink: output capacity too small");
+    return fail(DG_E_CAPACITY, "%s: output capacity too small (%llu rows, %llu ctx needed)", what,
+                (unsigned long long)total, (unsigned long long)total_ctx);
   TRY(set_device(e));
-  // Left fold through two ping-pong row buffers in device scratch.
-  const size_t row_bytes = 36;
-  const size_t ctx_bytes = 12;
-  const size_t half = total * row_bytes + total_ctx * ctx_bytes + 256;
-  void* fold = nullptr;
-  if (k > 2) {
-    if (hipMalloc(&fold, 2 * half) != hipSuccess)
-      return fail(DG_E_NOMEM, "dg_joink: scratch allocation failed");
-  }
-  auto carve = [&](int which, dg_store* st, dg_context* cx) {
-    char* p = (char*)fold + which * half;
-    st->key = (uint64_t*)p;
-    p += total * 8;
-    st->val = (uint64_t*)p;
-    p += total * 8;
-    st->ts = (int64_t*)p;
-    p += total * 8;
-    st->cnt = (uint64_t*)p;
-    p += total * 8;
-    cx->cnt = (uint64_t*)p;
-    p += total_ctx * 8;
-    st->node = (uint32_t*)p;
-    p += total * 4;
-    cx->node = (uint32_t*)p;
-    st->cap = total;
-    cx->cap = total_ctx;
-    st->n = 0;
-    cx->n = 0;
-  };
-  dg_store acc = stores[0];
-  dg_context acc_ctx = ctxs[0];
+  if (k == 0) return copy_state(e, state, ctx, out, out_ctx);
   dg_store buf[2];
   dg_context bufc[2];
-  if (k > 2) {
-    carve(0, &buf[0], &bufc[0]);
-    carve(1, &buf[1], &bufc[1]);
-  }
-  int rc = DG_OK;
-  if (k == 1) {
-    // join of a single store is the store itself
-    HIP_TRY(hipMemcpyAsync(out->key, acc.key, acc.n * 8, hipMemcpyDeviceToDevice, e->stream));
-    HIP_TRY(hipMemcpyAsync(out->val, acc.val, acc.n * 8, hipMemcpyDeviceToDevice, e->stream));
-    HIP_TRY(hipMemcpyAsync(out->ts, acc.ts, acc.n * 8, hipMemcpyDeviceToDevice, e->stream));
-    HIP_TRY(hipMemcpyAsync(out->node, acc.node, acc.n * 4, hipMemcpyDeviceToDevice, e->stream));
-    HIP_TRY(hipMemcpyAsync(out->cnt, acc.cnt, acc.n * 8, hipMemcpyDeviceToDevice, e->stream));
-    HIP_TRY(hipMemcpyAsync(out_ctx->node, acc_ctx.node, acc_ctx.n * 4, hipMemcpyDeviceToDevice, e->stream));
-    HIP_TRY(hipMemcpyAsync(out_ctx->cnt, acc_ctx.cnt, acc_ctx.n * 8, hipMemcpyDeviceToDevice, e->stream));
-    HIP_TRY(hipStreamSynchronize(e->stream));
-    out->n = acc.n;
-    out_ctx->n = acc_ctx.n;
-    out_ctx->kind = acc_ctx.kind;
-    return DG_OK;
-  }
-  for (int s = 1; s < k && rc == DG_OK; s++) {
+  if (k > 1) TRY(fold_buffers(e, total, total_ctx, buf, bufc));
+  dg_store acc = *state;
+  dg_context acc_ctx = *ctx;
+  for (int s = 0; s < k; s++) {
     dg_store* dst = (s == k - 1) ? out : &buf[s & 1];
     dg_context* dstc = (s == k - 1) ? out_ctx : &bufc[s & 1];
     dst->n = 0;
-    rc = dg_join2(e, &acc, &acc_ctx, &stores[s], &ctxs[s], nullptr, 0, dst, dstc);
+    const uint64_t* ks = keys ? keys[s] : nullptr;
+    const uint64_t nk = (keys && keys[s]) ? n_keys[s] : 0;
+    TRY(dg_join2(e, &acc, &acc_ctx, &stores[s], &ctxs[s], ks, nk, dst, dstc));
     acc = *dst;
     acc_ctx = *dstc;
   }
-  if (fold) hipFree(fold);
-  return rc;
+  return DG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dg_joink(dg_engine* e, int k, const dg_store* stores, const dg_context* ctxs, dg_store* out,
+             dg_context* out_ctx) {
+  if (!e) return fail(DG_E_INVAL, "null engine");
+  if (k <= 0 || !stores || !ctxs || !out || !out_ctx) return fail(DG_E_INVAL, "dg_joink: bad args");
+  TRY(check_store(&stores[0], "dg_joink store"));
+  TRY(check_ctx(&ctxs[0], "dg_joink ctx"));
+  return fold_join(e, &stores[0], &ctxs[0], k - 1, stores + 1, ctxs + 1, nullptr, nullptr, out,
+                   out_ctx, "dg_joink");
+}
+
+int dg_apply_deltas(dg_engine* e, const dg_store* state, const dg_context* ctx, int k,
+                    const dg_store* deltas, const dg_context* dctxs,
+                    const uint64_t* const* keys, const uint64_t* n_keys, dg_store* out,
+                    dg_context* out_ctx) {
+  if (!e) return fail(DG_E_INVAL, "null engine");
+  if (k < 0 || (k > 0 && (!deltas || !dctxs)) || !out || !out_ctx)
+    return fail(DG_E_INVAL, "dg_apply_deltas: bad args");
+  TRY(check_store(state, "dg_apply_deltas state"));
+  TRY(check_ctx(ctx, "dg_apply_deltas ctx"));
+  if (keys && !n_keys) return fail(DG_E_INVAL, "dg_apply_deltas: keys without n_keys");
+  return fold_join(e, state, ctx, k, deltas, dctxs, keys, n_keys, out, out_ctx,
+                   "dg_apply_deltas");
 }
 
 int dg_context_union(dg_engine* e, const dg_context* a, const dg_context* b, dg_context* out) {

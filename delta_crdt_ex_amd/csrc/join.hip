@@ -676,6 +676,7 @@ __device__ __forceinline__ void stripe_sums(const u32* cs, u64 base_t, u64 G, u6
     tot += __shfl_xor(tot, d, WAVE);
   }
   constexpr int NW = JB / WAVE;
+  __syncthreads();  // every wave is done reading s_red from the previous call
   if ((tid & (WAVE - 1)) == 0) {
     s_red[tid / WAVE] = lo;
     s_red[NW + tid / WAVE] = tot;

@@ -280,6 +280,40 @@ class Engine:
         out_ctx.kind = int(co.kind)
         return out, out_ctx
 
+    def apply_deltas(self, state: Store, ctx: Context, deltas, dctxs, keys=None,
+                     out: Store | None = None, out_ctx: Context | None = None):
+        """CausalCrdt's delta application (causal_crdt.ex:383-384): fold of
+        join(state, deltas[i], keys[i]); keys[i] a sorted unique device int64 tensor of
+        key ids, or None for a full-state join of that delta."""
+        self._order()
+        k = len(deltas)
+        arr_s = (_abi.dg_store * max(k, 1))(*[d.abi() for d in deltas])
+        arr_c = (_abi.dg_context * max(k, 1))(*[c.abi() for c in dctxs])
+        kp = kn = None
+        if keys is not None:
+            kp = (C.c_void_p * max(k, 1))(*[C.c_void_p(t.data_ptr() if t is not None and t.numel()
+                                                         else 0) for t in keys])
+            kn_np = np.array([int(t.numel()) if t is not None else 0 for t in keys] or [0],
+                             np.uint64)
+            kn = kn_np.ctypes.data_as(_abi.P64)
+            # an empty keyset is a join over no keys, not a full-state join: point it at
+            # a one-element dummy with n_keys = 0
+            dummy = torch.zeros(1, dtype=_I64, device=self.device)
+            for i, t in enumerate(keys):
+                if t is not None and t.numel() == 0:
+                    kp[i] = C.c_void_p(dummy.data_ptr())
+        if out is None:
+            out = Store.empty(state.n + sum(d.n for d in deltas), self.device)
+        if out_ctx is None:
+            out_ctx = Context.empty(DG_CTX_VV, ctx.n + sum(c.n for c in dctxs), self.device)
+        ss, xs, so, co = state.abi(), ctx.abi(), out.abi(), out_ctx.abi()
+        check(self.lib.dg_apply_deltas(self.h, C.byref(ss), C.byref(xs), k, arr_s, arr_c, kp, kn,
+                                       C.byref(so), C.byref(co)))
+        out.n = int(so.n)
+        out_ctx.n = int(co.n)
+        out_ctx.kind = int(co.kind)
+        return out, out_ctx
+
     # ---------------------------------------------------------------- contexts
     def context_union(self, a: Context, b: Context, out: Context | None = None) -> Context:
         self._order()

@@ -195,3 +195,112 @@ def random_pair(rng: np.random.Generator, n_keys: int, n_nodes: int = 4, max_ent
                       (merged[4][1:] == merged[4][:-1]))
         b["rows"] = tuple(c[m] for c in merged)
     return a, b
+
+
+def _take_rows(rows, key_ids):
+    """Rows whose key is in the sorted array key_ids (Map.take on the SoA store)."""
+    m = np.isin(rows[0], key_ids)
+    return tuple(c[m] for c in rows)
+
+
+def config3(n_keys: int = 10_000_000, n_replicas: int = 64, touch: float = 0.01,
+            remove_frac: float = 0.2, seed: int = 3):
+    """Config 3: a base state (node 0 wrote k = 1..n, counter k, ts = k * 1000) and
+    `n_replicas` replicas (nodes 1..R) that each touched ~touch * n keys of it: 80 %
+    re-added (AWLWWMap.add/4: the key's old entries go, one new entry with dot
+    {r, c}, c = 1, 2, ... in key order) and 20 % removed (remove/3).  Each replica
+    ships a sync-shaped delta (causal_crdt.ex:324-335): its VV, the rows of its touched
+    keys (Map.take) and the touched keys themselves.
+
+    Returns (base, deltas) where base = {"rows", "ctx"} and each delta =
+    {"rows", "ctx", "keys"} (keys: ascending unique key ids).  Applying them is the
+    fold join(state, delta_r, keys_r) over r = 1..R (causal_crdt.ex:383-384)."""
+    k = np.arange(1, n_keys + 1, dtype=np.uint64)
+    key = splitmix64_np(k)
+    base = {"rows": sort_rows(key, encode_int_value(k.astype(np.int64)),
+                              k.astype(np.int64) * 1000, np.zeros(n_keys, np.uint32), k.copy()),
+            "ctx": vv({0: n_keys})}
+    rng = np.random.default_rng(seed)
+    ts_base = n_keys * 1000 + 1000
+    m = max(1, int(round(touch * n_keys)))
+    deltas = []
+    for r in range(1, n_replicas + 1):
+        idx = np.unique(rng.integers(0, n_keys, m))  # touched keys (by index into k)
+        kid = key[idx]
+        order = np.argsort(kid)  # key-id order: counters follow it
+        kid = kid[order]
+        added = rng.random(len(kid)) >= remove_frac
+        na = int(added.sum())
+        vals = encode_int_value(rng.integers(0, 1 << 62, na, dtype=np.int64))
+        ts = ts_base + rng.integers(0, 1_000_000_000, na, dtype=np.int64)
+        rows = sort_rows(kid[added], vals, ts, np.full(na, r, np.uint32),
+                         np.arange(1, na + 1, dtype=np.uint64))
+        deltas.append({"rows": rows, "ctx": vv({0: n_keys, r: na}), "keys": kid})
+    return base, deltas
+
+
+def config4_shard(rank: int, world: int, keys_per_rank: int = 12_500_000,
+                  diff_frac: float = 0.01, seed: int = 4):
+    """Config 4, one key-hash shard: the shard `rank` of a world * keys_per_rank key
+    space of two replicas that differ on ~diff_frac of the keys (merkle_pair)."""
+    k = np.arange(1, world * keys_per_rank + 1, dtype=np.uint64)
+    mine = shard_of(splitmix64_np(k), world) == rank
+    return merkle_pair(keys=k[mine], diff_frac=diff_frac, seed=seed + rank)
+
+
+def sync_delta(rep, keys):
+    """The sync message a replica sends for `keys` (causal_crdt.ex:324-335): its
+    context and Map.take of its rows; `keys` ascending unique key ids."""
+    keys = np.asarray(keys, np.uint64)
+    return {"rows": _take_rows(rep["rows"], keys), "ctx": rep["ctx"], "keys": keys}
+
+
+def config5(n_keys: int = 100_000_000, n_nodes: int = 64, remove_frac: float = 0.5,
+            readd_frac: float = 0.2, ts_range: int = 16, max_entries: int = 3, seed: int = 5):
+    """Config 5, remove-heavy adversarial pair.  Base: every key holds 1..max_entries
+    concurrent entries written by random nodes 0..n_nodes-3 (dots {node, c}, c
+    counting per node in key order), small values and ts in [0, ts_range) so LWW ties
+    are everywhere.  Replicas A (node n_nodes-2) and B (node n_nodes-1) each saw the
+    whole base (dense VVs: they cover every dot they hold) and then independently
+    removed `remove_frac` of the keys and re-added (add/4: the key's entries replaced
+    by one new entry) `readd_frac` of the rest.  Returns (A, B)."""
+    rng = np.random.default_rng(seed)
+    k = np.arange(1, n_keys + 1, dtype=np.uint64)
+    key = splitmix64_np(k)
+    ne = rng.integers(1, min(max_entries, n_nodes - 2) + 1, n_keys)
+    ekey = np.repeat(key, ne)
+    E = len(ekey)
+    kidx = np.repeat(np.arange(n_keys), ne)
+    # entry j of key x comes from writer (h_x + j) mod (n_nodes - 2): distinct writers
+    # per key (a writer's second add to a key would replace its first)
+    first = np.r_[0, np.cumsum(ne)[:-1]]
+    j = np.arange(E) - np.repeat(first, ne)
+    h = rng.integers(0, n_nodes - 2, n_keys)
+    enode = ((h[kidx] + j) % (n_nodes - 2)).astype(np.uint32)
+    # counters per node in generation order (key index, then entry)
+    order = np.argsort(enode, kind="stable")
+    cnt = np.empty(E, np.uint64)
+    sn = enode[order]
+    starts = np.r_[0, np.flatnonzero(sn[1:] != sn[:-1]) + 1]
+    ranks = np.arange(E) - np.repeat(starts, np.diff(np.r_[starts, E]))
+    cnt[order] = ranks.astype(np.uint64) + 1
+    eval_ = encode_int_value(rng.integers(0, 4, E))
+    ets = rng.integers(0, ts_range, E).astype(np.int64)
+    base_vv = {}
+    for nd, c in zip(*np.unique(enode, return_counts=True)):
+        base_vv[int(nd)] = int(c)
+    reps = []
+    for node_id in (n_nodes - 2, n_nodes - 1):
+        removed = rng.random(n_keys) < remove_frac
+        readd = (~removed) & (rng.random(n_keys) < readd_frac)
+        keep_e = ~(removed | readd)[kidx]
+        na = int(readd.sum())
+        ak = key[readd]
+        av = encode_int_value(rng.integers(0, 4, na))
+        at = rng.integers(0, ts_range, na).astype(np.int64)
+        rows = sort_rows(np.concatenate([ekey[keep_e], ak]), np.concatenate([eval_[keep_e], av]),
+                         np.concatenate([ets[keep_e], at]),
+                         np.concatenate([enode[keep_e], np.full(na, node_id, np.uint32)]),
+                         np.concatenate([cnt[keep_e], np.arange(1, na + 1, dtype=np.uint64)]))
+        reps.append({"rows": rows, "ctx": vv({**base_vv, node_id: na})})
+    return reps[0], reps[1]

@@ -136,6 +136,20 @@ int dg_join2_async(dg_engine* e, const dg_store* a, const dg_context* ca, const 
 int dg_joink(dg_engine* e, int k, const dg_store* stores, const dg_context* ctxs, dg_store* out,
              dg_context* out_ctx);
 
+/* A batch of deltas applied to a state as CausalCrdt applies delta messages, one
+ * join/3 per delta with that delta's own `keys` (causal_crdt.ex:86-89,383-384, and
+ * the sync shape {%{dots: VV, value: Map.take(value, keys)}, keys} of :324-335):
+ *   out = join(...join(join(state, deltas[0], keys[0]), deltas[1], keys[1])...,
+ *              deltas[k-1], keys[k-1]).
+ * keys[i] (device, ascending unique, n_keys[i] entries) or keys == NULL / keys[i] ==
+ * NULL for a full-state join of that delta.  out->cap >= state->n + Σ deltas[i].n,
+ * out_ctx->cap >= ctx->n + Σ dctxs[i].n.  Intermediate states live in engine
+ * scratch.  Synchronous. */
+int dg_apply_deltas(dg_engine* e, const dg_store* state, const dg_context* ctx, int k,
+                    const dg_store* deltas, const dg_context* dctxs,
+                    const uint64_t* const* keys, const uint64_t* n_keys, dg_store* out,
+                    dg_context* out_ctx);
+
 /* ---- causal-context algebra ----------------------------------------------- */
 /* Dots.union/2 (aw_lww_map.ex:39-52): VV ⊔ VV = per-node max; VV ⊔ DOTS folds the
  * dots into the VV; DOTS ⊔ DOTS = set union. */

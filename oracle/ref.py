@@ -147,6 +147,14 @@ def joink(stores, ctxs):
     return tuple(col[: so.n] for col in out), (xo.kind, onode[: xo.n], ocnt[: xo.n])
 
 
+def apply_deltas(state, ctx, deltas, dctxs, keys=None):
+    """Left fold of join(state, delta_i, keys_i) (causal_crdt.ex:383-384): the C
+    restatement's join/3 applied once per delta.  keys[i] None = all keys."""
+    for i, (d, c) in enumerate(zip(deltas, dctxs)):
+        state, ctx = join2(state, ctx, d, c, None if keys is None else keys[i])
+    return state, ctx
+
+
 def context_union(ca, cb):
     xa, ca = _ctx(ca)
     xb, cb = _ctx(cb)

@@ -1,0 +1,161 @@
+"""BASELINE configs 3, 4 and 5 on the CPU: each generator against the term oracle
+replaying the same operations (AWLWWMap.add/4, remove/3 joined as CausalCrdt does),
+and the C oracle's keyed delta fold / join / read against the term oracle.  The GPU
+side of the same configs is tests/test_gpu_configs.py."""
+import numpy as np
+import pytest
+
+from delta_crdt_ex_amd import workloads as W
+from delta_crdt_ex_amd.interning import Universe, splitmix64
+from oracle import awlww_term as T
+from oracle import convert as CV
+from oracle import ref as R
+from test_c_oracle import ctx_equal, rows_equal, soa_to_term, term_to_soa_raw
+
+
+def _base_term(n):
+    """Node 0 adds k => k with ts = k * 1000 for k = 1..n (config 2/3 base)."""
+    st = T.compress_dots(T.new())
+    for k in range(1, n + 1):
+        st = T.join(st, T.add(k, k, 0, st, k * 1000), [k])
+    return st
+
+
+def _take(state, keys):
+    return T.AW(state.dots, {k: v for k, v in state.value.items() if k in keys})
+
+
+# ------------------------------------------------------------------ config 3
+
+def test_config3_generator_matches_term_replay():
+    n, R_ = 150, 3
+    U = Universe()
+    base, deltas = W.config3(n_keys=n, n_replicas=R_, touch=0.12, seed=11)
+    kterm = {splitmix64(k): k for k in range(1, n + 1)}
+    st0 = _base_term(n)
+    rows, ctx = CV.state_to_soa(st0, U)
+    assert rows_equal(rows, base["rows"]) and ctx_equal(ctx, base["ctx"])
+    for r, d in enumerate(deltas, start=1):
+        keys = [kterm[int(x)] for x in d["keys"]]
+        k, v, t, nd, c = d["rows"]
+        adds = {kterm[int(k[i])]: (int(v[i]) - (1 << 62), int(t[i]), int(c[i])) for i in range(len(k))}
+        st = st0
+        # adds in counter order (next_dot numbers them), removes anywhere
+        for key, (val, ts, _c) in sorted(adds.items(), key=lambda kv: kv[1][2]):
+            st = T.join(st, T.add(key, val, r, st, ts), [key])
+        for key in keys:
+            if key not in adds:
+                st = T.join(st, T.remove(key, r, st), [key])
+        delta = _take(st, set(keys))
+        drows, dctx = CV.state_to_soa(delta, U)
+        assert rows_equal(drows, d["rows"]), r
+        assert ctx_equal(dctx, d["ctx"]), r
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_config3_keyed_fold_two_oracles(seed):
+    """C restatement's fold of join(state, delta_i, keys_i) == the term oracle's."""
+    base, deltas = W.config3(n_keys=200, n_replicas=6, touch=0.1, seed=seed)
+    rows, ctx = R.apply_deltas(base["rows"], base["ctx"], [d["rows"] for d in deltas],
+                               [d["ctx"] for d in deltas], [d["keys"] for d in deltas])
+    st = soa_to_term(base["rows"], base["ctx"])
+    for d in deltas:
+        st = T.join(st, soa_to_term(d["rows"], d["ctx"]), [int(x) for x in d["keys"]])
+    wrows, wctx = term_to_soa_raw(st)
+    assert rows_equal(rows, wrows) and ctx_equal(ctx, wctx)
+    # every touched key: the base row is gone; added keys carry their new rows
+    touched = np.unique(np.concatenate([d["keys"] for d in deltas]))
+    assert not np.any(np.isin(rows[0][rows[3] == 0], touched))
+
+
+def test_config3_keys_outside_keyset_are_right_biased():
+    """A delta row whose key is not in the delta's keys replaces the state's rows of
+    that key (Map.merge(Map.drop(..)) at aw_lww_map.ex:185-188) -- both oracles."""
+    base, deltas = W.config3(n_keys=100, n_replicas=2, touch=0.2, seed=9)
+    d = deltas[0]
+    keys = d["keys"][: len(d["keys"]) // 2]
+    rows, ctx = R.apply_deltas(base["rows"], base["ctx"], [d["rows"]], [d["ctx"]], [keys])
+    st = T.join(soa_to_term(base["rows"], base["ctx"]), soa_to_term(d["rows"], d["ctx"]),
+                [int(x) for x in keys])
+    wrows, wctx = term_to_soa_raw(st)
+    assert rows_equal(rows, wrows) and ctx_equal(ctx, wctx)
+
+
+# ------------------------------------------------------------------ config 5
+
+def test_config5_generator_matches_term_replay():
+    n, nn = 50, 8
+    U = Universe()
+    a, b = W.config5(n_keys=n, n_nodes=nn, seed=3)
+    # the base: every writer node's own adds (the generator's draws, replayed in its
+    # order), joined -- concurrent entries of one key survive
+    rng = np.random.default_rng(3)
+    ne = rng.integers(1, 4, n)
+    E = int(ne.sum())
+    kidx = np.repeat(np.arange(n), ne)
+    first = np.r_[0, np.cumsum(ne)[:-1]]
+    h = rng.integers(0, nn - 2, n)
+    enode = (h[kidx] + np.arange(E) - np.repeat(first, ne)) % (nn - 2)
+    # counters per node in generation order
+    seen = {}
+    cnt = []
+    for x in enode:
+        seen[int(x)] = seen.get(int(x), 0) + 1
+        cnt.append(seen[int(x)])
+    evals = rng.integers(0, 4, E)
+    ets = rng.integers(0, 16, E)
+    writers = {}
+    for e in range(E):
+        writers.setdefault(int(enode[e]), []).append(e)
+    base = T.compress_dots(T.new())
+    for nd, es in writers.items():
+        st = T.compress_dots(T.new())
+        for e in es:
+            key = int(kidx[e]) + 1
+            st = T.join(st, T.add(key, int(evals[e]), nd, st, int(ets[e])), [key])
+        base = T.join(base, st, sorted(set(base.value) | set(st.value)))
+    for node_id, gen in ((nn - 2, a), (nn - 1, b)):
+        removed = rng.random(n) < 0.5
+        readd = (~removed) & (rng.random(n) < 0.2)
+        na = int(readd.sum())
+        av = rng.integers(0, 4, na)
+        at = rng.integers(0, 16, na)
+        st = base
+        for j, kk in enumerate(np.flatnonzero(readd)):
+            key = int(kk) + 1
+            st = T.join(st, T.add(key, int(av[j]), node_id, st, int(at[j])), [key])
+        for kk in np.flatnonzero(removed):
+            key = int(kk) + 1
+            st = T.join(st, T.remove(key, node_id, st), [key])
+        rows, ctx = CV.state_to_soa(st, U)
+        assert rows_equal(rows, gen["rows"]), node_id
+        assert ctx_equal(ctx, gen["ctx"]), node_id
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_config5_join_and_read_two_oracles(seed):
+    a, b = W.config5(n_keys=80, n_nodes=10, seed=seed)
+    rows, ctx = R.join2(a["rows"], a["ctx"], b["rows"], b["ctx"])
+    ta, tb = soa_to_term(a["rows"], a["ctx"]), soa_to_term(b["rows"], b["ctx"])
+    want = T.join(ta, tb, sorted(set(ta.value) | set(tb.value)))
+    wrows, wctx = term_to_soa_raw(want)
+    assert rows_equal(rows, wrows) and ctx_equal(ctx, wctx)
+    ok, ov = R.read_lww(rows)
+    assert dict(zip(map(int, ok), map(int, ov))) == T.read(want)
+
+
+# ------------------------------------------------------------------ config 4
+
+@pytest.mark.parametrize("rank", range(4))
+def test_config4_shard_anti_entropy_round(rank):
+    """Per key-hash shard: the Merkle diff is the exact set of differing keys, and
+    joining B's sync delta for those keys into A (causal_crdt.ex:324-335,383-384)
+    equals the full-state join of the shard."""
+    a, b = W.config4_shard(rank, 4, keys_per_rank=600, diff_frac=0.05)
+    diff = R.store_diff(a["rows"], b["rows"])
+    ta, tb = R.merkle_build(a["rows"], 8), R.merkle_build(b["rows"], 8)
+    assert np.array_equal(R.merkle_diff(ta, tb), diff)
+    d = W.sync_delta(b, diff)
+    rows, ctx = R.apply_deltas(a["rows"], a["ctx"], [d["rows"]], [d["ctx"]], [d["keys"]])
+    frows, fctx = R.join2(a["rows"], a["ctx"], b["rows"], b["ctx"])
+    assert rows_equal(rows, frows) and ctx_equal(ctx, fctx)
