@@ -108,6 +108,81 @@ def merkle_rate(eng, torch, dev, steps=20):
             "note": "two builds + one diff per round, synchronous API (includes host syncs)"}
 
 
+def _timed(torch, fn, reps):
+    """Median wall time of `reps` synchronous calls (each call ends in a host sync)."""
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts))
+
+
+def config3_rate(eng, torch, dev, n_keys=10_000_000, reps=3):
+    """Config 3: 64 sync-shaped deltas (1 % of the keys each, 80 % adds / 20 % removes)
+    applied to a 10M-key state with dg_apply_deltas (fold of join/3 with each delta's
+    keys).  Rate = Σ over the 64 joins of their input rows / wall time."""
+    from delta_crdt_ex_amd import workloads as W
+    from delta_crdt_ex_amd.store import Context, Store
+    base, deltas = W.config3(n_keys=n_keys, n_replicas=64, touch=0.01, seed=3)
+    sb = Store.from_numpy(*base["rows"], device=dev)
+    cb = Context.from_numpy(*base["ctx"], dev)
+    ds = [Store.from_numpy(*d["rows"], device=dev) for d in deltas]
+    dc = [Context.from_numpy(*d["ctx"], dev) for d in deltas]
+    ks = [torch.from_numpy(d["keys"].view(np.int64)).to(dev) for d in deltas]
+    out = Store.empty(sb.n + sum(d.n for d in ds), dev)
+    octx = Context.empty(0, cb.n + sum(c.n for c in dc), dev)
+    res = {}
+
+    def run():
+        o, c = eng.apply_deltas(sb, cb, ds, dc, ks, out=out, out_ctx=octx)
+        res["n"] = o.n
+
+    el = _timed(torch, run, reps)
+    # input rows of the 64 joins: the running state (~ the base rows: deltas replace
+    # rows of their keys) plus that delta
+    rows_in = 64 * sb.n + sum(d.n for d in ds)
+    return {"metric": "merged dots/s, config 3 (64 keyed sync deltas into a 10M-key state)",
+            "value": rows_in / el, "unit": "merged dots/s", "ms_per_batch": el * 1e3,
+            "state_rows": sb.n, "delta_rows": sum(d.n for d in ds), "rows_out": res["n"],
+            "note": "dg_apply_deltas: 64 joins (with keys) back to back, one host sync each"}
+
+
+def config5_rate(eng, torch, dev, n_keys=12_500_000, reps=5):
+    """Config 5 at one GPU's share of 100M keys over 8 GPUs: full-state join of two
+    remove-heavy replicas (50 % removes, 64 nodes, ts in [0,16): LWW ties everywhere),
+    then read/1 of the result."""
+    from delta_crdt_ex_amd import workloads as W
+    from delta_crdt_ex_amd.store import Context, Store
+    a, b = W.config5(n_keys=n_keys, n_nodes=64, seed=5)
+    sa, sb = Store.from_numpy(*a["rows"], device=dev), Store.from_numpy(*b["rows"], device=dev)
+    ca, cb = Context.from_numpy(*a["ctx"], dev), Context.from_numpy(*b["ctx"], dev)
+    out = Store.empty(sa.n + sb.n, dev)
+    octx = Context.empty(0, ca.n + cb.n, dev)
+    res = {}
+
+    def join():
+        o, _ = eng.join2(sa, ca, sb, cb, out=out, out_ctx=octx)
+        res["n"] = o.n
+
+    tj = _timed(torch, join, reps)
+
+    def read():
+        k, _ = eng.read_lww(out)
+        res["keys"] = int(k.numel())
+
+    tr = _timed(torch, read, reps)
+    n_in = sa.n + sb.n
+    return {"metric": "merged dots/s, config 5 (remove-heavy, LWW ties), 12.5M keys per GPU",
+            "value": n_in / tj, "unit": "merged dots/s", "ms_per_join": tj * 1e3,
+            "rows_in": n_in, "rows_out": res["n"], "read_keys_per_s": res["n"] / tr,
+            "ms_per_read": tr * 1e3, "read_keys": res["keys"],
+            "note": "synchronous dg_join2 / dg_read_lww (each includes a host sync)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -115,6 +190,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-merkle", action="store_true")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the secondary config-3 / config-5 measurements")
     ap.add_argument("--rotate", type=int, default=4,
                     help="distinct replica pairs joined round-robin (defeats cache residency)")
     ap.add_argument("--calibrate", action="store_true",
@@ -248,8 +325,8 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "join2 = join2_partition_kernel + join2_slot_kernel + join2_compact_kernel "
-                          "(events bracket all three)",
+                "kernel": "join2 = join2_partition_kernel + join2_stream_kernel "
+                          "(events bracket both)",
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_launch_us": avg_launch_s * 1e6,
                 "launch_timing": "median of per-step HIP event pairs on the engine stream",
@@ -257,6 +334,11 @@ def main():
         }
         if not args.no_merkle:
             res["merkle"] = merkle_rate(eng, torch, dev)
+        if not args.no_configs:
+            for r in pairs:  # free the config-2 replicas before the larger configs
+                r.clear()
+            res["config3"] = config3_rate(eng, torch, dev)
+            res["config5"] = config5_rate(eng, torch, dev)
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(a, b)
         elif not args.no_cpu_baseline:
