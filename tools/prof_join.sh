@@ -3,7 +3,7 @@ set -o pipefail
 TAG=${1:-join}
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/prof_$TAG
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o $TAG --output-format csv -- python -u bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-merkle > gpurun_out/prof_$TAG/bench.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o $TAG --output-format csv -- python -u bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-merkle --no-configs > gpurun_out/prof_$TAG/bench.log 2>&1 || exit 1
 python - "$TAG" <<'PY'
 import csv, sys, collections
 tag = sys.argv[1]
