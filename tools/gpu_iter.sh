@@ -11,7 +11,7 @@ for lib in delta_crdt_ex_amd/libdeltagpu.so delta_crdt_ex_amd/libdeltagpu_DG*.so
   [ -e "$lib" ] || continue
   for mode in ${MODES:-1}; do
     DG_JOIN_MODE=$mode DG_LIB_PATH=$PWD/$lib timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_golden.py -x -q --timeout 120 --timeout-method thread -m gpu -k "join or golden" > gpurun_out/v_tests.log 2>&1 || { echo "$lib mode $mode TESTS_FAILED"; tail -30 gpurun_out/v_tests.log; exit 1; }
-    DG_JOIN_MODE=$mode DG_LIB_PATH=$PWD/$lib timeout -k 10 200 python -u bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-merkle > gpurun_out/v.log 2>&1 || { echo "$lib FAILED"; tail -5 gpurun_out/v.log; exit 1; }
+    DG_JOIN_MODE=$mode DG_LIB_PATH=$PWD/$lib timeout -k 10 200 python -u bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-merkle --no-configs > gpurun_out/v.log 2>&1 || { echo "$lib FAILED"; tail -5 gpurun_out/v.log; exit 1; }
     echo -n "$lib mode $mode ($(tail -1 gpurun_out/v_tests.log)): "; python -c "$BR" < gpurun_out/v.log
     if [ -n "$PROF_ALL" ]; then
       DG_JOIN_MODE=$mode DG_LIB_PATH=$PWD/$lib bash tools/prof_join.sh v > gpurun_out/prof_v.txt 2>&1 || { tail -5 gpurun_out/prof_v.txt; exit 1; }

@@ -5,7 +5,7 @@ mkdir -p gpurun_out/pmc
 i=0
 for set in "$@"; do
   i=$((i+1))
-  timeout -s KILL 90 rocprofv3 --pmc $set -d gpurun_out/pmc -o pass$i --output-format csv -- python -u bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-merkle > gpurun_out/pmc/pass$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/pmc/pass$i.log; exit 1; }
+  timeout -s KILL 90 rocprofv3 --pmc $set -d gpurun_out/pmc -o pass$i --output-format csv -- python -u bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-merkle --no-configs > gpurun_out/pmc/pass$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/pmc/pass$i.log; exit 1; }
 done
 python - <<'PY'
 import csv, glob, collections

@@ -36,7 +36,7 @@ def run(counter, tag, reuse=False):
         return collect(d, json.load(open(os.path.join(d, "bench.json"))))
     cmd = ["timeout", "-s", "KILL", "120", "rocprofv3", "--pmc", counter, "-d", d, "-o", tag,
            "--output-format", "csv", "--", sys.executable, "-u", "bench.py", "--steps", "16",
-           "--warmup", "4", "--no-cpu-baseline", "--no-merkle", "--calibrate"]
+           "--warmup", "4", "--no-cpu-baseline", "--no-merkle", "--no-configs", "--calibrate"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, env=dict(os.environ, TMPDIR="/tmp"))
     if r.returncode != 0:
         raise SystemExit(f"rocprofv3 {counter} failed:\n{r.stdout[-2000:]}\n{r.stderr[-2000:]}")
