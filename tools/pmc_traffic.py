@@ -22,6 +22,7 @@ import csv
 import glob
 import json
 import os
+import re
 import subprocess
 import sys
 
@@ -54,9 +55,9 @@ def collect(d, bench):
             if "store_check" in k:
                 check += float(row["Counter_Value"])
                 continue
-            name = ("partition" if "partition" in k else "slot" if "slot" in k else
-                    "compact" if "compact" in k else "tiles" if "tiles" in k else None)
-            if name:
+            m = re.search(r"join2_(\w+?)_kernel", k)  # partition / stream / slot / compact
+            if m:
+                name = m.group(1)
                 vals.setdefault(name, []).append(float(row["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in vals.items()}, check, bench
 
