@@ -20,14 +20,18 @@
 //      round finishes it (~5 cache lines per array instead of a 21-step search); any
 //      key distribution stays exact through a 128-ary fallback search.  One extra
 //      workgroup computes the context union Dots.union(c1, c2) (:155).
-//   2. join2_main_kernel (single pass): one workgroup per tile of JT merged
-//      positions, numbered by an atomic ticket (launch order, so the look-back only
-//      waits on resident tiles).  Every lane issues all of its row loads before the
-//      first LDS write; each thread merges JI positions from LDS and decides
-//      keep/drop; a block scan builds the compaction list; the tile publishes its
-//      count, resolves its output offset with a block-wide decoupled look-back and
-//      writes its kept rows coalesced.  Inputs are read once and outputs written
-//      once: 36 B x (N_in + N_out) of HBM traffic plus the partition's probes.
+//   2. join2_stream_kernel (single pass, the default): a persistent grid of G
+//      resident workgroups (occupancy API) walks the tiles statically, t = w + k*G,
+//      so tiles k*G .. k*G+G-1 form "stripe" k.  Per iteration a workgroup commits
+//      the tile it prefetched into registers to one of two LDS buffers, issues the
+//      loads of its next tile, merges JI positions per thread from LDS (keep/drop),
+//      block-scans the keep flags into a u16 compaction list and publishes the
+//      tile's count as an {epoch, count} granule in a per-stripe array.  The tile is
+//      written out one iteration LATER: by then every workgroup has published its
+//      count for that stripe, so each workgroup sums the G counts of the stripe
+//      itself (a 1-4 KB coalesced read) instead of chaining look-backs, and the
+//      output offset is a running sum over stripes.  Inputs are read once, outputs
+//      written once: 36 B x (N_in + N_out) of HBM traffic plus the partition's probes.
 //   (join2_slot_kernel + join2_compact_kernel: the two-pass variant, selected with
 //    DG_JOIN_MODE=2, kept for A/B measurement.)
 //
