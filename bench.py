@@ -123,10 +123,12 @@ def _timed(torch, fn, reps):
 
 def config3_rate(eng, torch, dev, n_keys=10_000_000, reps=3):
     """Config 3: 64 sync-shaped deltas (1 % of the keys each, 80 % adds / 20 % removes)
-    applied to a 10M-key state with dg_apply_deltas (fold of join/3 with each delta's
-    keys).  Rate = Σ over the 64 joins of their input rows / wall time."""
+    applied to a 10M-key state with dg_apply_deltas (the fold of join/3 with each
+    delta's keys; one pass over the state, csrc/kfold.hip).  Rate = (state rows + delta
+    rows) / wall time, SURVEY §8(d)'s N_in ≈ 15M; the delta-by-delta fold is timed beside
+    it (DG_APPLY_MODE=fold)."""
     from delta_crdt_ex_amd import workloads as W
-    from delta_crdt_ex_amd.store import Context, Store
+    from delta_crdt_ex_amd.store import Context, Engine, Store
     base, deltas = W.config3(n_keys=n_keys, n_replicas=64, touch=0.01, seed=3)
     sb = Store.from_numpy(*base["rows"], device=dev)
     cb = Context.from_numpy(*base["ctx"], dev)
@@ -137,18 +139,31 @@ def config3_rate(eng, torch, dev, n_keys=10_000_000, reps=3):
     octx = Context.empty(0, cb.n + sum(c.n for c in dc), dev)
     res = {}
 
-    def run():
-        o, c = eng.apply_deltas(sb, cb, ds, dc, ks, out=out, out_ctx=octx)
+    def run(e):
+        o, c = e.apply_deltas(sb, cb, ds, dc, ks, out=out, out_ctx=octx)
         res["n"] = o.n
 
-    el = _timed(torch, run, reps)
-    # input rows of the 64 joins: the running state (~ the base rows: deltas replace
-    # rows of their keys) plus that delta
-    rows_in = 64 * sb.n + sum(d.n for d in ds)
+    el = _timed(torch, lambda: run(eng), reps)
+    os.environ["DG_APPLY_MODE"] = "fold"
+    try:
+        fe = Engine(0)
+    finally:
+        del os.environ["DG_APPLY_MODE"]
+    n_one = res["n"]
+    el_fold = _timed(torch, lambda: run(fe), reps)
+    fe.close()
+    assert res["n"] == n_one
+    d_rows = sum(d.n for d in ds)
+    n_keys_total = sum(int(k.numel()) for k in ks)
+    rows_in = sb.n + d_rows
+    alg = 36 * (rows_in + res["n"]) + 8 * n_keys_total
     return {"metric": "merged dots/s, config 3 (64 keyed sync deltas into a 10M-key state)",
             "value": rows_in / el, "unit": "merged dots/s", "ms_per_batch": el * 1e3,
-            "state_rows": sb.n, "delta_rows": sum(d.n for d in ds), "rows_out": res["n"],
-            "note": "dg_apply_deltas: 64 joins (with keys) back to back, one host sync each"}
+            "alg_bytes": alg, "alg_GBps": alg / el / 1e9,
+            "state_rows": sb.n, "delta_rows": d_rows, "keyset_entries": n_keys_total,
+            "rows_out": res["n"], "stepwise_ms_per_batch": el_fold * 1e3,
+            "note": "dg_apply_deltas, synchronous (one host sync); stepwise = 64 joins of "
+                    "join/3 back to back"}
 
 
 def config5_rate(eng, torch, dev, n_keys=12_500_000, reps=5):

@@ -38,6 +38,11 @@ struct dg_engine {
   size_t tmp_cap = 0;
   int join_mode = JOIN_SINGLE_PASS;  // DG_JOIN_MODE=2: two-pass count/compact variant
   int join_workers = 0;           // persistent pass-1 workgroups (0: all resident ones)
+  // dg_apply_deltas: 0 one pass per <= 64 deltas, delta by delta where an input needs it;
+  // DG_APPLY_MODE=fold: always delta by delta; =onepass: never (DG_E_INVAL instead)
+  int apply_mode = 0;
+  void* h_stage = nullptr;        // pinned staging of kernel descriptors
+  size_t h_stage_cap = 0;
 };
 
 namespace {
@@ -247,6 +252,9 @@ int dg_engine_create(int device, void* hip_stream, dg_engine** out) {
     if (v && atoi(v) > 0) e->join_workers = atoi(v);
     const char* m = getenv("DG_JOIN_MODE");
     if (m && m[0] == '2') e->join_mode = JOIN_TWO_PASS;
+    const char* am = getenv("DG_APPLY_MODE");
+    if (am && strcmp(am, "fold") == 0) e->apply_mode = 1;
+    if (am && strcmp(am, "onepass") == 0) e->apply_mode = 2;
   }
   int rc = set_device(e);
   if (rc != DG_OK) {
@@ -293,6 +301,7 @@ int dg_engine_destroy(dg_engine* e) {
   if (e->tmp) hipFree(e->tmp);
   if (e->counts) hipFree(e->counts);
   if (e->fold) hipFree(e->fold);
+  if (e->h_stage) hipHostFree(e->h_stage);
   if (e->own_stream && e->stream) hipStreamDestroy(e->stream);
   delete e;
   return DG_OK;
@@ -446,6 +455,147 @@ int fold_join(dg_engine* e, const dg_store* state, const dg_context* ctx, int k,
   return DG_OK;
 }
 
+// One pass of dg_apply_deltas over k <= KFOLD_MAX_K deltas (kfold.hip).  *stepwise is
+// set when this input needs the delta-by-delta fold instead: a context that is not a
+// version vector, a node id >= KNT, or a key bucket over its LDS capacity (keys far
+// from uniform hashes).  The state and deltas are only read.
+int kfold_pass(dg_engine* e, const dg_store* state, const dg_context* ctx, int k,
+               const dg_store* deltas, const dg_context* dctxs, const uint64_t* const* keys,
+               const uint64_t* n_keys, dg_store* out, dg_context* out_ctx, bool* stepwise) {
+  *stepwise = true;
+  if (k < 1 || k > KFOLD_MAX_K || ctx->kind != DG_CTX_VV) return DG_OK;
+  u64 m_rows = 0, m_keys = 0, allmask = 0;
+  for (int i = 0; i < k; i++) {
+    if (dctxs[i].kind != DG_CTX_VV || deltas[i].n >= (1ull << 32)) return DG_OK;
+    const bool full = !keys || !keys[i];
+    const u64 nk = full ? 0 : n_keys[i];
+    if (nk >= (1ull << 32)) return DG_OK;
+    if (full) allmask |= 1ull << i;
+    m_rows += deltas[i].n;
+    m_keys += nk;
+  }
+  auto ceil_div = [](u64 a, u64 b) { return (a + b - 1) / b; };
+  const u64 T0 = std::max<u64>({ceil_div(state->n, KFOLD_MEAN_S), ceil_div(m_rows, KFOLD_MEAN_D),
+                                ceil_div(m_keys, KFOLD_MEAN_M), 1});
+  // a bucket over capacity (key groups far larger than the mean, or keys that are not
+  // uniform hashes) is retried once with 8x the buckets
+  for (int attempt = 0; attempt < 2; attempt++) {
+    const u64 T = T0 << (3 * attempt);
+    if (T >= (1ull << 31)) return DG_OK;
+    // device scratch: runs | flat | sstart | dstart | tabC | tabP | flag
+    auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+    const size_t b_runs = al(k * sizeof(KRun)), b_flat = al((2 * k + 2) * sizeof(u64));
+    const size_t b_ss = al((T + 1) * 8), b_ds = al((T + 1) * 2 * k * 4), b_tab = al((size_t)k * KNT * 8);
+    const size_t bytes = b_runs + b_flat + b_ss + b_ds + 2 * b_tab + 256;
+    TRY(ensure_state(e, T + 2));
+    TRY(ensure_tmp(e, bytes));
+    const size_t hb = b_runs + b_flat;
+    if (hb > e->h_stage_cap) {
+      HIP_TRY(hipStreamSynchronize(e->stream));
+      if (e->h_stage) HIP_TRY(hipHostFree(e->h_stage));
+      e->h_stage = nullptr;
+      e->h_stage_cap = 0;
+      if (hipHostMalloc(&e->h_stage, hb, 0) != hipSuccess)
+        return fail(DG_E_NOMEM, "pinned staging of %zu bytes failed", hb);
+      e->h_stage_cap = hb;
+    }
+    KRun* hr = (KRun*)e->h_stage;
+    u64* hf = (u64*)((char*)e->h_stage + b_runs);
+    for (int i = 0; i < k; i++) {
+      hr[i].rows = rows_of(&deltas[i]);
+      const bool full = !keys || !keys[i];
+      hr[i].keys = full ? nullptr : keys[i];
+      hr[i].n_keys = full ? 0 : n_keys[i];
+      hr[i].ctx = ctx_of(&dctxs[i]);
+    }
+    hf[0] = 0;
+    for (int i = 0; i < k; i++) hf[i + 1] = hf[i] + deltas[i].n;
+    for (int i = 0; i < k; i++) hf[k + i + 1] = hf[k + i] + hr[i].n_keys;
+    hf[2 * k + 1] = hf[2 * k] + state->n;
+    char* d = (char*)e->tmp;
+    KFoldArgs p{};
+    p.s = rows_of(state);
+    p.c0 = ctx_of(ctx);
+    p.runs = (const KRun*)d;
+    p.flat = (const u64*)(d + b_runs);
+    p.sstart = (u64*)(d + b_runs + b_flat);
+    p.dstart = (u32*)(d + b_runs + b_flat + b_ss);
+    p.tabC = (u64*)(d + b_runs + b_flat + b_ss + b_ds);
+    p.tabP = (u64*)(d + b_runs + b_flat + b_ss + b_ds + b_tab);
+    p.flag = (u32*)(d + b_runs + b_flat + b_ss + b_ds + 2 * b_tab);
+    p.k = k;
+    p.allmask = allmask;
+    p.T = T;
+    p.n_run_elems = m_rows + m_keys;
+    p.out = rows_out_of(out);
+    p.out_ctx_node = out_ctx->node;
+    p.out_ctx_cnt = out_ctx->cnt;
+    p.d_counts = e->d_counts;
+    HIP_TRY(hipMemcpyAsync(d, e->h_stage, hb, hipMemcpyHostToDevice, e->stream));
+    // start tables (empty runs keep 0), VV tables (absent node = 0) and the flag
+    HIP_TRY(hipMemsetAsync(p.sstart, 0, b_ss + b_ds + 2 * b_tab + 256, e->stream));
+    TRY(next_scan(e, &p.scan));
+    HIP_TRY(launch_kfold(p, e->stream));
+    HIP_TRY(hipMemcpyAsync(&e->h_counts[5], p.flag, sizeof(u32), hipMemcpyDeviceToHost, e->stream));
+    TRY(read_counts(e, 2));  // synchronizes; the staging buffer is free again
+    u32 flag = 0;
+    memcpy(&flag, &e->h_counts[5], sizeof(u32));
+    if (flag & KF_PREP_FAIL) return DG_OK;
+    if (flag) continue;
+    out->n = e->h_counts[0];
+    out_ctx->n = e->h_counts[1];
+    out_ctx->kind = DG_CTX_VV;
+    *stepwise = false;
+    return DG_OK;
+  }
+  return DG_OK;
+}
+
+// dg_apply_deltas: passes of up to KFOLD_MAX_K deltas (each a one-pass fold), or the
+// delta-by-delta fold when an input needs it.
+int apply_deltas(dg_engine* e, const dg_store* state, const dg_context* ctx, int k,
+                 const dg_store* deltas, const dg_context* dctxs, const uint64_t* const* keys,
+                 const uint64_t* n_keys, dg_store* out, dg_context* out_ctx) {
+  if (e->apply_mode == 1 || k == 0)
+    return fold_join(e, state, ctx, k, deltas, dctxs, keys, n_keys, out, out_ctx,
+                     "dg_apply_deltas");
+  u64 total = state->n, total_ctx = ctx->n;
+  for (int s = 0; s < k; s++) {
+    TRY(check_store(&deltas[s], "dg_apply_deltas delta"));
+    TRY(check_ctx(&dctxs[s], "dg_apply_deltas delta ctx"));
+    total += deltas[s].n;
+    total_ctx += dctxs[s].n;
+  }
+  if (out->cap < total || out_ctx->cap < total_ctx)
+    return fail(DG_E_CAPACITY, "dg_apply_deltas: output capacity too small (%llu rows, %llu ctx needed)",
+                (unsigned long long)total, (unsigned long long)total_ctx);
+  if (total && (!out->key || !out->val || !out->ts || !out->node || !out->cnt))
+    return fail(DG_E_INVAL, "dg_apply_deltas: null output column");
+  TRY(set_device(e));
+  const int passes = (k + KFOLD_MAX_K - 1) / KFOLD_MAX_K;
+  dg_store buf[2];
+  dg_context bufc[2];
+  if (passes > 1) TRY(fold_buffers(e, total, total_ctx, buf, bufc));
+  dg_store acc = *state;
+  dg_context acc_ctx = *ctx;
+  for (int q = 0; q < passes; q++) {
+    const int i0 = q * KFOLD_MAX_K, kq = std::min(KFOLD_MAX_K, k - i0);
+    dg_store* dst = (q == passes - 1) ? out : &buf[q & 1];
+    dg_context* dstc = (q == passes - 1) ? out_ctx : &bufc[q & 1];
+    bool stepwise = false;
+    TRY(kfold_pass(e, &acc, &acc_ctx, kq, deltas + i0, dctxs + i0, keys ? keys + i0 : nullptr,
+                   n_keys ? n_keys + i0 : nullptr, dst, dstc, &stepwise));
+    if (stepwise && e->apply_mode == 2)
+      return fail(DG_E_INVAL, "dg_apply_deltas: one-pass fold not applicable to this input");
+    if (stepwise)  // from the original state: fold_join reuses the ping-pong buffers
+      return fold_join(e, state, ctx, k, deltas, dctxs, keys, n_keys, out, out_ctx,
+                       "dg_apply_deltas");
+    acc = *dst;
+    acc_ctx = *dstc;
+  }
+  return DG_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -470,8 +620,7 @@ int dg_apply_deltas(dg_engine* e, const dg_store* state, const dg_context* ctx, 
   TRY(check_store(state, "dg_apply_deltas state"));
   TRY(check_ctx(ctx, "dg_apply_deltas ctx"));
   if (keys && !n_keys) return fail(DG_E_INVAL, "dg_apply_deltas: keys without n_keys");
-  return fold_join(e, state, ctx, k, deltas, dctxs, keys, n_keys, out, out_ctx,
-                   "dg_apply_deltas");
+  return apply_deltas(e, state, ctx, k, deltas, dctxs, keys, n_keys, out, out_ctx);
 }
 
 int dg_context_union(dg_engine* e, const dg_context* a, const dg_context* b, dg_context* out) {

@@ -55,6 +55,44 @@ inline size_t ctx_union_tmp_bytes(u64 na, u64 nb) {
   return (size_t)(na + nb) * 4 + (size_t)(na + nb) * 8 + (size_t)(na + nb + 1) * 4 + 64;
 }
 
+// ---- kfold.hip (dg_apply_deltas in one pass; see the file header)
+constexpr int KFOLD_BLOCK = 256;
+constexpr int KFOLD_CAP_S = 1024;  // LDS capacity per key bucket: state rows,
+constexpr int KFOLD_CAP_D = 512;   //   delta rows,
+constexpr int KFOLD_CAP_M = 512;   //   keyset entries
+constexpr int KFOLD_MAX_K = 64;    // deltas per pass (delta masks are u64)
+constexpr int KNT = 1024;          // VV tables cover node ids < KNT
+constexpr u32 KF_PREP_FAIL = 1, KF_OVERFLOW = 2;
+// mean fill per bucket the host sizes T for (capacity / mean >= 1.6: > 10 sigma)
+constexpr u64 KFOLD_MEAN_S = 640, KFOLD_MEAN_D = 320, KFOLD_MEAN_M = 320;
+struct KRun {  // delta i: its rows, keyset (keys == nullptr: every key) and context
+  Rows rows;
+  const u64* keys;
+  u64 n_keys;
+  Ctx ctx;
+};
+struct KFoldArgs {
+  Rows s;              // the state
+  Ctx c0;              // its context (a VV)
+  const KRun* runs;    // k deltas (device array)
+  int k;
+  u64 allmask;         // bit i: delta i joins every key (keys_i == NULL)
+  u64 T;               // key buckets
+  const u64* flat;     // 2k+2 prefix sums of run lengths: delta rows, keysets, state
+  u64 n_run_elems;     // delta rows + keyset entries
+  u64* sstart;         // T+1
+  u32* dstart;         // (T+1) x 2k
+  u64* tabC;           // k x KNT: c_i
+  u64* tabP;           // k x KNT: the state's context before delta i
+  RowsOut out;
+  u32* out_ctx_node;
+  u64* out_ctx_cnt;
+  Scan scan;
+  u64* d_counts;       // [0] output rows, [1] output context entries
+  u32* flag;           // KF_* bits: the caller must re-run the fold step by step
+};
+hipError_t launch_kfold(const KFoldArgs& p, hipStream_t st);
+
 // ---- segred.hip (segmented reductions over key runs)
 constexpr int SEG_BLOCK = 256;
 constexpr int SEG_ITEMS = 4;

@@ -159,3 +159,26 @@ def test_config4_shard_anti_entropy_round(rank):
     rows, ctx = R.apply_deltas(a["rows"], a["ctx"], [d["rows"]], [d["ctx"]], [d["keys"]])
     frows, fctx = R.join2(a["rows"], a["ctx"], b["rows"], b["ctx"])
     assert rows_equal(rows, frows) and ctx_equal(ctx, fctx)
+
+
+# ------------------------------------------------------------------ keyed fold, adversarial
+
+@pytest.mark.parametrize("seed", range(3))
+def test_random_keyed_fold_two_oracles(seed):
+    """The adversarial generator the GPU one-pass fold is tested on (tests/kfold_cases.py):
+    the C restatement's delta-by-delta fold == the term oracle's, including shared tuples,
+    rows outside keysets, full-state deltas and empty keysets."""
+    from kfold_cases import random_fold
+    st, ds = random_fold(seed, n_keys=40, k=6, rows_per_key=4, p_keys=0.3, p_take=0.6,
+                         p_outside=0.1, p_full=0.2)
+    if seed == 1:
+        ds[0] = dict(ds[0], keys=np.zeros(0, np.uint64))
+    rows, ctx = R.apply_deltas(st["rows"], st["ctx"], [d["rows"] for d in ds],
+                               [d["ctx"] for d in ds], [d["keys"] for d in ds])
+    t = soa_to_term(st["rows"], st["ctx"])
+    for d in ds:
+        dt = soa_to_term(d["rows"], d["ctx"])
+        ks = sorted(set(t.value) | set(dt.value)) if d["keys"] is None else [int(x) for x in d["keys"]]
+        t = T.join(t, dt, ks)
+    wrows, wctx = term_to_soa_raw(t)
+    assert rows_equal(rows, wrows) and ctx_equal(ctx, wctx)

@@ -1,0 +1,144 @@
+"""dg_apply_deltas' one-pass keyed fold (csrc/kfold.hip) on cuda:0, bit-exact against the
+C oracle's delta-by-delta fold of join/3 (causal_crdt.ex:383-384; tests/test_configs.py
+pins that fold to the term oracle on the same generator).  The `strict` engine runs with
+DG_APPLY_MODE=onepass, so a test that passes on it proves the one-pass kernels produced
+the result (that engine errors instead of falling back to the step-by-step fold).  The
+default engine covers the inputs the one-pass fold hands to the step-by-step fold."""
+import os
+
+import numpy as np
+import pytest
+
+from delta_crdt_ex_amd import workloads as W
+from delta_crdt_ex_amd._abi import DeltaGpuError
+from delta_crdt_ex_amd.store import Engine
+from kfold_cases import random_fold
+from oracle import ref as R
+from test_gpu_configs import keys_dev
+from test_gpu_parity import ctx_eq, rows_eq, up
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(mode):
+    os.environ["DG_APPLY_MODE"] = mode
+    try:
+        return Engine(0)
+    finally:
+        del os.environ["DG_APPLY_MODE"]
+
+
+@pytest.fixture(scope="module")
+def strict():
+    e = _engine("onepass")
+    yield e
+    e.close()
+
+
+@pytest.fixture(scope="module")
+def stepwise():
+    e = _engine("fold")
+    yield e
+    e.close()
+
+
+def run(engine, st, ds, keys=True):
+    s, c = up(st)
+    dd = [up(d) for d in ds]
+    ks = None
+    if keys:
+        ks = [None if d["keys"] is None else keys_dev(d["keys"]) for d in ds]
+    return engine.apply_deltas(s, c, [x[0] for x in dd], [x[1] for x in dd], ks)
+
+
+def want(st, ds, keys=True):
+    return R.apply_deltas(st["rows"], st["ctx"], [d["rows"] for d in ds],
+                          [d["ctx"] for d in ds], [d["keys"] for d in ds] if keys else None)
+
+
+def check(engine, st, ds, keys=True):
+    out, octx = run(engine, st, ds, keys)
+    wr, wc = want(st, ds, keys)
+    rows_eq(out, wr)
+    ctx_eq(octx, wc)
+
+
+@pytest.mark.parametrize("seed,k", [(0, 1), (1, 3), (2, 8), (3, 17), (4, 64)])
+def test_onepass_random(strict, seed, k):
+    st, ds = random_fold(seed, n_keys=3000, k=k)
+    check(strict, st, ds)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_onepass_crowded_keys(strict, seed):
+    """Many deltas touching the same keys with the same tuples: big key groups, tuples
+    held by the state and several deltas, adds and removes interleaved."""
+    st, ds = random_fold(10 + seed, n_keys=400, k=24, rows_per_key=8, p_keys=0.4, p_take=0.8,
+                         p_outside=0.05)
+    check(strict, st, ds)
+
+
+def test_onepass_full_state_deltas(strict):
+    """keys_i NULL (a full-state join of that delta) mixed with keyed deltas, and
+    keys=None for every delta."""
+    st, ds = random_fold(20, n_keys=2000, k=12, p_full=0.3)
+    assert any(d["keys"] is None for d in ds) and any(d["keys"] is not None for d in ds)
+    check(strict, st, ds)
+    check(strict, st, ds, keys=False)
+
+
+def test_onepass_empty_inputs(strict):
+    st, ds = random_fold(21, n_keys=1500, k=6)
+    # empty keysets: every delta row is carried right-biased
+    d0 = dict(ds[0], keys=np.zeros(0, np.uint64))
+    # an empty delta (no rows) with a keyset: removals only
+    e = tuple(c[:0] for c in ds[1]["rows"])
+    d1 = dict(ds[1], rows=e)
+    check(strict, st, [d0, d1] + ds[2:])
+    # an empty state
+    es = {"rows": tuple(c[:0] for c in st["rows"]), "ctx": st["ctx"]}
+    check(strict, es, ds)
+
+
+def test_onepass_large_node_ids_in_rows(strict):
+    """Row node ids >= the VV table width that no context names: never covered."""
+    st, ds = random_fold(22, n_keys=2000, k=8, n_nodes=40, node_base=1000, ctx_node_max=1024)
+    assert st["rows"][3].max() >= 1024
+    check(strict, st, ds)
+
+
+def test_onepass_two_passes(strict):
+    """70 deltas: two one-pass folds of 64 and 6 deltas."""
+    st, ds = random_fold(23, n_keys=3000, k=70, p_keys=0.02)
+    check(strict, st, ds)
+
+
+@pytest.mark.parametrize("case", ["context node ids", "unhashed keys", "dot-set contexts"])
+def test_stepwise_fallback(engine, strict, case):
+    """Inputs the one-pass fold does not take: the strict engine refuses them, the
+    default engine folds them delta by delta, bit-exact."""
+    if case == "context node ids":
+        st, ds = random_fold(30, n_keys=2000, k=6, n_nodes=40, node_base=1000)
+    elif case == "unhashed keys":  # every key in bucket 0: over the LDS capacity
+        st, ds = random_fold(31, n_keys=3000, k=6, hashed=False)
+    else:
+        st, ds = random_fold(32, n_keys=800, k=5, dots_ctx=True)
+    with pytest.raises(DeltaGpuError, match="one-pass fold not applicable"):
+        run(strict, st, ds)
+    check(engine, st, ds)
+
+
+def test_config3_onepass(strict):
+    base, deltas = W.config3(n_keys=200_000, n_replicas=64, touch=0.01, seed=5)
+    check(strict, base, deltas)
+
+
+def test_config3_onepass_equals_stepwise_large(strict, stepwise):
+    """2M keys x 64 deltas: the one-pass fold and the step-by-step fold of join/3 agree
+    row for row."""
+    base, deltas = W.config3(n_keys=2_000_000, n_replicas=64, touch=0.01, seed=6)
+    a, ac = run(strict, base, deltas)
+    b, bc = run(stepwise, base, deltas)
+    x, y = a.to_numpy(), b.to_numpy()
+    assert a.n == b.n and all(np.array_equal(p, q) for p, q in zip(x, y))
+    assert all(np.array_equal(p, q) for p, q in zip(ac.to_numpy(), bc.to_numpy()))
