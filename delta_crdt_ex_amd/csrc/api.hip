@@ -508,10 +508,11 @@ int kfold_pass(dg_engine* e, const dg_store* state, const dg_context* ctx, int k
       hr[i].n_keys = full ? 0 : n_keys[i];
       hr[i].ctx = ctx_of(&dctxs[i]);
     }
+    auto chunks = [&](u64 n) { return ceil_div(n, KFOLD_FILL_CHUNK); };
     hf[0] = 0;
-    for (int i = 0; i < k; i++) hf[i + 1] = hf[i] + deltas[i].n;
-    for (int i = 0; i < k; i++) hf[k + i + 1] = hf[k + i] + hr[i].n_keys;
-    hf[2 * k + 1] = hf[2 * k] + state->n;
+    for (int i = 0; i < k; i++) hf[i + 1] = hf[i] + chunks(deltas[i].n);
+    for (int i = 0; i < k; i++) hf[k + i + 1] = hf[k + i] + chunks(hr[i].n_keys);
+    hf[2 * k + 1] = hf[2 * k] + chunks(state->n);
     char* d = (char*)e->tmp;
     KFoldArgs p{};
     p.s = rows_of(state);
@@ -526,7 +527,7 @@ int kfold_pass(dg_engine* e, const dg_store* state, const dg_context* ctx, int k
     p.k = k;
     p.allmask = allmask;
     p.T = T;
-    p.n_run_elems = m_rows + m_keys;
+    p.n_fill_chunks = hf[2 * k + 1];
     p.out = rows_out_of(out);
     p.out_ctx_node = out_ctx->node;
     p.out_ctx_cnt = out_ctx->cnt;

@@ -56,13 +56,14 @@ inline size_t ctx_union_tmp_bytes(u64 na, u64 nb) {
 }
 
 // ---- kfold.hip (dg_apply_deltas in one pass; see the file header)
-constexpr int KFOLD_BLOCK = 256;
+constexpr int KFOLD_BLOCK = 512;
 constexpr int KFOLD_CAP_S = 1024;  // LDS capacity per key bucket: state rows,
 constexpr int KFOLD_CAP_D = 512;   //   delta rows,
 constexpr int KFOLD_CAP_M = 512;   //   keyset entries
 constexpr int KFOLD_MAX_K = 64;    // deltas per pass (delta masks are u64)
 constexpr int KNT = 1024;          // VV tables cover node ids < KNT
 constexpr u32 KF_PREP_FAIL = 1, KF_OVERFLOW = 2;
+constexpr u64 KFOLD_FILL_CHUNK = 256 * 8;  // elements per workgroup of the bucket fill
 // mean fill per bucket the host sizes T for (capacity / mean >= 1.6: > 10 sigma)
 constexpr u64 KFOLD_MEAN_S = 640, KFOLD_MEAN_D = 320, KFOLD_MEAN_M = 320;
 struct KRun {  // delta i: its rows, keyset (keys == nullptr: every key) and context
@@ -78,8 +79,9 @@ struct KFoldArgs {
   int k;
   u64 allmask;         // bit i: delta i joins every key (keys_i == NULL)
   u64 T;               // key buckets
-  const u64* flat;     // 2k+2 prefix sums of run lengths: delta rows, keysets, state
-  u64 n_run_elems;     // delta rows + keyset entries
+  const u64* flat;     // 2k+2 prefix sums of run lengths in KFOLD_FILL_CHUNKs: delta
+                       // rows, keysets, state
+  u64 n_fill_chunks;   // flat[2k+1]
   u64* sstart;         // T+1
   u32* dstart;         // (T+1) x 2k
   u64* tabC;           // k x KNT: c_i

@@ -46,7 +46,6 @@ constexpr int CM = KFOLD_CAP_M;  // keyset markers per bucket
 constexpr int CU = CD + CM;
 constexpr u32 MARK = 1u << 15;   // utag: (src << 16) | MARK? | pre-sort slot
 constexpr u32 SLOT = MARK - 1;
-static_assert(CS <= 4 * KB && CU <= 4 * KB, "scan_flags covers 4 items per thread");
 static_assert(2 * KFOLD_MAX_K <= KB, "one thread per run");
 static_assert(CU <= SLOT + 1, "slot bits");
 
@@ -90,9 +89,9 @@ __global__ __launch_bounds__(KNT) void kfold_prep_kernel(KFoldArgs p) {
     p.tabP[nd] = p.c0.cnt[e];
     pres[nd] = 1;
   }
-  for (int i = 0; i < k; i++) {
+  for (int i = n / WAVE; i < k; i += KNT / WAVE) {  // one wave per delta context
     const Ctx c = p.runs[i].ctx;
-    for (u64 e = n; e < c.n; e += KNT) {
+    for (u64 e = n % WAVE; e < c.n; e += WAVE) {
       const u32 nd = c.node[e];
       if (nd >= (u32)KNT) {
         atomicOr(p.flag, KF_PREP_FAIL);
@@ -103,11 +102,18 @@ __global__ __launch_bounds__(KNT) void kfold_prep_kernel(KFoldArgs p) {
     }
   }
   __syncthreads();
-  // prefix unions: C_i = C_{i-1} ⊔ c_i, per node the max (absent = 0)
+  // prefix unions: C_i = C_{i-1} ⊔ c_i, per node the max (absent = 0); loads batched
+  // ahead of the stores they would otherwise be ordered behind
   u64 acc = p.tabP[n];
-  for (int i = 0; i < k; i++) {
-    acc = max(acc, p.tabC[(u64)i * KNT + n]);
-    if (i + 1 < k) p.tabP[(u64)(i + 1) * KNT + n] = acc;
+  for (int i0 = 0; i0 < k; i0 += 8) {
+    u64 c[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) c[q] = i0 + q < k ? p.tabC[(u64)(i0 + q) * KNT + n] : 0ull;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      acc = max(acc, c[q]);
+      if (i0 + q + 1 < k) p.tabP[(u64)(i0 + q + 1) * KNT + n] = acc;
+    }
   }
   // C_k in node order
   u32 tot;
@@ -135,55 +141,89 @@ __device__ __forceinline__ const u64* run_keys(const KFoldArgs& p, int r, u64* n
   return p.s.key;
 }
 
+// One workgroup per chunk of FILL_CHUNK elements of ONE run (chunk prefix sums per run
+// in p.flat), so the run's key pointer is uniform and the key loads coalesce.
+constexpr u64 FILL_CHUNK = KFOLD_FILL_CHUNK;
 __global__ __launch_bounds__(256) void kfold_fill_kernel(KFoldArgs p) {
   __shared__ u64 flat[2 * KFOLD_MAX_K + 2];
   const int nr = 2 * p.k + 1;  // runs incl. the state
   for (int i = threadIdx.x; i <= nr; i += 256) flat[i] = p.flat[i];
   __syncthreads();
-  const u64 total = flat[nr], T = p.T;
-  const u32 stride = 2 * p.k;
-  for (u64 g = (u64)blockIdx.x * 256 + threadIdx.x; g < total; g += (u64)gridDim.x * 256) {
-    int lo = 0, hi = nr;  // flat[lo] <= g < flat[hi]; empty runs are skipped
+  const u64 T = p.T, stride = 2 * (u64)p.k;
+  for (u64 c = blockIdx.x; c < flat[nr]; c += gridDim.x) {
+    int lo = 0, hi = nr;  // flat[lo] <= c < flat[hi]; empty runs are skipped
     while (hi - lo > 1) {
       const int mid = (lo + hi) >> 1;
-      if (flat[mid] <= g)
+      if (flat[mid] <= c)
         lo = mid;
       else
         hi = mid;
     }
     const int r = lo;
-    const u64 j = g - flat[r];
     u64 n;
     const u64* keys = run_keys(p, r, &n);
-    const u64 b = bucket_of(keys[j], T);
-    u64 bb = j == 0 ? 0 : bucket_of(keys[j - 1], T) + 1;
-    const u64 end = (j == n - 1) ? T : b;
-    for (; bb <= end; bb++) {
-      const u64 v = bb <= b ? j : n;
-      if (r == nr - 1)
-        p.sstart[bb] = v;
-      else
-        p.dstart[bb * stride + r] = (u32)v;
+    const u64 j0 = (c - flat[r]) * FILL_CHUNK;
+    for (u64 j = j0 + threadIdx.x; j < min<u64>(j0 + FILL_CHUNK, n); j += 256) {
+      const u64 b = bucket_of(keys[j], T);
+      u64 bb = j == 0 ? 0 : bucket_of(keys[j - 1], T) + 1;
+      const u64 end = (j == n - 1) ? T : b;
+      for (; bb <= end; bb++) {
+        const u64 v = bb <= b ? j : n;
+        if (r == nr - 1)
+          p.sstart[bb] = v;
+        else
+          p.dstart[bb * stride + r] = (u32)v;
+      }
     }
   }
 }
 
 // ------------------------------------------------------------------------ main
+#ifdef DG_STAMPS
+// Diagnostic build only (DG_STAMPS=1): per-bucket phase timestamps (s_memrealtime) by
+// lane 0, read back with dg_debug_kfold_stamps (tools/kfold_stamps.py).
+__device__ u64 g_kf_stamps[65536 * 8];
+#define KSTAMP(tile, k)                                                              \
+  do {                                                                               \
+    __syncthreads();                                                                 \
+    if (threadIdx.x == 0 && (tile) < 65536)                                          \
+      g_kf_stamps[(tile) * 8 + (k)] = __builtin_amdgcn_s_memrealtime();              \
+  } while (0)
+#else
+#define KSTAMP(tile, k) \
+  do {                  \
+  } while (0)
+#endif
+
+constexpr int NSUB = 512;  // sub-buckets of a bucket's key range (LDS counting sort)
+constexpr int PER = 2;     // items per thread in the block scans
+static_assert(CS <= PER * KB && CU <= PER * KB && NSUB <= PER * KB, "scan coverage");
+
 struct KLds {
   u64 skey[CS], sval[CS], scnt[CS];
   i64 sts[CS];
   u32 snode[CS];
-  u64 dkey[CD], dval[CD], dcnt[CD];
+  u64 dkey[CD], dval[CD], dcnt[CD];  // delta rows by slot (= pre-sort item index)
   i64 dts[CD];
   u32 dnode[CD];
-  u64 ukey[CU];
-  u32 utag[CU];
-  unsigned short spre[CS + 1], upre[CU + 1], slbu[CS];
-  unsigned char ssurv[CS], usurv[CU];
+  u64 ukey[CU];                       // items: delta rows [0, nD), keyset markers [nD, nU)
+  u32 utag[CU];                       // (src << 16) | MARK? | slot
+  unsigned short order[CU];           // items in (key, tag) order
+  unsigned short ustart[NSUB + 1];    // sub-bucket b: order[ustart[b], ustart[b+1])
+  unsigned short sfirst[NSUB + 1];    //               state rows [sfirst[b], sfirst[b+1])
+  union {
+    u32 ucnt[NSUB];                   // counting-sort histogram / fill counters
+    struct {
+      unsigned short spre[CS + 1], upre[CU + 1];  // exclusive survivor prefixes
+    } pre;
+  } x;
+  unsigned short slbu[CS];            // state row -> first sorted item with key >= its key
+  unsigned char ssurv[CS], usurv[CU]; // usurv by sorted position
   u32 roff[2 * KFOLD_MAX_K + 1];
   u32 rbeg[2 * KFOLD_MAX_K];
   u32 wave[KB / WAVE + 1];
-  u64 bcast[2];
+  u64 lb[3 * (KB / WAVE) + 2];
+  u64 bcast[1];
 };
 
 __device__ __forceinline__ Row srow(const KLds& s, u32 i) {
@@ -206,58 +246,29 @@ __device__ __forceinline__ Row drow(const KLds& s, u32 d) {
   return r;
 }
 
-// first sorted item with key >= x
-__device__ __forceinline__ u32 lower_key(const u64* a, u32 n, u64 x) {
-  u32 lo = 0, hi = n;
-  while (lo < hi) {
-    const u32 mid = (lo + hi) >> 1;
-    if (a[mid] < x)
-      lo = mid + 1;
-    else
-      hi = mid;
-  }
-  return lo;
+// sub-bucket of a key of bucket t: the next log2(NSUB) bits of its position in key space
+__device__ __forceinline__ u32 sub_of(u64 key, u64 T, u64 t) {
+  return (u32)(__umul64hi(key, T * NSUB) - t * NSUB);
 }
 
-// exclusive prefix of n <= 4*KB flags into pre[0..n]
-__device__ __forceinline__ void scan_flags(const unsigned char* f, u32 n, unsigned short* pre,
-                                           u32* wave) {
-  const u32 b = threadIdx.x * 4;
-  u32 c[4], sum = 0;
+// exclusive prefix of n <= PER*KB values into pre[0..n] (pre[n] = total)
+template <class V>
+__device__ __forceinline__ void scan_excl(const V* in, u32 n, unsigned short* pre, u32* wave) {
+  const u32 b = threadIdx.x * PER;
+  u32 c[PER], sum = 0;
 #pragma unroll
-  for (int q = 0; q < 4; q++) {
-    c[q] = (b + q < n) ? f[b + q] : 0u;
+  for (int q = 0; q < PER; q++) {
+    c[q] = (b + q < n) ? (u32)in[b + q] : 0u;
     sum += c[q];
   }
   u32 tot;
   u32 off = block_excl_scan<KB>(sum, wave, &tot);
 #pragma unroll
-  for (int q = 0; q < 4; q++) {
+  for (int q = 0; q < PER; q++) {
     if (b + q < n) pre[b + q] = (unsigned short)off;
     off += c[q];
   }
   if (threadIdx.x == 0) pre[n] = (unsigned short)tot;
-}
-
-// bitonic sort of n (a power of two) (key, tag) pairs, ascending
-__device__ __forceinline__ void sort_items(u64* key, u32* tag, u32 n) {
-  for (u32 size = 2; size <= n; size <<= 1)
-    for (u32 stride = size >> 1; stride > 0; stride >>= 1) {
-      for (u32 idx = threadIdx.x; idx < n / 2; idx += KB) {
-        const u32 i = ((idx & ~(stride - 1)) << 1) | (idx & (stride - 1));
-        const u32 j = i + stride;
-        const u64 ki = key[i], kj = key[j];
-        const u32 ti = tag[i], tj = tag[j];
-        const bool gt = ki > kj || (ki == kj && ti > tj);
-        if (gt == ((i & size) == 0)) {
-          key[i] = kj;
-          key[j] = ki;
-          tag[i] = tj;
-          tag[j] = ti;
-        }
-      }
-      __syncthreads();
-    }
 }
 
 __global__ __launch_bounds__(KB) void kfold_kernel(KFoldArgs p) {
@@ -265,13 +276,15 @@ __global__ __launch_bounds__(KB) void kfold_kernel(KFoldArgs p) {
   if (*p.flag & KF_PREP_FAIL) return;  // every workgroup leaves: no ticket is taken
   const int tid = threadIdx.x;
   const int k = p.k, nr = 2 * k;
+  const u64 T = p.T;
   if (tid == 0) {
     const u32 t = atomicAdd(p.scan.ticket, 1u);
-    if ((u64)t == p.T - 1) atomicExch(p.scan.ticket, 0u);
+    if ((u64)t == T - 1) atomicExch(p.scan.ticket, 0u);
     s.bcast[0] = t;
   }
   __syncthreads();
   const u64 t = s.bcast[0];
+  KSTAMP(t, 0);
   const u64 s0 = p.sstart[t];
   u32 nS = (u32)min<u64>(p.sstart[t + 1] - s0, 0xffffffffull);
   u32 len = 0;
@@ -328,25 +341,58 @@ __global__ __launch_bounds__(KB) void kfold_kernel(KFoldArgs p) {
       s.utag[q] = ((u32)(lo - k) << 16) | MARK | q;
     }
   }
-  u32 np2 = 2;
-  while (np2 < nU) np2 <<= 1;
-  for (u32 q = nU + tid; q < np2; q += KB) {
-    s.ukey[q] = ~0ull;
-    s.utag[q] = ~0u;
+  for (u32 b = tid; b < NSUB; b += KB) s.x.ucnt[b] = 0;
+  KSTAMP(t, 1);
+  __syncthreads();
+
+  // ---- counting sort of the items by sub-bucket, then (key, tag) within one
+  for (u32 q = tid; q < nU; q += KB) atomicAdd(&s.x.ucnt[sub_of(s.ukey[q], T, t)], 1u);
+  for (u32 i = tid; i < nS; i += KB) {  // state rows: first row of every sub-bucket
+    const u32 sb = sub_of(s.skey[i], T, t);
+    u32 b = i == 0 ? 0 : sub_of(s.skey[i - 1], T, t) + 1;
+    for (; b <= sb; b++) s.sfirst[b] = (unsigned short)i;
+    if (i == nS - 1)
+      for (b = sb + 1; b <= (u32)NSUB; b++) s.sfirst[b] = (unsigned short)nS;
+  }
+  if (nS == 0)
+    for (u32 b = tid; b <= (u32)NSUB; b += KB) s.sfirst[b] = 0;
+  __syncthreads();
+  scan_excl(s.x.ucnt, NSUB, s.ustart, s.wave);
+  __syncthreads();
+  for (u32 b = tid; b < NSUB; b += KB) s.x.ucnt[b] = 0;
+  __syncthreads();
+  unsigned short* bin = s.slbu;  // items grouped by sub-bucket (slbu is free until evaluation)
+  for (u32 q = tid; q < nU; q += KB) {
+    const u32 sb = sub_of(s.ukey[q], T, t);
+    bin[s.ustart[sb] + atomicAdd(&s.x.ucnt[sb], 1u)] = (unsigned short)q;
   }
   __syncthreads();
-  if (nU > 1) sort_items(s.ukey, s.utag, np2);
+  for (u32 q = tid; q < nU; q += KB) {  // rank by (key, tag) within the (small) sub-bucket
+    const u64 kq = s.ukey[q];
+    const u32 tq = s.utag[q], sb = sub_of(kq, T, t), lo = s.ustart[sb], hi = s.ustart[sb + 1];
+    u32 rank = 0;
+    for (u32 e = lo; e < hi; e++) {
+      const u32 w = bin[e];
+      const u64 kw = s.ukey[w];
+      rank += (kw < kq || (kw == kq && s.utag[w] < tq)) ? 1u : 0u;
+    }
+    s.order[lo + rank] = (unsigned short)q;
+  }
+  KSTAMP(t, 2);
+  __syncthreads();
 
-  // ---- evaluate every candidate
+  // ---- evaluate every candidate (a key's items and state rows share its sub-bucket)
   const u64 all = p.allmask;
   for (u32 i = tid; i < nS; i += KB) {
-    const u64 x = s.skey[i];
-    const u32 lb = lower_key(s.ukey, nU, x);
-    s.slbu[i] = (unsigned short)lb;
-    u64 K = all, R = 0, M = 0;
     const Row r = srow(s, i);
-    for (u32 q = lb; q < nU && s.ukey[q] == x; q++) {
-      const u32 tg = s.utag[q], src = tg >> 16;
+    const u32 sb = sub_of(r.key, T, t);
+    u32 q = s.ustart[sb];
+    const u32 qe = s.ustart[sb + 1];
+    while (q < qe && s.ukey[s.order[q]] < r.key) q++;
+    s.slbu[i] = (unsigned short)q;
+    u64 K = all, R = 0, M = 0;
+    for (; q < qe && s.ukey[s.order[q]] == r.key; q++) {
+      const u32 tg = s.utag[s.order[q]], src = tg >> 16;
       if (tg & MARK) {
         K |= 1ull << src;
       } else {
@@ -357,18 +403,17 @@ __global__ __launch_bounds__(KB) void kfold_kernel(KFoldArgs p) {
     s.ssurv[i] = present(true, K, R, M, r.node, r.cnt, p.tabC, p.tabP);
   }
   for (u32 q = tid; q < nU; q += KB) {
-    const u32 tg = s.utag[q];
+    const u32 tg = s.utag[s.order[q]];
     bool surv = false;
     if (!(tg & MARK)) {
-      const u64 x = s.ukey[q];
       const u32 src = tg >> 16;
       const Row r = drow(s, tg & SLOT);
-      u32 gb = q;
-      while (gb > 0 && s.ukey[gb - 1] == x) gb--;
+      const u32 sb = sub_of(r.key, T, t);
       u64 K = all, R = 0, M = 0;
       bool rep = true;  // the first holder of this tuple: the state, else the lowest delta
-      for (u32 e = gb; e < nU && s.ukey[e] == x; e++) {
-        const u32 te = s.utag[e], se = te >> 16;
+      for (u32 e = s.ustart[sb], ee = s.ustart[sb + 1]; e < ee; e++) {
+        const u32 te = s.utag[s.order[e]], se = te >> 16;
+        if (s.ukey[s.order[e]] != r.key) continue;
         if (te & MARK) {
           K |= 1ull << se;
         } else {
@@ -379,49 +424,45 @@ __global__ __launch_bounds__(KB) void kfold_kernel(KFoldArgs p) {
           }
         }
       }
-      if (rep) {  // a tuple the state holds is evaluated (and emitted) as the state's row
-        u32 lo = lower_key(s.skey, nS, x);
-        while (lo < nS && s.skey[lo] == x && row_cmp(srow(s, lo), r) < 0) lo++;
-        if (lo < nS && row_eq(srow(s, lo), r)) rep = false;
-      }
+      // a tuple the state holds is evaluated (and emitted) as the state's row
+      for (u32 i = s.sfirst[sb], ie = s.sfirst[sb + 1]; rep && i < ie; i++)
+        if (row_eq(srow(s, i), r)) rep = false;
       if (rep) surv = present(false, K, R, M, r.node, r.cnt, p.tabC, p.tabP);
     }
     s.usurv[q] = surv;
   }
+  KSTAMP(t, 3);
   __syncthreads();
-  scan_flags(s.ssurv, nS, s.spre, s.wave);
-  scan_flags(s.usurv, nU, s.upre, s.wave);
+  scan_excl(s.ssurv, nS, s.x.pre.spre, s.wave);
+  scan_excl(s.usurv, nU, s.x.pre.upre, s.wave);
   __syncthreads();
+  KSTAMP(t, 4);
 
   // ---- output offset of the bucket (decoupled look-back in ticket order)
-  const u32 total = (u32)s.spre[nS] + s.upre[nU];
-  if (tid < WAVE) {
-    u64 prefix = 0;
-    if (t == 0) {
-      if (tid == 0) lb_publish(p.scan.state, 0, p.scan.epoch, LB_INC, total);
-    } else {
-      if (tid == 0) lb_publish(p.scan.state, t, p.scan.epoch, LB_AGG, total);
-      prefix = lb_lookback(p.scan.state, t, p.scan.epoch, p.scan.err);
-      if (tid == 0) lb_publish(p.scan.state, t, p.scan.epoch, LB_INC, prefix + total);
-    }
-    if (tid == 0) {
-      s.bcast[1] = prefix;
-      if (t == p.T - 1) p.d_counts[0] = prefix + total;
-    }
+  const u32 total = (u32)s.x.pre.spre[nS] + s.x.pre.upre[nU];
+  u64 base = 0;
+  if (t == 0) {
+    if (tid == 0) lb_publish(p.scan.state, 0, p.scan.epoch, LB_INC, total);
+  } else {  // block-wide: one round trip reaches a whole launch round of predecessors
+    if (tid == 0) lb_publish(p.scan.state, t, p.scan.epoch, LB_AGG, total);
+    base = lb_lookback_block<KB, 1>(p.scan.state, t, p.scan.epoch, p.scan.err, s.lb);
+    if (tid == 0) lb_publish(p.scan.state, t, p.scan.epoch, LB_INC, base + total);
   }
-  __syncthreads();
-  const u64 base = s.bcast[1];
+  if (tid == 0 && t == T - 1) p.d_counts[0] = base + total;
+  KSTAMP(t, 5);
 
   // ---- survivors in tuple order: rank = survivors of smaller keys + of the same key
   //      with a smaller tuple
+  const unsigned short* spre = s.x.pre.spre;
+  const unsigned short* upre = s.x.pre.upre;
   for (u32 i = tid; i < nS; i += KB) {
     if (!s.ssurv[i]) continue;
     const Row r = srow(s, i);
     const u32 lb = s.slbu[i];
     u32 less = 0;
-    for (u32 q = lb; q < nU && s.ukey[q] == r.key; q++)
-      if (s.usurv[q] && row_cmp(drow(s, s.utag[q] & SLOT), r) < 0) less++;
-    const u64 o = base + s.spre[i] + s.upre[lb] + less;
+    for (u32 q = lb; q < nU && s.ukey[s.order[q]] == r.key; q++)
+      if (s.usurv[q] && row_cmp(drow(s, s.utag[s.order[q]] & SLOT), r) < 0) less++;
+    const u64 o = base + spre[i] + upre[lb] + less;
     p.out.key[o] = r.key;
     p.out.val[o] = r.val;
     p.out.ts[o] = r.ts;
@@ -430,32 +471,42 @@ __global__ __launch_bounds__(KB) void kfold_kernel(KFoldArgs p) {
   }
   for (u32 q = tid; q < nU; q += KB) {
     if (!s.usurv[q]) continue;
-    const Row r = drow(s, s.utag[q] & SLOT);
-    u32 gb = q;
-    while (gb > 0 && s.ukey[gb - 1] == r.key) gb--;
+    const Row r = drow(s, s.utag[s.order[q]] & SLOT);
+    const u32 sb = sub_of(r.key, T, t);
+    u32 gb = s.ustart[sb];
+    while (s.ukey[s.order[gb]] != r.key) gb++;
     u32 less = 0;
-    for (u32 e = gb; e < nU && s.ukey[e] == r.key; e++)
-      if (s.usurv[e] && row_cmp(drow(s, s.utag[e] & SLOT), r) < 0) less++;
-    const u32 ls = lower_key(s.skey, nS, r.key);
+    for (u32 e = gb; e < nU && s.ukey[s.order[e]] == r.key; e++)
+      if (s.usurv[e] && row_cmp(drow(s, s.utag[s.order[e]] & SLOT), r) < 0) less++;
+    u32 ls = s.sfirst[sb];
+    const u32 le = s.sfirst[sb + 1];
+    while (ls < le && s.skey[ls] < r.key) ls++;
     u32 sl = 0;
-    for (u32 i = ls; i < nS && s.skey[i] == r.key; i++)
+    for (u32 i = ls; i < le && s.skey[i] == r.key; i++)
       if (s.ssurv[i] && row_cmp(srow(s, i), r) < 0) sl++;
-    const u64 o = base + s.spre[ls] + sl + s.upre[gb] + less;
+    const u64 o = base + spre[ls] + sl + upre[gb] + less;
     p.out.key[o] = r.key;
     p.out.val[o] = r.val;
     p.out.ts[o] = r.ts;
     p.out.node[o] = r.node;
     p.out.cnt[o] = r.cnt;
   }
+  KSTAMP(t, 6);
 }
 
 }  // namespace
 
+#ifdef DG_STAMPS
+extern "C" int dg_debug_kfold_stamps(unsigned long long* host, size_t n) {
+  if (n > 65536 * 8) n = 65536 * 8;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_kf_stamps), n * 8) == hipSuccess ? 0 : -3;
+}
+#endif
+
 hipError_t launch_kfold(const KFoldArgs& p, hipStream_t st) {
   hipLaunchKernelGGL(kfold_prep_kernel, dim3(1), dim3(KNT), 0, st, p);
-  const u64 total = p.s.n + p.n_run_elems;
-  if (total) {
-    const u64 g = std::min<u64>((total + 255) / 256, 4096);
+  if (p.n_fill_chunks) {
+    const u64 g = std::min<u64>(p.n_fill_chunks, 8192);
     hipLaunchKernelGGL(kfold_fill_kernel, dim3((u32)g), dim3(256), 0, st, p);
   }
   hipLaunchKernelGGL(kfold_kernel, dim3((u32)p.T), dim3(KB), 0, st, p);
