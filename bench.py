@@ -12,8 +12,9 @@ Rank 0 prints ONE JSON line.  `value` = Σ input rows over all ranks x K / the m
 over ranks of the timed region.  `roofline` prices the join kernel (one launch per
 step: rows + context union) by its algorithmic bytes 36·(N_in + N_out) + 12·(|c_a| +
 |c_b| + |c_out|) over its average duration from HIP events on the engine stream.
-`cpu_baseline` times the C restatement (oracle/deltaref.c, 1 thread) on the same
-config-2 inputs, repeated for ~10 s.  A secondary Merkle hash+diff rate (config-4
+`cpu_baseline` times the C restatement (oracle/deltaref.c) on the same config-2
+inputs on all host cores (OpenMP over key shards, oracle/deltaref_mt.c) and on one core,
+~6 s each.  A secondary Merkle hash+diff rate (config-4
 shape, 1M keys, 1 % differing) is reported under `merkle`.
 """
 from __future__ import annotations
@@ -62,24 +63,45 @@ def _traffic_from_profiles(n_in, n_out):
     return d.get("hbm_bytes_per_launch")
 
 
-def cpu_baseline(a, b, budget_s=10.0):
+def _host_threads():
+    """The host cores this process may use (the GPU box pins OMP_NUM_THREADS to its
+    CPU share; os.cpu_count() there shows the whole machine)."""
+    v = os.environ.get("OMP_NUM_THREADS")
+    if v and v.isdigit() and int(v) > 0:
+        return int(v)
+    return len(os.sched_getaffinity(0))
+
+
+def cpu_baseline(a, b, budget_s=6.0):
+    """The C restatement of join/3 on the same config-2 replicas: on all host cores
+    (deltaref_mt.c, OpenMP over key shards; the reported value) and on one core."""
     from oracle import ref as R  # the checker / CPU baseline only
     R.lib()
     n_in = len(a["rows"][0]) + len(b["rows"][0])
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        R.join2(a["rows"], a["ctx"], b["rows"], b["ctx"])
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or reps >= 1000:
-            break
+
+    def rate(fn):
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            fn()
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= budget_s or reps >= 2000:
+                return n_in * reps / el, reps, el
+
+    threads = _host_threads()
+    mt = R.JoinMT(a["rows"], a["ctx"], b["rows"], b["ctx"], threads)
+    v_mt, r_mt, e_mt = rate(mt)
+    v_1, r_1, e_1 = rate(R.JoinMT(a["rows"], a["ctx"], b["rows"], b["ctx"], 1))
     return {
-        "value": n_in * reps / el,
+        "value": v_mt,
         "unit": "merged dots/s",
-        "cores": 1,
+        "cores": threads,
         "kind": "port",
-        "sample": f"C restatement of aw_lww_map.ex join/3 (oracle/deltaref.c, gcc -O2, 1 thread) on "
-                  f"the same config-2 replicas ({n_in} rows in), {reps} joins in {el:.1f} s",
+        "sample": f"C restatement of aw_lww_map.ex join/3 (oracle/deltaref.c + deltaref_mt.c, gcc "
+                  f"-O2 -fopenmp, {threads} threads over key-range shards) on the same config-2 "
+                  f"replicas ({n_in} rows in), {r_mt} joins in {e_mt:.1f} s",
+        "single_core": {"value": v_1, "cores": 1,
+                        "sample": f"the same, 1 thread: {r_1} joins in {e_1:.1f} s"},
     }
 
 

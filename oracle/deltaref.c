@@ -187,11 +187,10 @@ static void join_dot_sets(const dg_store* a, uint64_t p, uint64_t pe, const dg_c
   }
 }
 
-/* join/3 (aw_lww_map.ex:153-158) = Dots.union of contexts + join_or_maps/4. */
-int ref_join2(const dg_store* a, const dg_context* ca, const dg_store* b, const dg_context* cb,
-              const uint64_t* keys, uint64_t n_keys, dg_store* out, dg_context* out_ctx) {
+/* join_or_maps/4 over the rows (aw_lww_map.ex:161-193); out->n = rows written. */
+int ref_join2_rows(const dg_store* a, const dg_context* ca, const dg_store* b,
+                   const dg_context* cb, const uint64_t* keys, uint64_t n_keys, dg_store* out) {
   if (out->cap < a->n + b->n) REF_E(DG_E_CAPACITY);
-  if (out_ctx->cap < ca->n + cb->n) REF_E(DG_E_CAPACITY);
   out->n = 0;
   uint64_t i = 0, j = 0;
   while (i < a->n || j < b->n) {
@@ -230,6 +229,16 @@ int ref_join2(const dg_store* a, const dg_context* ca, const dg_store* b, const 
     i = ie;
     j = je;
   }
+  return DG_OK;
+}
+
+/* join/3 (aw_lww_map.ex:153-158) = Dots.union of contexts + join_or_maps/4. */
+int ref_join2(const dg_store* a, const dg_context* ca, const dg_store* b, const dg_context* cb,
+              const uint64_t* keys, uint64_t n_keys, dg_store* out, dg_context* out_ctx) {
+  if (out->cap < a->n + b->n) REF_E(DG_E_CAPACITY);
+  if (out_ctx->cap < ca->n + cb->n) REF_E(DG_E_CAPACITY);
+  int rc = ref_join2_rows(a, ca, b, cb, keys, n_keys, out);
+  if (rc != DG_OK) return rc;
   return ref_context_union(ca, cb, out_ctx);
 }
 

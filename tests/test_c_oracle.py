@@ -198,3 +198,18 @@ def test_config2_generator_matches_term_replay():
         rows, ctx = CV.state_to_soa(st, U)
         assert rows_equal(rows, gen["rows"])
         assert ctx_equal(ctx, gen["ctx"])
+
+
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_join2_mt_equals_single_thread(threads):
+    """deltaref_mt.c (bench.py's all-core CPU baseline) == ref_join2, including more
+    shards than keys and a skewed split."""
+    from delta_crdt_ex_amd import workloads as W
+    a, b = W.config2(n_keys=20_000, seed=5)
+    want_rows, want_ctx = R.join2(a["rows"], a["ctx"], b["rows"], b["ctx"])
+    got_rows, got_ctx = R.JoinMT(a["rows"], a["ctx"], b["rows"], b["ctx"], threads)()
+    assert rows_equal(got_rows, want_rows) and ctx_equal(got_ctx, want_ctx)
+    small = tuple(c[:5] for c in a["rows"])
+    want_rows, _ = R.join2(small, a["ctx"], b["rows"], b["ctx"])
+    got_rows, _ = R.JoinMT(small, a["ctx"], b["rows"], b["ctx"], threads)()
+    assert rows_equal(got_rows, want_rows)
