@@ -91,6 +91,10 @@ _SIGS = {
     "dg_join2": (C.c_int, [C.c_void_p, C.POINTER(dg_store), C.POINTER(dg_context),
                            C.POINTER(dg_store), C.POINTER(dg_context), P64, C.c_uint64,
                            C.POINTER(dg_store), C.POINTER(dg_context)]),
+    "dg_join2_changes": (C.c_int, [C.c_void_p, C.POINTER(dg_store), C.POINTER(dg_context),
+                                   C.POINTER(dg_store), C.POINTER(dg_context), P64, C.c_uint64,
+                                   C.POINTER(dg_store), C.POINTER(dg_context), P64, C.c_uint64,
+                                   P64]),
     "dg_join2_async": (C.c_int, [C.c_void_p, C.POINTER(dg_store), C.POINTER(dg_context),
                                  C.POINTER(dg_store), C.POINTER(dg_context), P64, C.c_uint64,
                                  C.POINTER(dg_store), C.POINTER(dg_context), P64]),

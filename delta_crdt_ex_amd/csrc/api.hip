@@ -197,9 +197,11 @@ int check_ctx(const dg_context* c, const char* what) {
     if (_r != DG_OK) return _r; \
   } while (0)
 
+// chg (optional): the join also records its change events (dg_join2_changes); *chg
+// receives their scratch for launch_join2_changes.
 int join2_enqueue(dg_engine* e, const dg_store* a, const dg_context* ca, const dg_store* b,
                   const dg_context* cb, const uint64_t* keys, uint64_t n_keys, dg_store* out,
-                  dg_context* out_ctx, uint64_t* d_counts) {
+                  dg_context* out_ctx, uint64_t* d_counts, void** chg = nullptr) {
   TRY(check_store(a, "dg_join2 a"));
   TRY(check_store(b, "dg_join2 b"));
   TRY(check_ctx(ca, "dg_join2 ca"));
@@ -216,16 +218,20 @@ int join2_enqueue(dg_engine* e, const dg_store* a, const dg_context* ca, const d
     return fail(DG_E_INVAL, "dg_join2: null output column");
   TRY(set_device(e));
   TRY(ensure_state(e, 2 * join2_tiles(a->n, b->n) + 2));  // granules + tile splits
-  if (e->join_mode == JOIN_SINGLE_PASS) TRY(ensure_counts(e, join2_tiles(a->n, b->n)));
+  const bool two_pass = e->join_mode == JOIN_TWO_PASS && !chg;  // changes: single pass
+  if (!two_pass) TRY(ensure_counts(e, join2_tiles(a->n, b->n)));
   const size_t ctx_bytes = (ctx_union_tmp_bytes(ca->n, cb->n) + 255) / 256 * 256;
-  const size_t pass_bytes = e->join_mode == JOIN_TWO_PASS ? join2_pass_tmp_bytes(a->n, b->n) : 0;
-  TRY(ensure_tmp(e, ctx_bytes + pass_bytes));
+  const size_t pass_bytes = two_pass ? (join2_pass_tmp_bytes(a->n, b->n) + 255) / 256 * 256 : 0;
+  const size_t chg_bytes = chg ? join2_changes_tmp_bytes(a->n, b->n) : 0;
+  TRY(ensure_tmp(e, ctx_bytes + pass_bytes + chg_bytes));
+  void* chg_tmp = chg ? (char*)e->tmp + ctx_bytes + pass_bytes : nullptr;
+  if (chg) *chg = chg_tmp;
   Scan sc;
   TRY(next_scan(e, &sc));
   HIP_TRY(launch_join2(rows_of(a), ctx_of(ca), rows_of(b), ctx_of(cb), keys, keys ? n_keys : 0,
                        rows_out_of(out), out_ctx->node, out_ctx->cnt, e->tmp,
-                       (char*)e->tmp + ctx_bytes, e->join_mode, sc, e->join_workers, d_counts,
-                       e->stream));
+                       (char*)e->tmp + ctx_bytes, two_pass ? JOIN_TWO_PASS : JOIN_SINGLE_PASS,
+                       sc, e->join_workers, d_counts, e->stream, chg_tmp));
   out_ctx->kind = (ca->kind == DG_CTX_DOTS && cb->kind == DG_CTX_DOTS) ? DG_CTX_DOTS : DG_CTX_VV;
   return DG_OK;
 }
@@ -355,6 +361,28 @@ int dg_join2(dg_engine* e, const dg_store* a, const dg_context* ca, const dg_sto
   TRY(read_counts(e, 2));
   out->n = e->h_counts[0];
   out_ctx->n = e->h_counts[1];
+  return DG_OK;
+}
+
+int dg_join2_changes(dg_engine* e, const dg_store* a, const dg_context* ca, const dg_store* b,
+                     const dg_context* cb, const uint64_t* keys, uint64_t n_keys, dg_store* out,
+                     dg_context* out_ctx, uint64_t* changed, uint64_t cap, uint64_t* n_changed) {
+  if (!e) return fail(DG_E_INVAL, "null engine");
+  if (!n_changed || (cap && !changed)) return fail(DG_E_INVAL, "dg_join2_changes: null output");
+  void* chg = nullptr;
+  TRY(join2_enqueue(e, a, ca, b, cb, keys, n_keys, out, out_ctx, e->d_counts, &chg));
+  Scan gather, unique;
+  TRY(next_scan(e, &gather));
+  TRY(next_scan(e, &unique));
+  HIP_TRY(launch_join2_changes(a->n, b->n, chg, changed, cap, gather, unique, e->d_counts + 2,
+                               e->stream));
+  TRY(read_counts(e, 4));
+  out->n = e->h_counts[0];
+  out_ctx->n = e->h_counts[1];
+  *n_changed = e->h_counts[3];
+  if (*n_changed > cap)
+    return fail(DG_E_CAPACITY, "dg_join2_changes: %llu changed keys > cap %llu",
+                (unsigned long long)*n_changed, (unsigned long long)cap);
   return DG_OK;
 }
 

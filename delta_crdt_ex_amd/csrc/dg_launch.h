@@ -42,7 +42,22 @@ enum { JOIN_SINGLE_PASS = 0, JOIN_TWO_PASS = 1 };
 hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& cb,
                         const u64* keys, u64 n_keys, const RowsOut& out, u32* out_ctx_node,
                         u64* out_ctx_cnt, void* ctx_tmp, void* pass_tmp, int mode,
-                        const Scan& scan, int workers, u64* d_counts, hipStream_t st);
+                        const Scan& scan, int workers, u64* d_counts, hipStream_t st,
+                        void* chg_tmp = nullptr);
+// Changed keys (dg_join2_changes): with chg_tmp (join2_changes_tmp_bytes) the join
+// records per-tile change events (always the single-pass kernel); launch_join2_changes
+// then gathers them (d_counts[0] = events) and drops repeats into out[0, cap)
+// (d_counts[1] = changed keys).  Both use look-back granules [0, ntiles) of their Scans.
+inline size_t join2_changes_dense_offset(u64 na, u64 nb) {
+  const u64 t = join2_tiles(na, nb);
+  return ((t * (u64)JOIN_TILE * 8 + t * 4 + 255) / 256) * 256;
+}
+inline size_t join2_changes_tmp_bytes(u64 na, u64 nb) {
+  return join2_changes_dense_offset(na, nb) + (na + nb) * 8 + 256;
+}
+hipError_t launch_join2_changes(u64 na, u64 nb, void* chg_tmp, u64* out, u64 cap,
+                                const Scan& gather, const Scan& unique, u64* d_counts,
+                                hipStream_t st);
 inline size_t join2_pass_tmp_bytes(u64 na, u64 nb) {
   const u64 t = join2_tiles(na, nb);
   return ((t * 4 + 255) / 256) * 256 + t * (u64)JOIN_TILE * 2 + 256;  // counts + slot lists

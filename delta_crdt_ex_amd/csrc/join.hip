@@ -235,7 +235,9 @@ struct JoinArgs {
   RowsOut out;
   Scan scan;  // look-back granules + tile tickets
   u64* d_count;
-  unsigned short* lists;  // two-pass only: tile t's compaction list at lists[t * JT ...]
+  unsigned short* lists;
+  u64* chg_tmp;  // CHG: JT change-event keys per tile
+  u32* chg_cnt;  // CHG: events per tile  // two-pass only: tile t's compaction list at lists[t * JT ...]
   u32* counts;            // two-pass only: kept rows per tile
 };
 
@@ -432,11 +434,14 @@ constexpr int STOP = search_top(JT);
 // the key search runs a fixed number of binary-lifting steps and each merge step
 // selects between the a and b candidates instead of branching (divergent branches
 // cost exec-mask SALU work on every path).
-template <bool FAST>
+// CHG: also set bit k of `ev` when item k changes its key's rows (diff/3 of
+// causal_crdt.ex:343-351 over `keys`): a dropped a row or a newly kept b row.
+template <bool FAST, bool CHG = false>
 __device__ __forceinline__ void merge_items(const Ctx& ca, const Ctx& cb, const u64* tab_a,
                                             const u64* tab_b, const u64* keys, const u64 n_keys,
                                             const u64 nb, const Buf& s, int nat, int nbt, u64 a0,
-                                            u64 b0, u32& keep, unsigned short (&src)[JI]) {
+                                            u64 b0, u32& keep, unsigned short (&src)[JI],
+                                            u32* ev = nullptr) {
   const int tid = threadIdx.x;
   const int offB = nat + 2;
   const int tt = nat + nbt;
@@ -469,6 +474,7 @@ __device__ __forceinline__ void merge_items(const Ctx& ca, const Ctx& cb, const 
   bool dup = (a0 + (u64)i) >= 1 && row_eq(lds_row(s, i), rb);
   Row xa = lds_row(s, 2 + i), xb = lds_row(s, offB + 2 + j);
   keep = 0;
+  if (CHG) *ev = 0;
 #pragma unroll
   for (int k = 0; k < JI; k++) {
     const bool valid = diag + k < dend;
@@ -477,6 +483,7 @@ __device__ __forceinline__ void merge_items(const Ctx& ca, const Ctx& cb, const 
     const bool takeA = i < nat && (j >= nbt || c <= 0);
     const bool inB = bvalid && c == 0;
     bool kp;
+    bool jn = true;  // the key is joined (in `keys`), not carried right-biased
     if (FAST) {
       // Dots.member?(c_other, dot of the taken row): one LDS table read
       const u32 dn = takeA ? ra.node : rb.node;
@@ -494,7 +501,8 @@ __device__ __forceinline__ void merge_items(const Ctx& ca, const Ctx& cb, const 
       }
       kp = takeA ? (inB || !cov) : (!dup && !cov);
     } else if (takeA) {
-      if (keys == nullptr || keyset_has(keys, n_keys, ra.key)) {
+      jn = keys == nullptr || keyset_has(keys, n_keys, ra.key);
+      if (jn) {
         kp = inB || !covers<FAST>(tab_b, cb, ra.node, ra.cnt);
       } else {
         // Map.merge(Map.drop(a), Map.drop(b)): a's rows survive iff b lacks the key
@@ -503,13 +511,15 @@ __device__ __forceinline__ void merge_items(const Ctx& ca, const Ctx& cb, const 
         kp = !(bprev || bnext);
       }
     } else {
-      if (keys == nullptr || keyset_has(keys, n_keys, rb.key))
+      jn = keys == nullptr || keyset_has(keys, n_keys, rb.key);
+      if (jn)
         kp = !dup && !covers<FAST>(tab_a, ca, rb.node, rb.cnt);
       else
         kp = true;
     }
     src[k] = valid ? (unsigned short)(takeA ? 1 + i : offB + 1 + j) : (unsigned short)0;
     if (valid && kp) keep |= 1u << k;
+    if (CHG && valid && jn && (takeA ? !kp : kp)) *ev |= 1u << k;
     // advance the taken side; the next row after it is read one step ahead
     // (b rows are unique and larger than every a row merged so far, so a taken b row
     // clears dup; a taken a row passes its inB on to the b row it tied with)
@@ -711,7 +721,7 @@ __device__ __forceinline__ void write_tile(const JoinArgs& p, const StreamLds& s
   }
 }
 
-template <bool FAST>
+template <bool FAST, bool CHG>
 __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void join2_stream_kernel(JoinArgs p) {
   __shared__ StreamLds s;
   const int tid = threadIdx.x;
@@ -751,10 +761,10 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     }
     StripeCounts sc;  // stripe k-1's counts, in flight during the merge
     if (k > 0) stripe_load(cs, t - G - w, G, ntiles, epoch, sc);
-    u32 keep;
+    u32 keep, ev = 0;
     unsigned short src[JI];
-    merge_items<FAST>(p.ca, p.cb, s.tab[0], s.tab[1], p.keys, p.n_keys, B.n, s.buf[bi], nat, nbt,
-                      a0, b0, keep, src);
+    merge_items<FAST, CHG>(p.ca, p.cb, s.tab[0], s.tab[1], p.keys, p.n_keys, B.n, s.buf[bi], nat,
+                           nbt, a0, b0, keep, src, &ev);
     JSTAMP(t, 3);
     u32 n;
     u32 pos = block_excl_scan<JB>(__popc(keep), s.wave, &n);
@@ -763,6 +773,15 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       if (keep & (1u << q)) s.comp[bi][pos++] = src[q];
     if (tid == 0) publish_count(cs, t, epoch, n);
     __syncthreads();
+    if (CHG) {  // the tile's change events (keys, ascending, repeats allowed) -> chg_tmp
+      u32 n2;
+      u32 p2 = block_excl_scan<JB>(__popc(ev), s.wave, &n2);
+      u64* dst = p.chg_tmp + t * (u64)JT;
+#pragma unroll
+      for (int q = 0; q < JI; q++)
+        if (ev & (1u << q)) dst[p2++] = buf_key(s.buf[bi], src[q]);
+      if (tid == 0) p.chg_cnt[t] = n2;
+    }
     JSTAMP(t, 4);
     if (k > 0) {  // stripe k-1: this workgroup's tile t - G
       u64 below, all;
@@ -790,6 +809,82 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     b0 = b0n;
     __syncthreads();  // buffer bi^1 written out: free for the next commit
   }
+}
+
+// ---------------------------------------------------------------- changed keys
+// The keys whose rows the join changed (CausalCrdt's diff/3 after every join,
+// causal_crdt.ex:343-351, over `keys`), ascending and unique, from the stream
+// kernel's per-tile change events (ascending, a key repeated when several of its rows
+// changed, possibly across tiles):
+//   chg_gather_kernel  tile t's events -> dense[prefix_t ..], prefix by look-back
+//   chg_unique_kernel  dense -> out without repeats (a key is kept where it differs
+//                      from its predecessor), compacted by look-back; launched over an
+//                      upper bound of the event count, workgroups past it publish 0.
+constexpr int GB = 256;
+constexpr int UI = 4, UT = GB * UI;  // unique: keys per workgroup
+
+__device__ __forceinline__ u64 take_ticket(u32* ticket, u64 ntiles, u64* s_b) {
+  if (threadIdx.x == 0) {
+    const u32 t = atomicAdd(ticket, 1u);
+    if ((u64)t == ntiles - 1) atomicExch(ticket, 0u);
+    *s_b = t;
+  }
+  __syncthreads();
+  return *s_b;
+}
+
+// exclusive prefix of `total` over tiles in ticket order (wave 0 runs the look-back)
+__device__ __forceinline__ u64 tile_prefix(const Scan& scan, u64 t, u64 total, u64* s_b) {
+  if (threadIdx.x < WAVE) {
+    u64 prefix = 0;
+    if (t == 0) {
+      if (threadIdx.x == 0) lb_publish(scan.state, 0, scan.epoch, LB_INC, total);
+    } else {
+      if (threadIdx.x == 0) lb_publish(scan.state, t, scan.epoch, LB_AGG, total);
+      prefix = lb_lookback(scan.state, t, scan.epoch, scan.err);
+      if (threadIdx.x == 0) lb_publish(scan.state, t, scan.epoch, LB_INC, prefix + total);
+    }
+    if (threadIdx.x == 0) *s_b = prefix;
+  }
+  __syncthreads();
+  return *s_b;
+}
+
+__global__ __launch_bounds__(GB) void chg_gather_kernel(const u64* tmp, const u32* cnt, u64 ntiles,
+                                                       u64* dense, Scan scan, u64* d_count) {
+  __shared__ u64 s_b[2];
+  const u64 t = take_ticket(scan.ticket, ntiles, &s_b[0]);
+  const u32 n = cnt[t];
+  const u64 prefix = tile_prefix(scan, t, n, &s_b[1]);
+  for (u32 i = threadIdx.x; i < n; i += GB) dense[prefix + i] = tmp[t * (u64)JT + i];
+  if (threadIdx.x == 0 && t == ntiles - 1) d_count[0] = prefix + n;
+}
+
+__global__ __launch_bounds__(GB) void chg_unique_kernel(const u64* dense, const u64* d_n, u64 ntiles,
+                                                       u64* out, u64 cap, Scan scan, u64* d_count) {
+  __shared__ u64 s_b[2];
+  __shared__ u32 s_wave[GB / WAVE + 1];
+  const u64 t = take_ticket(scan.ticket, ntiles, &s_b[0]);
+  const u64 n = *d_n;
+  const u64 i0 = t * UT + (u64)threadIdx.x * UI;
+  u64 v[UI];
+  u32 keep = 0;
+#pragma unroll
+  for (int q = 0; q < UI; q++) {
+    const u64 i = i0 + q;
+    v[q] = i < n ? dense[i] : 0;
+    if (i < n && (i == 0 || dense[i - 1] != v[q])) keep |= 1u << q;
+  }
+  u32 tot;
+  u32 pos = block_excl_scan<GB>(__popc(keep), s_wave, &tot);
+  const u64 prefix = tile_prefix(scan, t, tot, &s_b[1]);
+#pragma unroll
+  for (int q = 0; q < UI; q++)
+    if (keep & (1u << q)) {
+      const u64 o = prefix + pos++;
+      if (o < cap) out[o] = v[q];
+    }
+  if (threadIdx.x == 0 && t == ntiles - 1) d_count[0] = prefix + tot;
 }
 
 // ---------------------------------------------------------------- two-pass join
@@ -926,7 +1021,8 @@ static CtxUnionArgs make_cu(const Ctx& a, const Ctx& b, u32* out_node, u64* out_
 hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& cb,
                         const u64* keys, u64 n_keys, const RowsOut& out, u32* out_ctx_node,
                         u64* out_ctx_cnt, void* ctx_tmp, void* pass_tmp, int mode,
-                        const Scan& scan, int workers, u64* d_counts, hipStream_t st) {
+                        const Scan& scan, int workers, u64* d_counts, hipStream_t st,
+                        void* chg_tmp) {
   JoinArgs p;
   p.a = a;
   p.b = b;
@@ -943,6 +1039,8 @@ hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& 
   p.d_count = d_counts;
   p.lists = nullptr;
   p.counts = nullptr;
+  p.chg_tmp = chg_tmp ? (u64*)chg_tmp : nullptr;
+  p.chg_cnt = chg_tmp ? (u32*)((char*)chg_tmp + p.ntiles * (u64)JT * 8) : nullptr;
   if (p.ntiles == 0) {
     // no rows: only the context union runs
     hipError_t e = hipMemsetAsync(d_counts, 0, sizeof(u64), st);
@@ -955,7 +1053,7 @@ hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& 
                      p.ntiles, splits, cu);
   // full-state join of two version vectors: LDS VV table, no key list
   const bool fast = keys == nullptr && ca.kind == 0 && cb.kind == 0;
-  if (mode == JOIN_TWO_PASS) {
+  if (mode == JOIN_TWO_PASS && !chg_tmp) {
     char* t = (char*)pass_tmp;
     p.counts = (u32*)t;
     t += ((p.ntiles * 4 + 255) / 256) * 256;
@@ -966,11 +1064,28 @@ hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& 
                        p.splits, p.lists, p.counts, p.ntiles, out, d_counts);
     return hipGetLastError();
   }
-  auto kern = fast ? join2_stream_kernel<true> : join2_stream_kernel<false>;
+  auto kern = fast ? join2_stream_kernel<true, false> : join2_stream_kernel<false, false>;
+  if (chg_tmp) kern = fast ? join2_stream_kernel<true, true> : join2_stream_kernel<false, true>;
   u64 g = workers > 0 ? (u64)workers : 0;
   if (!g) g = resident_grid((const void*)kern);
   g = std::min<u64>(std::min<u64>(p.ntiles, g), (u64)CQ * JB);  // stripe counts: CQ per thread
   hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(JB), 0, st, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_join2_changes(u64 na, u64 nb, void* chg_tmp, u64* out, u64 cap,
+                                const Scan& gather, const Scan& unique, u64* d_counts,
+                                hipStream_t st) {
+  const u64 ntiles = join2_tiles(na, nb);
+  if (ntiles == 0) return hipMemsetAsync(d_counts, 0, 2 * sizeof(u64), st);
+  const u64* tmp = (const u64*)chg_tmp;
+  const u32* cnt = (const u32*)((const char*)chg_tmp + ntiles * (u64)JT * 8);
+  u64* dense = (u64*)((char*)chg_tmp + join2_changes_dense_offset(na, nb));
+  hipLaunchKernelGGL(chg_gather_kernel, dim3((unsigned)ntiles), dim3(GB), 0, st, tmp, cnt, ntiles,
+                     dense, gather, d_counts);
+  const u64 ut = (na + nb + UT - 1) / UT;  // events <= merged positions
+  hipLaunchKernelGGL(chg_unique_kernel, dim3((unsigned)ut), dim3(GB), 0, st, dense, d_counts, ut,
+                     out, cap, unique, d_counts + 1);
   return hipGetLastError();
 }
 

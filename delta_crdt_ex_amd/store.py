@@ -214,6 +214,18 @@ class Engine:
         check(self.lib.dg_engine_sync(self.h))
 
     # ---------------------------------------------------------------- join
+    def _keys(self, keys: torch.Tensor | None):
+        """(pointer, n) of a `keys` argument: None -> NULL (every key); an empty tensor
+        -> a valid pointer with n = 0 (no key -- an empty tensor's data_ptr() is 0,
+        which the C-ABI would read as NULL)."""
+        if keys is None:
+            return None, 0
+        if keys.numel() == 0:
+            if getattr(self, "_no_keys", None) is None:
+                self._no_keys = torch.zeros(1, dtype=_I64, device=self.device)
+            return _ptr(self._no_keys, _abi.P64), 0
+        return _ptr(keys, _abi.P64), int(keys.numel())
+
     def join2(self, a: Store, ca: Context, b: Store, cb: Context, keys: torch.Tensor | None = None,
               out: Store | None = None, out_ctx: Context | None = None):
         self._order()
@@ -223,14 +235,38 @@ class Engine:
             out_ctx = Context.empty(DG_CTX_VV, ca.n + cb.n, self.device)
         so, co = out.abi(), out_ctx.abi()
         sa, sb, xa, xb = a.abi(), b.abi(), ca.abi(), cb.abi()
-        kp = _ptr(keys, _abi.P64) if keys is not None else None
-        nk = int(keys.numel()) if keys is not None else 0
+        kp, nk = self._keys(keys)
         check(self.lib.dg_join2(self.h, C.byref(sa), C.byref(xa), C.byref(sb), C.byref(xb),
                                 kp, nk, C.byref(so), C.byref(co)))
         out.n = int(so.n)
         out_ctx.n = int(co.n)
         out_ctx.kind = int(co.kind)
         return out, out_ctx
+
+    def join2_changes(self, a: Store, ca: Context, b: Store, cb: Context,
+                      keys: torch.Tensor | None = None, out: Store | None = None,
+                      out_ctx: Context | None = None):
+        """join/3 plus CausalCrdt's changed-key diff (diff/3, causal_crdt.ex:343-351):
+        returns (out, out_ctx, changed) with `changed` the ascending device int64 tensor
+        of the keys (of `keys`, or all) whose rows in `out` differ from those in `a`."""
+        self._order()
+        if out is None:
+            out = Store.empty(a.n + b.n, self.device)
+        if out_ctx is None:
+            out_ctx = Context.empty(DG_CTX_VV, ca.n + cb.n, self.device)
+        cap = max(a.n + b.n, 1)
+        changed = torch.empty(cap, dtype=_I64, device=self.device)
+        so, co = out.abi(), out_ctx.abi()
+        sa, sb, xa, xb = a.abi(), b.abi(), ca.abi(), cb.abi()
+        kp, nk = self._keys(keys)
+        n = C.c_uint64(0)
+        check(self.lib.dg_join2_changes(self.h, C.byref(sa), C.byref(xa), C.byref(sb), C.byref(xb),
+                                        kp, nk, C.byref(so), C.byref(co), _ptr(changed, _abi.P64),
+                                        cap, C.byref(n)))
+        out.n = int(so.n)
+        out_ctx.n = int(co.n)
+        out_ctx.kind = int(co.kind)
+        return out, out_ctx, changed[: n.value]
 
     def join2_async(self, a: Store, ca: Context, b: Store, cb: Context, out: Store,
                     out_ctx: Context, keys: torch.Tensor | None = None, d_counts=None):
@@ -240,8 +276,7 @@ class Engine:
             d_counts = self._d_counts
         so, co = out.abi(), out_ctx.abi()
         sa, sb, xa, xb = a.abi(), b.abi(), ca.abi(), cb.abi()
-        kp = _ptr(keys, _abi.P64) if keys is not None else None
-        nk = int(keys.numel()) if keys is not None else 0
+        kp, nk = self._keys(keys)
         check(self.lib.dg_join2_async(self.h, C.byref(sa), C.byref(xa), C.byref(sb), C.byref(xb),
                                       kp, nk, C.byref(so), C.byref(co), _ptr(d_counts, _abi.P64)))
         out_ctx.kind = int(co.kind)
@@ -253,8 +288,7 @@ class Engine:
         returns a zero-argument callable that enqueues dg_join2_async."""
         args = [a.abi(), ca.abi(), b.abi(), cb.abi(), out.abi(), out_ctx.abi()]
         refs = [C.byref(x) for x in args]
-        kp = _ptr(keys, _abi.P64) if keys is not None else None
-        nk = int(keys.numel()) if keys is not None else 0
+        kp, nk = self._keys(keys)
         dp = _ptr(d_counts, _abi.P64)
         f, h = self.lib.dg_join2_async, self.h
 
@@ -343,8 +377,7 @@ class Engine:
         ov = torch.empty(cap, dtype=_I64, device=self.device)
         n = C.c_uint64()
         ss = s.abi()
-        kp = _ptr(keys, _abi.P64) if keys is not None else None
-        nk = int(keys.numel()) if keys is not None else 0
+        kp, nk = self._keys(keys)
         check(self.lib.dg_read_lww(self.h, C.byref(ss), kp, nk, _ptr(ok, _abi.P64),
                                    _ptr(ov, _abi.P64), cap, C.byref(n)))
         return ok[: n.value], ov[: n.value]

@@ -129,6 +129,18 @@ int dg_join2_async(dg_engine* e, const dg_store* a, const dg_context* ca, const 
                    const dg_context* cb, const uint64_t* keys, uint64_t n_keys,
                    dg_store* out, dg_context* out_ctx, uint64_t* d_counts);
 
+/* join/3 (as dg_join2) plus the changed-key diff CausalCrdt computes after every join
+ * (update_state_with_delta/3 -> diff/3, causal_crdt.ex:343-351,383-393): the keys of
+ * `keys` (every key when NULL) whose rows in `out` differ from their rows in `a` --
+ * removed keys, new keys and keys whose entries or dots changed -- ascending and
+ * unique, into changed[0, cap), *n_changed = their number (DG_E_CAPACITY if > cap).
+ * The caller's on_diffs / MerkleMap work (:386-404) reads these keys (dg_read_lww
+ * with them as `keys` on `a` and `out`).  Recorded inside the join's merge; always the
+ * single-pass join kernel.  Synchronous. */
+int dg_join2_changes(dg_engine* e, const dg_store* a, const dg_context* ca, const dg_store* b,
+                     const dg_context* cb, const uint64_t* keys, uint64_t n_keys, dg_store* out,
+                     dg_context* out_ctx, uint64_t* changed, uint64_t cap, uint64_t* n_changed);
+
 /* Fold of join/3 over k stores (how CausalCrdt applies k deltas in a row,
  * causal_crdt.ex:86-89,383-384): out = join(...join(join(s0, s1), s2)..., s_{k-1})
  * over all keys.  A row survives iff for every input i it is present in s_i or its

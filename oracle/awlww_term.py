@@ -254,3 +254,17 @@ def canon(state):
 def join_k(states, keys):
     """Left fold of join/3 — how CausalCrdt applies a stream of deltas."""
     return list(itertools.accumulate(states, lambda a, b: join(a, b, keys)))[-1]
+
+
+def causal_diff(old, new, keys):
+    """causal_crdt.ex:343-351 (diff/3): per key of `keys`, in order, {:add, key,
+    new_value_map} when the raw per-key value maps differ and the key survives,
+    {:remove, key} when it does not."""
+    out = []
+    for key in keys:
+        o, n = old.value.get(key), new.value.get(key)
+        if o == n:
+            continue
+        out.append(("remove", key) if n is None else ("add", key, n))
+    return out
+

@@ -276,6 +276,16 @@ def store_diff(ra, rb):
     return out[: int(n[0])]
 
 
+def changed_keys(old_rows, new_rows, keys=None):
+    """CausalCrdt's diff/3 (causal_crdt.ex:343-351) on SoA rows: the keys (of `keys`, or
+    all) whose row sets differ between the state before and after a join -- equal
+    per-key value maps are equal row sets -- ascending."""
+    d = store_diff(old_rows, new_rows)
+    if keys is None:
+        return d
+    return d[np.isin(d, np.asarray(keys, np.uint64))]
+
+
 def store_check(rows) -> bool:
     s, _ = _store(rows)
     return lib().ref_store_check(C.byref(s)) == 0

@@ -182,3 +182,24 @@ def test_random_keyed_fold_two_oracles(seed):
         t = T.join(t, dt, ks)
     wrows, wctx = term_to_soa_raw(t)
     assert rows_equal(rows, wrows) and ctx_equal(ctx, wctx)
+
+
+# ------------------------------------------------------------------ changed keys (§8(f).1)
+
+@pytest.mark.parametrize("seed", range(4))
+def test_changed_keys_two_oracles(seed):
+    """The changed keys dg_join2_changes is checked against (ref.changed_keys: the
+    exact per-key row-set diff, restricted to `keys`) == the keys of the term oracle's
+    diff/3 (causal_crdt.ex:343-351) after join/3."""
+    from kfold_cases import random_fold
+    st, ds = random_fold(40 + seed, n_keys=60, k=1, rows_per_key=4, p_keys=0.4, p_take=0.6,
+                         p_outside=0.1, p_full=0.3 if seed == 3 else 0.0)
+    d = ds[0]
+    rows, ctx = R.join2(st["rows"], st["ctx"], d["rows"], d["ctx"], d["keys"])
+    got = R.changed_keys(st["rows"], rows, d["keys"])
+    old, dt = soa_to_term(st["rows"], st["ctx"]), soa_to_term(d["rows"], d["ctx"])
+    keys = sorted(set(old.value) | set(dt.value)) if d["keys"] is None else [int(x) for x in d["keys"]]
+    new = T.join(old, dt, keys)
+    want = sorted(x[1] for x in T.causal_diff(old, new, keys))
+    assert [int(x) for x in got] == want
+    assert len(want) > 0
