@@ -188,6 +188,27 @@ def config3_rate(eng, torch, dev, n_keys=10_000_000, reps=3):
                     "join/3 back to back"}
 
 
+def changes_rate(eng, torch, pr, reps=20):
+    """SURVEY §8(f).1 on config 2: dg_join2_changes (the join plus the changed-key diff
+    of update_state_with_delta) next to the plain synchronous dg_join2, same inputs."""
+    res = {}
+
+    def chg():
+        _, _, c = eng.join2_changes(pr["sa"], pr["ca"], pr["sb"], pr["cb"], out=pr["out"],
+                                    out_ctx=pr["octx"])
+        res["n"] = int(c.numel())
+
+    def plain():
+        eng.join2(pr["sa"], pr["ca"], pr["sb"], pr["cb"], out=pr["out"], out_ctx=pr["octx"])
+
+    el_c = _timed(torch, chg, reps)
+    el_p = _timed(torch, plain, reps)
+    return {"metric": "dg_join2_changes on config 2 (join + changed keys)",
+            "us_per_call": el_c * 1e6, "join2_us_per_call": el_p * 1e6,
+            "changed_keys": res["n"],
+            "note": "synchronous calls (host sync each), median of reps"}
+
+
 def config5_rate(eng, torch, dev, n_keys=12_500_000, reps=5):
     """Config 5 at one GPU's share of 100M keys over 8 GPUs: full-state join of two
     remove-heavy replicas (50 % removes, 64 nodes, ts in [0,16): LWW ties everywhere),
@@ -372,6 +393,7 @@ def main():
         if not args.no_merkle:
             res["merkle"] = merkle_rate(eng, torch, dev)
         if not args.no_configs:
+            res["changes"] = changes_rate(eng, torch, pairs[0])
             for r in pairs:  # free the config-2 replicas before the larger configs
                 r.clear()
             res["config3"] = config3_rate(eng, torch, dev)

@@ -95,6 +95,8 @@ _SIGS = {
                                    C.POINTER(dg_store), C.POINTER(dg_context), P64, C.c_uint64,
                                    C.POINTER(dg_store), C.POINTER(dg_context), P64, C.c_uint64,
                                    P64]),
+    "dg_take_keys": (C.c_int, [C.c_void_p, C.POINTER(dg_store), P64, C.c_uint64,
+                               C.POINTER(dg_store)]),
     "dg_join2_async": (C.c_int, [C.c_void_p, C.POINTER(dg_store), C.POINTER(dg_context),
                                  C.POINTER(dg_store), C.POINTER(dg_context), P64, C.c_uint64,
                                  C.POINTER(dg_store), C.POINTER(dg_context), P64]),

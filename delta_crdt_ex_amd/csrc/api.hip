@@ -371,15 +371,13 @@ int dg_join2_changes(dg_engine* e, const dg_store* a, const dg_context* ca, cons
   if (!n_changed || (cap && !changed)) return fail(DG_E_INVAL, "dg_join2_changes: null output");
   void* chg = nullptr;
   TRY(join2_enqueue(e, a, ca, b, cb, keys, n_keys, out, out_ctx, e->d_counts, &chg));
-  Scan gather, unique;
-  TRY(next_scan(e, &gather));
-  TRY(next_scan(e, &unique));
-  HIP_TRY(launch_join2_changes(a->n, b->n, chg, changed, cap, gather, unique, e->d_counts + 2,
-                               e->stream));
-  TRY(read_counts(e, 4));
+  Scan sc;
+  TRY(next_scan(e, &sc));
+  HIP_TRY(launch_join2_changes(a->n, b->n, chg, changed, cap, sc, e->d_counts + 2, e->stream));
+  TRY(read_counts(e, 3));
   out->n = e->h_counts[0];
   out_ctx->n = e->h_counts[1];
-  *n_changed = e->h_counts[3];
+  *n_changed = e->h_counts[2];
   if (*n_changed > cap)
     return fail(DG_E_CAPACITY, "dg_join2_changes: %llu changed keys > cap %llu",
                 (unsigned long long)*n_changed, (unsigned long long)cap);
@@ -650,6 +648,27 @@ int dg_apply_deltas(dg_engine* e, const dg_store* state, const dg_context* ctx, 
   TRY(check_ctx(ctx, "dg_apply_deltas ctx"));
   if (keys && !n_keys) return fail(DG_E_INVAL, "dg_apply_deltas: keys without n_keys");
   return apply_deltas(e, state, ctx, k, deltas, dctxs, keys, n_keys, out, out_ctx);
+}
+
+int dg_take_keys(dg_engine* e, const dg_store* s, const uint64_t* keys, uint64_t n_keys,
+                 dg_store* out) {
+  if (!e) return fail(DG_E_INVAL, "null engine");
+  TRY(check_store(s, "dg_take_keys"));
+  if (!out || (n_keys && !keys)) return fail(DG_E_INVAL, "dg_take_keys: null argument");
+  if (out->cap && (!out->key || !out->val || !out->ts || !out->node || !out->cnt))
+    return fail(DG_E_INVAL, "dg_take_keys: null output column");
+  TRY(set_device(e));
+  TRY(ensure_state(e, take_tiles(n_keys) + 1));
+  Scan sc;
+  TRY(next_scan(e, &sc));
+  HIP_TRY(launch_take_keys(rows_of(s), keys, n_keys, rows_out_of(out), out->cap, sc, e->d_counts,
+                           e->stream));
+  TRY(read_counts(e, 1));
+  out->n = e->h_counts[0];
+  if (out->n > out->cap)
+    return fail(DG_E_CAPACITY, "dg_take_keys: %llu rows > cap %llu", (unsigned long long)out->n,
+                (unsigned long long)out->cap);
+  return DG_OK;
 }
 
 int dg_context_union(dg_engine* e, const dg_context* a, const dg_context* b, dg_context* out) {

@@ -46,18 +46,14 @@ hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& 
                         void* chg_tmp = nullptr);
 // Changed keys (dg_join2_changes): with chg_tmp (join2_changes_tmp_bytes) the join
 // records per-tile change events (always the single-pass kernel); launch_join2_changes
-// then gathers them (d_counts[0] = events) and drops repeats into out[0, cap)
-// (d_counts[1] = changed keys).  Both use look-back granules [0, ntiles) of their Scans.
-inline size_t join2_changes_dense_offset(u64 na, u64 nb) {
-  const u64 t = join2_tiles(na, nb);
-  return ((t * (u64)JOIN_TILE * 8 + t * 4 + 255) / 256) * 256;
-}
+// then drops repeats and compacts them into out[0, cap) (*d_count = changed keys),
+// using look-back granules [0, ntiles) of its Scan.
 inline size_t join2_changes_tmp_bytes(u64 na, u64 nb) {
-  return join2_changes_dense_offset(na, nb) + (na + nb) * 8 + 256;
+  const u64 t = join2_tiles(na, nb);
+  return t * (u64)JOIN_TILE * 8 + t * 4 + 256;
 }
 hipError_t launch_join2_changes(u64 na, u64 nb, void* chg_tmp, u64* out, u64 cap,
-                                const Scan& gather, const Scan& unique, u64* d_counts,
-                                hipStream_t st);
+                                const Scan& scan, u64* d_count, hipStream_t st);
 inline size_t join2_pass_tmp_bytes(u64 na, u64 nb) {
   const u64 t = join2_tiles(na, nb);
   return ((t * 4 + 255) / 256) * 256 + t * (u64)JOIN_TILE * 2 + 256;  // counts + slot lists
@@ -109,6 +105,13 @@ struct KFoldArgs {
   u32* flag;           // KF_* bits: the caller must re-run the fold step by step
 };
 hipError_t launch_kfold(const KFoldArgs& p, hipStream_t st);
+
+// ---- take.hip (sync-delta values: Map.take(value, keys))
+inline u64 take_tiles(u64 n_keys) { return (n_keys + 1023) / 1024; }
+// rows of s whose key is in keys (ascending) into out[0, cap); *d_count = their number.
+// Uses look-back granules [0, take_tiles(n_keys)).
+hipError_t launch_take_keys(const Rows& s, const u64* keys, u64 n_keys, const RowsOut& out,
+                            u64 cap, const Scan& scan, u64* d_count, hipStream_t st);
 
 // ---- segred.hip (segmented reductions over key runs)
 constexpr int SEG_BLOCK = 256;

@@ -814,77 +814,85 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
 // ---------------------------------------------------------------- changed keys
 // The keys whose rows the join changed (CausalCrdt's diff/3 after every join,
 // causal_crdt.ex:343-351, over `keys`), ascending and unique, from the stream
-// kernel's per-tile change events (ascending, a key repeated when several of its rows
-// changed, possibly across tiles):
-//   chg_gather_kernel  tile t's events -> dense[prefix_t ..], prefix by look-back
-//   chg_unique_kernel  dense -> out without repeats (a key is kept where it differs
-//                      from its predecessor), compacted by look-back; launched over an
-//                      upper bound of the event count, workgroups past it publish 0.
-constexpr int GB = 256;
-constexpr int UI = 4, UT = GB * UI;  // unique: keys per workgroup
+// kernel's per-tile change events (ascending; a key repeats when several of its rows
+// changed, possibly across tiles).  chg_compact_kernel, one workgroup per tile in
+// ticket order: an event is kept where it differs from the event before it -- inside
+// the tile, or for the tile's first event the last event of the nearest non-empty
+// earlier tile (wave 0 scans the per-tile counts back 64 at a time; only tiles with
+// events scan, so the scans add up to O(tiles)) -- and the kept keys are compacted
+// by decoupled look-back.
+constexpr int GB = 256, GI = (JT + GB - 1) / GB;
 
-__device__ __forceinline__ u64 take_ticket(u32* ticket, u64 ntiles, u64* s_b) {
-  if (threadIdx.x == 0) {
-    const u32 t = atomicAdd(ticket, 1u);
-    if ((u64)t == ntiles - 1) atomicExch(ticket, 0u);
-    *s_b = t;
-  }
-  __syncthreads();
-  return *s_b;
-}
-
-// exclusive prefix of `total` over tiles in ticket order (wave 0 runs the look-back)
-__device__ __forceinline__ u64 tile_prefix(const Scan& scan, u64 t, u64 total, u64* s_b) {
-  if (threadIdx.x < WAVE) {
-    u64 prefix = 0;
-    if (t == 0) {
-      if (threadIdx.x == 0) lb_publish(scan.state, 0, scan.epoch, LB_INC, total);
-    } else {
-      if (threadIdx.x == 0) lb_publish(scan.state, t, scan.epoch, LB_AGG, total);
-      prefix = lb_lookback(scan.state, t, scan.epoch, scan.err);
-      if (threadIdx.x == 0) lb_publish(scan.state, t, scan.epoch, LB_INC, prefix + total);
-    }
-    if (threadIdx.x == 0) *s_b = prefix;
-  }
-  __syncthreads();
-  return *s_b;
-}
-
-__global__ __launch_bounds__(GB) void chg_gather_kernel(const u64* tmp, const u32* cnt, u64 ntiles,
-                                                       u64* dense, Scan scan, u64* d_count) {
-  __shared__ u64 s_b[2];
-  const u64 t = take_ticket(scan.ticket, ntiles, &s_b[0]);
-  const u32 n = cnt[t];
-  const u64 prefix = tile_prefix(scan, t, n, &s_b[1]);
-  for (u32 i = threadIdx.x; i < n; i += GB) dense[prefix + i] = tmp[t * (u64)JT + i];
-  if (threadIdx.x == 0 && t == ntiles - 1) d_count[0] = prefix + n;
-}
-
-__global__ __launch_bounds__(GB) void chg_unique_kernel(const u64* dense, const u64* d_n, u64 ntiles,
-                                                       u64* out, u64 cap, Scan scan, u64* d_count) {
-  __shared__ u64 s_b[2];
+__global__ __launch_bounds__(GB) void chg_compact_kernel(const u64* tmp, const u32* cnt, u64 ntiles,
+                                                        u64* out, u64 cap, Scan scan,
+                                                        u64* d_count) {
+  __shared__ u64 s_b[3];
   __shared__ u32 s_wave[GB / WAVE + 1];
-  const u64 t = take_ticket(scan.ticket, ntiles, &s_b[0]);
-  const u64 n = *d_n;
-  const u64 i0 = t * UT + (u64)threadIdx.x * UI;
-  u64 v[UI];
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    const u32 t = atomicAdd(scan.ticket, 1u);
+    if ((u64)t == ntiles - 1) atomicExch(scan.ticket, 0u);
+    s_b[0] = t;
+  }
+  __syncthreads();
+  const u64 t = s_b[0];
+  const u32 n = cnt[t];
+  const u64* ev = tmp + t * (u64)JT;
+  if (n > 0 && tid < WAVE) {  // last event before this tile, if any
+    u64 prev = ~0ull, has = 0;
+    for (i64 base = (i64)t - 1; base >= 0; base -= WAVE) {
+      const i64 q = base - tid;
+      const u32 c = q >= 0 ? cnt[q] : 0u;
+      const u64 m = __ballot(c > 0);
+      if (m) {
+        const int l = __ffsll((long long)m) - 1;  // the nearest: smallest lane
+        const i64 qq = base - l;
+        prev = tmp[qq * (i64)JT + __shfl(c, l, WAVE) - 1];
+        has = 1;
+        break;
+      }
+    }
+    if (tid == 0) {
+      s_b[1] = prev;
+      s_b[2] = has;
+    }
+  }
+  __syncthreads();
+  u64 v[GI];
   u32 keep = 0;
 #pragma unroll
-  for (int q = 0; q < UI; q++) {
-    const u64 i = i0 + q;
-    v[q] = i < n ? dense[i] : 0;
-    if (i < n && (i == 0 || dense[i - 1] != v[q])) keep |= 1u << q;
+  for (int q = 0; q < GI; q++) {
+    const u32 i = tid * GI + q;
+    v[q] = i < n ? ev[i] : 0;
+    if (i < n) {
+      const bool dup = i > 0 ? ev[i - 1] == v[q] : (s_b[2] && s_b[1] == v[q]);
+      if (!dup) keep |= 1u << q;
+    }
   }
   u32 tot;
   u32 pos = block_excl_scan<GB>(__popc(keep), s_wave, &tot);
-  const u64 prefix = tile_prefix(scan, t, tot, &s_b[1]);
+  if (tid < WAVE) {
+    u64 prefix = 0;
+    if (t == 0) {
+      if (tid == 0) lb_publish(scan.state, 0, scan.epoch, LB_INC, tot);
+    } else {
+      if (tid == 0) lb_publish(scan.state, t, scan.epoch, LB_AGG, tot);
+      prefix = lb_lookback(scan.state, t, scan.epoch, scan.err);
+      if (tid == 0) lb_publish(scan.state, t, scan.epoch, LB_INC, prefix + tot);
+    }
+    if (tid == 0) {
+      s_b[1] = prefix;
+      if (t == ntiles - 1) d_count[0] = prefix + tot;
+    }
+  }
+  __syncthreads();
+  const u64 base = s_b[1];
 #pragma unroll
-  for (int q = 0; q < UI; q++)
+  for (int q = 0; q < GI; q++)
     if (keep & (1u << q)) {
-      const u64 o = prefix + pos++;
+      const u64 o = base + pos++;
       if (o < cap) out[o] = v[q];
     }
-  if (threadIdx.x == 0 && t == ntiles - 1) d_count[0] = prefix + tot;
 }
 
 // ---------------------------------------------------------------- two-pass join
@@ -1074,18 +1082,13 @@ hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& 
 }
 
 hipError_t launch_join2_changes(u64 na, u64 nb, void* chg_tmp, u64* out, u64 cap,
-                                const Scan& gather, const Scan& unique, u64* d_counts,
-                                hipStream_t st) {
+                                const Scan& scan, u64* d_count, hipStream_t st) {
   const u64 ntiles = join2_tiles(na, nb);
-  if (ntiles == 0) return hipMemsetAsync(d_counts, 0, 2 * sizeof(u64), st);
+  if (ntiles == 0) return hipMemsetAsync(d_count, 0, sizeof(u64), st);
   const u64* tmp = (const u64*)chg_tmp;
   const u32* cnt = (const u32*)((const char*)chg_tmp + ntiles * (u64)JT * 8);
-  u64* dense = (u64*)((char*)chg_tmp + join2_changes_dense_offset(na, nb));
-  hipLaunchKernelGGL(chg_gather_kernel, dim3((unsigned)ntiles), dim3(GB), 0, st, tmp, cnt, ntiles,
-                     dense, gather, d_counts);
-  const u64 ut = (na + nb + UT - 1) / UT;  // events <= merged positions
-  hipLaunchKernelGGL(chg_unique_kernel, dim3((unsigned)ut), dim3(GB), 0, st, dense, d_counts, ut,
-                     out, cap, unique, d_counts + 1);
+  hipLaunchKernelGGL(chg_compact_kernel, dim3((unsigned)ntiles), dim3(GB), 0, st, tmp, cnt, ntiles,
+                     out, cap, scan, d_count);
   return hipGetLastError();
 }
 

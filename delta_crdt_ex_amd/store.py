@@ -348,6 +348,18 @@ class Engine:
         out_ctx.kind = int(co.kind)
         return out, out_ctx
 
+    def take_keys(self, s: Store, keys: torch.Tensor, out: Store | None = None) -> Store:
+        """Map.take(value, keys) of a sync delta (causal_crdt.ex:324-335): the rows of `s`
+        whose key is in `keys` (ascending unique device int64), in store order."""
+        self._order()
+        if out is None:
+            out = Store.empty(max(s.n, 1), self.device)
+        so, ss = out.abi(), s.abi()
+        kp, nk = self._keys(keys)
+        check(self.lib.dg_take_keys(self.h, C.byref(ss), kp, nk, C.byref(so)))
+        out.n = int(so.n)
+        return out
+
     # ---------------------------------------------------------------- contexts
     def context_union(self, a: Context, b: Context, out: Context | None = None) -> Context:
         self._order()

@@ -165,6 +165,17 @@ int dg_apply_deltas(dg_engine* e, const dg_store* state, const dg_context* ctx, 
                     const uint64_t* const* keys, const uint64_t* n_keys, dg_store* out,
                     dg_context* out_ctx);
 
+/* ---- sync deltas ----------------------------------------------------------- */
+/* The value half of a sync delta, Map.take(state.value, keys) (causal_crdt.ex:112-123,
+ * 324-335: {:diff, %{state | dots: diff.dots, value: Map.take(value, keys)}, keys}):
+ * the rows of `s` whose key is in `keys` (device, ascending unique), in store order,
+ * into out[0, out->cap); out->n = their number (DG_E_CAPACITY if > out->cap).  The
+ * delta's context is the caller's VV snapshot (diff.dots); with it and `keys` the
+ * result goes straight into dg_join2 / dg_apply_deltas on the receiving side.
+ * Synchronous. */
+int dg_take_keys(dg_engine* e, const dg_store* s, const uint64_t* keys, uint64_t n_keys,
+                 dg_store* out);
+
 /* ---- causal-context algebra ----------------------------------------------- */
 /* Dots.union/2 (aw_lww_map.ex:39-52): VV ⊔ VV = per-node max; VV ⊔ DOTS folds the
  * dots into the VV; DOTS ⊔ DOTS = set union. */

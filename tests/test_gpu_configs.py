@@ -125,3 +125,34 @@ def test_config4_shard_round(engine, rank):
     rows_eq(out, wr)
     ctx_eq(octx, wc)
     assert isinstance(out, Store)
+
+
+# ------------------------------------------------------------------ sync deltas (§8(f).2)
+
+def test_take_keys_edges(engine):
+    a, b = W.config4_shard(1, 8, keys_per_rank=20_000, diff_frac=0.02)
+    sb, _ = up(b)
+    bk = np.unique(b["rows"][0])
+    for keys in (np.zeros(0, np.uint64),                       # no key
+                 np.array([1, 2, 3], np.uint64),               # keys the store lacks
+                 bk,                                            # every key: the store itself
+                 bk[::7], np.concatenate([bk[:5], bk[-5:]])):   # spread / both ends
+        got = engine.take_keys(sb, keys_dev(keys))
+        want = W.sync_delta(b, keys)["rows"]
+        rows_eq(got, want)
+
+
+@pytest.mark.parametrize("rank", [0, 5])
+def test_config4_round_device_resident(engine, rank):
+    """The anti-entropy round entirely on the device: Merkle build + diff, the sync
+    delta Map.take(B.value, diff keys) (dg_take_keys) with B's context, and the keyed
+    join into A -- equal to the full-state join of the shard."""
+    a, b = W.config4_shard(rank, 8, keys_per_rank=80_000, diff_frac=0.01)
+    sa, ca = up(a)
+    sb, cb = up(b)
+    diff = engine.merkle_diff(engine.merkle_build(sa, 14), engine.merkle_build(sb, 14))
+    delta = engine.take_keys(sb, diff)
+    out, octx = engine.join2(sa, ca, delta, cb, keys=diff)
+    wr, wc = R.join2(a["rows"], a["ctx"], b["rows"], b["ctx"])
+    rows_eq(out, wr)
+    ctx_eq(octx, wc)
