@@ -371,9 +371,7 @@ int dg_join2_changes(dg_engine* e, const dg_store* a, const dg_context* ca, cons
   if (!n_changed || (cap && !changed)) return fail(DG_E_INVAL, "dg_join2_changes: null output");
   void* chg = nullptr;
   TRY(join2_enqueue(e, a, ca, b, cb, keys, n_keys, out, out_ctx, e->d_counts, &chg));
-  Scan sc;
-  TRY(next_scan(e, &sc));
-  HIP_TRY(launch_join2_changes(a->n, b->n, chg, changed, cap, sc, e->d_counts + 2, e->stream));
+  HIP_TRY(launch_join2_changes(a->n, b->n, chg, changed, cap, e->d_counts + 2, e->stream));
   TRY(read_counts(e, 3));
   out->n = e->h_counts[0];
   out_ctx->n = e->h_counts[1];

@@ -46,14 +46,14 @@ hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& 
                         void* chg_tmp = nullptr);
 // Changed keys (dg_join2_changes): with chg_tmp (join2_changes_tmp_bytes) the join
 // records per-tile change events (always the single-pass kernel); launch_join2_changes
-// then drops repeats and compacts them into out[0, cap) (*d_count = changed keys),
-// using look-back granules [0, ntiles) of its Scan.
+// then drops repeats and compacts them into out[0, cap) (*d_count = changed keys).
+// chg_tmp: JOIN_TILE u64 events + u64 offset + 3 u32 per tile.
 inline size_t join2_changes_tmp_bytes(u64 na, u64 nb) {
   const u64 t = join2_tiles(na, nb);
-  return t * (u64)JOIN_TILE * 8 + t * 4 + 256;
+  return t * ((u64)JOIN_TILE * 8 + 8 + 12) + 256;
 }
-hipError_t launch_join2_changes(u64 na, u64 nb, void* chg_tmp, u64* out, u64 cap,
-                                const Scan& scan, u64* d_count, hipStream_t st);
+hipError_t launch_join2_changes(u64 na, u64 nb, void* chg_tmp, u64* out, u64 cap, u64* d_count,
+                                hipStream_t st);
 inline size_t join2_pass_tmp_bytes(u64 na, u64 nb) {
   const u64 t = join2_tiles(na, nb);
   return ((t * 4 + 255) / 256) * 256 + t * (u64)JOIN_TILE * 2 + 256;  // counts + slot lists

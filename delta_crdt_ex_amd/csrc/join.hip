@@ -815,83 +815,119 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
 // The keys whose rows the join changed (CausalCrdt's diff/3 after every join,
 // causal_crdt.ex:343-351, over `keys`), ascending and unique, from the stream
 // kernel's per-tile change events (ascending; a key repeats when several of its rows
-// changed, possibly across tiles).  chg_compact_kernel, one workgroup per tile in
-// ticket order: an event is kept where it differs from the event before it -- inside
-// the tile, or for the tile's first event the last event of the nearest non-empty
-// earlier tile (wave 0 scans the per-tile counts back 64 at a time; only tiles with
-// events scan, so the scans add up to O(tiles)) -- and the kept keys are compacted
-// by decoupled look-back.
+// changed, possibly across tiles).  An event is kept where it differs from the event
+// before it: inside its tile, or -- for a tile's first event -- the last event of the
+// nearest non-empty earlier tile.  Every tile of the launch is resident at once, so
+// instead of a look-back (which would spin on the whole launch) three short passes:
+//   chg_count_kernel  per tile: events differing from their in-tile predecessor
+//   chg_scan_kernel   one workgroup over the tiles: nearest non-empty predecessor
+//                     (max-scan), the first event's repeat flag, exclusive offsets
+//   chg_write_kernel  per tile: the kept events at the tile's offset
 constexpr int GB = 256, GI = (JT + GB - 1) / GB;
+constexpr int SB = 1024;  // chg_scan_kernel threads
 
-__global__ __launch_bounds__(GB) void chg_compact_kernel(const u64* tmp, const u32* cnt, u64 ntiles,
-                                                        u64* out, u64 cap, Scan scan,
-                                                        u64* d_count) {
-  __shared__ u64 s_b[3];
+struct ChgArgs {
+  const u64* tmp;  // JT events per tile
+  const u32* cnt;  // events per tile
+  u32* wu;         // events after the first that differ from their predecessor
+  u32* first_dup;  // the tile's first event repeats the previous tile's last one
+  u64* off;        // output offset of the tile
+  u64 ntiles;
+  u64* out;
+  u64 cap;
+  u64* d_count;
+};
+
+__global__ __launch_bounds__(GB) void chg_count_kernel(ChgArgs p) {
   __shared__ u32 s_wave[GB / WAVE + 1];
-  const int tid = threadIdx.x;
-  if (tid == 0) {
-    const u32 t = atomicAdd(scan.ticket, 1u);
-    if ((u64)t == ntiles - 1) atomicExch(scan.ticket, 0u);
-    s_b[0] = t;
-  }
+  const u64 t = blockIdx.x;
+  const u32 n = p.cnt[t];
+  const u64* ev = p.tmp + t * (u64)JT;
+  u32 c = 0;
+  for (u32 i = threadIdx.x + 1; i < n; i += GB) c += ev[i] != ev[i - 1] ? 1u : 0u;
+  u32 tot;
+  block_excl_scan<GB>(c, s_wave, &tot);
+  if (threadIdx.x == 0) p.wu[t] = tot;
+}
+
+__global__ __launch_bounds__(SB) void chg_scan_kernel(ChgArgs p) {
+  __shared__ u32 s_wave[SB / WAVE + 1];
+  __shared__ i64 s_last[SB / WAVE + 1];
+  __shared__ u64 s_carry[2];  // [0] output offset, [1] last non-empty tile (+1; 0 = none)
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
+  if (tid == 0) s_carry[0] = s_carry[1] = 0;
   __syncthreads();
-  const u64 t = s_b[0];
-  const u32 n = cnt[t];
-  const u64* ev = tmp + t * (u64)JT;
-  if (n > 0 && tid < WAVE) {  // last event before this tile, if any
-    u64 prev = ~0ull, has = 0;
-    for (i64 base = (i64)t - 1; base >= 0; base -= WAVE) {
-      const i64 q = base - tid;
-      const u32 c = q >= 0 ? cnt[q] : 0u;
-      const u64 m = __ballot(c > 0);
-      if (m) {
-        const int l = __ffsll((long long)m) - 1;  // the nearest: smallest lane
-        const i64 qq = base - l;
-        prev = tmp[qq * (i64)JT + __shfl(c, l, WAVE) - 1];
-        has = 1;
-        break;
-      }
+  for (u64 c0 = 0; c0 < p.ntiles; c0 += SB) {
+    const u64 t = c0 + tid;
+    const u32 n = t < p.ntiles ? p.cnt[t] : 0u;
+    // nearest non-empty tile before t: inclusive max-scan of (t+1 if non-empty)
+    i64 m = n > 0 ? (i64)t + 1 : 0;
+    for (int d = 1; d < WAVE; d <<= 1) {
+      const i64 o = __shfl_up(m, d, WAVE);
+      if (lane >= d) m = max(m, o);
     }
+    if (lane == WAVE - 1) s_last[w] = m;
+    __syncthreads();
     if (tid == 0) {
-      s_b[1] = prev;
-      s_b[2] = has;
+      i64 run = (i64)s_carry[1];
+      for (int i = 0; i < SB / WAVE; i++) {
+        const i64 v = s_last[i];
+        s_last[i] = run;  // exclusive over waves
+        run = max(run, v);
+      }
+      s_last[SB / WAVE] = run;
     }
+    __syncthreads();
+    const i64 before_wave = s_last[w];
+    i64 prev_incl = max(m, before_wave);  // nearest non-empty <= t
+    i64 prev = __shfl_up(prev_incl, 1, WAVE);  // nearest non-empty < t
+    if (lane == 0) prev = before_wave;
+    u32 dup = 0, uc = 0;
+    if (n > 0) {
+      if (prev > 0) {
+        const u64 q = (u64)prev - 1;
+        dup = p.tmp[t * (u64)JT] == p.tmp[q * (u64)JT + p.cnt[q] - 1] ? 1u : 0u;
+      }
+      uc = p.wu[t] + 1 - dup;
+    }
+    u32 tot;
+    const u32 o = block_excl_scan<SB>(uc, s_wave, &tot);
+    if (t < p.ntiles) {
+      p.first_dup[t] = dup;
+      p.off[t] = s_carry[0] + o;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      s_carry[0] += tot;
+      s_carry[1] = (u64)s_last[SB / WAVE];
+    }
+    __syncthreads();
   }
-  __syncthreads();
+  if (tid == 0) p.d_count[0] = s_carry[0];
+}
+
+__global__ __launch_bounds__(GB) void chg_write_kernel(ChgArgs p) {
+  __shared__ u32 s_wave[GB / WAVE + 1];
+  const u64 t = blockIdx.x;
+  const u32 n = p.cnt[t];
+  const u64* ev = p.tmp + t * (u64)JT;
+  const bool dup0 = p.first_dup[t] != 0;
   u64 v[GI];
   u32 keep = 0;
 #pragma unroll
   for (int q = 0; q < GI; q++) {
-    const u32 i = tid * GI + q;
+    const u32 i = threadIdx.x * GI + q;
     v[q] = i < n ? ev[i] : 0;
-    if (i < n) {
-      const bool dup = i > 0 ? ev[i - 1] == v[q] : (s_b[2] && s_b[1] == v[q]);
-      if (!dup) keep |= 1u << q;
-    }
+    if (i < n && (i > 0 ? ev[i - 1] != v[q] : !dup0)) keep |= 1u << q;
   }
   u32 tot;
   u32 pos = block_excl_scan<GB>(__popc(keep), s_wave, &tot);
-  if (tid < WAVE) {
-    u64 prefix = 0;
-    if (t == 0) {
-      if (tid == 0) lb_publish(scan.state, 0, scan.epoch, LB_INC, tot);
-    } else {
-      if (tid == 0) lb_publish(scan.state, t, scan.epoch, LB_AGG, tot);
-      prefix = lb_lookback(scan.state, t, scan.epoch, scan.err);
-      if (tid == 0) lb_publish(scan.state, t, scan.epoch, LB_INC, prefix + tot);
-    }
-    if (tid == 0) {
-      s_b[1] = prefix;
-      if (t == ntiles - 1) d_count[0] = prefix + tot;
-    }
-  }
-  __syncthreads();
-  const u64 base = s_b[1];
+  const u64 base = p.off[t];
 #pragma unroll
   for (int q = 0; q < GI; q++)
     if (keep & (1u << q)) {
       const u64 o = base + pos++;
-      if (o < cap) out[o] = v[q];
+      if (o < p.cap) p.out[o] = v[q];
     }
 }
 
@@ -1048,7 +1084,7 @@ hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& 
   p.lists = nullptr;
   p.counts = nullptr;
   p.chg_tmp = chg_tmp ? (u64*)chg_tmp : nullptr;
-  p.chg_cnt = chg_tmp ? (u32*)((char*)chg_tmp + p.ntiles * (u64)JT * 8) : nullptr;
+  p.chg_cnt = chg_tmp ? (u32*)((char*)chg_tmp + p.ntiles * ((u64)JT * 8 + 8)) : nullptr;
   if (p.ntiles == 0) {
     // no rows: only the context union runs
     hipError_t e = hipMemsetAsync(d_counts, 0, sizeof(u64), st);
@@ -1081,14 +1117,28 @@ hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& 
   return hipGetLastError();
 }
 
-hipError_t launch_join2_changes(u64 na, u64 nb, void* chg_tmp, u64* out, u64 cap,
-                                const Scan& scan, u64* d_count, hipStream_t st) {
+hipError_t launch_join2_changes(u64 na, u64 nb, void* chg_tmp, u64* out, u64 cap, u64* d_count,
+                                hipStream_t st) {
   const u64 ntiles = join2_tiles(na, nb);
   if (ntiles == 0) return hipMemsetAsync(d_count, 0, sizeof(u64), st);
-  const u64* tmp = (const u64*)chg_tmp;
-  const u32* cnt = (const u32*)((const char*)chg_tmp + ntiles * (u64)JT * 8);
-  hipLaunchKernelGGL(chg_compact_kernel, dim3((unsigned)ntiles), dim3(GB), 0, st, tmp, cnt, ntiles,
-                     out, cap, scan, d_count);
+  char* c = (char*)chg_tmp;
+  ChgArgs p;
+  p.tmp = (const u64*)c;
+  c += ntiles * (u64)JT * 8;
+  p.off = (u64*)c;
+  c += ntiles * 8;
+  p.cnt = (const u32*)c;
+  c += ntiles * 4;
+  p.wu = (u32*)c;
+  c += ntiles * 4;
+  p.first_dup = (u32*)c;
+  p.ntiles = ntiles;
+  p.out = out;
+  p.cap = cap;
+  p.d_count = d_count;
+  hipLaunchKernelGGL(chg_count_kernel, dim3((unsigned)ntiles), dim3(GB), 0, st, p);
+  hipLaunchKernelGGL(chg_scan_kernel, dim3(1), dim3(SB), 0, st, p);
+  hipLaunchKernelGGL(chg_write_kernel, dim3((unsigned)ntiles), dim3(GB), 0, st, p);
   return hipGetLastError();
 }
 
