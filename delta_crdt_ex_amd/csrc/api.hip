@@ -709,11 +709,9 @@ int dg_read_lww(dg_engine* e, const dg_store* s, const uint64_t* keys, uint64_t 
     return fail(DG_E_CAPACITY, "dg_read_lww: cap %llu < %llu", (unsigned long long)cap,
                 (unsigned long long)need);
   TRY(set_device(e));
-  TRY(ensure_state(e, seg_tiles(s->n)));
-  Scan sc;
-  TRY(next_scan(e, &sc));
-  HIP_TRY(launch_read_lww(rows_of(s), keys, keys ? n_keys : 0, out_key, out_val, sc, e->d_counts,
-                          e->stream));
+  TRY(ensure_state(e, 2 * seg_tiles(s->n) + 2));  // raw per-tile counts and offsets
+  HIP_TRY(launch_read_lww(rows_of(s), keys, keys ? n_keys : 0, out_key, out_val, e->state,
+                          e->d_counts, e->stream));
   TRY(read_counts(e, 1));
   *n_out = e->h_counts[0];
   return DG_OK;
@@ -727,11 +725,9 @@ int dg_merkle_build(dg_engine* e, const dg_store* s, dg_merkle* t) {
   if (t->depth < 1 || t->depth > 26) return fail(DG_E_INVAL, "dg_merkle_build: depth %u", t->depth);
   if (t->cap_keys < s->n) return fail(DG_E_CAPACITY, "dg_merkle_build: cap_keys < rows");
   TRY(set_device(e));
-  TRY(ensure_state(e, seg_tiles(s->n)));
-  Scan sc;
-  TRY(next_scan(e, &sc));
-  HIP_TRY(launch_merkle_leaves(rows_of(s), t->depth, t->leaf_key, t->leaf_hash, t->bucket_off, sc,
-                               e->d_counts, e->stream));
+  TRY(ensure_state(e, 2 * seg_tiles(s->n) + 2));  // raw per-tile counts and offsets
+  HIP_TRY(launch_merkle_leaves(rows_of(s), t->depth, t->leaf_key, t->leaf_hash, t->bucket_off,
+                               e->state, e->d_counts, e->stream));
   HIP_TRY(launch_merkle_levels(t->depth, t->leaf_hash, t->bucket_off, t->nodes, e->stream));
   TRY(read_counts(e, 1));
   t->n_keys = e->h_counts[0];

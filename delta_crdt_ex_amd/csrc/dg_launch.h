@@ -118,11 +118,12 @@ constexpr int SEG_BLOCK = 256;
 constexpr int SEG_ITEMS = 4;
 constexpr int SEG_TILE = SEG_BLOCK * SEG_ITEMS;
 inline u64 seg_tiles(u64 n) { return (n + SEG_TILE - 1) / SEG_TILE; }
+// scratch: 2 * seg_tiles(n) u64 (per-tile counts and offsets).
 hipError_t launch_read_lww(const Rows& s, const u64* keys, u64 n_keys, u64* out_key, u64* out_val,
-                           const Scan& scan, u64* d_count, hipStream_t st);
+                           u64* scratch, u64* d_count, hipStream_t st);
 // Merkle leaves: (key, Σ row hashes) per key + bucket_off[b] = first leaf of bucket >= b.
 hipError_t launch_merkle_leaves(const Rows& s, u32 depth, u64* leaf_key, u64* leaf_hash,
-                                u64* bucket_off, const Scan& scan, u64* d_count, hipStream_t st);
+                                u64* bucket_off, u64* scratch, u64* d_count, hipStream_t st);
 // Sortedness check: sets *d_bad to nonzero if rows are not strictly ascending.
 hipError_t launch_store_check(const Rows& s, u32* d_bad, hipStream_t st);
 

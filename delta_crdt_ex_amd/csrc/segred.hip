@@ -11,8 +11,10 @@
 //
 // Shape: one tile = 1024 rows = 256 threads x 4 consecutive rows; a thread owning a
 // key head walks the key's run forward (runs are short: one row per dot, <= 32
-// entries per key in the reference's reproducible regime); heads are compacted
-// with the same single-pass decoupled look-back as the join.
+// entries per key in the reference's reproducible regime).  Heads are compacted in
+// three passes -- count per tile (key column only), one-workgroup offset scan, write
+// -- not by a decoupled look-back: thousands of tiles finishing in lock-step rounds
+// made every tile walk back a whole round of predecessors.
 #include "dg_hash.h"
 #include "dg_launch.h"
 
@@ -34,111 +36,169 @@ struct SegArgs {
   u64* out_b;  // value id / leaf hash
   u64* bucket_off;
   u32 depth;
-  Scan scan;
+  u64* cnt;    // heads per tile
+  u64* off;    // output offset per tile
   u64 ntiles;
   u64* d_count;
 };
 
-template <SegOp OP>
-__global__ __launch_bounds__(SB) void segred_kernel(SegArgs p) {
-  __shared__ u64 s_a[ST], s_b[ST], s_row[ST];
-  __shared__ u32 s_wave[SB / WAVE + 1];
-  __shared__ u64 s_bcast[2];
-  const int tid = threadIdx.x;
-  const u64 n = p.s.n;
-  if (tid == 0) {
-    u32 t = atomicAdd(p.scan.ticket, 1u);
-    if ((u64)t == p.ntiles - 1) atomicExch(p.scan.ticket, 0u);
-    s_bcast[0] = t;
-  }
-  __syncthreads();
-  const u64 tile = s_bcast[0];
-  const u64 r0 = tile * ST + (u64)tid * SI;
 
-  u64 oa[SI], ob[SI];
-  u32 heads = 0;
-  u64 prev_key = (r0 > 0 && r0 - 1 < n) ? p.s.key[r0 - 1] : 0;
+// Pass 1: key heads per tile (a head opens a key's run; with a key list only listed
+// keys count -- read/2, aw_lww_map.ex:218-220).  Coalesced: thread tid looks at rows
+// tid, tid + SB, ... of the tile and at the row before each.
+template <SegOp OP>
+__global__ __launch_bounds__(SB) void seg_count_kernel(SegArgs p) {
+  __shared__ u32 s_wave[SB / WAVE + 1];
+  const u64 t = blockIdx.x, n = p.s.n;
+  u32 c = 0;
 #pragma unroll
   for (int k = 0; k < SI; k++) {
-    oa[k] = 0;
-    ob[k] = 0;
-    const u64 i = r0 + k;
+    const u64 i = t * ST + (u64)k * SB + threadIdx.x;
     if (i < n) {
       const u64 key = p.s.key[i];
-      bool head = (i == 0) || key != prev_key;
-      prev_key = key;
-      if (head && p.keys != nullptr) head = keyset_has(p.keys, p.n_keys, key);
-      if (head) {
-        oa[k] = key;
-        if (OP == SegOp::Read) {
-          i64 best_ts = p.s.ts[i];
-          u64 best_val = p.s.val[i];
-          for (u64 e = i + 1; e < n && p.s.key[e] == key; e++) {
-            i64 t = p.s.ts[e];
-            if (t > best_ts) {
-              best_ts = t;
-              best_val = p.s.val[e];
-            }
-          }
-          ob[k] = best_val;
-        } else {
-          u64 h = 0;
-          for (u64 e = i; e < n && p.s.key[e] == key; e++)
-            h += row_hash(key, p.s.val[e], p.s.ts[e], p.s.node[e], p.s.cnt[e]);
-          ob[k] = h;
-        }
-        heads |= 1u << k;
+      bool head = i == 0 || key != p.s.key[i - 1];
+      if (OP == SegOp::Read && head && p.keys != nullptr) head = keyset_has(p.keys, p.n_keys, key);
+      c += head ? 1u : 0u;
+    }
+  }
+  u32 tot;
+  block_excl_scan<SB>(c, s_wave, &tot);
+  if (threadIdx.x == 0) p.cnt[t] = tot;
+}
+
+// Pass 2: exclusive offsets of the tile counts (one workgroup; a tile count is
+// <= ST, so 1024 tiles sum below 2^32 per chunk).
+constexpr int SSB = 1024;
+__global__ __launch_bounds__(SSB) void seg_scan_kernel(SegArgs p) {
+  __shared__ u32 s_wave[SSB / WAVE + 1];
+  __shared__ u64 s_carry;
+  if (threadIdx.x == 0) s_carry = 0;
+  __syncthreads();
+  for (u64 c0 = 0; c0 < p.ntiles; c0 += SSB) {
+    const u64 t = c0 + threadIdx.x;
+    const u32 v = t < p.ntiles ? (u32)p.cnt[t] : 0u;
+    u32 tot;
+    const u32 o = block_excl_scan<SSB>(v, s_wave, &tot);
+    if (t < p.ntiles) p.off[t] = s_carry + o;
+    __syncthreads();
+    if (threadIdx.x == 0) s_carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) p.d_count[0] = s_carry;
+}
+
+// Pass 3: one output per head at the tile's offset -- (key, read value) or (key, leaf
+// hash).  The tile's rows are staged in LDS by coalesced loads (Read: key, val, ts;
+// Leaves: key and the row's hash, computed while loading); each thread then reduces
+// the key runs that start among its SI consecutive rows from LDS (a run that leaves
+// the tile continues from global memory), and the heads are compacted in LDS and
+// written coalesced.
+template <SegOp OP>
+__global__ __launch_bounds__(SB) void seg_write_kernel(SegArgs p) {
+  __shared__ u64 s_key[ST + 1], s_x[ST], s_y[ST];  // Read: val, ts.  Leaves: hash, row
+  __shared__ u32 s_wave[SB / WAVE + 1];
+  const int tid = threadIdx.x;
+  const u64 n = p.s.n, tile = blockIdx.x, t0 = tile * ST;
+  const u32 nt = (u32)min<u64>(ST, n - t0);
+#pragma unroll
+  for (int k = 0; k < SI; k++) {
+    const u32 j = k * SB + tid;
+    if (j < nt) {
+      const u64 i = t0 + j;
+      const u64 key = p.s.key[i];
+      s_key[j + 1] = key;
+      if (OP == SegOp::Read) {
+        s_x[j] = p.s.val[i];
+        s_y[j] = (u64)p.s.ts[i];
+      } else {
+        s_x[j] = row_hash(key, p.s.val[i], p.s.ts[i], p.s.node[i], p.s.cnt[i]);
       }
+    }
+  }
+  if (tid == 0) s_key[0] = t0 > 0 ? p.s.key[t0 - 1] : ~p.s.key[0];
+  __syncthreads();
+  const u32 j0 = tid * SI;
+  u32 heads = 0;
+  u64 oa[SI], ob[SI];
+#pragma unroll
+  for (int k = 0; k < SI; k++) {
+    const u32 j = j0 + k;
+    oa[k] = ob[k] = 0;
+    if (j >= nt) continue;
+    const u64 key = s_key[j + 1];
+    if (key == s_key[j]) continue;  // not a head
+    if (OP == SegOp::Read && p.keys != nullptr && !keyset_has(p.keys, p.n_keys, key)) continue;
+    heads |= 1u << k;
+    oa[k] = key;
+    u32 e = j + 1;
+    if (OP == SegOp::Read) {
+      i64 best_ts = (i64)s_y[j];
+      u64 best_val = s_x[j];
+      for (; e < nt && s_key[e + 1] == key; e++) {
+        const i64 ts = (i64)s_y[e];
+        if (ts > best_ts) {
+          best_ts = ts;
+          best_val = s_x[e];
+        }
+      }
+      for (u64 g = t0 + e; e == nt && g < n && p.s.key[g] == key; g++) {
+        const i64 ts = p.s.ts[g];
+        if (ts > best_ts) {
+          best_ts = ts;
+          best_val = p.s.val[g];
+        }
+      }
+      ob[k] = best_val;
+    } else {
+      u64 h = s_x[j];
+      for (; e < nt && s_key[e + 1] == key; e++) h += s_x[e];
+      for (u64 g = t0 + e; e == nt && g < n && p.s.key[g] == key; g++)
+        h += row_hash(key, p.s.val[g], p.s.ts[g], p.s.node[g], p.s.cnt[g]);
+      ob[k] = h;
     }
   }
   u32 tile_total;
   u32 pos = block_excl_scan<SB>(__popc(heads), s_wave, &tile_total);
+  __syncthreads();  // the staged rows are read; their arrays take the compacted heads
 #pragma unroll
   for (int k = 0; k < SI; k++)
     if (heads & (1u << k)) {
-      s_a[pos] = oa[k];
-      s_b[pos] = ob[k];
-      s_row[pos] = r0 + k;
+      s_x[pos] = oa[k];
+      s_y[pos] = ob[k];
+      s_key[pos] = t0 + j0 + k;  // the head's row
       pos++;
     }
-
-  if (tid < WAVE) {
-    u64 prefix = 0;
-    if (tile == 0) {
-      if (tid == 0) lb_publish(p.scan.state, 0, p.scan.epoch, LB_INC, tile_total);
-    } else {
-      if (tid == 0) lb_publish(p.scan.state, tile, p.scan.epoch, LB_AGG, tile_total);
-      prefix = lb_lookback(p.scan.state, tile, p.scan.epoch, p.scan.err);
-      if (tid == 0) lb_publish(p.scan.state, tile, p.scan.epoch, LB_INC, prefix + tile_total);
-    }
-    if (tid == 0) {
-      s_bcast[1] = prefix;
-      if (tile == p.ntiles - 1) p.d_count[0] = prefix + tile_total;
-    }
-  }
   __syncthreads();
-  const u64 base = s_bcast[1];
+  const u64 base = p.off[tile];
   for (u32 q = tid; q < tile_total; q += SB) {
     const u64 o = base + q;
-    p.out_a[o] = s_a[q];
-    p.out_b[o] = s_b[q];
+    p.out_a[o] = s_x[q];
+    p.out_b[o] = s_y[q];
     if (OP == SegOp::Leaves) {
       // bucket_off[b] = index of the first leaf whose bucket >= b, for every bucket
       // strictly after the previous key's bucket and up to this key's bucket.
       const u32 sh = 64 - p.depth;
-      const u64 row = s_row[q];
-      const u64 bk = s_a[q] >> sh;
+      const u64 row = s_key[q], key = s_x[q];
+      const u64 bk = key >> sh;
       const u64 bstart = row == 0 ? 0 : (p.s.key[row - 1] >> sh) + 1;
       for (u64 b = bstart; b <= bk; b++) p.bucket_off[b] = o;
       // after the store's last key: the trailing buckets (and the end sentinel)
       u64 e = row + 1;
-      while (e < n && p.s.key[e] == s_a[q]) e++;
+      while (e < n && p.s.key[e] == key) e++;
       if (e == n) {
         const u64 nbk = 1ull << p.depth;
         for (u64 b = bk + 1; b <= nbk; b++) p.bucket_off[b] = o + 1;
       }
     }
   }
+}
+
+template <SegOp OP>
+hipError_t launch_seg(SegArgs& p, hipStream_t st) {
+  hipLaunchKernelGGL(seg_count_kernel<OP>, dim3((unsigned)p.ntiles), dim3(SB), 0, st, p);
+  hipLaunchKernelGGL(seg_scan_kernel, dim3(1), dim3(SSB), 0, st, p);
+  hipLaunchKernelGGL(seg_write_kernel<OP>, dim3((unsigned)p.ntiles), dim3(SB), 0, st, p);
+  return hipGetLastError();
 }
 
 __global__ void store_check_kernel(Rows s, u32* bad) {
@@ -156,39 +216,39 @@ __global__ void fill_u64_kernel(u64* p, u64 n, u64 v) {
 }  // namespace
 
 hipError_t launch_read_lww(const Rows& s, const u64* keys, u64 n_keys, u64* out_key, u64* out_val,
-                           const Scan& scan, u64* d_count, hipStream_t st) {
+                           u64* scratch, u64* d_count, hipStream_t st) {
   SegArgs p{};
   p.s = s;
   p.keys = keys;
   p.n_keys = n_keys;
   p.out_a = out_key;
   p.out_b = out_val;
-  p.scan = scan;
   p.ntiles = seg_tiles(s.n);
+  p.cnt = scratch;
+  p.off = scratch + p.ntiles;
   p.d_count = d_count;
   if (p.ntiles == 0) return hipMemsetAsync(d_count, 0, sizeof(u64), st);
-  hipLaunchKernelGGL(segred_kernel<SegOp::Read>, dim3((unsigned)p.ntiles), dim3(SB), 0, st, p);
-  return hipGetLastError();
+  return launch_seg<SegOp::Read>(p, st);
 }
 
 hipError_t launch_merkle_leaves(const Rows& s, u32 depth, u64* leaf_key, u64* leaf_hash,
-                                u64* bucket_off, const Scan& scan, u64* d_count, hipStream_t st) {
+                                u64* bucket_off, u64* scratch, u64* d_count, hipStream_t st) {
   SegArgs p{};
   p.s = s;
   p.out_a = leaf_key;
   p.out_b = leaf_hash;
   p.bucket_off = bucket_off;
   p.depth = depth;
-  p.scan = scan;
   p.ntiles = seg_tiles(s.n);
+  p.cnt = scratch;
+  p.off = scratch + p.ntiles;
   p.d_count = d_count;
   if (p.ntiles == 0) {
     hipLaunchKernelGGL(fill_u64_kernel, dim3(256), dim3(256), 0, st, bucket_off,
                        (1ull << depth) + 1, 0ull);
     return hipMemsetAsync(d_count, 0, sizeof(u64), st);
   }
-  hipLaunchKernelGGL(segred_kernel<SegOp::Leaves>, dim3((unsigned)p.ntiles), dim3(SB), 0, st, p);
-  return hipGetLastError();
+  return launch_seg<SegOp::Leaves>(p, st);
 }
 
 hipError_t launch_store_check(const Rows& s, u32* d_bad, hipStream_t st) {
