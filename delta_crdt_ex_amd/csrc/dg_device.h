@@ -199,6 +199,29 @@ __device__ __forceinline__ u32 block_excl_scan(u32 v, u32* s_wave, u32* total) {
   return s_wave[w] + inc - v;
 }
 
+// ---------------------------------------------------------------- tile offsets
+// Exclusive offsets of per-tile counts by ONE workgroup of NT threads (the middle pass
+// of count / scan / write compactions, used where every tile of a launch is resident
+// at once and a decoupled look-back would make each tile poll a whole round of
+// predecessors).  cnt values must be < 2^32 / NT.  *total = the sum.
+template <int NT>
+__device__ __forceinline__ void scan_tile_counts(const u64* cnt, u64* off, u64 ntiles, u64* total,
+                                                 u32* s_wave, u64* s_carry) {
+  if (threadIdx.x == 0) *s_carry = 0;
+  __syncthreads();
+  for (u64 c0 = 0; c0 < ntiles; c0 += NT) {
+    const u64 t = c0 + threadIdx.x;
+    const u32 v = t < ntiles ? (u32)cnt[t] : 0u;
+    u32 tot;
+    const u32 o = block_excl_scan<NT>(v, s_wave, &tot);
+    if (t < ntiles) off[t] = *s_carry + o;
+    __syncthreads();
+    if (threadIdx.x == 0) *s_carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *total = *s_carry;
+}
+
 // ---------------------------------------------------------------- look-back
 constexpr u64 LB_VALUE_MASK = (1ull << 42) - 1;
 constexpr u32 LB_AGG = 1, LB_INC = 2;

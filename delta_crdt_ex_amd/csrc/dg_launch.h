@@ -135,7 +135,7 @@ inline u64 diff_tiles(u32 depth) { return depth >= 8 ? (1ull << (depth - 8)) : 1
 hipError_t launch_merkle_diff(u32 depth, const u64* nodes_a, const u64* leaf_key_a,
                               const u64* leaf_hash_a, const u64* off_a, const u64* nodes_b,
                               const u64* leaf_key_b, const u64* leaf_hash_b, const u64* off_b,
-                              u64* out_keys, u64 cap, const Scan& scan, u64* d_count,
-                              hipStream_t st);
+                              u64* out_keys, u64 cap, u64* scratch, u64* d_count,
+                              hipStream_t st);  // scratch: 2 * diff_tiles(depth) u64
 
 }  // namespace dg

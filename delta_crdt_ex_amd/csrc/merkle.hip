@@ -68,7 +68,8 @@ struct DiffArgs {
   const u64 *nb, *kb, *hb, *ob;
   u64* out;
   u64 cap;
-  Scan scan;
+  u64* cnt;  // differing keys per tile
+  u64* off;  // their output offset
   u64 ntiles;
   u64* d_count;
 };
@@ -101,48 +102,49 @@ __device__ __forceinline__ u32 diff_bucket(const DiffArgs& p, u64 b, u64* out, u
   return c;
 }
 
-__global__ __launch_bounds__(DB) void merkle_diff_kernel(DiffArgs p) {
-  __shared__ u32 s_wave[DB / WAVE + 1];
-  __shared__ u64 s_bcast[2];
-  const int tid = threadIdx.x;
-  if (tid == 0) {
-    u32 t = atomicAdd(p.scan.ticket, 1u);
-    if ((u64)t == p.ntiles - 1) atomicExch(p.scan.ticket, 0u);
-    s_bcast[0] = t;
-  }
-  __syncthreads();
-  const u64 tile = s_bcast[0];
-  const u32 rl = p.depth >= 8 ? p.depth - 8 : 0;      // subtree root level
+// The differing keys in three passes (every tile of a launch is resident at once, so
+// a look-back would poll whole rounds of predecessors): per tile of 256 buckets the
+// count, one workgroup's offset scan, then the write.  A bucket is walked only where
+// its subtree root and its own node differ.
+__device__ __forceinline__ u64 diff_bucket_of(const DiffArgs& p, u64 tile, int tid, bool* walk) {
+  const u32 rl = p.depth >= 8 ? p.depth - 8 : 0;  // subtree root level
   const u64 root = ((1ull << rl) - 1) + tile;
   const u64 nbk = 1ull << p.depth;
-  const u64 bpt = p.depth >= 8 ? 256ull : nbk;          // buckets per tile
+  const u64 bpt = p.depth >= 8 ? 256ull : nbk;      // buckets per tile
   const u64 b = tile * bpt + tid;
-  const bool subtree_differs = p.na[root] != p.nb[root];
-  bool differs = false;
-  u32 c = 0;
-  if (subtree_differs && (u64)tid < bpt) {
+  *walk = false;
+  if ((u64)tid < bpt && p.na[root] != p.nb[root]) {
     const u64 leaf = (nbk - 1) + b;
-    differs = p.na[leaf] != p.nb[leaf];
-    if (differs) c = diff_bucket<false>(p, b, nullptr, 0, 0);
+    *walk = p.na[leaf] != p.nb[leaf];
   }
-  u32 tile_total;
-  u32 ex = block_excl_scan<DB>(c, s_wave, &tile_total);
-  if (tid < WAVE) {
-    u64 prefix = 0;
-    if (tile == 0) {
-      if (tid == 0) lb_publish(p.scan.state, 0, p.scan.epoch, LB_INC, tile_total);
-    } else {
-      if (tid == 0) lb_publish(p.scan.state, tile, p.scan.epoch, LB_AGG, tile_total);
-      prefix = lb_lookback(p.scan.state, tile, p.scan.epoch, p.scan.err);
-      if (tid == 0) lb_publish(p.scan.state, tile, p.scan.epoch, LB_INC, prefix + tile_total);
-    }
-    if (tid == 0) {
-      s_bcast[1] = prefix;
-      if (tile == p.ntiles - 1) p.d_count[0] = prefix + tile_total;
-    }
-  }
-  __syncthreads();
-  if (c) diff_bucket<true>(p, b, p.out, s_bcast[1] + ex, p.cap);
+  return b;
+}
+
+__global__ __launch_bounds__(DB) void merkle_diff_count_kernel(DiffArgs p) {
+  __shared__ u32 s_wave[DB / WAVE + 1];
+  bool walk;
+  const u64 b = diff_bucket_of(p, blockIdx.x, threadIdx.x, &walk);
+  const u32 c = walk ? diff_bucket<false>(p, b, nullptr, 0, 0) : 0u;
+  u32 tot;
+  block_excl_scan<DB>(c, s_wave, &tot);
+  if (threadIdx.x == 0) p.cnt[blockIdx.x] = tot;
+}
+
+constexpr int DSB = 1024;
+__global__ __launch_bounds__(DSB) void merkle_diff_scan_kernel(DiffArgs p) {
+  __shared__ u32 s_wave[DSB / WAVE + 1];
+  __shared__ u64 s_carry;
+  scan_tile_counts<DSB>(p.cnt, p.off, p.ntiles, p.d_count, s_wave, &s_carry);
+}
+
+__global__ __launch_bounds__(DB) void merkle_diff_write_kernel(DiffArgs p) {
+  __shared__ u32 s_wave[DB / WAVE + 1];
+  bool walk;
+  const u64 b = diff_bucket_of(p, blockIdx.x, threadIdx.x, &walk);
+  const u32 c = walk ? diff_bucket<false>(p, b, nullptr, 0, 0) : 0u;
+  u32 tot;
+  const u32 ex = block_excl_scan<DB>(c, s_wave, &tot);
+  if (c) diff_bucket<true>(p, b, p.out, p.off[blockIdx.x] + ex, p.cap);
 }
 
 }  // namespace
@@ -168,7 +170,7 @@ hipError_t launch_merkle_levels(u32 depth, const u64* leaf_hash, const u64* buck
 hipError_t launch_merkle_diff(u32 depth, const u64* nodes_a, const u64* leaf_key_a,
                               const u64* leaf_hash_a, const u64* off_a, const u64* nodes_b,
                               const u64* leaf_key_b, const u64* leaf_hash_b, const u64* off_b,
-                              u64* out_keys, u64 cap, const Scan& scan, u64* d_count,
+                              u64* out_keys, u64 cap, u64* scratch, u64* d_count,
                               hipStream_t st) {
   DiffArgs p;
   p.depth = depth;
@@ -182,10 +184,13 @@ hipError_t launch_merkle_diff(u32 depth, const u64* nodes_a, const u64* leaf_key
   p.ob = off_b;
   p.out = out_keys;
   p.cap = cap;
-  p.scan = scan;
   p.ntiles = diff_tiles(depth);
+  p.cnt = scratch;
+  p.off = scratch + p.ntiles;
   p.d_count = d_count;
-  hipLaunchKernelGGL(merkle_diff_kernel, dim3((unsigned)p.ntiles), dim3(DB), 0, st, p);
+  hipLaunchKernelGGL(merkle_diff_count_kernel, dim3((unsigned)p.ntiles), dim3(DB), 0, st, p);
+  hipLaunchKernelGGL(merkle_diff_scan_kernel, dim3(1), dim3(DSB), 0, st, p);
+  hipLaunchKernelGGL(merkle_diff_write_kernel, dim3((unsigned)p.ntiles), dim3(DB), 0, st, p);
   return hipGetLastError();
 }
 

@@ -66,25 +66,12 @@ __global__ __launch_bounds__(SB) void seg_count_kernel(SegArgs p) {
   if (threadIdx.x == 0) p.cnt[t] = tot;
 }
 
-// Pass 2: exclusive offsets of the tile counts (one workgroup; a tile count is
-// <= ST, so 1024 tiles sum below 2^32 per chunk).
+// Pass 2: exclusive offsets of the tile counts (one workgroup).
 constexpr int SSB = 1024;
 __global__ __launch_bounds__(SSB) void seg_scan_kernel(SegArgs p) {
   __shared__ u32 s_wave[SSB / WAVE + 1];
   __shared__ u64 s_carry;
-  if (threadIdx.x == 0) s_carry = 0;
-  __syncthreads();
-  for (u64 c0 = 0; c0 < p.ntiles; c0 += SSB) {
-    const u64 t = c0 + threadIdx.x;
-    const u32 v = t < p.ntiles ? (u32)p.cnt[t] : 0u;
-    u32 tot;
-    const u32 o = block_excl_scan<SSB>(v, s_wave, &tot);
-    if (t < p.ntiles) p.off[t] = s_carry + o;
-    __syncthreads();
-    if (threadIdx.x == 0) s_carry += tot;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) p.d_count[0] = s_carry;
+  scan_tile_counts<SSB>(p.cnt, p.off, p.ntiles, p.d_count, s_wave, &s_carry);
 }
 
 // Pass 3: one output per head at the tile's offset -- (key, read value) or (key, leaf
