@@ -1,0 +1,167 @@
+"""SoA snapshots of a replica's state: what `DeltaCrdt.Storage`
+persists -- `{node_id, sequence_number, crdt_state, merkle_map}` (reference
+lib/delta_crdt/storage.ex:12-16, written by causal_crdt.ex:238-250 after every delta
+and read back at start-up by :216-234) -- stored as the device-resident dot store
+itself instead of the term tree.
+
+    storage.write(path, node_id, sequence_number, state)      # AWLWWMap mirror state
+    node_id, sequence_number, state = storage.read(path)
+
+File layout (little-endian), one self-describing file per replica:
+
+    b"DGSNAP01" | u64 header length | header (msgpack) | column bytes ...
+
+The header holds node_id, sequence_number, the row and context counts, the context
+kind, the byte length and xxh64 of each column, and the exact interning tables of
+the state's Universe (keys, values and nodes as tagged terms), so `read` restores the
+same terms, ids and rows.  Columns are the raw SoA arrays (key, val, ts, node, cnt,
+ctx node, ctx cnt): 36 B per dot + 12 B per context entry, copied device -> host by
+one D2H copy each.  The MerkleMap is not stored: it is a function of the rows
+(dg_merkle_build rebuilds it, which is how the reference's read_from_storage path
+treats a missing map too).  A checksum mismatch raises.
+"""
+from __future__ import annotations
+
+import struct
+
+import msgpack
+import numpy as np
+import xxhash
+
+from . import interning
+from .terms import Atom, EList, EMap
+
+MAGIC = b"DGSNAP01"
+_COLS = (("key", np.uint64), ("val", np.uint64), ("ts", np.int64), ("node", np.uint32),
+         ("cnt", np.uint64))
+
+
+def _pack(t):
+    """A term as a tagged msgpack-able value (exact: no pickling)."""
+    if t is None:
+        return ["n"]
+    if isinstance(t, bool):
+        return ["b", t]
+    if isinstance(t, Atom):
+        return ["a", str(t)]
+    if isinstance(t, int):
+        return ["i", str(t)]
+    if isinstance(t, float):
+        return ["f", t]
+    if isinstance(t, EList):
+        return ["l", [_pack(x) for x in t]]
+    if isinstance(t, EMap):
+        return ["m", [[_pack(k), _pack(v)] for k, v in t]]
+    if isinstance(t, tuple):
+        return ["t", [_pack(x) for x in t]]
+    if isinstance(t, str):
+        return ["s", t]
+    if isinstance(t, bytes):
+        return ["y", t]
+    raise TypeError(f"cannot snapshot term {t!r}")
+
+
+def _unpack(x):
+    tag = x[0]
+    if tag == "n":
+        return None
+    if tag == "b":
+        return bool(x[1])
+    if tag == "a":
+        return Atom(x[1])
+    if tag == "i":
+        return int(x[1])
+    if tag == "f":
+        return float(x[1])
+    if tag == "l":
+        return EList(_unpack(v) for v in x[1])
+    if tag == "m":
+        return EMap((_unpack(k), _unpack(v)) for k, v in x[1])
+    if tag == "t":
+        return tuple(_unpack(v) for v in x[1])
+    if tag == "s":
+        return x[1]
+    if tag == "y":
+        return bytes(x[1])
+    raise ValueError(f"bad term tag {tag!r}")
+
+
+def _universe_tables(U: interning.Universe):
+    return {
+        "keys": [[str(k), _pack(t)] for k, t in U._key_term.items()],
+        "vals": [[str(v), _pack(t)] for v, t in U._val_term.items()],
+        "nodes": [[n, _pack(t)] for n, t in U._node_term.items()],
+        "class_next": [[c, s] for c, s in U._class_next.items()],
+        "node_next": U._node_next,
+    }
+
+
+def _universe_from(tables) -> interning.Universe:
+    U = interning.Universe()
+    for k, t in tables["keys"]:
+        term = _unpack(t)
+        U._key_term[int(k)] = term
+        U._key_id[interning._hkey(term)] = int(k)
+    for v, t in tables["vals"]:
+        term = _unpack(t)
+        U._val_term[int(v)] = term
+        U._val_id[interning._hkey(term)] = int(v)
+    for n, t in tables["nodes"]:
+        term = _unpack(t)
+        U._node_term[int(n)] = term
+        U._node_id[interning._hkey(term)] = int(n)
+    U._class_next = {int(c): int(s) for c, s in tables["class_next"]}
+    U._node_next = int(tables["node_next"])
+    return U
+
+
+def write(path, node_id, sequence_number: int, state) -> None:
+    """Storage.write/2's payload for an AWLWWMap mirror state (aw_lww_map.AWLWWMap)."""
+    cols = list(state.rows.to_numpy()) + list(state.ctx.to_numpy())
+    blobs = [np.ascontiguousarray(c).tobytes() for c in cols]
+    header = {
+        "node_id": _pack(node_id),
+        "sequence_number": int(sequence_number),
+        "rows": int(state.rows.n),
+        "ctx_kind": int(state.ctx.kind),
+        "ctx_n": int(state.ctx.n),
+        "columns": [[len(b), xxhash.xxh64_intdigest(b)] for b in blobs],
+        "universe": _universe_tables(state.universe),
+    }
+    h = msgpack.packb(header, use_bin_type=True)
+    with open(path, "wb") as f:
+        f.write(MAGIC)
+        f.write(struct.pack("<Q", len(h)))
+        f.write(h)
+        for b in blobs:
+            f.write(b)
+
+
+def read(path, device=None):
+    """Storage.read/1: (node_id, sequence_number, state) or None if `path` is absent."""
+    import os
+
+    from . import aw_lww_map as M
+    from .store import Context, Store
+    if not os.path.exists(path):
+        return None
+    with open(path, "rb") as f:
+        if f.read(8) != MAGIC:
+            raise ValueError(f"{path}: not a deltagpu snapshot")
+        (hl,) = struct.unpack("<Q", f.read(8))
+        header = msgpack.unpackb(f.read(hl), raw=False, strict_map_key=False)
+        arrays = []
+        dtypes = [d for _, d in _COLS] + [np.uint32, np.uint64]
+        for (nbytes, digest), dt in zip(header["columns"], dtypes):
+            b = f.read(nbytes)
+            if len(b) != nbytes or xxhash.xxh64_intdigest(b) != digest:
+                raise ValueError(f"{path}: column checksum mismatch")
+            arrays.append(np.frombuffer(b, dtype=dt).copy())
+    dev = device or M._dev()
+    rows = Store.from_numpy(*arrays[:5], device=dev)
+    ctx = Context.from_numpy(header["ctx_kind"], arrays[5], arrays[6], dev)
+    state = M.AWLWWMap(rows, ctx, _universe_from(header["universe"]))
+    return _unpack(header["node_id"]), header["sequence_number"], state
+
+
+__all__ = ["write", "read", "MAGIC"]
