@@ -235,10 +235,13 @@ struct JoinArgs {
   RowsOut out;
   Scan scan;  // look-back granules + tile tickets
   u64* d_count;
-  unsigned short* lists;
-  u64* chg_tmp;  // CHG: JT change-event keys per tile
-  u32* chg_cnt;  // CHG: events per tile  // two-pass only: tile t's compaction list at lists[t * JT ...]
+  unsigned short* lists;  // two-pass only: tile t's compaction list at lists[t * JT ...]
   u32* counts;            // two-pass only: kept rows per tile
+  u64* chg_tmp;           // CHG: JT change-event keys per tile
+  u32* chg_cnt;           // CHG: events per tile
+  int fused;              // stream kernel: splits searched in-kernel (no partition launch);
+                          // the grid's last workgroup computes the context union
+  CtxUnionArgs cu;
 };
 
 // ------------------------------------------------------------------ partition
@@ -615,12 +618,15 @@ __device__ __forceinline__ void commit_tile(const Staged& r, Buf& s) {
 // No look-back chain and no ticket: a stripe's counts were all published one merge
 // earlier, so step 4 rarely waits; its cost is one G-word read per iteration, issued
 // before the merge.  Spins stay bounded (scan.err bit 0 on timeout).
+constexpr int FUSE_IT = JB / WAVE / 2;  // fused splits: one wave per boundary, 2 per tile
+
 struct StreamLds {
   Buf buf[2];
   unsigned short comp[2][JT];
   u64 tab[2][VT];
   u32 wave[JB / WAVE + 1];
   u64 red[2 * (JB / WAVE)];
+  u64 spl[2 * FUSE_IT];  // fused: splits of this workgroup's tiles (start, end per tile)
 };
 
 constexpr u32 CNT_BITS = 12;  // count field of a tile-count granule (JT < 4096)
@@ -725,15 +731,34 @@ template <bool FAST, bool CHG>
 __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void join2_stream_kernel(JoinArgs p) {
   __shared__ StreamLds s;
   const int tid = threadIdx.x;
-  const u64 total = p.a.n + p.b.n, ntiles = p.ntiles, G = gridDim.x, w = blockIdx.x;
+  const u64 total = p.a.n + p.b.n, ntiles = p.ntiles, w = blockIdx.x;
+  const u64 G = gridDim.x - (p.fused ? 1 : 0);  // tile workgroups
   u32* cs = p.scan.counts;  // tile-count granules
   const u32 epoch = p.scan.epoch;
   const Rows& A = p.a;
   const Rows& B = p.b;
+  if (p.fused) {
+    if (w == G) {  // Dots.union(c1, c2) (aw_lww_map.ex:155), beside the tiles
+      ctx_union_block<JB>(p.cu, s.wave);
+      return;
+    }
+    // merge-path splits of this workgroup's (<= FUSE_IT) tiles, one wave per boundary
+    const int wv = tid / WAVE;
+    const u64 tk = w + (u64)(wv >> 1) * G;
+    if (tk < ntiles) {
+      const u64 sp = mp_split(A, B, min((tk + (wv & 1)) * (u64)JT, total));
+      if ((tid & (WAVE - 1)) == 0) s.spl[wv] = sp;
+    }
+  }
   if (FAST)
     for (int x = tid; x < 2 * VT; x += JB) (&s.tab[0][0])[x] = 0;
+  if (p.fused) __syncthreads();
+  // split of boundary `side` (0 start, 1 end) of the tile of iteration k
+  auto split = [&](u64 tile, int k, int side) -> u64 {
+    return p.fused ? s.spl[2 * k + side] : p.splits[tile + side];
+  };
   u64 t = w;
-  u64 a0 = p.splits[t], a1 = p.splits[t + 1];
+  u64 a0 = split(t, 0, 0), a1 = split(t, 0, 1);
   int nat, nbt;
   u64 b0;
   tile_geom(t, a0, a1, total, &nat, &nbt, &b0);
@@ -754,8 +779,8 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     u64 a0n = 0, a1n = 0, b0n = 0;
     int natn = 0, nbtn = 0;
     if (tn < ntiles) {
-      a0n = p.splits[tn];
-      a1n = p.splits[tn + 1];
+      a0n = split(tn, k + 1, 0);
+      a1n = split(tn, k + 1, 1);
       tile_geom(tn, a0n, a1n, total, &natn, &nbtn, &b0n);
       issue_tile(A, B, natn, nbtn, a0n, b0n, r);
     }
@@ -1092,12 +1117,36 @@ hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& 
     hipLaunchKernelGGL(ctx_union_kernel, dim3(1), dim3(CB), 0, st, cu);
     return hipGetLastError();
   }
+  // full-state join of two version vectors: LDS VV table, no key list
+  const bool fast = keys == nullptr && ca.kind == 0 && cb.kind == 0;
+  p.fused = 0;
+  p.cu = cu;
+  auto kern = fast ? join2_stream_kernel<true, false> : join2_stream_kernel<false, false>;
+  if (chg_tmp) kern = fast ? join2_stream_kernel<true, true> : join2_stream_kernel<false, true>;
+  const bool stream = mode != JOIN_TWO_PASS || chg_tmp;
+  u64 g = 0;
+  if (stream) {
+    g = workers > 0 ? (u64)workers : resident_grid((const void*)kern);
+    g = std::min<u64>(std::min<u64>(p.ntiles, g), (u64)CQ * JB);  // stripe counts: CQ per thread
+    // small joins (<= FUSE_IT tiles per workgroup): the splits are searched inside the
+    // stream kernel and the context union runs in one extra co-resident workgroup, so
+    // the partition launch (~5 us of mostly fixed cost) disappears
+    static const bool no_fuse = [] {
+      const char* v = getenv("DG_JOIN_FUSE");
+      return v && v[0] == '0';
+    }();
+    const u64 gr = workers > 0 ? g + 1 : resident_grid((const void*)kern);
+    const u64 gt = std::min<u64>(std::min<u64>(p.ntiles, gr - 1), (u64)CQ * JB);
+    if (!no_fuse && gr >= 2 && p.ntiles <= (u64)FUSE_IT * gt) {
+      p.fused = 1;
+      hipLaunchKernelGGL(kern, dim3((unsigned)gt + 1), dim3(JB), 0, st, p);
+      return hipGetLastError();
+    }
+  }
   const u64 nb_part = (p.ntiles + 1 + (PB / WAVE) - 1) / (PB / WAVE);
   hipLaunchKernelGGL(join2_partition_kernel, dim3((unsigned)nb_part + 1), dim3(PB), 0, st, a, b,
                      p.ntiles, splits, cu);
-  // full-state join of two version vectors: LDS VV table, no key list
-  const bool fast = keys == nullptr && ca.kind == 0 && cb.kind == 0;
-  if (mode == JOIN_TWO_PASS && !chg_tmp) {
+  if (!stream) {
     char* t = (char*)pass_tmp;
     p.counts = (u32*)t;
     t += ((p.ntiles * 4 + 255) / 256) * 256;
@@ -1108,11 +1157,6 @@ hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& 
                        p.splits, p.lists, p.counts, p.ntiles, out, d_counts);
     return hipGetLastError();
   }
-  auto kern = fast ? join2_stream_kernel<true, false> : join2_stream_kernel<false, false>;
-  if (chg_tmp) kern = fast ? join2_stream_kernel<true, true> : join2_stream_kernel<false, true>;
-  u64 g = workers > 0 ? (u64)workers : 0;
-  if (!g) g = resident_grid((const void*)kern);
-  g = std::min<u64>(std::min<u64>(p.ntiles, g), (u64)CQ * JB);  // stripe counts: CQ per thread
   hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(JB), 0, st, p);
   return hipGetLastError();
 }
