@@ -392,7 +392,7 @@ def main():
         }
         if not args.no_merkle:
             res["merkle"] = merkle_rate(eng, torch, dev)
-        if not args.no_configs:
+        if not args.no_configs and world == 1:  # per-GPU secondaries: measured at N=1
             res["changes"] = changes_rate(eng, torch, pairs[0])
             for r in pairs:  # free the config-2 replicas before the larger configs
                 r.clear()
