@@ -55,18 +55,38 @@ __device__ __forceinline__ u64 vv_at(const u64* tab, u32 i, u32 node) {
   return node < (u32)KNT ? tab[(u64)i * KNT + node] : 0ull;
 }
 
-// P after the touching deltas (bits of K | R, in delta order); see the header.
+// P after the touching deltas (bits of K | R, in delta order); see the header.  Both
+// tables are read for up to PB touching deltas at a time, before P decides which one
+// applies, so those L2 reads overlap instead of waiting on each other.
+constexpr int PB = 4;
 __device__ __forceinline__ bool present(bool P, u64 K, u64 R, u64 M, u32 node, u64 cnt,
                                         const u64* tabC, const u64* tabP) {
   u64 bits = K | R;
   while (bits) {
-    const u32 i = (u32)__builtin_ctzll(bits);
-    bits &= bits - 1;
-    const bool inD = (M >> i) & 1;
-    if ((K >> i) & 1)
-      P = P ? (inD || vv_at(tabC, i, node) < cnt) : (inD && vv_at(tabP, i, node) < cnt);
-    else
-      P = inD;
+    u32 ib[PB];
+    u64 c[PB], q[PB];
+    int nb = 0;
+#pragma unroll
+    for (int j = 0; j < PB; j++) {
+      ib[j] = bits ? (u32)__builtin_ctzll(bits) : 0u;
+      nb += bits ? 1 : 0;
+      bits &= bits - 1;
+    }
+#pragma unroll
+    for (int j = 0; j < PB; j++) {
+      c[j] = j < nb ? vv_at(tabC, ib[j], node) : 0ull;
+      q[j] = j < nb ? vv_at(tabP, ib[j], node) : 0ull;
+    }
+#pragma unroll
+    for (int j = 0; j < PB; j++) {
+      if (j >= nb) break;
+      const u32 i = ib[j];
+      const bool inD = (M >> i) & 1;
+      if ((K >> i) & 1)
+        P = P ? (inD || c[j] < cnt) : (inD && q[j] < cnt);
+      else
+        P = inD;
+    }
   }
   return P;
 }
