@@ -39,6 +39,7 @@
 // through a direct-indexed LDS table of the VVs' counters for node ids < VT (one
 // ds_read per row); larger node ids and explicit dot sets use a binary search.
 #include <algorithm>
+#include <mutex>
 
 #include "dg_launch.h"
 
@@ -1060,14 +1061,33 @@ __global__ __launch_bounds__(CPB) void join2_compact_kernel(Rows a, Rows b, cons
 
 // Workgroups of kernel `k` (JB threads) resident at once on the current device: the
 // grid of a persistent kernel whose workgroups wait on each other.
+// Workgroups of kernel k resident on the current device at once.  Cached per (kernel,
+// device): the occupancy query costs microseconds of host time on every launch otherwise.
 static u64 resident_grid(const void* k) {
-  int per_cu = 0, dev = 0, cus = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+  struct Entry {
+    const void* k;
+    int dev;
+    u64 n;
+  };
+  static Entry cache[32];
+  static int used = 0;
+  static std::mutex mu;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    for (int i = 0; i < used; i++)
+      if (cache[i].k == k && cache[i].dev == dev) return cache[i].n;
+  }
+  int per_cu = 0, cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, JB, 0) != hipSuccess || per_cu <= 0 ||
       cus <= 0)
     return 256;
-  return (u64)per_cu * (u64)cus;
+  const u64 n = (u64)per_cu * (u64)cus;
+  std::lock_guard<std::mutex> g(mu);
+  if (used < 32) cache[used++] = {k, dev, n};
+  return n;
 }
 
 static CtxUnionArgs make_cu(const Ctx& a, const Ctx& b, u32* out_node, u64* out_cnt,
