@@ -97,6 +97,10 @@ _SIGS = {
                                    P64]),
     "dg_take_keys": (C.c_int, [C.c_void_p, C.POINTER(dg_store), P64, C.c_uint64,
                                C.POINTER(dg_store)]),
+    "dg_mutate_batch": (C.c_int, [C.c_void_p, C.POINTER(dg_store), C.POINTER(dg_context),
+                                  C.c_uint32, C.c_uint64, C.c_void_p, P64, P64, PI64, P64,
+                                  C.c_uint64, C.POINTER(dg_store), C.POINTER(dg_context), P64,
+                                  C.c_uint64, P64]),
     "dg_join2_async": (C.c_int, [C.c_void_p, C.POINTER(dg_store), C.POINTER(dg_context),
                                  C.POINTER(dg_store), C.POINTER(dg_context), P64, C.c_uint64,
                                  C.POINTER(dg_store), C.POINTER(dg_context), P64]),

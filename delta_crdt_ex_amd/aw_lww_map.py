@@ -184,5 +184,39 @@ def read(state: AWLWWMap, keys=None) -> dict:
     return {U.key_term(int(k)): U.value_term(int(v)) for k, v in zip(u64(ok), u64(ov))}
 
 
+def mutate_batch(ops, node_id, state: AWLWWMap):
+    """Many add/4 and remove/3 calls by one node as ONE delta on the GPU
+    (dg_mutate_batch): ops = [("add", key, value[, ts]) or ("remove",
+    key)] in order.  Returns (delta, keys): join(state, delta, keys) equals applying the
+    ops one by one as CausalCrdt does.  The state's context must be a version vector
+    (compress_dots/1, as CausalCrdt keeps it)."""
+    U = state.universe
+    nid = U.node(node_id)
+    m = len(ops)
+    kind = np.zeros(m, np.uint8)
+    key = np.zeros(m, np.uint64)
+    val = np.zeros(m, np.uint64)
+    ts = np.zeros(m, np.int64)
+    for i, op in enumerate(ops):
+        key[i] = U.key(op[1])
+        if op[0] == "add":
+            kind[i] = 1
+            val[i] = U.value(op[2])
+            ts[i] = op[3] if len(op) > 3 else time.monotonic_ns()
+        elif op[0] != "remove":
+            raise ValueError(f"unknown op {op[0]!r}")
+    rank = np.cumsum(kind, dtype=np.uint64) - kind  # adds before each op, batch order
+    order = np.argsort(key, kind="stable")           # by key, batch order within a key
+    dev = _dev()
+
+    def d(a, view):
+        return torch.from_numpy(np.ascontiguousarray(a[order]).view(view)).to(dev)
+
+    delta, dots, keys = engine().mutate_batch(
+        state.rows, state.ctx, nid, torch.from_numpy(kind[order]).to(dev), d(key, np.int64),
+        d(val, np.int64), d(ts, np.int64), d(rank, np.int64), int(kind.sum()))
+    return AWLWWMap(delta, dots, U), [U.key_term(int(k)) for k in u64(keys)]
+
+
 __all__ = ["AWLWWMap", "new", "compress_dots", "add", "remove", "clear", "join", "join_all", "read",
-           "DG_CTX_VV", "DG_CTX_DOTS"]
+           "mutate_batch", "DG_CTX_VV", "DG_CTX_DOTS"]

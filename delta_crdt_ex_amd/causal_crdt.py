@@ -47,4 +47,12 @@ def update_state_with_delta(state: M.AWLWWMap, delta: M.AWLWWMap, keys):
     return new, diffs
 
 
-__all__ = ["update_state_with_delta"]
+def apply_ops(state: M.AWLWWMap, ops, node_id):
+    """A batch of mutate/3 calls (causal_crdt.ex:337-342 per op) applied as ONE delta:
+    (new_state, diffs) as update_state_with_delta/3 would give for the batch's touched
+    keys (on_diffs sees the batch's net changes, not each op's)."""
+    delta, keys = M.mutate_batch(ops, node_id, state)
+    return update_state_with_delta(state, delta, keys)
+
+
+__all__ = ["update_state_with_delta", "apply_ops"]

@@ -23,7 +23,7 @@ struct dg_engine {
   // decoupled look-back scratch
   u64* state = nullptr;
   u64 state_cap = 0;
-  u32* ticket = nullptr;  // [0] ticket, [1] error bits, [2] store_check flag
+  u32* ticket = nullptr;  // [0] ticket, [1] error bits, [2] store_check flag, [3] op order flag
   u32* counts = nullptr;  // single-pass join tile-count granules
   u64 counts_cap = 0;
   // ping-pong intermediate states of dg_joink / dg_apply_deltas
@@ -666,6 +666,64 @@ int dg_take_keys(dg_engine* e, const dg_store* s, const uint64_t* keys, uint64_t
   if (out->n > out->cap)
     return fail(DG_E_CAPACITY, "dg_take_keys: %llu rows > cap %llu", (unsigned long long)out->n,
                 (unsigned long long)out->cap);
+  return DG_OK;
+}
+
+int dg_mutate_batch(dg_engine* e, const dg_store* state, const dg_context* ctx, uint32_t node,
+                    uint64_t m, const uint8_t* kind, const uint64_t* key, const uint64_t* val,
+                    const int64_t* ts, const uint64_t* add_rank, uint64_t n_adds, dg_store* delta,
+                    dg_context* delta_dots, uint64_t* keys_out, uint64_t keys_cap,
+                    uint64_t* n_keys_out) {
+  if (!e) return fail(DG_E_INVAL, "null engine");
+  TRY(check_store(state, "dg_mutate_batch state"));
+  TRY(check_ctx(ctx, "dg_mutate_batch ctx"));
+  if (ctx->kind != DG_CTX_VV)
+    return fail(DG_E_INVAL, "dg_mutate_batch: the state's context must be a version vector "
+                            "(compress_dots/1 it first)");
+  if (!delta || !delta_dots || !n_keys_out || (m && (!kind || !key || !val || !ts || !add_rank)))
+    return fail(DG_E_INVAL, "dg_mutate_batch: null argument");
+  if (n_adds > m) return fail(DG_E_INVAL, "dg_mutate_batch: n_adds > m");
+  TRY(set_device(e));
+  const u64 nt = mutate_tiles(m);
+  TRY(ensure_state(e, 6 * nt + 2));  // raw per-tile counts and offsets
+  HIP_TRY(hipMemsetAsync(e->ticket + 3, 0, sizeof(u32), e->stream));
+  u32* err = e->ticket + 3;
+  HIP_TRY(launch_mutate_count(rows_of(state), ctx_of(ctx), node, kind, key, val, ts, add_rank, m,
+                              e->state, e->d_counts, err, e->stream));
+  TRY(read_counts(e, 3));
+  const u64 n_keys = e->h_counts[0], n_rows = e->h_counts[1], n_sdots = e->h_counts[2];
+  u32 bad = 0;
+  HIP_TRY(hipMemcpyAsync(&e->h_counts[6], err, sizeof(u32), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  memcpy(&bad, &e->h_counts[6], sizeof(u32));
+  if (bad & 1u) return fail(DG_E_ORDER, "dg_mutate_batch: ops are not sorted by key");
+  const u64 n_dots = n_sdots + n_adds;
+  if (keys_cap < n_keys || delta->cap < n_rows || delta_dots->cap < n_dots)
+    return fail(DG_E_CAPACITY,
+                "dg_mutate_batch: needs %llu keys, %llu delta rows, %llu context dots",
+                (unsigned long long)n_keys, (unsigned long long)n_rows, (unsigned long long)n_dots);
+  if ((n_keys && !keys_out) || (n_rows && (!delta->key || !delta->val || !delta->ts ||
+                                           !delta->node || !delta->cnt)) ||
+      (n_dots && (!delta_dots->node || !delta_dots->cnt)))
+    return fail(DG_E_INVAL, "dg_mutate_batch: null output column");
+  auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+  const size_t sort_b = al(mutate_sort_tmp_bytes(n_dots)), n4 = al(n_dots * 4), n8 = al(n_dots * 8);
+  TRY(ensure_tmp(e, 2 * (n4 + n8) + sort_b + 256));
+  char* t = (char*)e->tmp;
+  u32* dnode = (u32*)t;
+  u64* dcnt = (u64*)(t + n4);
+  u32* tnode = (u32*)(t + n4 + n8);
+  u64* tcnt = (u64*)(t + 2 * n4 + n8);
+  void* sort_tmp = t + 2 * (n4 + n8);
+  HIP_TRY(launch_mutate_write(rows_of(state), ctx_of(ctx), node, kind, key, val, ts, add_rank, m,
+                              e->state, keys_out, rows_out_of(delta), dnode, dcnt, err, e->stream));
+  HIP_TRY(launch_mutate_dots(ctx_of(ctx), node, n_adds, n_sdots, dnode, dcnt, tnode, tcnt, sort_tmp,
+                             sort_b, delta_dots->node, delta_dots->cnt, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  delta->n = n_rows;
+  delta_dots->n = n_dots;
+  delta_dots->kind = DG_CTX_DOTS;
+  *n_keys_out = n_keys;
   return DG_OK;
 }
 

@@ -113,6 +113,24 @@ inline u64 take_tiles(u64 n_keys) { return (n_keys + 1023) / 1024; }
 hipError_t launch_take_keys(const Rows& s, const u64* keys, u64 n_keys, const RowsOut& out,
                             u64 cap, const Scan& scan, u64* d_count, hipStream_t st);
 
+// ---- mutate.hip (a batch of add/remove ops as one delta; see the file header)
+inline u64 mutate_tiles(u64 m) { return (m + 1023) / 1024; }
+// count + scan: d_counts[0..2] = touched keys, delta rows, state dots; scratch: 6 *
+// mutate_tiles(m) u64; err bit 0: ops not sorted by key.
+hipError_t launch_mutate_count(const Rows& s, const Ctx& c, u32 node, const uint8_t* kind,
+                               const u64* key, const u64* val, const i64* ts, const u64* rank,
+                               u64 m, u64* scratch, u64* d_counts, u32* err, hipStream_t st);
+// keys_out, rows_out and the state dots into dnode/dcnt[0, n_state_dots)
+hipError_t launch_mutate_write(const Rows& s, const Ctx& c, u32 node, const uint8_t* kind,
+                               const u64* key, const u64* val, const i64* ts, const u64* rank,
+                               u64 m, u64* scratch, u64* keys_out, const RowsOut& rows_out,
+                               u32* dnode, u64* dcnt, u32* err, hipStream_t st);
+size_t mutate_sort_tmp_bytes(u64 n);
+// the adds' dots after the state dots, then the (node, counter) sort through t* into out_*
+hipError_t launch_mutate_dots(const Ctx& c, u32 node, u64 n_adds, u64 n_state_dots, u32* dnode,
+                              u64* dcnt, u32* tnode, u64* tcnt, void* sort_tmp,
+                              size_t sort_tmp_bytes, u32* out_node, u64* out_cnt, hipStream_t st);
+
 // ---- segred.hip (segmented reductions over key runs)
 constexpr int SEG_BLOCK = 256;
 constexpr int SEG_ITEMS = 4;

@@ -360,6 +360,35 @@ class Engine:
         out.n = int(so.n)
         return out
 
+    def mutate_batch(self, state: Store, ctx: Context, node: int, kind: torch.Tensor,
+                     key: torch.Tensor, val: torch.Tensor, ts: torch.Tensor,
+                     add_rank: torch.Tensor, n_adds: int):
+        """A batch of add/remove ops by `node` as one delta (aw_lww_map.ex:99-146):
+        device arrays sorted by key (batch order within a key); kind uint8 (1 add),
+        add_rank = adds before the op in batch order.  Returns (delta Store, its dot-list
+        Context, touched keys) -- join the delta with those keys."""
+        self._order()
+        m = int(key.numel())
+        out = Store.empty(max(m, 1), self.device)
+        keys = torch.empty(max(m, 1), dtype=_I64, device=self.device)
+        nk = C.c_uint64(0)
+        ss, xs, so = state.abi(), ctx.abi(), out.abi()
+        args = [_ptr(kind, C.c_void_p) if m else None, _ptr(key, _abi.P64), _ptr(val, _abi.P64),
+                _ptr(ts, _abi.PI64), _ptr(add_rank, _abi.P64)]
+        for cap in (8 * m + n_adds + 1, state.n + n_adds + 1):
+            dots = Context.empty(DG_CTX_DOTS, cap, self.device)
+            xd = dots.abi()
+            rc = self.lib.dg_mutate_batch(self.h, C.byref(ss), C.byref(xs), node, m, *args, n_adds,
+                                          C.byref(so), C.byref(xd), _ptr(keys, _abi.P64),
+                                          max(m, 1), C.byref(nk))
+            if rc != _abi.DG_E_CAPACITY:
+                break
+        check(rc)
+        out.n = int(so.n)
+        dots.n = int(xd.n)
+        dots.kind = int(xd.kind)
+        return out, dots, keys[: nk.value]
+
     # ---------------------------------------------------------------- contexts
     def context_union(self, a: Context, b: Context, out: Context | None = None) -> Context:
         self._order()

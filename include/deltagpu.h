@@ -176,6 +176,27 @@ int dg_apply_deltas(dg_engine* e, const dg_store* state, const dg_context* ctx, 
 int dg_take_keys(dg_engine* e, const dg_store* s, const uint64_t* keys, uint64_t n_keys,
                  dg_store* out);
 
+/* ---- batched mutations ----------------------------------------------------- */
+/* A batch of AWLWWMap.add/4 and remove/3 operations by node `node` as ONE delta
+ * (aw_lww_map.ex:99-146; CausalCrdt applies each op's delta with keys = [key] as the op
+ * arrives, causal_crdt.ex:337-342).  The m ops (device arrays) are sorted by key,
+ * ascending, in batch order within a key (DG_E_ORDER otherwise): kind[i] 1 = add
+ * (value val[i] at ts[i]), 0 = remove; add_rank[i] = the number of adds before op i in
+ * batch order; n_adds = the batch's adds.  Outputs:
+ *   delta      one row per touched key whose last op is an add, with dot
+ *              {node, C[node] + 1 + add_rank} (C = ctx, a version vector);
+ *   delta_dots the delta's context as a sorted dot list: the dots of the touched keys'
+ *              rows in `state` plus the dot of every add;
+ *   keys_out   the touched keys, ascending, *n_keys_out of them (cap keys_cap).
+ * dg_join2(state, ctx, delta, delta_dots, keys_out, ...) then equals applying the ops
+ * one by one.  Capacities: delta->cap >= touched keys, delta_dots->cap >= touched
+ * keys' rows + n_adds (DG_E_CAPACITY names the sizes).  Synchronous. */
+int dg_mutate_batch(dg_engine* e, const dg_store* state, const dg_context* ctx, uint32_t node,
+                    uint64_t m, const uint8_t* kind, const uint64_t* key, const uint64_t* val,
+                    const int64_t* ts, const uint64_t* add_rank, uint64_t n_adds, dg_store* delta,
+                    dg_context* delta_dots, uint64_t* keys_out, uint64_t keys_cap,
+                    uint64_t* n_keys_out);
+
 /* ---- causal-context algebra ----------------------------------------------- */
 /* Dots.union/2 (aw_lww_map.ex:39-52): VV ⊔ VV = per-node max; VV ⊔ DOTS folds the
  * dots into the VV; DOTS ⊔ DOTS = set union. */

@@ -286,6 +286,36 @@ def changed_keys(old_rows, new_rows, keys=None):
     return d[np.isin(d, np.asarray(keys, np.uint64))]
 
 
+def mutate_batch(rows, ctx, node, ops):
+    """A batch of add/4 and remove/3 ops by `node` as one delta (aw_lww_map.ex:99-146
+    per op, folded in batch order): ops = [(kind, key, val, ts)] with kind "add" /
+    "remove", key/val ids.  ctx is the state's VV.  Returns (delta rows, delta context
+    as a sorted dot list, touched keys ascending) -- see csrc/mutate.hip's header for
+    the derivation, which tests/test_configs.py checks against the term oracle."""
+    kind, node_ids, cnts = ctx
+    assert kind == VV
+    vv = {int(n): int(c) for n, c in zip(node_ids, cnts)}
+    c0 = vv.get(int(node), 0) + 1
+    last, gen, r = {}, [], 0
+    for k, key, val, ts in ops:
+        if k == "add":
+            last[int(key)] = (int(val), int(ts), c0 + r)
+            gen.append((int(node), c0 + r))
+            r += 1
+        else:
+            last[int(key)] = None
+    keys = np.array(sorted(last), np.uint64)
+    drows = [(k, v, t, int(node), c) for k, x in sorted(last.items()) if x is not None
+             for (v, t, c) in [x]]
+    sel = np.isin(rows[0], keys)
+    dots = sorted(set(zip(rows[3][sel].tolist(), rows[4][sel].tolist())) | set(gen))
+    delta = (np.array([x[0] for x in drows], np.uint64), np.array([x[1] for x in drows], np.uint64),
+             np.array([x[2] for x in drows], np.int64), np.array([x[3] for x in drows], np.uint32),
+             np.array([x[4] for x in drows], np.uint64))
+    dctx = (DOTS, np.array([d[0] for d in dots], np.uint32), np.array([d[1] for d in dots], np.uint64))
+    return delta, dctx, keys
+
+
 def store_check(rows) -> bool:
     s, _ = _store(rows)
     return lib().ref_store_check(C.byref(s)) == 0

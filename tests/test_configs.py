@@ -203,3 +203,37 @@ def test_changed_keys_two_oracles(seed):
     want = sorted(x[1] for x in T.causal_diff(old, new, keys))
     assert [int(x) for x in got] == want
     assert len(want) > 0
+
+
+# ------------------------------------------------------------------ batched mutations (§8(f).3)
+
+@pytest.mark.parametrize("seed", range(4))
+def test_mutate_batch_equals_op_by_op(seed):
+    """The batch delta (ref.mutate_batch, which dg_mutate_batch is checked against)
+    joined with keys = the touched keys equals applying the ops one by one as
+    CausalCrdt does (causal_crdt.ex:337-342: join(state, add/remove delta, [key]))."""
+    from kfold_cases import random_fold
+    rng = np.random.default_rng(seed)
+    st0, _ = random_fold(60 + seed, n_keys=30, k=0, n_nodes=4, rows_per_key=3, p_state=0.7)
+    ctx = R.compress_dots((1, *[np.asarray(x) for x in st0["ctx"][1:]])) if st0["ctx"][0] == 1 \
+        else st0["ctx"]
+    keys = np.unique(st0["rows"][0])
+    node = 7
+    ops = []
+    for i in range(40):
+        k = int(keys[rng.integers(0, len(keys))]) if rng.random() < 0.8 else int(rng.integers(1, 1 << 60))
+        if rng.random() < 0.7:
+            ops.append(("add", k, int(rng.integers(0, 5)) + (1 << 62), int(rng.integers(0, 50))))
+        else:
+            ops.append(("remove", k, 0, 0))
+    # op by op on the term oracle
+    t = soa_to_term(st0["rows"], ctx)
+    for kind, k, v, ts in ops:
+        d = T.add(k, v, node, t, ts) if kind == "add" else T.remove(k, node, t)
+        t = T.join(t, d, [k])
+    want_rows, want_ctx = term_to_soa_raw(t)
+    # the batch delta, joined once
+    drows, dctx, dkeys = R.mutate_batch(st0["rows"], ctx, node, ops)
+    got_rows, got_ctx = R.join2(st0["rows"], ctx, drows, dctx, dkeys)
+    assert rows_equal(got_rows, want_rows)
+    assert ctx_equal(got_ctx, want_ctx)
