@@ -15,7 +15,7 @@ from delta_crdt_ex_amd.store import Engine
 from kfold_cases import random_fold
 from oracle import ref as R
 from test_gpu_configs import keys_dev
-from test_gpu_parity import ctx_eq, rows_eq, up
+from test_gpu_parity import DEV, ctx_eq, rows_eq, up
 
 pytestmark = pytest.mark.gpu
 
@@ -142,3 +142,20 @@ def test_config3_onepass_equals_stepwise_large(strict, stepwise):
     x, y = a.to_numpy(), b.to_numpy()
     assert a.n == b.n and all(np.array_equal(p, q) for p, q in zip(x, y))
     assert all(np.array_equal(p, q) for p, q in zip(ac.to_numpy(), bc.to_numpy()))
+
+
+def test_prepared_apply_deltas(engine):
+    """prepare_apply_deltas (arguments marshalled once, called repeatedly) == apply_deltas."""
+    from delta_crdt_ex_amd.store import Context, Store
+    st, ds = random_fold(24, n_keys=3000, k=10, p_full=0.2)
+    s, c = up(st)
+    dd = [up(d) for d in ds]
+    ks = [None if d["keys"] is None else keys_dev(d["keys"]) for d in ds]
+    a, ac = engine.apply_deltas(s, c, [x[0] for x in dd], [x[1] for x in dd], ks)
+    out = Store.empty(s.n + sum(x[0].n for x in dd), DEV)
+    octx = Context.empty(0, c.n + sum(x[1].n for x in dd), DEV)
+    call = engine.prepare_apply_deltas(s, c, [x[0] for x in dd], [x[1] for x in dd], ks, out, octx)
+    for _ in range(2):
+        b, bc = call()
+        assert a.n == b.n and all(np.array_equal(x, y) for x, y in zip(a.to_numpy(), b.to_numpy()))
+        assert all(np.array_equal(x, y) for x, y in zip(ac.to_numpy(), bc.to_numpy()))
