@@ -227,9 +227,8 @@ struct KLds {
   i64 dts[CD];
   u32 dnode[CD];
   u64 ukey[CU];                       // items: delta rows [0, nD), keyset markers [nD, nU)
-  u32 utag[CU];                       // (src << 16) | MARK? | slot
-  unsigned short order[CU];           // items in (key, tag) order
-  unsigned short ustart[NSUB + 1];    // sub-bucket b: order[ustart[b], ustart[b+1])
+  u32 utag[CU];                       // (src << 16) | MARK? | slot; (key, tag) order once sorted
+  unsigned short ustart[NSUB + 1];    // sub-bucket b: items [ustart[b], ustart[b+1])
   unsigned short sfirst[NSUB + 1];    //               state rows [sfirst[b], sfirst[b+1])
   union {
     u32 ucnt[NSUB];                   // counting-sort histogram / fill counters
@@ -387,7 +386,16 @@ __global__ __launch_bounds__(KB) void kfold_kernel(KFoldArgs p) {
     bin[s.ustart[sb] + atomicAdd(&s.x.ucnt[sb], 1u)] = (unsigned short)q;
   }
   __syncthreads();
-  for (u32 q = tid; q < nU; q += KB) {  // rank by (key, tag) within the (small) sub-bucket
+  // rank by (key, tag) within the (small) sub-bucket, then every item moves itself to
+  // its sorted position (the items of a thread are read before the barrier, written
+  // after it), so later phases index ukey/utag directly
+  u64 mk[(CU + KB - 1) / KB];
+  u32 mt[(CU + KB - 1) / KB], mp[(CU + KB - 1) / KB];
+#pragma unroll
+  for (int j = 0; j < (CU + KB - 1) / KB; j++) {
+    const u32 q = tid + j * KB;
+    mp[j] = ~0u;
+    if (q >= nU) continue;
     const u64 kq = s.ukey[q];
     const u32 tq = s.utag[q], sb = sub_of(kq, T, t), lo = s.ustart[sb], hi = s.ustart[sb + 1];
     u32 rank = 0;
@@ -396,8 +404,17 @@ __global__ __launch_bounds__(KB) void kfold_kernel(KFoldArgs p) {
       const u64 kw = s.ukey[w];
       rank += (kw < kq || (kw == kq && s.utag[w] < tq)) ? 1u : 0u;
     }
-    s.order[lo + rank] = (unsigned short)q;
+    mk[j] = kq;
+    mt[j] = tq;
+    mp[j] = lo + rank;
   }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < (CU + KB - 1) / KB; j++)
+    if (mp[j] != ~0u) {
+      s.ukey[mp[j]] = mk[j];
+      s.utag[mp[j]] = mt[j];
+    }
   KSTAMP(t, 2);
   __syncthreads();
 
@@ -408,11 +425,11 @@ __global__ __launch_bounds__(KB) void kfold_kernel(KFoldArgs p) {
     const u32 sb = sub_of(r.key, T, t);
     u32 q = s.ustart[sb];
     const u32 qe = s.ustart[sb + 1];
-    while (q < qe && s.ukey[s.order[q]] < r.key) q++;
+    while (q < qe && s.ukey[q] < r.key) q++;
     s.slbu[i] = (unsigned short)q;
     u64 K = all, R = 0, M = 0;
-    for (; q < qe && s.ukey[s.order[q]] == r.key; q++) {
-      const u32 tg = s.utag[s.order[q]], src = tg >> 16;
+    for (; q < qe && s.ukey[q] == r.key; q++) {
+      const u32 tg = s.utag[q], src = tg >> 16;
       if (tg & MARK) {
         K |= 1ull << src;
       } else {
@@ -423,7 +440,7 @@ __global__ __launch_bounds__(KB) void kfold_kernel(KFoldArgs p) {
     s.ssurv[i] = present(true, K, R, M, r.node, r.cnt, p.tabC, p.tabP);
   }
   for (u32 q = tid; q < nU; q += KB) {
-    const u32 tg = s.utag[s.order[q]];
+    const u32 tg = s.utag[q];
     bool surv = false;
     if (!(tg & MARK)) {
       const u32 src = tg >> 16;
@@ -432,8 +449,8 @@ __global__ __launch_bounds__(KB) void kfold_kernel(KFoldArgs p) {
       u64 K = all, R = 0, M = 0;
       bool rep = true;  // the first holder of this tuple: the state, else the lowest delta
       for (u32 e = s.ustart[sb], ee = s.ustart[sb + 1]; e < ee; e++) {
-        const u32 te = s.utag[s.order[e]], se = te >> 16;
-        if (s.ukey[s.order[e]] != r.key) continue;
+        const u32 te = s.utag[e], se = te >> 16;
+        if (s.ukey[e] != r.key) continue;
         if (te & MARK) {
           K |= 1ull << se;
         } else {
@@ -480,8 +497,8 @@ __global__ __launch_bounds__(KB) void kfold_kernel(KFoldArgs p) {
     const Row r = srow(s, i);
     const u32 lb = s.slbu[i];
     u32 less = 0;
-    for (u32 q = lb; q < nU && s.ukey[s.order[q]] == r.key; q++)
-      if (s.usurv[q] && row_cmp(drow(s, s.utag[s.order[q]] & SLOT), r) < 0) less++;
+    for (u32 q = lb; q < nU && s.ukey[q] == r.key; q++)
+      if (s.usurv[q] && row_cmp(drow(s, s.utag[q] & SLOT), r) < 0) less++;
     const u64 o = base + spre[i] + upre[lb] + less;
     p.out.key[o] = r.key;
     p.out.val[o] = r.val;
@@ -491,13 +508,13 @@ __global__ __launch_bounds__(KB) void kfold_kernel(KFoldArgs p) {
   }
   for (u32 q = tid; q < nU; q += KB) {
     if (!s.usurv[q]) continue;
-    const Row r = drow(s, s.utag[s.order[q]] & SLOT);
+    const Row r = drow(s, s.utag[q] & SLOT);
     const u32 sb = sub_of(r.key, T, t);
     u32 gb = s.ustart[sb];
-    while (s.ukey[s.order[gb]] != r.key) gb++;
+    while (s.ukey[gb] != r.key) gb++;
     u32 less = 0;
-    for (u32 e = gb; e < nU && s.ukey[s.order[e]] == r.key; e++)
-      if (s.usurv[e] && row_cmp(drow(s, s.utag[s.order[e]] & SLOT), r) < 0) less++;
+    for (u32 e = gb; e < nU && s.ukey[e] == r.key; e++)
+      if (s.usurv[e] && row_cmp(drow(s, s.utag[e] & SLOT), r) < 0) less++;
     u32 ls = s.sfirst[sb];
     const u32 le = s.sfirst[sb + 1];
     while (ls < le && s.skey[ls] < r.key) ls++;
