@@ -24,15 +24,18 @@ struct dg_engine {
   u64* state = nullptr;
   u64 state_cap = 0;
   u32* ticket = nullptr;  // [0] ticket, [1] error bits, [2] store_check flag, [3] op order flag
+                          // (16 words right behind d_counts: one allocation, see below)
   u32* counts = nullptr;  // single-pass join tile-count granules
   u64 counts_cap = 0;
   // ping-pong intermediate states of dg_joink / dg_apply_deltas
   void* fold = nullptr;
   size_t fold_cap = 0;
   u32 epoch = 0;
-  // small device counters + pinned host mirror
-  u64* d_counts = nullptr;  // 8 entries
-  u64* h_counts = nullptr;  // pinned, 8 entries
+  // small device counters + pinned host mirror.  d_counts[0..8) and ticket[0..16) are one
+  // device allocation (ticket == (u32*)(d_counts + 8)), so a synchronous call brings its
+  // counts and the error bits home in ONE copy (read_counts).
+  u64* d_counts = nullptr;  // 8 entries, then the ticket words
+  u64* h_counts = nullptr;  // pinned, 16 entries (a mirror of the whole block)
   // general scratch
   void* tmp = nullptr;
   size_t tmp_cap = 0;
@@ -130,14 +133,15 @@ int next_scan(dg_engine* e, Scan* s) {
   return DG_OK;
 }
 
+// The first n counts and the error bits (ticket[1]) in one copy: d_counts[0..8) and
+// ticket[0..2) are contiguous on the device and land in h_counts[0..9).
 int read_counts(dg_engine* e, int n) {
-  HIP_TRY(hipMemcpyAsync(e->h_counts, e->d_counts, n * sizeof(u64), hipMemcpyDeviceToHost,
-                         e->stream));
-  u32 err = 0;
-  HIP_TRY(hipMemcpyAsync(&e->h_counts[7], e->ticket + 1, sizeof(u32), hipMemcpyDeviceToHost,
-                         e->stream));
+  (void)n;
+  HIP_TRY(hipMemcpyAsync(e->h_counts, e->d_counts, 8 * sizeof(u64) + 2 * sizeof(u32),
+                         hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
-  memcpy(&err, &e->h_counts[7], sizeof(u32));
+  u32 err = 0;
+  memcpy(&err, (const char*)&e->h_counts[8] + sizeof(u32), sizeof(u32));
   if (err) {
     HIP_TRY(hipMemsetAsync(e->ticket, 0, 4 * sizeof(u32), e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -276,14 +280,13 @@ int dg_engine_create(int device, void* hip_stream, dg_engine** out) {
     }
     e->own_stream = true;
   }
-  if (hipMalloc(&e->ticket, 16 * sizeof(u32)) != hipSuccess ||
-      hipMalloc(&e->d_counts, 8 * sizeof(u64)) != hipSuccess ||
-      hipHostMalloc(&e->h_counts, 8 * sizeof(u64), 0) != hipSuccess) {
+  if (hipMalloc(&e->d_counts, 8 * sizeof(u64) + 16 * sizeof(u32)) != hipSuccess ||
+      hipHostMalloc(&e->h_counts, 16 * sizeof(u64), 0) != hipSuccess) {
     dg_engine_destroy(e);
     return fail(DG_E_NOMEM, "dg_engine_create: allocation failed");
   }
-  if (hipMemsetAsync(e->ticket, 0, 16 * sizeof(u32), e->stream) != hipSuccess ||
-      hipMemsetAsync(e->d_counts, 0, 8 * sizeof(u64), e->stream) != hipSuccess) {
+  e->ticket = (u32*)(e->d_counts + 8);
+  if (hipMemsetAsync(e->d_counts, 0, 8 * sizeof(u64) + 16 * sizeof(u32), e->stream) != hipSuccess) {
     dg_engine_destroy(e);
     return fail(DG_E_DEVICE, "dg_engine_create: hipMemsetAsync failed");
   }
@@ -301,7 +304,6 @@ int dg_engine_destroy(dg_engine* e) {
   hipSetDevice(e->device);
   if (e->stream) hipStreamSynchronize(e->stream);
   if (e->state) hipFree(e->state);
-  if (e->ticket) hipFree(e->ticket);
   if (e->d_counts) hipFree(e->d_counts);
   if (e->h_counts) hipHostFree(e->h_counts);
   if (e->tmp) hipFree(e->tmp);
@@ -319,10 +321,10 @@ int dg_engine_sync(dg_engine* e) {
   if (!e) return fail(DG_E_INVAL, "null engine");
   TRY(set_device(e));
   u32 err = 0;
-  HIP_TRY(hipMemcpyAsync(&e->h_counts[7], e->ticket + 1, sizeof(u32), hipMemcpyDeviceToHost,
+  HIP_TRY(hipMemcpyAsync(&e->h_counts[12], e->ticket + 1, sizeof(u32), hipMemcpyDeviceToHost,
                          e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
-  memcpy(&err, &e->h_counts[7], sizeof(u32));
+  memcpy(&err, &e->h_counts[12], sizeof(u32));
   if (err) {
     HIP_TRY(hipMemsetAsync(e->ticket, 0, 4 * sizeof(u32), e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -338,10 +340,10 @@ int dg_store_check(dg_engine* e, const dg_store* s) {
   HIP_TRY(hipMemsetAsync(e->ticket + 2, 0, sizeof(u32), e->stream));
   HIP_TRY(launch_store_check(rows_of(s), e->ticket + 2, e->stream));
   u32 bad = 0;
-  HIP_TRY(hipMemcpyAsync(&e->h_counts[6], e->ticket + 2, sizeof(u32), hipMemcpyDeviceToHost,
+  HIP_TRY(hipMemcpyAsync(&e->h_counts[11], e->ticket + 2, sizeof(u32), hipMemcpyDeviceToHost,
                          e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
-  memcpy(&bad, &e->h_counts[6], sizeof(u32));
+  memcpy(&bad, &e->h_counts[11], sizeof(u32));
   if (bad) return fail(DG_E_ORDER, "store rows are not strictly ascending");
   return DG_OK;
 }
@@ -561,10 +563,10 @@ int kfold_pass(dg_engine* e, const dg_store* state, const dg_context* ctx, int k
     HIP_TRY(hipMemsetAsync(p.sstart, 0, b_ss + b_ds + 2 * b_tab + 256, e->stream));
     TRY(next_scan(e, &p.scan));
     HIP_TRY(launch_kfold(p, e->stream));
-    HIP_TRY(hipMemcpyAsync(&e->h_counts[5], p.flag, sizeof(u32), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipMemcpyAsync(&e->h_counts[10], p.flag, sizeof(u32), hipMemcpyDeviceToHost, e->stream));
     TRY(read_counts(e, 2));  // synchronizes; the staging buffer is free again
     u32 flag = 0;
-    memcpy(&flag, &e->h_counts[5], sizeof(u32));
+    memcpy(&flag, &e->h_counts[10], sizeof(u32));
     if (flag & KF_PREP_FAIL) return DG_OK;
     if (flag) continue;
     out->n = e->h_counts[0];
@@ -693,9 +695,9 @@ int dg_mutate_batch(dg_engine* e, const dg_store* state, const dg_context* ctx, 
   TRY(read_counts(e, 3));
   const u64 n_keys = e->h_counts[0], n_rows = e->h_counts[1], n_sdots = e->h_counts[2];
   u32 bad = 0;
-  HIP_TRY(hipMemcpyAsync(&e->h_counts[6], err, sizeof(u32), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipMemcpyAsync(&e->h_counts[11], err, sizeof(u32), hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
-  memcpy(&bad, &e->h_counts[6], sizeof(u32));
+  memcpy(&bad, &e->h_counts[11], sizeof(u32));
   if (bad & 1u) return fail(DG_E_ORDER, "dg_mutate_batch: ops are not sorted by key");
   const u64 n_dots = n_sdots + n_adds;
   if (keys_cap < n_keys || delta->cap < n_rows || delta_dots->cap < n_dots)
