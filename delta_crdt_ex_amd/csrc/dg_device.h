@@ -87,12 +87,19 @@ __device__ __forceinline__ T gload(const T* p, u64 g) {  // a global_load, not a
 }
 
 __device__ __forceinline__ Row load_row_sel(const Rows& A, const Rows& B, bool fb, u64 g) {
+  // (both opaque values first, then the select: an asm inside each arm of the select
+  // makes the compiler branch per column and reload spilled argument SGPRs per branch)
+  const u64 *ak = opaque_ptr(A.key), *bk = opaque_ptr(B.key);
+  const u64 *av = opaque_ptr(A.val), *bv = opaque_ptr(B.val);
+  const i64 *at = opaque_ptr(A.ts), *bt = opaque_ptr(B.ts);
+  const u32 *an = opaque_ptr(A.node), *bn = opaque_ptr(B.node);
+  const u64 *ac = opaque_ptr(A.cnt), *bc = opaque_ptr(B.cnt);
   Row x;
-  x.key = gload(fb ? opaque_ptr(B.key) : opaque_ptr(A.key), g);
-  x.val = gload(fb ? opaque_ptr(B.val) : opaque_ptr(A.val), g);
-  x.ts = gload(fb ? opaque_ptr(B.ts) : opaque_ptr(A.ts), g);
-  x.node = gload(fb ? opaque_ptr(B.node) : opaque_ptr(A.node), g);
-  x.cnt = gload(fb ? opaque_ptr(B.cnt) : opaque_ptr(A.cnt), g);
+  x.key = gload(fb ? bk : ak, g);
+  x.val = gload(fb ? bv : av, g);
+  x.ts = gload(fb ? bt : at, g);
+  x.node = gload(fb ? bn : an, g);
+  x.cnt = gload(fb ? bc : ac, g);
   return x;
 }
 
