@@ -47,10 +47,10 @@ hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& 
 // Changed keys (dg_join2_changes): with chg_tmp (join2_changes_tmp_bytes) the join
 // records per-tile change events (always the single-pass kernel); launch_join2_changes
 // then drops repeats and compacts them into out[0, cap) (*d_count = changed keys).
-// chg_tmp: JOIN_TILE u64 events + u64 offset + 3 u32 per tile.
+// chg_tmp: JOIN_TILE u64 events + u64 offset + 3 u32 + first/last event (2 u64) per tile.
 inline size_t join2_changes_tmp_bytes(u64 na, u64 nb) {
   const u64 t = join2_tiles(na, nb);
-  return t * ((u64)JOIN_TILE * 8 + 8 + 12) + 256;
+  return t * ((u64)JOIN_TILE * 8 + 8 + 12 + 16) + 8 + 256;
 }
 hipError_t launch_join2_changes(u64 na, u64 nb, void* chg_tmp, u64* out, u64 cap, u64* d_count,
                                 hipStream_t st);

@@ -858,6 +858,8 @@ struct ChgArgs {
   u32* wu;         // events after the first that differ from their predecessor
   u32* first_dup;  // the tile's first event repeats the previous tile's last one
   u64* off;        // output offset of the tile
+  u64* fk;         // the tile's first and last event (written when it has any), so the
+  u64* lk;         //   scan needs no dependent load of a predecessor tile's events
   u64 ntiles;
   u64* out;
   u64 cap;
@@ -873,61 +875,135 @@ __global__ __launch_bounds__(GB) void chg_count_kernel(ChgArgs p) {
   for (u32 i = threadIdx.x + 1; i < n; i += GB) c += ev[i] != ev[i - 1] ? 1u : 0u;
   u32 tot;
   block_excl_scan<GB>(c, s_wave, &tot);
-  if (threadIdx.x == 0) p.wu[t] = tot;
+  if (threadIdx.x == 0) {
+    p.wu[t] = tot;
+    if (n > 0) {
+      p.fk[t] = ev[0];
+      p.lk[t] = ev[n - 1];
+    }
+  }
 }
 
+// One chunk of SB tiles' scan inputs (chg_scan_kernel loads the next chunk's while it
+// scans the current one).
+struct ChgIn {
+  u32 n, wu;
+  u64 fk, lk;
+};
+
+__device__ __forceinline__ ChgIn chg_in(const ChgArgs& p, u64 t) {
+  ChgIn x{0, 0, 0, 0};
+  if (t < p.ntiles) {
+    x.n = p.cnt[t];
+    x.wu = p.wu[t];
+    x.fk = p.fk[t];  // (unwritten for an empty tile, and then unused)
+    x.lk = p.lk[t];
+  }
+  return x;
+}
+
+// Nearest non-empty tile before each tile (a max-scan of t+1 over non-empty tiles that
+// carries that tile's last event along), the first event's repeat flag, and the tiles'
+// exclusive output offsets.  Chunks of SB * ST tiles (ST consecutive tiles per thread,
+// scanned serially), the carry held in LDS; the next chunk's inputs load during a chunk.
+constexpr int ST = 4;  // tiles per chg_scan_kernel thread per chunk
+
 __global__ __launch_bounds__(SB) void chg_scan_kernel(ChgArgs p) {
-  __shared__ u32 s_wave[SB / WAVE + 1];
-  __shared__ i64 s_last[SB / WAVE + 1];
-  __shared__ u64 s_carry[2];  // [0] output offset, [1] last non-empty tile (+1; 0 = none)
+  constexpr int NW = SB / WAVE;
+  __shared__ u32 s_wave[NW + 1];
+  __shared__ i64 s_last[NW + 1];
+  __shared__ u64 s_lkey[NW + 1];
+  __shared__ u64 s_carry[3];  // output offset; last non-empty tile (+1; 0 = none); its last event
   const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
-  if (tid == 0) s_carry[0] = s_carry[1] = 0;
+  if (tid == 0) s_carry[0] = s_carry[1] = s_carry[2] = 0;
   __syncthreads();
-  for (u64 c0 = 0; c0 < p.ntiles; c0 += SB) {
-    const u64 t = c0 + tid;
-    const u32 n = t < p.ntiles ? p.cnt[t] : 0u;
-    // nearest non-empty tile before t: inclusive max-scan of (t+1 if non-empty)
-    i64 m = n > 0 ? (i64)t + 1 : 0;
-    for (int d = 1; d < WAVE; d <<= 1) {
+  ChgIn cur[ST];
+#pragma unroll
+  for (int q = 0; q < ST; q++) cur[q] = chg_in(p, (u64)tid * ST + q);
+  for (u64 c0 = 0; c0 < p.ntiles; c0 += (u64)SB * ST) {
+    const u64 t0 = c0 + (u64)tid * ST;  // this thread's first tile
+    ChgIn nxt[ST];                      // in flight during this chunk
+#pragma unroll
+    for (int q = 0; q < ST; q++) nxt[q] = chg_in(p, t0 + (u64)SB * ST + q);
+    // the thread's own last non-empty tile (+1) and its last event
+    i64 m = 0;
+    u64 mk = 0;
+#pragma unroll
+    for (int q = 0; q < ST; q++)
+      if (cur[q].n > 0) {
+        m = (i64)(t0 + q) + 1;
+        mk = cur[q].lk;
+      }
+    for (int d = 1; d < WAVE; d <<= 1) {  // inclusive max-scan over the wave's threads
       const i64 o = __shfl_up(m, d, WAVE);
-      if (lane >= d) m = max(m, o);
+      const u64 ok = __shfl_up(mk, d, WAVE);
+      if (lane >= d && o > m) {
+        m = o;
+        mk = ok;
+      }
     }
-    if (lane == WAVE - 1) s_last[w] = m;
+    if (lane == WAVE - 1) {
+      s_last[w] = m;
+      s_lkey[w] = mk;
+    }
     __syncthreads();
     if (tid == 0) {
       i64 run = (i64)s_carry[1];
-      for (int i = 0; i < SB / WAVE; i++) {
+      u64 rk = s_carry[2];
+      for (int i = 0; i < NW; i++) {
         const i64 v = s_last[i];
+        const u64 vk = s_lkey[i];
         s_last[i] = run;  // exclusive over waves
-        run = max(run, v);
+        s_lkey[i] = rk;
+        if (v > run) {
+          run = v;
+          rk = vk;
+        }
       }
-      s_last[SB / WAVE] = run;
+      s_last[NW] = run;
+      s_lkey[NW] = rk;
     }
     __syncthreads();
-    const i64 before_wave = s_last[w];
-    i64 prev_incl = max(m, before_wave);  // nearest non-empty <= t
-    i64 prev = __shfl_up(prev_incl, 1, WAVE);  // nearest non-empty < t
-    if (lane == 0) prev = before_wave;
-    u32 dup = 0, uc = 0;
-    if (n > 0) {
-      if (prev > 0) {
-        const u64 q = (u64)prev - 1;
-        dup = p.tmp[t * (u64)JT] == p.tmp[q * (u64)JT + p.cnt[q] - 1] ? 1u : 0u;
+    const i64 bw = s_last[w];
+    const u64 bk = s_lkey[w];
+    const bool own = m > bw;  // nearest non-empty tile up to this thread's last
+    i64 prev = __shfl_up(own ? m : bw, 1, WAVE);  // ... before this thread's first tile
+    u64 pk = __shfl_up(own ? mk : bk, 1, WAVE);
+    if (lane == 0) {
+      prev = bw;
+      pk = bk;
+    }
+    u32 dup[ST], uc[ST], sum = 0;
+#pragma unroll
+    for (int q = 0; q < ST; q++) {
+      dup[q] = 0;
+      uc[q] = 0;
+      if (cur[q].n > 0) {
+        dup[q] = (prev > 0 && cur[q].fk == pk) ? 1u : 0u;
+        uc[q] = cur[q].wu + 1 - dup[q];
+        prev = (i64)(t0 + q) + 1;
+        pk = cur[q].lk;
       }
-      uc = p.wu[t] + 1 - dup;
+      sum += uc[q];
     }
     u32 tot;
-    const u32 o = block_excl_scan<SB>(uc, s_wave, &tot);
-    if (t < p.ntiles) {
-      p.first_dup[t] = dup;
-      p.off[t] = s_carry[0] + o;
-    }
+    u64 o = s_carry[0] + block_excl_scan<SB>(sum, s_wave, &tot);
+#pragma unroll
+    for (int q = 0; q < ST; q++)
+      if (t0 + q < p.ntiles) {
+        p.first_dup[t0 + q] = dup[q];
+        p.off[t0 + q] = o;
+        o += uc[q];
+      }
     __syncthreads();
     if (tid == 0) {
       s_carry[0] += tot;
-      s_carry[1] = (u64)s_last[SB / WAVE];
+      s_carry[1] = (u64)s_last[NW];
+      s_carry[2] = s_lkey[NW];
     }
     __syncthreads();
+#pragma unroll
+    for (int q = 0; q < ST; q++) cur[q] = nxt[q];
   }
   if (tid == 0) p.d_count[0] = s_carry[0];
 }
@@ -1196,6 +1272,11 @@ hipError_t launch_join2_changes(u64 na, u64 nb, void* chg_tmp, u64* out, u64 cap
   p.wu = (u32*)c;
   c += ntiles * 4;
   p.first_dup = (u32*)c;
+  c += ntiles * 4;
+  c = (char*)(((uintptr_t)c + 7) & ~(uintptr_t)7);
+  p.fk = (u64*)c;
+  c += ntiles * 8;
+  p.lk = (u64*)c;
   p.ntiles = ntiles;
   p.out = out;
   p.cap = cap;

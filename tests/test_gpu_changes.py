@@ -90,3 +90,16 @@ def test_delta_subscriber_scenario():
     # a key the delta does not touch: no diff at all
     st, diffs = CC.update_state_with_delta(st, M.add("Other", 1, 1, st), ["Nope"])
     assert diffs is None
+
+
+def test_changes_sparse_keyed_multichunk(engine):
+    """A keyed join touching a few dozen keys of a 4.3M-key state: ~4200 tiles, almost all
+    without change events, so an event tile's nearest non-empty predecessor can lie a
+    chunk (of 4096 tiles) back in the changed-key scan."""
+    a, b = W.config2(n_keys=4_300_000, seed=11)
+    rng = np.random.default_rng(11)
+    keys = np.unique(rng.choice(a["rows"][0], size=40, replace=False)).astype(np.uint64)
+    sel = np.isin(b["rows"][0], keys)
+    bs = {"rows": tuple(c[sel] for c in b["rows"]), "ctx": b["ctx"]}
+    n = check(engine, a, bs, keys)
+    assert 0 < n <= len(keys)
