@@ -226,6 +226,39 @@ __global__ __launch_bounds__(CB) void ctx_union_kernel(CtxUnionArgs p) {
   ctx_union_block<CB>(p, s_wave);
 }
 
+// Scratch of dg_join2_changes (join2_changes_tmp_bytes): per tile JT event keys, then
+// per-tile arrays: output offset, event count, differing-event count, first-event repeat
+// flag, first and last event.
+struct ChgLayout {
+  u64* ev;
+  u64* off;
+  u32* cnt;
+  u32* wu;
+  u32* first_dup;
+  u64* fk;
+  u64* lk;
+};
+
+static __host__ ChgLayout chg_layout(void* tmp, u64 ntiles) {
+  ChgLayout l;
+  char* c = (char*)tmp;
+  l.ev = (u64*)c;
+  c += ntiles * (u64)JT * 8;
+  l.off = (u64*)c;
+  c += ntiles * 8;
+  l.cnt = (u32*)c;
+  c += ntiles * 4;
+  l.wu = (u32*)c;
+  c += ntiles * 4;
+  l.first_dup = (u32*)c;
+  c += ntiles * 4;
+  c = (char*)(((uintptr_t)c + 7) & ~(uintptr_t)7);
+  l.fk = (u64*)c;
+  c += ntiles * 8;
+  l.lk = (u64*)c;
+  return l;
+}
+
 struct JoinArgs {
   Rows a, b;
   Ctx ca, cb;
@@ -240,6 +273,9 @@ struct JoinArgs {
   u32* counts;            // two-pass only: kept rows per tile
   u64* chg_tmp;           // CHG: JT change-event keys per tile
   u32* chg_cnt;           // CHG: events per tile
+  u32* chg_wu;            // CHG: events after the tile's first that differ from their predecessor
+  u64* chg_fk;            // CHG: the tile's first and last event (tiles with events)
+  u64* chg_lk;
   int fused;              // stream kernel: splits searched in-kernel (no partition launch);
                           // the grid's last workgroup computes the context union
   CtxUnionArgs cu;
@@ -628,6 +664,8 @@ struct StreamLds {
   u32 wave[JB / WAVE + 1];
   u64 red[2 * (JB / WAVE)];
   u64 spl[2 * FUSE_IT];  // fused: splits of this workgroup's tiles (start, end per tile)
+  u64 chk[JB / WAVE];    // CHG: each wave's last change event, and 1 + its lane (0: none)
+  int chf[JB / WAVE];
 };
 
 constexpr u32 CNT_BITS = 12;  // count field of a tile-count granule (JT < 4096)
@@ -799,14 +837,66 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       if (keep & (1u << q)) s.comp[bi][pos++] = src[q];
     if (tid == 0) publish_count(cs, t, epoch, n);
     __syncthreads();
-    if (CHG) {  // the tile's change events (keys, ascending, repeats allowed) -> chg_tmp
-      u32 n2;
-      u32 p2 = block_excl_scan<JB>(__popc(ev), s.wave, &n2);
-      u64* dst = p.chg_tmp + t * (u64)JT;
+    if (CHG) {  // the tile's change events (keys, ascending, repeats allowed) -> chg_tmp,
+                // with the per-tile figures the changed-key scan needs (chg_scan_kernel)
+      const Buf& cb = s.buf[bi];
+      const int ne = __popc(ev);
+      u64 fkey = 0, lkey = 0;
+      u32 diff = 0;  // own events after this thread's first that differ from their predecessor
+      bool seen = false;
 #pragma unroll
       for (int q = 0; q < JI; q++)
-        if (ev & (1u << q)) dst[p2++] = buf_key(s.buf[bi], src[q]);
-      if (tid == 0) p.chg_cnt[t] = n2;
+        if (ev & (1u << q)) {
+          const u64 k = buf_key(cb, src[q]);
+          if (seen && k != lkey) diff++;
+          if (!seen) fkey = k;
+          lkey = k;
+          seen = true;
+        }
+      // the event before this thread's first: a max-scan of (lane + 1, last event) over
+      // the wave's lanes with events, then the nearest earlier wave with events
+      const int lane = tid & (WAVE - 1), wv = tid / WAVE;
+      int m = ne ? lane + 1 : 0;
+      u64 mk = lkey;
+      for (int d = 1; d < WAVE; d <<= 1) {
+        const int o = __shfl_up(m, d, WAVE);
+        const u64 ok = __shfl_up(mk, d, WAVE);
+        if (lane >= d && o > m) {
+          m = o;
+          mk = ok;
+        }
+      }
+      if (lane == WAVE - 1) {
+        s.chf[wv] = m;
+        s.chk[wv] = mk;
+      }
+      int pm = __shfl_up(m, 1, WAVE);
+      u64 pkey = __shfl_up(mk, 1, WAVE);
+      if (lane == 0) pm = 0;
+      __syncthreads();
+      if (pm == 0)
+        for (int w2 = wv - 1; w2 >= 0; w2--)
+          if (s.chf[w2] > 0) {
+            pm = 1;
+            pkey = s.chk[w2];
+            break;
+          }
+      if (ne && pm > 0 && fkey != pkey) diff++;
+      // one scan for both: events (low 16 bits) and differing events (high 16 bits)
+      u32 tot2;
+      const u32 sc2 = block_excl_scan<JB>((diff << 16) | (u32)ne, s.wave, &tot2);
+      const u32 n2 = tot2 & 0xffffu, p0 = sc2 & 0xffffu;
+      u64* dst = p.chg_tmp + t * (u64)JT;
+      u32 p2 = p0;
+#pragma unroll
+      for (int q = 0; q < JI; q++)
+        if (ev & (1u << q)) dst[p2++] = buf_key(cb, src[q]);
+      if (tid == 0) {
+        p.chg_cnt[t] = n2;
+        p.chg_wu[t] = tot2 >> 16;
+      }
+      if (ne && p0 == 0) p.chg_fk[t] = fkey;
+      if (ne && p2 == n2) p.chg_lk[t] = lkey;
     }
     JSTAMP(t, 4);
     if (k > 0) {  // stripe k-1: this workgroup's tile t - G
@@ -844,8 +934,9 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
 // changed, possibly across tiles).  An event is kept where it differs from the event
 // before it: inside its tile, or -- for a tile's first event -- the last event of the
 // nearest non-empty earlier tile.  Every tile of the launch is resident at once, so
-// instead of a look-back (which would spin on the whole launch) three short passes:
-//   chg_count_kernel  per tile: events differing from their in-tile predecessor
+// instead of a look-back (which would spin on the whole launch):
+//   join2_stream_kernel<_, CHG>  per tile: its events, their count, the events that
+//                     differ from their in-tile predecessor, the first and last event
 //   chg_scan_kernel   one workgroup over the tiles: nearest non-empty predecessor
 //                     (max-scan), the first event's repeat flag, exclusive offsets
 //   chg_write_kernel  per tile: the kept events at the tile's offset
@@ -865,24 +956,6 @@ struct ChgArgs {
   u64 cap;
   u64* d_count;
 };
-
-__global__ __launch_bounds__(GB) void chg_count_kernel(ChgArgs p) {
-  __shared__ u32 s_wave[GB / WAVE + 1];
-  const u64 t = blockIdx.x;
-  const u32 n = p.cnt[t];
-  const u64* ev = p.tmp + t * (u64)JT;
-  u32 c = 0;
-  for (u32 i = threadIdx.x + 1; i < n; i += GB) c += ev[i] != ev[i - 1] ? 1u : 0u;
-  u32 tot;
-  block_excl_scan<GB>(c, s_wave, &tot);
-  if (threadIdx.x == 0) {
-    p.wu[t] = tot;
-    if (n > 0) {
-      p.fk[t] = ev[0];
-      p.lk[t] = ev[n - 1];
-    }
-  }
-}
 
 // One chunk of SB tiles' scan inputs (chg_scan_kernel loads the next chunk's while it
 // scans the current one).
@@ -1205,7 +1278,15 @@ hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& 
   p.lists = nullptr;
   p.counts = nullptr;
   p.chg_tmp = chg_tmp ? (u64*)chg_tmp : nullptr;
-  p.chg_cnt = chg_tmp ? (u32*)((char*)chg_tmp + p.ntiles * ((u64)JT * 8 + 8)) : nullptr;
+  p.chg_cnt = p.chg_wu = nullptr;
+  p.chg_fk = p.chg_lk = nullptr;
+  if (chg_tmp) {
+    const ChgLayout l = chg_layout(chg_tmp, p.ntiles);
+    p.chg_cnt = l.cnt;
+    p.chg_wu = l.wu;
+    p.chg_fk = l.fk;
+    p.chg_lk = l.lk;
+  }
   if (p.ntiles == 0) {
     // no rows: only the context union runs
     hipError_t e = hipMemsetAsync(d_counts, 0, sizeof(u64), st);
@@ -1261,27 +1342,19 @@ hipError_t launch_join2_changes(u64 na, u64 nb, void* chg_tmp, u64* out, u64 cap
                                 hipStream_t st) {
   const u64 ntiles = join2_tiles(na, nb);
   if (ntiles == 0) return hipMemsetAsync(d_count, 0, sizeof(u64), st);
-  char* c = (char*)chg_tmp;
+  const ChgLayout l = chg_layout(chg_tmp, ntiles);
   ChgArgs p;
-  p.tmp = (const u64*)c;
-  c += ntiles * (u64)JT * 8;
-  p.off = (u64*)c;
-  c += ntiles * 8;
-  p.cnt = (const u32*)c;
-  c += ntiles * 4;
-  p.wu = (u32*)c;
-  c += ntiles * 4;
-  p.first_dup = (u32*)c;
-  c += ntiles * 4;
-  c = (char*)(((uintptr_t)c + 7) & ~(uintptr_t)7);
-  p.fk = (u64*)c;
-  c += ntiles * 8;
-  p.lk = (u64*)c;
+  p.tmp = l.ev;
+  p.off = l.off;
+  p.cnt = l.cnt;
+  p.wu = l.wu;
+  p.first_dup = l.first_dup;
+  p.fk = l.fk;
+  p.lk = l.lk;
   p.ntiles = ntiles;
   p.out = out;
   p.cap = cap;
   p.d_count = d_count;
-  hipLaunchKernelGGL(chg_count_kernel, dim3((unsigned)ntiles), dim3(GB), 0, st, p);
   hipLaunchKernelGGL(chg_scan_kernel, dim3(1), dim3(SB), 0, st, p);
   hipLaunchKernelGGL(chg_write_kernel, dim3((unsigned)ntiles), dim3(GB), 0, st, p);
   return hipGetLastError();
