@@ -397,8 +397,9 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "join2 = join2_partition_kernel + join2_stream_kernel "
-                          "(events bracket both)",
+                "kernel": "join2_stream_kernel (splits searched in-kernel at this size; joins "
+                          "over 4 tiles per workgroup add a join2_partition_kernel launch, "
+                          "and the events bracket both)",
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_launch_us": avg_launch_s * 1e6,
                 "launch_timing": "HIP events on the engine stream around the timed region / steps",
