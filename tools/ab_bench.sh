@@ -4,8 +4,8 @@ BR='import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); pr
 timeout -k 10 300 python -u -m pytest tests/ -x -q --timeout 120 --timeout-method thread -m gpu > gpurun_out/gpu_tests.log 2>&1 || { echo TESTS_FAILED; tail -30 gpurun_out/gpu_tests.log; exit 1; }
 tail -1 gpurun_out/gpu_tests.log
 for rep in 1 2; do
-for l in libdeltagpu.so libdeltagpu_DG_OLDAPI.so; do
-  DG_LIB_PATH=$PWD/delta_crdt_ex_amd/$l timeout -k 10 300 python -u bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-merkle > gpurun_out/ab_$l.log 2>&1 || { echo "$l FAILED"; tail -5 gpurun_out/ab_$l.log; exit 1; }
+for l in $(cd delta_crdt_ex_amd && ls libdeltagpu*.so | grep -v stamps); do
+  DG_LIB_PATH=$PWD/delta_crdt_ex_amd/$l timeout -k 10 300 python -u bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-merkle ${AB_FLAGS:-} > gpurun_out/ab_$l.log 2>&1 || { echo "$l FAILED"; tail -5 gpurun_out/ab_$l.log; exit 1; }
   echo -n "$l: "; python -c "$BR" < gpurun_out/ab_$l.log
 done
 done
