@@ -802,7 +802,7 @@ int dg_merkle_diff(dg_engine* e, const dg_merkle* a, const dg_merkle* b, uint64_
   if (a->depth < 1 || a->depth > 26) return fail(DG_E_INVAL, "dg_merkle_diff: depth %u", a->depth);
   if (cap && !out_keys) return fail(DG_E_INVAL, "dg_merkle_diff: null out_keys");
   TRY(set_device(e));
-  TRY(ensure_state(e, 2 * diff_tiles(a->depth) + 2));  // raw per-tile counts and offsets
+  TRY(ensure_state(e, diff_scratch_words(a->depth) + 2));  // tile counts, offsets, bucket counts
   HIP_TRY(launch_merkle_diff(a->depth, a->nodes, a->leaf_key, a->leaf_hash, a->bucket_off, b->nodes,
                              b->leaf_key, b->leaf_hash, b->bucket_off, out_keys, cap, e->state,
                              e->d_counts, e->stream));

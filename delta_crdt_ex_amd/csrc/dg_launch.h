@@ -150,10 +150,12 @@ hipError_t launch_merkle_levels(u32 depth, const u64* leaf_hash, const u64* buck
                                 u64* nodes, hipStream_t st);
 constexpr int DIFF_BLOCK = 256;
 inline u64 diff_tiles(u32 depth) { return depth >= 8 ? (1ull << (depth - 8)) : 1ull; }
+// per-tile counts and offsets, then one u32 count per bucket
+inline u64 diff_scratch_words(u32 depth) { return 2 * diff_tiles(depth) + ((1ull << depth) + 1) / 2; }
 hipError_t launch_merkle_diff(u32 depth, const u64* nodes_a, const u64* leaf_key_a,
                               const u64* leaf_hash_a, const u64* off_a, const u64* nodes_b,
                               const u64* leaf_key_b, const u64* leaf_hash_b, const u64* off_b,
                               u64* out_keys, u64 cap, u64* scratch, u64* d_count,
-                              hipStream_t st);  // scratch: 2 * diff_tiles(depth) u64
+                              hipStream_t st);  // scratch: diff_scratch_words(depth) u64
 
 }  // namespace dg

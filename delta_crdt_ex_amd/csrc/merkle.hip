@@ -70,6 +70,7 @@ struct DiffArgs {
   u64 cap;
   u64* cnt;  // differing keys per tile
   u64* off;  // their output offset
+  u32* bc;   // differing keys per bucket (the count pass's walk, reused by the write pass)
   u64 ntiles;
   u64* d_count;
 };
@@ -105,7 +106,12 @@ __device__ __forceinline__ u32 diff_bucket(const DiffArgs& p, u64 b, u64* out, u
 // The differing keys in three passes (every tile of a launch is resident at once, so
 // a look-back would poll whole rounds of predecessors): per tile of 256 buckets the
 // count, one workgroup's offset scan, then the write.  A bucket is walked only where
-// its subtree root and its own node differ.
+// its subtree root and its own node differ; the write pass re-reads the count pass's
+// per-bucket counts instead of walking every differing bucket a second time.
+__device__ __forceinline__ u64 diff_bpt(const DiffArgs& p) {  // buckets per tile
+  return p.depth >= 8 ? 256ull : (1ull << p.depth);
+}
+
 __device__ __forceinline__ u64 diff_bucket_of(const DiffArgs& p, u64 tile, int tid, bool* walk) {
   const u32 rl = p.depth >= 8 ? p.depth - 8 : 0;  // subtree root level
   const u64 root = ((1ull << rl) - 1) + tile;
@@ -125,6 +131,7 @@ __global__ __launch_bounds__(DB) void merkle_diff_count_kernel(DiffArgs p) {
   bool walk;
   const u64 b = diff_bucket_of(p, blockIdx.x, threadIdx.x, &walk);
   const u32 c = walk ? diff_bucket<false>(p, b, nullptr, 0, 0) : 0u;
+  if ((u64)threadIdx.x < diff_bpt(p)) p.bc[b] = c;
   u32 tot;
   block_excl_scan<DB>(c, s_wave, &tot);
   if (threadIdx.x == 0) p.cnt[blockIdx.x] = tot;
@@ -139,9 +146,9 @@ __global__ __launch_bounds__(DSB) void merkle_diff_scan_kernel(DiffArgs p) {
 
 __global__ __launch_bounds__(DB) void merkle_diff_write_kernel(DiffArgs p) {
   __shared__ u32 s_wave[DB / WAVE + 1];
-  bool walk;
-  const u64 b = diff_bucket_of(p, blockIdx.x, threadIdx.x, &walk);
-  const u32 c = walk ? diff_bucket<false>(p, b, nullptr, 0, 0) : 0u;
+  const u64 bpt = diff_bpt(p);
+  const u64 b = blockIdx.x * bpt + threadIdx.x;
+  const u32 c = (u64)threadIdx.x < bpt ? p.bc[b] : 0u;
   u32 tot;
   const u32 ex = block_excl_scan<DB>(c, s_wave, &tot);
   if (c) diff_bucket<true>(p, b, p.out, p.off[blockIdx.x] + ex, p.cap);
@@ -187,6 +194,7 @@ hipError_t launch_merkle_diff(u32 depth, const u64* nodes_a, const u64* leaf_key
   p.ntiles = diff_tiles(depth);
   p.cnt = scratch;
   p.off = scratch + p.ntiles;
+  p.bc = (u32*)(scratch + 2 * p.ntiles);
   p.d_count = d_count;
   hipLaunchKernelGGL(merkle_diff_count_kernel, dim3((unsigned)p.ntiles), dim3(DB), 0, st, p);
   hipLaunchKernelGGL(merkle_diff_scan_kernel, dim3(1), dim3(DSB), 0, st, p);
