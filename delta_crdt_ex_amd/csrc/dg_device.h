@@ -103,6 +103,18 @@ __device__ __forceinline__ Row load_row_sel(const Rows& A, const Rows& B, bool f
   return x;
 }
 
+// Output row o of a join or fold, with non-temporal stores: the kernels never read their
+// output back, and keeping it out of the caches measured 9 % faster on the config-2 join
+// (46.5 -> 42.4 us, A/B on one box; non-temporal LOADS of the inputs were slower than
+// stores alone).
+__device__ __forceinline__ void store_row_nt(const RowsOut& out, u64 o, const Row& x) {
+  __builtin_nontemporal_store(x.key, out.key + o);
+  __builtin_nontemporal_store(x.val, out.val + o);
+  __builtin_nontemporal_store(x.ts, out.ts + o);
+  __builtin_nontemporal_store(x.node, out.node + o);
+  __builtin_nontemporal_store(x.cnt, out.cnt + o);
+}
+
 // c ? x : y field by field (a conditional on two Row objects selects an ADDRESS and
 // copies through it, which keeps both rows in scratch memory).
 __device__ __forceinline__ Row row_sel(bool c, const Row& x, const Row& y) {

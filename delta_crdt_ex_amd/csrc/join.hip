@@ -757,12 +757,7 @@ __device__ __forceinline__ void write_tile(const JoinArgs& p, const StreamLds& s
   const Buf& b = s.buf[bi];
   for (u32 q = threadIdx.x; q < n; q += JB) {
     const Row x = lds_row(b, s.comp[bi][q]);
-    const u64 o = o0 + q;
-    p.out.key[o] = x.key;
-    p.out.val[o] = x.val;
-    p.out.ts[o] = x.ts;
-    p.out.node[o] = x.node;
-    p.out.cnt[o] = x.cnt;
+    store_row_nt(p.out, o0 + q, x);
   }
 }
 
@@ -1198,11 +1193,7 @@ __global__ __launch_bounds__(CPB) void join2_compact_kernel(Rows a, Rows b, cons
     const bool fb = x >= nat + 2;
     const u64 g = fb ? b0 - 1 + (u64)(x - nat - 2) : a0 - 1 + (u64)x;
     const Row r = load_row_sel(a, b, fb, g);
-    out.key[base + q] = r.key;
-    out.val[base + q] = r.val;
-    out.ts[base + q] = r.ts;
-    out.node[base + q] = r.node;
-    out.cnt[base + q] = r.cnt;
+    store_row_nt(out, base + q, r);
   }
 }
 

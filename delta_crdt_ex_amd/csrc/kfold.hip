@@ -500,11 +500,7 @@ __global__ __launch_bounds__(KB) void kfold_kernel(KFoldArgs p) {
     for (u32 q = lb; q < nU && s.ukey[q] == r.key; q++)
       if (s.usurv[q] && row_cmp(drow(s, s.utag[q] & SLOT), r) < 0) less++;
     const u64 o = base + spre[i] + upre[lb] + less;
-    p.out.key[o] = r.key;
-    p.out.val[o] = r.val;
-    p.out.ts[o] = r.ts;
-    p.out.node[o] = r.node;
-    p.out.cnt[o] = r.cnt;
+    store_row_nt(p.out, o, r);
   }
   for (u32 q = tid; q < nU; q += KB) {
     if (!s.usurv[q]) continue;
@@ -522,11 +518,7 @@ __global__ __launch_bounds__(KB) void kfold_kernel(KFoldArgs p) {
     for (u32 i = ls; i < le && s.skey[i] == r.key; i++)
       if (s.ssurv[i] && row_cmp(srow(s, i), r) < 0) sl++;
     const u64 o = base + spre[ls] + sl + upre[gb] + less;
-    p.out.key[o] = r.key;
-    p.out.val[o] = r.val;
-    p.out.ts[o] = r.ts;
-    p.out.node[o] = r.node;
-    p.out.cnt[o] = r.cnt;
+    store_row_nt(p.out, o, r);
   }
   KSTAMP(t, 6);
 }
