@@ -13,6 +13,6 @@ timeout -k 10 400 python -u tools/pmc_traffic.py > $OUT/pmc_traffic.log 2>&1 || 
 cp gpurun_out/join2_pmc.json $OUT/join2_pmc.json
 cp gpurun_out/pmc_traffic/fetch/*counter_collection.csv $OUT/join2_fetch_size.csv
 cp gpurun_out/pmc_traffic/write/*counter_collection.csv $OUT/join2_write_size.csv
-mkdir -p profiles && cp $OUT/join2_pmc.json profiles/join2_pmc.json
+mkdir -p profiles && cp $OUT/join2_pmc.json profiles/join2_pmc.json  # (box-side copy for the bench below; locally, copy gpurun_out/profiles_TAG/join2_pmc.json to profiles/ afterwards)
 timeout -k 10 400 python -u bench.py > $OUT/bench_full.log 2>&1 || { tail -20 $OUT/bench_full.log; exit 1; }
 tail -1 $OUT/bench_full.log
