@@ -115,6 +115,7 @@ _SIGS = {
     "dg_compress_dots": (C.c_int, [C.c_void_p, C.POINTER(dg_context), C.POINTER(dg_context)]),
     "dg_read_lww": (C.c_int, [C.c_void_p, C.POINTER(dg_store), P64, C.c_uint64, P64, P64,
                               C.c_uint64, P64]),
+    "dg_remap_values": (C.c_int, [C.c_void_p, C.POINTER(dg_store), P64, P64, C.c_uint64]),
     "dg_merkle_build": (C.c_int, [C.c_void_p, C.POINTER(dg_store), C.POINTER(dg_merkle)]),
     "dg_merkle_diff": (C.c_int, [C.c_void_p, C.POINTER(dg_merkle), C.POINTER(dg_merkle), P64,
                                  C.c_uint64, P64]),

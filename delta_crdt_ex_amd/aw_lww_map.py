@@ -17,6 +17,7 @@ There is no CPU fallback: without a GPU the Engine raises.
 from __future__ import annotations
 
 import time
+import weakref
 
 import numpy as np
 import torch
@@ -26,6 +27,7 @@ from ._abi import DG_CTX_DOTS, DG_CTX_VV, FunctionClauseError
 from .store import Context, Engine, Store, u64
 
 _ENGINE: Engine | None = None
+_LIVE: "weakref.WeakSet[AWLWWMap]" = weakref.WeakSet()  # host row caches to drop on a relabel
 
 
 def engine() -> Engine:
@@ -39,16 +41,34 @@ def _dev():
     return engine().device
 
 
+def _remap_hook(universe: interning.Universe):
+    """The Universe's relabel hook: rewrite the val column of every device store that
+    still holds its ids (dg_remap_values; the map is monotone, stores stay sorted)."""
+    def hook(old_ids, new_ids):
+        eng = engine()
+        for st in universe.tracked():
+            if st.n:
+                eng.remap_values(st, old_ids, new_ids)
+        for m in list(_LIVE):
+            if m.universe is universe:
+                m._host = None
+    return hook
+
+
 class AWLWWMap:
     """`%DeltaCrdt.AWLWWMap{dots, value}` (aw_lww_map.ex:2-3), device-resident."""
 
-    __slots__ = ("rows", "ctx", "universe", "_host")
+    __slots__ = ("rows", "ctx", "universe", "_host", "__weakref__")
 
     def __init__(self, rows: Store, ctx: Context, universe: interning.Universe):
         self.rows = rows
         self.ctx = ctx
         self.universe = universe
         self._host = None
+        if universe.remap_hook is None:
+            universe.remap_hook = _remap_hook(universe)
+        universe.track(rows)
+        _LIVE.add(self)
 
     # -- host views (small states / single keys only)
     def _host_rows(self):
@@ -197,14 +217,17 @@ def mutate_batch(ops, node_id, state: AWLWWMap):
     key = np.zeros(m, np.uint64)
     val = np.zeros(m, np.uint64)
     ts = np.zeros(m, np.int64)
+    for op in ops:  # intern every value first: a relabel would stale earlier ids
+        if op[0] == "add":
+            U.value(op[2])
+        elif op[0] != "remove":
+            raise ValueError(f"unknown op {op[0]!r}")
     for i, op in enumerate(ops):
         key[i] = U.key(op[1])
         if op[0] == "add":
             kind[i] = 1
             val[i] = U.value(op[2])
             ts[i] = op[3] if len(op) > 3 else time.monotonic_ns()
-        elif op[0] != "remove":
-            raise ValueError(f"unknown op {op[0]!r}")
     rank = np.cumsum(kind, dtype=np.uint64) - kind  # adds before each op, batch order
     order = np.argsort(key, kind="stable")           # by key, batch order within a key
     dev = _dev()

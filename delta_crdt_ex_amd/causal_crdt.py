@@ -25,10 +25,17 @@ from .store import u64
 def update_state_with_delta(state: M.AWLWWMap, delta: M.AWLWWMap, keys):
     """Returns (new_state, diffs): diffs is what on_diffs would receive -- None when no
     key's value map changed (diffs_to_callback/3 is not reached), else a list of
-    ("add", key, value) / ("remove", key) in `keys` order (possibly empty)."""
+    ("add", key, value) / ("remove", key) in `keys` order (possibly empty).  Keys are
+    deduplicated and values compared exactly (`=:=`: 1, 1.0 and true stay distinct),
+    as the reference's map lookups and `{old, old}` match do."""
     U = state.universe
-    order = list(dict.fromkeys(keys))
-    kids = np.unique(np.array([U.key(k) for k in order], dtype=np.uint64))
+    order, seen = [], set()
+    for k in keys:  # dedup by interned id, not Python equality
+        kid = U.key(k)
+        if kid not in seen:
+            seen.add(kid)
+            order.append((kid, k))
+    kids = np.array(sorted(seen), dtype=np.uint64)
     kt = torch.from_numpy(np.ascontiguousarray(kids).view(np.int64)).to(M._dev())
     out, octx, changed = M.engine().join2_changes(state.rows, state.ctx, delta.rows, delta.ctx,
                                                   keys=kt)
@@ -36,15 +43,25 @@ def update_state_with_delta(state: M.AWLWWMap, delta: M.AWLWWMap, keys):
     if changed.numel() == 0:
         return new, None
     ch = set(int(x) for x in u64(changed))
-    ckeys = [k for k in order if U.key(k) in ch]
-    old_v, new_v = M.read(state, ckeys), M.read(new, ckeys)
+    ckeys = [(kid, k) for kid, k in order if kid in ch]
+    old_v, new_v = _read_ids(state, ckeys), _read_ids(new, ckeys)
     diffs = []
-    for k in ckeys:
-        o, n = old_v.get(k), new_v.get(k)
-        if o == n:
+    for kid, k in ckeys:
+        o, n = old_v.get(kid), new_v.get(kid)
+        if o == n:  # value ids: equal exactly when the terms are =:=
             continue
-        diffs.append(("remove", k) if n is None else ("add", k, n))
+        diffs.append(("remove", k) if n is None else ("add", k, U.value_term(n)))
     return new, diffs
+
+
+def _read_ids(state: M.AWLWWMap, ckeys):
+    """read/2 on the device for the (key id, key) pairs: {key id: value id}."""
+    if state.rows.n == 0 or not ckeys:
+        return {}
+    kids = np.array(sorted(kid for kid, _ in ckeys), dtype=np.uint64)
+    kt = torch.from_numpy(np.ascontiguousarray(kids).view(np.int64)).to(M._dev())
+    ok, ov = M.engine().read_lww(state.rows, keys=kt)
+    return {int(k): int(v) for k, v in zip(u64(ok), u64(ov))}
 
 
 def apply_ops(state: M.AWLWWMap, ops, node_id):

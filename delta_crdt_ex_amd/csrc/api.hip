@@ -814,4 +814,22 @@ int dg_merkle_diff(dg_engine* e, const dg_merkle* a, const dg_merkle* b, uint64_
   return DG_OK;
 }
 
+int dg_remap_values(dg_engine* e, dg_store* s, const uint64_t* old_ids, const uint64_t* new_ids,
+                    uint64_t n_ids) {
+  if (!e) return fail(DG_E_INVAL, "null engine");
+  TRY(check_store(s, "dg_remap_values"));
+  if (n_ids && (!old_ids || !new_ids)) return fail(DG_E_INVAL, "dg_remap_values: null id table");
+  if (s->n == 0) return DG_OK;
+  TRY(set_device(e));
+  HIP_TRY(hipMemsetAsync(e->ticket + 3, 0, sizeof(u32), e->stream));
+  HIP_TRY(launch_remap_values(s->val, s->n, old_ids, new_ids, n_ids, e->ticket + 3, e->stream));
+  u32 bad = 0;
+  HIP_TRY(hipMemcpyAsync(&e->h_counts[11], e->ticket + 3, sizeof(u32), hipMemcpyDeviceToHost,
+                         e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  memcpy(&bad, &e->h_counts[11], sizeof(u32));
+  if (bad) return fail(DG_E_INVAL, "dg_remap_values: a row's value id is not in old_ids");
+  return DG_OK;
+}
+
 }  // extern "C"

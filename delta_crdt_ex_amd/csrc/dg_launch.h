@@ -145,6 +145,12 @@ hipError_t launch_merkle_leaves(const Rows& s, u32 depth, u64* leaf_key, u64* le
 // Sortedness check: sets *d_bad to nonzero if rows are not strictly ascending.
 hipError_t launch_store_check(const Rows& s, u32* d_bad, hipStream_t st);
 
+// ---- remap.hip (value ids after a host relabel)
+// val[i] <- new_ids[j] where old_ids[j] == val[i] (old_ids ascending); err bit 0 if a
+// value is not in old_ids.
+hipError_t launch_remap_values(u64* val, u64 n, const u64* old_ids, const u64* new_ids, u64 n_ids,
+                               u32* err, hipStream_t st);
+
 // ---- merkle.hip
 hipError_t launch_merkle_levels(u32 depth, const u64* leaf_hash, const u64* bucket_off,
                                 u64* nodes, hipStream_t st);

@@ -22,6 +22,7 @@ treats a missing map too).  A checksum mismatch raises.
 """
 from __future__ import annotations
 
+import os
 import struct
 
 import msgpack
@@ -87,12 +88,12 @@ def _unpack(x):
 
 
 def _universe_tables(U: interning.Universe):
+    ids, terms = U.value_ids()
     return {
         "keys": [[str(k), _pack(t)] for k, t in U._key_term.items()],
-        "vals": [[str(v), _pack(t)] for v, t in U._val_term.items()],
-        "nodes": [[n, _pack(t)] for n, t in U._node_term.items()],
-        "class_next": [[c, s] for c, s in U._class_next.items()],
-        "node_next": U._node_next,
+        "vals": [[str(v), _pack(t)] for v, t in zip(ids, terms)],   # ascending ids
+        "nodes": [_pack(t) for t in U._node_term],                  # dense ids 0..n-1
+        "val_epoch": U.val_epoch,
     }
 
 
@@ -102,16 +103,16 @@ def _universe_from(tables) -> interning.Universe:
         term = _unpack(t)
         U._key_term[int(k)] = term
         U._key_id[interning._hkey(term)] = int(k)
-    for v, t in tables["vals"]:
+    for v, t in tables["vals"]:  # ascending ids = term order: appends keep the lists sorted
         term = _unpack(t)
+        hk = interning._hkey(term)
         U._val_term[int(v)] = term
-        U._val_id[interning._hkey(term)] = int(v)
-    for n, t in tables["nodes"]:
-        term = _unpack(t)
-        U._node_term[int(n)] = term
-        U._node_id[interning._hkey(term)] = int(n)
-    U._class_next = {int(c): int(s) for c, s in tables["class_next"]}
-    U._node_next = int(tables["node_next"])
+        U._val_id[hk] = int(v)
+        U._val_keys.append(hk)
+        U._val_ids.append(int(v))
+    for t in tables["nodes"]:
+        U.node(_unpack(t))
+    U.val_epoch = int(tables.get("val_epoch", 0))
     return U
 
 
@@ -129,12 +130,17 @@ def write(path, node_id, sequence_number: int, state) -> None:
         "universe": _universe_tables(state.universe),
     }
     h = msgpack.packb(header, use_bin_type=True)
-    with open(path, "wb") as f:
+    # write-then-rename: a crash mid-write leaves the previous snapshot intact
+    tmp = f"{path}.tmp"
+    with open(tmp, "wb") as f:
         f.write(MAGIC)
         f.write(struct.pack("<Q", len(h)))
         f.write(h)
         for b in blobs:
             f.write(b)
+        f.flush()
+        os.fsync(f.fileno())
+    os.replace(tmp, path)
 
 
 def read(path, device=None):

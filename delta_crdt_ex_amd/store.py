@@ -478,6 +478,17 @@ class Engine:
                                       C.byref(n)))
         return out[: n.value]
 
+    # ---------------------------------------------------------------- interning
+    def remap_values(self, s: Store, old_ids: np.ndarray, new_ids: np.ndarray):
+        """Rewrite s.val in place after a value relabel (dg_remap_values): old_ids /
+        new_ids ascending uint64, the monotone map the Universe produced."""
+        self._order()
+        o = _np_to_dev(np.asarray(old_ids, np.uint64), np.int64, self.device)
+        w = _np_to_dev(np.asarray(new_ids, np.uint64), np.int64, self.device)
+        ss = s.abi()
+        check(self.lib.dg_remap_values(self.h, C.byref(ss), _ptr(o, _abi.P64), _ptr(w, _abi.P64),
+                                       int(len(old_ids))))
+
     def store_check(self, s: Store):
         self._order()
         ss = s.abi()

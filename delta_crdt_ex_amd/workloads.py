@@ -5,19 +5,61 @@ Every generator builds exactly the state the reference's mutators would reach
 `join(state, delta, [key])` as CausalCrdt does, causal_crdt.ex:337-342,383-384),
 but vectorised with numpy: keys/values are integers (as in
 bench/basic_operations.exs:4), key ids are splitmix64(k), value ids the
-order-preserving integer encoding, node ids u32, ts i64.  tests/ check the
-generators against the term-level oracle replaying the same operations.
+order-preserving integer encoding, ts i64.  Node ids are what the boundary's
+marshalling produces for REAL replica ids: every replica draws a 30-bit node id as
+CausalCrdt does (`:rand.uniform(1_000_000_000)`, causal_crdt.ex:65) and a Universe
+interns those terms to dense u32 ids (interning.py), so the kernels see the dense ids
+a NIF caller would hand them.  tests/ check the generators against the term-level
+oracle replaying the same operations with the 30-bit terms.
 
-A replica is a dict: {"rows": (key, val, ts, node, cnt) sorted, "ctx": (kind, node, cnt)}.
+A replica is a dict: {"rows": (key, val, ts, node, cnt) sorted, "ctx": (kind, node, cnt),
+"nodes": NodeTable}.
 """
 from __future__ import annotations
 
 import numpy as np
 
-from .interning import encode_int_value, splitmix64_np
+from .interning import Universe, encode_int_value, splitmix64_np
 from .sharding import shard_of
 
 VV, DOTS = 0, 1
+
+
+def node_terms(n: int, seed: int) -> np.ndarray:
+    """n distinct replica node ids as CausalCrdt draws them,
+    :rand.uniform(1_000_000_000) (1..1e9, 30 bits; causal_crdt.ex:65)."""
+    rng = np.random.default_rng([seed, 0x6E6F6465])
+    out: list[int] = []
+    seen: set[int] = set()
+    while len(out) < n:
+        for x in rng.integers(1, 1_000_000_001, n).tolist():
+            if x not in seen and len(out) < n:
+                seen.add(x)
+                out.append(x)
+    return np.array(out, np.int64)
+
+
+class NodeTable:
+    """Logical replica i of a workload has the 30-bit node term raw[i]; the rows and
+    contexts carry the dense id the boundary's interning gives that term
+    (Universe.node_ids over all of them: dense ids follow ascending term order)."""
+
+    def __init__(self, n: int, seed: int):
+        self.raw = node_terms(n, seed)
+        self.universe = Universe()
+        self.dense = self.universe.node_ids(self.raw).astype(np.uint32)
+
+    def __getitem__(self, logical) -> int:
+        return int(self.dense[logical])
+
+    def ids(self, logical: np.ndarray) -> np.ndarray:
+        return self.dense[np.asarray(logical, np.int64)]
+
+    def term_of_dense(self) -> dict:
+        return {int(d): int(r) for d, r in zip(self.dense, self.raw)}
+
+    def dense_of_term(self) -> dict:
+        return {int(r): int(d) for d, r in zip(self.dense, self.raw)}
 
 
 def sort_rows(k, v, t, n, c):
@@ -32,20 +74,21 @@ def vv(d: dict):
     return (VV, np.array([a for a, _ in items], np.uint32), np.array([b for _, b in items], np.uint64))
 
 
-def config1(n_keys: int = 10_000):
-    """Config 1 (bench/basic_operations.exs-style, CPU plumbing): node 1 adds
-    k => k for k = 1..n; B := A; A removes k % 10 == 0; B (node 2) re-adds
+def config1(n_keys: int = 10_000, nodes: NodeTable | None = None):
+    """Config 1 (bench/basic_operations.exs-style, CPU plumbing): replica 1 adds
+    k => k for k = 1..n; B := A; A removes k % 10 == 0; B (replica 2) re-adds
     k % 10 == 5 with v = k + 1.  Returns (A, B)."""
+    N = nodes or NodeTable(3, 1)
     k = np.arange(1, n_keys + 1, dtype=np.uint64)
     key = splitmix64_np(k)
     val = encode_int_value(k.astype(np.int64))
     ts = k.astype(np.int64) * 1000
-    node = np.full(n_keys, 1, np.uint32)
+    node = np.full(n_keys, N[1], np.uint32)
     cnt = k.copy()
     # A: removes k % 10 == 0 (remove/3 ctx = the removed dots; the VV absorbs them)
     keep_a = (k % 10) != 0
     A = {"rows": sort_rows(key[keep_a], val[keep_a], ts[keep_a], node[keep_a], cnt[keep_a]),
-         "ctx": vv({1: n_keys})}
+         "ctx": vv({N[1]: n_keys}), "nodes": N}
     # B: re-adds k % 10 == 5 with v = k + 1 as node 2, counters 1.. in key order
     re = (k % 10) == 5
     nre = int(re.sum())
@@ -55,18 +98,21 @@ def config1(n_keys: int = 10_000):
     cnt_b = cnt.copy()
     val_b[re] = encode_int_value(k[re].astype(np.int64) + 1)
     ts_b[re] = n_keys * 1000 + k[re].astype(np.int64)
-    node_b[re] = 2
+    node_b[re] = N[2]
     cnt_b[re] = np.arange(1, nre + 1, dtype=np.uint64)
-    B = {"rows": sort_rows(key, val_b, ts_b, node_b, cnt_b), "ctx": vv({1: n_keys, 2: nre})}
+    B = {"rows": sort_rows(key, val_b, ts_b, node_b, cnt_b), "ctx": vv({N[1]: n_keys, N[2]: nre}),
+         "nodes": N}
     return A, B
 
 
-def config2(n_keys: int = 1_000_000, seed: int = 2, key_lo: int = 1, keys=None):
-    """Config 2: base node 0 writes k = key_lo..key_lo+n-1 (counter = k,
-    ts = k * 1000); replicas A (node 1) and B (node 2) both overwrite the ~10 % of
+def config2(n_keys: int = 1_000_000, seed: int = 2, key_lo: int = 1, keys=None,
+            nodes: NodeTable | None = None):
+    """Config 2: base replica 0 writes k = key_lo..key_lo+n-1 (counter = k,
+    ts = k * 1000); replicas A (1) and B (2) both overwrite the ~10 % of
     keys with splitmix64(k ^ seed) % 10 == 0 with fresh random values, ts = base +
     U[0, 1e9).  `keys` (uint64 array of k) overrides the key range (sharding).
     Returns (A, B); N_in ~= 2 n, N_out ~= 1.1 n."""
+    N = nodes or NodeTable(3, 2)
     if keys is None:
         k = np.arange(key_lo, key_lo + n_keys, dtype=np.uint64)
     else:
@@ -86,14 +132,14 @@ def config2(n_keys: int = 1_000_000, seed: int = 2, key_lo: int = 1, keys=None):
         t_new = ts_base + rng.integers(0, 1_000_000_000, nc, dtype=np.int64)
         val_r = val.copy()
         ts_r = ts.copy()
-        node_r = np.zeros(n, np.uint32)
+        node_r = np.full(n, N[0], np.uint32)
         cnt_r = cnt0.copy()
         val_r[conflict] = encode_int_value(v_new)
         ts_r[conflict] = t_new
-        node_r[conflict] = node_id
+        node_r[conflict] = N[node_id]
         cnt_r[conflict] = np.arange(1, nc + 1, dtype=np.uint64)
         out.append({"rows": sort_rows(key, val_r, ts_r, node_r, cnt_r),
-                    "ctx": vv({0: int(k.max()) if n else 0, node_id: nc})})
+                    "ctx": vv({N[0]: int(k.max()) if n else 0, N[node_id]: nc}), "nodes": N})
     return out[0], out[1]
 
 
@@ -102,12 +148,15 @@ def config2_shard(rank: int, world: int, keys_per_rank: int = 1_000_000, seed: i
     range-sharded by key hash and rank `rank` builds its shard of A and B."""
     k = np.arange(1, world * keys_per_rank + 1, dtype=np.uint64)
     mine = shard_of(splitmix64_np(k), world) == rank
-    return config2(seed=seed, keys=k[mine])
+    return config2(seed=seed, keys=k[mine], nodes=NodeTable(3, 2))
 
 
-def merkle_pair(n_keys: int = 1_000_000, diff_frac: float = 0.01, seed: int = 4, keys=None):
-    """Config-4-shaped pair: two replicas of the same base that differ on ~diff_frac
-    of the keys (one side re-added them as node 2).  Returns (A, B)."""
+def merkle_pair(n_keys: int = 1_000_000, diff_frac: float = 0.01, seed: int = 4, keys=None,
+                nodes: NodeTable | None = None):
+    """Config-4-shaped pair: two replicas of the same base (written by replica 0) that
+    differ on ~diff_frac of the keys (one side re-added them as replica 2).  Returns
+    (A, B)."""
+    N = nodes or NodeTable(3, 4)
     if keys is None:
         k = np.arange(1, n_keys + 1, dtype=np.uint64)
     else:
@@ -116,18 +165,19 @@ def merkle_pair(n_keys: int = 1_000_000, diff_frac: float = 0.01, seed: int = 4,
     key = splitmix64_np(k)
     val = encode_int_value(k.astype(np.int64))
     ts = k.astype(np.int64) * 1000
-    node = np.zeros(n, np.uint32)
+    node = np.full(n, N[0], np.uint32)
     cnt = np.arange(1, n + 1, dtype=np.uint64)
-    A = {"rows": sort_rows(key, val, ts, node, cnt), "ctx": vv({0: n})}
+    A = {"rows": sort_rows(key, val, ts, node, cnt), "ctx": vv({N[0]: n}), "nodes": N}
     rng = np.random.default_rng(seed)
     d = rng.random(n) < diff_frac
     nd = int(d.sum())
     val_b, ts_b, node_b, cnt_b = val.copy(), ts.copy(), node.copy(), cnt.copy()
     val_b[d] = encode_int_value(rng.integers(0, 1 << 62, nd, dtype=np.int64))
     ts_b[d] = int(ts.max() if n else 0) + 1000 + rng.integers(0, 1_000_000_000, nd, dtype=np.int64)
-    node_b[d] = 2
+    node_b[d] = N[2]
     cnt_b[d] = np.arange(1, nd + 1, dtype=np.uint64)
-    B = {"rows": sort_rows(key, val_b, ts_b, node_b, cnt_b), "ctx": vv({0: n, 2: nd})}
+    B = {"rows": sort_rows(key, val_b, ts_b, node_b, cnt_b), "ctx": vv({N[0]: n, N[2]: nd}),
+         "nodes": N}
     return A, B
 
 
@@ -204,7 +254,7 @@ def _take_rows(rows, key_ids):
 
 
 def config3(n_keys: int = 10_000_000, n_replicas: int = 64, touch: float = 0.01,
-            remove_frac: float = 0.2, seed: int = 3):
+            remove_frac: float = 0.2, seed: int = 3, nodes: NodeTable | None = None):
     """Config 3: a base state (node 0 wrote k = 1..n, counter k, ts = k * 1000) and
     `n_replicas` replicas (nodes 1..R) that each touched ~touch * n keys of it: 80 %
     re-added (AWLWWMap.add/4: the key's old entries go, one new entry with dot
@@ -215,11 +265,12 @@ def config3(n_keys: int = 10_000_000, n_replicas: int = 64, touch: float = 0.01,
     Returns (base, deltas) where base = {"rows", "ctx"} and each delta =
     {"rows", "ctx", "keys"} (keys: ascending unique key ids).  Applying them is the
     fold join(state, delta_r, keys_r) over r = 1..R (causal_crdt.ex:383-384)."""
+    N = nodes or NodeTable(n_replicas + 1, seed)
     k = np.arange(1, n_keys + 1, dtype=np.uint64)
     key = splitmix64_np(k)
     base = {"rows": sort_rows(key, encode_int_value(k.astype(np.int64)),
-                              k.astype(np.int64) * 1000, np.zeros(n_keys, np.uint32), k.copy()),
-            "ctx": vv({0: n_keys})}
+                              k.astype(np.int64) * 1000, np.full(n_keys, N[0], np.uint32), k.copy()),
+            "ctx": vv({N[0]: n_keys}), "nodes": N}
     rng = np.random.default_rng(seed)
     ts_base = n_keys * 1000 + 1000
     m = max(1, int(round(touch * n_keys)))
@@ -233,9 +284,9 @@ def config3(n_keys: int = 10_000_000, n_replicas: int = 64, touch: float = 0.01,
         na = int(added.sum())
         vals = encode_int_value(rng.integers(0, 1 << 62, na, dtype=np.int64))
         ts = ts_base + rng.integers(0, 1_000_000_000, na, dtype=np.int64)
-        rows = sort_rows(kid[added], vals, ts, np.full(na, r, np.uint32),
+        rows = sort_rows(kid[added], vals, ts, np.full(na, N[r], np.uint32),
                          np.arange(1, na + 1, dtype=np.uint64))
-        deltas.append({"rows": rows, "ctx": vv({0: n_keys, r: na}), "keys": kid})
+        deltas.append({"rows": rows, "ctx": vv({N[0]: n_keys, N[r]: na}), "keys": kid, "nodes": N})
     return base, deltas
 
 
@@ -245,7 +296,7 @@ def config4_shard(rank: int, world: int, keys_per_rank: int = 12_500_000,
     space of two replicas that differ on ~diff_frac of the keys (merkle_pair)."""
     k = np.arange(1, world * keys_per_rank + 1, dtype=np.uint64)
     mine = shard_of(splitmix64_np(k), world) == rank
-    return merkle_pair(keys=k[mine], diff_frac=diff_frac, seed=seed + rank)
+    return merkle_pair(keys=k[mine], diff_frac=diff_frac, seed=seed + rank, nodes=NodeTable(3, seed))
 
 
 def sync_delta(rep, keys):
@@ -256,7 +307,8 @@ def sync_delta(rep, keys):
 
 
 def config5(n_keys: int = 100_000_000, n_nodes: int = 64, remove_frac: float = 0.5,
-            readd_frac: float = 0.2, ts_range: int = 16, max_entries: int = 3, seed: int = 5):
+            readd_frac: float = 0.2, ts_range: int = 16, max_entries: int = 3, seed: int = 5,
+            nodes: NodeTable | None = None):
     """Config 5, remove-heavy adversarial pair.  Base: every key holds 1..max_entries
     concurrent entries written by random nodes 0..n_nodes-3 (dots {node, c}, c
     counting per node in key order), small values and ts in [0, ts_range) so LWW ties
@@ -264,6 +316,7 @@ def config5(n_keys: int = 100_000_000, n_nodes: int = 64, remove_frac: float = 0
     whole base (dense VVs: they cover every dot they hold) and then independently
     removed `remove_frac` of the keys and re-added (add/4: the key's entries replaced
     by one new entry) `readd_frac` of the rest.  Returns (A, B)."""
+    N = nodes or NodeTable(n_nodes, seed)
     rng = np.random.default_rng(seed)
     k = np.arange(1, n_keys + 1, dtype=np.uint64)
     key = splitmix64_np(k)
@@ -276,7 +329,7 @@ def config5(n_keys: int = 100_000_000, n_nodes: int = 64, remove_frac: float = 0
     first = np.r_[0, np.cumsum(ne)[:-1]]
     j = np.arange(E) - np.repeat(first, ne)
     h = rng.integers(0, n_nodes - 2, n_keys)
-    enode = ((h[kidx] + j) % (n_nodes - 2)).astype(np.uint32)
+    enode = ((h[kidx] + j) % (n_nodes - 2)).astype(np.uint32)  # logical writer
     # counters per node in generation order (key index, then entry)
     order = np.argsort(enode, kind="stable")
     cnt = np.empty(E, np.uint64)
@@ -288,7 +341,8 @@ def config5(n_keys: int = 100_000_000, n_nodes: int = 64, remove_frac: float = 0
     ets = rng.integers(0, ts_range, E).astype(np.int64)
     base_vv = {}
     for nd, c in zip(*np.unique(enode, return_counts=True)):
-        base_vv[int(nd)] = int(c)
+        base_vv[N[int(nd)]] = int(c)
+    enode = N.ids(enode).astype(np.uint32)  # the interned (dense) ids of the writers
     reps = []
     for node_id in (n_nodes - 2, n_nodes - 1):
         removed = rng.random(n_keys) < remove_frac
@@ -300,7 +354,7 @@ def config5(n_keys: int = 100_000_000, n_nodes: int = 64, remove_frac: float = 0
         at = rng.integers(0, ts_range, na).astype(np.int64)
         rows = sort_rows(np.concatenate([ekey[keep_e], ak]), np.concatenate([eval_[keep_e], av]),
                          np.concatenate([ets[keep_e], at]),
-                         np.concatenate([enode[keep_e], np.full(na, node_id, np.uint32)]),
+                         np.concatenate([enode[keep_e], np.full(na, N[node_id], np.uint32)]),
                          np.concatenate([cnt[keep_e], np.arange(1, na + 1, dtype=np.uint64)]))
-        reps.append({"rows": rows, "ctx": vv({**base_vv, node_id: na})})
+        reps.append({"rows": rows, "ctx": vv({**base_vv, N[node_id]: na}), "nodes": N})
     return reps[0], reps[1]

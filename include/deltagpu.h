@@ -213,6 +213,16 @@ int dg_compress_dots(dg_engine* e, const dg_context* dots, dg_context* out_vv);
 int dg_read_lww(dg_engine* e, const dg_store* s, const uint64_t* keys, uint64_t n_keys,
                 uint64_t* out_key, uint64_t* out_val, uint64_t cap, uint64_t* n_out);
 
+/* ---- interning maintenance -------------------------------------------------- */
+/* Value ids are order-preserving ranks in Erlang term order with gaps (the read
+ * tie-break, aw_lww_map.ex:211-216).  When the host's value table runs out of room
+ * between two neighbours it re-spaces every id (a strictly increasing map); this
+ * rewrites s->val in place: val = new_ids[j] where old_ids[j] == val.  old_ids /
+ * new_ids: device arrays of n_ids entries, both ascending.  The store stays sorted.
+ * DG_E_INVAL if a row's value is not in old_ids.  Synchronous. */
+int dg_remap_values(dg_engine* e, dg_store* s, const uint64_t* old_ids, const uint64_t* new_ids,
+                    uint64_t n_ids);
+
 /* ---- Merkle anti-entropy (MerkleMap role) --------------------------------- */
 /* Build leaves + level-wise bucket hashes for `s` (MerkleMap.put/update_hashes,
  * causal_crdt.ex:94,254,390-394).  t->depth and capacities set by the caller. */

@@ -38,6 +38,9 @@ def ctx_arrays(dots, U: Universe):
 
 
 def state_to_soa(state: T.AW, U: Universe):
+    for entries in state.value.values():  # intern every value first (a relabel re-spaces ids)
+        for (val, _t) in entries:
+            U.value(val)
     ks, vs, ts, ns, cs = [], [], [], [], []
     for key, entries in state.value.items():
         kid = U.key(key)
@@ -51,6 +54,31 @@ def state_to_soa(state: T.AW, U: Universe):
                 cs.append(c)
     rows = sort_rows(ks, vs, ts, ns, cs)
     return rows, ctx_arrays(state.dots, U)
+
+
+def state_to_soa_ints(state: T.AW, nodes):
+    """A term state whose keys and values are integers -> SoA rows in the synthetic
+    workloads' id space (key = splitmix64(k), val = encode_int_value(v)) with node
+    terms interned through `nodes` (a workloads.NodeTable: 30-bit term -> dense id)."""
+    from delta_crdt_ex_amd.interning import encode_int_value, splitmix64
+    dense = nodes.dense_of_term()
+    ks, vs, ts, ns, cs = [], [], [], [], []
+    for key, entries in state.value.items():
+        for (val, t), dots in entries.items():
+            for (nd, c) in dots:
+                ks.append(splitmix64(key))
+                vs.append(int(encode_int_value(val)))
+                ts.append(t)
+                ns.append(dense[nd])
+                cs.append(c)
+    rows = sort_rows(ks, vs, ts, ns, cs)
+    d = state.dots
+    if isinstance(d, (frozenset, set)):
+        pairs, kind = sorted((dense[nd], c) for (nd, c) in d), DOTS
+    else:
+        pairs, kind = sorted((dense[nd], c) for nd, c in d.items()), VV
+    return rows, (kind, np.array([p[0] for p in pairs], np.uint32),
+                  np.array([p[1] for p in pairs], np.uint64))
 
 
 def soa_canon(rows, ctx, U: Universe):

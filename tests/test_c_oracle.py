@@ -147,55 +147,54 @@ def test_merkle_diff_is_exact_store_diff(seed):
 
 def test_config1_generator_matches_term_replay():
     n = 200
-    U = Universe()
-    clock = iter(range(10**9))
-    # node 1 adds k => k with ts = k * 1000
+    ga, gb = W.config1(n)
+    N = ga["nodes"]
+    n1, n2 = int(N.raw[1]), int(N.raw[2])  # the replicas' 30-bit node terms
+    # replica 1 adds k => k with ts = k * 1000
     A = T.compress_dots(T.new())
     for k in range(1, n + 1):
-        A = T.join(A, T.add(k, k, 1, A, k * 1000), [k])
+        A = T.join(A, T.add(k, k, n1, A, k * 1000), [k])
     B = A
     for k in range(1, n + 1):
         if k % 10 == 0:
-            A = T.join(A, T.remove(k, 1, A), [k])
+            A = T.join(A, T.remove(k, n1, A), [k])
     for k in range(1, n + 1):
         if k % 10 == 5:
-            B = T.join(B, T.add(k, k + 1, 2, B, n * 1000 + k), [k])
-    ga, gb = W.config1(n)
+            B = T.join(B, T.add(k, k + 1, n2, B, n * 1000 + k), [k])
     for term_state, gen in ((A, ga), (B, gb)):
-        rows, ctx = CV.state_to_soa(term_state, U)
+        rows, ctx = CV.state_to_soa_ints(term_state, N)
         assert rows_equal(rows, gen["rows"])
         assert ctx_equal(ctx, gen["ctx"])
     # and the config-1 join (CPU path) agrees across the two oracles
     rows, ctx = R.join2(ga["rows"], ga["ctx"], gb["rows"], gb["ctx"])
     want = T.join(A, B, sorted(set(A.value) | set(B.value)))
-    wrows, wctx = CV.state_to_soa(want, U)
+    wrows, wctx = CV.state_to_soa_ints(want, N)
     assert rows_equal(rows, wrows) and ctx_equal(ctx, wctx)
     ok, ov = R.read_lww(rows)
-    got = {U.key_term(int(k)): U.value_term(int(v)) for k, v in zip(ok, ov)}
+    kterm = {splitmix64(k): k for k in range(1, n + 1)}
+    got = {kterm[int(k)]: int(v) - (1 << 62) for k, v in zip(ok, ov)}
     assert got == T.read(want)
-    del clock
 
 
 def test_config2_generator_matches_term_replay():
     n = 300
-    U = Universe()
     ga, gb = W.config2(n_keys=n, seed=5)
+    N = ga["nodes"]
     base = T.compress_dots(T.new())
     for k in range(1, n + 1):
-        base = T.join(base, T.add(k, k, 0, base, k * 1000), [k])
+        base = T.join(base, T.add(k, k, int(N.raw[0]), base, k * 1000), [k])
+    kterm = {splitmix64(k): k for k in range(1, n + 1)}
     # recover the generator's choices (which keys, which values/ts) from its rows
-    for node_id, gen in ((1, ga), (2, gb)):
+    for logical, gen in ((1, ga), (2, gb)):
         k, v, t, nd, c = gen["rows"]
-        mine = nd == node_id
+        mine = nd == N[logical]
         order = np.argsort(c[mine])
         st = base
         for kid, vid, ts in zip(k[mine][order], v[mine][order], t[mine][order]):
-            key = U.key_term(int(kid)) if int(kid) in U._key_term else None
-            if key is None:
-                key = next(x for x in range(1, n + 1) if splitmix64(x) == int(kid))
+            key = kterm[int(kid)]
             val = int(vid) - (1 << 62)
-            st = T.join(st, T.add(key, val, node_id, st, int(ts)), [key])
-        rows, ctx = CV.state_to_soa(st, U)
+            st = T.join(st, T.add(key, val, int(N.raw[logical]), st, int(ts)), [key])
+        rows, ctx = CV.state_to_soa_ints(st, N)
         assert rows_equal(rows, gen["rows"])
         assert ctx_equal(ctx, gen["ctx"])
 

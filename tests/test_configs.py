@@ -13,11 +13,12 @@ from oracle import ref as R
 from test_c_oracle import ctx_equal, rows_equal, soa_to_term, term_to_soa_raw
 
 
-def _base_term(n):
-    """Node 0 adds k => k with ts = k * 1000 for k = 1..n (config 2/3 base)."""
+def _base_term(n, node=0):
+    """Replica `node` (a node term) adds k => k with ts = k * 1000 for k = 1..n (config
+    2/3 base)."""
     st = T.compress_dots(T.new())
     for k in range(1, n + 1):
-        st = T.join(st, T.add(k, k, 0, st, k * 1000), [k])
+        st = T.join(st, T.add(k, k, node, st, k * 1000), [k])
     return st
 
 
@@ -29,11 +30,12 @@ def _take(state, keys):
 
 def test_config3_generator_matches_term_replay():
     n, R_ = 150, 3
-    U = Universe()
     base, deltas = W.config3(n_keys=n, n_replicas=R_, touch=0.12, seed=11)
+    N = base["nodes"]
+    assert all(1 <= x <= 1_000_000_000 for x in N.raw.tolist())  # :rand.uniform(1e9) terms
     kterm = {splitmix64(k): k for k in range(1, n + 1)}
-    st0 = _base_term(n)
-    rows, ctx = CV.state_to_soa(st0, U)
+    st0 = _base_term(n, int(N.raw[0]))
+    rows, ctx = CV.state_to_soa_ints(st0, N)
     assert rows_equal(rows, base["rows"]) and ctx_equal(ctx, base["ctx"])
     for r, d in enumerate(deltas, start=1):
         keys = [kterm[int(x)] for x in d["keys"]]
@@ -42,12 +44,12 @@ def test_config3_generator_matches_term_replay():
         st = st0
         # adds in counter order (next_dot numbers them), removes anywhere
         for key, (val, ts, _c) in sorted(adds.items(), key=lambda kv: kv[1][2]):
-            st = T.join(st, T.add(key, val, r, st, ts), [key])
+            st = T.join(st, T.add(key, val, int(N.raw[r]), st, ts), [key])
         for key in keys:
             if key not in adds:
-                st = T.join(st, T.remove(key, r, st), [key])
+                st = T.join(st, T.remove(key, int(N.raw[r]), st), [key])
         delta = _take(st, set(keys))
-        drows, dctx = CV.state_to_soa(delta, U)
+        drows, dctx = CV.state_to_soa_ints(delta, N)
         assert rows_equal(drows, d["rows"]), r
         assert ctx_equal(dctx, d["ctx"]), r
 
@@ -65,7 +67,7 @@ def test_config3_keyed_fold_two_oracles(seed):
     assert rows_equal(rows, wrows) and ctx_equal(ctx, wctx)
     # every touched key: the base row is gone; added keys carry their new rows
     touched = np.unique(np.concatenate([d["keys"] for d in deltas]))
-    assert not np.any(np.isin(rows[0][rows[3] == 0], touched))
+    assert not np.any(np.isin(rows[0][rows[3] == base["nodes"][0]], touched))
 
 
 def test_config3_keys_outside_keyset_are_right_biased():
@@ -85,8 +87,8 @@ def test_config3_keys_outside_keyset_are_right_biased():
 
 def test_config5_generator_matches_term_replay():
     n, nn = 50, 8
-    U = Universe()
     a, b = W.config5(n_keys=n, n_nodes=nn, seed=3)
+    N = a["nodes"]
     # the base: every writer node's own adds (the generator's draws, replayed in its
     # order), joined -- concurrent entries of one key survive
     rng = np.random.default_rng(3)
@@ -112,7 +114,7 @@ def test_config5_generator_matches_term_replay():
         st = T.compress_dots(T.new())
         for e in es:
             key = int(kidx[e]) + 1
-            st = T.join(st, T.add(key, int(evals[e]), nd, st, int(ets[e])), [key])
+            st = T.join(st, T.add(key, int(evals[e]), int(N.raw[nd]), st, int(ets[e])), [key])
         base = T.join(base, st, sorted(set(base.value) | set(st.value)))
     for node_id, gen in ((nn - 2, a), (nn - 1, b)):
         removed = rng.random(n) < 0.5
@@ -123,11 +125,11 @@ def test_config5_generator_matches_term_replay():
         st = base
         for j, kk in enumerate(np.flatnonzero(readd)):
             key = int(kk) + 1
-            st = T.join(st, T.add(key, int(av[j]), node_id, st, int(at[j])), [key])
+            st = T.join(st, T.add(key, int(av[j]), int(N.raw[node_id]), st, int(at[j])), [key])
         for kk in np.flatnonzero(removed):
             key = int(kk) + 1
-            st = T.join(st, T.remove(key, node_id, st), [key])
-        rows, ctx = CV.state_to_soa(st, U)
+            st = T.join(st, T.remove(key, int(N.raw[node_id]), st), [key])
+        rows, ctx = CV.state_to_soa_ints(st, N)
         assert rows_equal(rows, gen["rows"]), node_id
         assert ctx_equal(ctx, gen["ctx"]), node_id
 
