@@ -105,29 +105,103 @@ def cpu_baseline(a, b, budget_s=6.0):
     }
 
 
-def merkle_rate(eng, torch, dev, steps=20):
+def config4_round(eng, torch, dev, rank=0, world=1, keys_per_rank=12_500_000, steps=10,
+                  max_sync_size=None):
+    """BASELINE config 4 on this rank's key-hash shard (12.5M keys per GPU: 100M over 8):
+    two replicas differing on 1 % of the keys.  Measures
+      * build: dg_merkle_build_async of both replicas' shard trees (MerkleMap over every
+        key), HIP events on the engine stream around `steps` builds -> the roofline of
+        the build kernels (36 B/row read + the bucket level written, read by the upsweep
+        and the upper levels written: 24 B/bucket);
+      * the anti-entropy round as CausalCrdt runs it (causal_crdt.ex:91-123,324-335,
+        383-394), each a synchronous call: Merkle diff (keys, truncated to
+        max_sync_size), the sync delta Map.take(B.value, keys) (dg_take_keys), the
+        keyed join with its changed keys (dg_join2_changes), and the MerkleMap
+        put/delete + update_hashes of those keys (dg_merkle_update, incremental);
+      * at world > 1: the shard roots all-gathered and folded (== the unsharded root)
+        and the VV all-reduce(max), over RCCL."""
+    import torch.distributed as dist
+
+    from delta_crdt_ex_amd import sharding as S
     from delta_crdt_ex_amd import workloads as W
-    from delta_crdt_ex_amd.store import Store
-    a, b = W.merkle_pair(n_keys=KEYS_PER_GPU, diff_frac=0.01, seed=4)
-    sa = Store.from_numpy(*a["rows"], device=dev)
-    sb = Store.from_numpy(*b["rows"], device=dev)
-    depth = 18
-    ta = eng.merkle_build(sa, depth)
-    tb = eng.merkle_build(sb, depth)
-    d = eng.merkle_diff(ta, tb)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
+    from delta_crdt_ex_amd.store import Context, MerkleTree, Store
+    a, b = W.config4_shard(rank, max(world, 1), keys_per_rank=keys_per_rank, diff_frac=0.01)
+    sa, sb = Store.from_numpy(*a["rows"], device=dev), Store.from_numpy(*b["rows"], device=dev)
+    ca, cb = Context.from_numpy(*a["ctx"], dev), Context.from_numpy(*b["ctx"], dev)
+    sbits = S.shard_bits(world) if world > 1 else 0
+    n_keys = len(a["rows"][0])
+    depth = max(8, min(28, int(np.ceil(np.log2(max(n_keys, 2) / 3)))))  # ~3 keys per bucket
+    ta = MerkleTree.empty(depth, dev, sbits, rank if sbits else 0)
+    tb = MerkleTree.empty(depth, dev, sbits, rank if sbits else 0)
+    dk = torch.zeros(8, dtype=torch.int64, device=dev)
+    la, lb = eng.prepare_merkle_build(sa, ta, dk[0:1]), eng.prepare_merkle_build(sb, tb, dk[1:2])
+    la(), lb()
+    eng.sync()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(eng.stream)
     for _ in range(steps):
-        eng.merkle_build(sa, depth, ta)
-        eng.merkle_build(sb, depth, tb)
-        d = eng.merkle_diff(ta, tb)
-    torch.cuda.synchronize()
-    el = (time.perf_counter() - t0) / steps
-    keys = ta.n_keys + tb.n_keys
-    return {"metric": "Merkle hash+diff keys/s (config-4 shape, 1 GPU shard)",
-            "value": keys / el, "unit": "keys/s", "ms_per_round": el * 1e3,
-            "keys": keys, "differing_keys": int(d.numel()), "depth": depth,
-            "note": "two builds + one diff per round, synchronous API (includes host syncs)"}
+        la()
+        lb()
+    ev1.record(eng.stream)
+    eng.sync()
+    build_us = ev0.elapsed_time(ev1) * 1e3 / (2 * steps)
+    rows = (sa.n + sb.n) / 2
+    nb = 1 << depth
+    build_alg = 36 * rows + 24 * nb
+    eng.merkle_build(sa, depth, ta, sbits, rank if sbits else 0)  # n_keys, shard check
+    eng.merkle_build(sb, depth, tb, sbits, rank if sbits else 0)
+    cap = max_sync_size or (ta.n_keys + tb.n_keys)
+
+    def one_round():
+        t = {}
+        t0 = time.perf_counter()
+        keys, total = eng.merkle_diff(ta, tb, cap=cap, with_total=True)
+        t1 = time.perf_counter()
+        delta = eng.take_keys(sb, keys)
+        t2 = time.perf_counter()
+        out, octx, changed = eng.join2_changes(sa, ca, delta, cb, keys=keys)
+        t3 = time.perf_counter()
+        tt = MerkleTree(ta.depth, ta.nodes.clone(), ta.n_keys, ta.shard_bits, ta.shard, sa)
+        t4 = time.perf_counter()
+        eng.merkle_update(tt, out, changed)
+        torch.cuda.synchronize()
+        t5 = time.perf_counter()
+        t.update(diff=t1 - t0, take=t2 - t1, join=t3 - t2, update=t5 - t4, total=(t5 - t4) + (t3 - t0),
+                 keys=int(keys.numel()), total_keys=total, rows=delta.n, changed=int(changed.numel()))
+        t["ok"] = tt.root() == eng.merkle_build(out, depth, None, sbits, rank if sbits else 0).root()
+        return t
+
+    one_round()
+    rounds = [one_round() for _ in range(5)]
+    med = {k: float(np.median([r[k] for r in rounds])) for k in ("diff", "take", "join", "update", "total")}
+    last = rounds[-1]
+    res = {
+        "metric": "Merkle diff keys/s, config 4 (key-hash shard of 100M keys, 1 % differing)",
+        "keys_per_gpu": n_keys, "depth": depth, "shard_bits": sbits,
+        "value": 2 * n_keys / (2 * build_us * 1e-6 + med["diff"]), "unit": "keys/s",
+        "note": "value = keys of both replicas / (hash both: two full builds + the diff)",
+        "build_us": build_us,
+        "roofline": {"bound": "hbm", "kernel": "merkle_build_kernel + merkle_upsweep_kernel",
+                     "alg_bytes_per_launch": build_alg, "avg_launch_us": build_us,
+                     "achieved": build_alg / (build_us * 1e-6) / 1e9, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s",
+                     "frac": build_alg / (build_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                     "launch_timing": "HIP events on the engine stream around the async builds"},
+        "round_us": {k: v * 1e6 for k, v in med.items()},
+        "round_keys": last["keys"], "round_total_keys": last["total_keys"],
+        "round_delta_rows": last["rows"], "round_changed_keys": last["changed"],
+        "update_equals_rebuild": all(r["ok"] for r in rounds),
+        "round_note": "synchronous calls: merkle_diff -> take_keys -> join2_changes (keyed) -> "
+                      "merkle_update (incremental put/delete + update_hashes of the changed keys)",
+    }
+    if world > 1:
+        t0 = time.perf_counter()
+        roots_a, root_a = S.merkle_roots(ta.root())
+        node, cnt = ca.to_numpy()
+        S.vv_allreduce_max(node, cnt)
+        res["collectives_us"] = (time.perf_counter() - t0) * 1e6
+        res["replica_root"] = hex(root_a)
+    return res
 
 
 def _timed(torch, fn, reps):
@@ -406,8 +480,11 @@ def main():
                 "per_step_event_median_us": step_event_median_us,
             },
         }
-        if not args.no_merkle:
-            res["merkle"] = merkle_rate(eng, torch, dev)
+    if not args.no_merkle:  # every rank runs its shard's round; rank 0 reports its own
+        c4 = config4_round(eng, torch, dev, rank, world)
+        if rank == 0:
+            res["merkle"] = c4
+    if rank == 0:
         if not args.no_configs and world == 1:  # per-GPU secondaries: measured at N=1
             res["changes"] = changes_rate(eng, torch, pairs[0])
             for r in pairs:  # free the config-2 replicas before the larger configs

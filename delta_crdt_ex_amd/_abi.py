@@ -56,13 +56,24 @@ class dg_context(C.Structure):
 class dg_merkle(C.Structure):
     _fields_ = [
         ("depth", C.c_uint32),
-        ("reserved", C.c_uint32),
+        ("shard_bits", C.c_uint32),
+        ("shard", C.c_uint64),
         ("nodes", P64),
-        ("bucket_off", P64),
-        ("leaf_key", P64),
-        ("leaf_hash", P64),
         ("n_keys", C.c_uint64),
-        ("cap_keys", C.c_uint64),
+    ]
+
+
+class dg_merkle_cont(C.Structure):
+    _fields_ = [
+        ("level", C.c_uint32),
+        ("reserved", C.c_uint32),
+        ("pos", P64),
+        ("hash", P64),
+        ("n", C.c_uint64),
+        ("cap", C.c_uint64),
+        ("bucket", P64),
+        ("n_buckets", C.c_uint64),
+        ("cap_buckets", C.c_uint64),
     ]
 
 
@@ -117,8 +128,22 @@ _SIGS = {
                               C.c_uint64, P64]),
     "dg_remap_values": (C.c_int, [C.c_void_p, C.POINTER(dg_store), P64, P64, C.c_uint64]),
     "dg_merkle_build": (C.c_int, [C.c_void_p, C.POINTER(dg_store), C.POINTER(dg_merkle)]),
-    "dg_merkle_diff": (C.c_int, [C.c_void_p, C.POINTER(dg_merkle), C.POINTER(dg_merkle), P64,
-                                 C.c_uint64, P64]),
+    "dg_merkle_build_async": (C.c_int, [C.c_void_p, C.POINTER(dg_store), C.POINTER(dg_merkle),
+                                        P64]),
+    "dg_merkle_update": (C.c_int, [C.c_void_p, C.POINTER(dg_merkle), C.POINTER(dg_store),
+                                   C.POINTER(dg_store), P64, C.c_uint64]),
+    "dg_merkle_diff": (C.c_int, [C.c_void_p, C.POINTER(dg_merkle), C.POINTER(dg_store),
+                                 C.POINTER(dg_merkle), C.POINTER(dg_store), P64, C.c_uint64, P64,
+                                 P64]),
+    "dg_merkle_prepare": (C.c_int, [C.c_void_p, C.POINTER(dg_merkle), C.c_uint32,
+                                    C.POINTER(dg_merkle_cont)]),
+    "dg_merkle_continue": (C.c_int, [C.c_void_p, C.POINTER(dg_merkle), C.POINTER(dg_store),
+                                     C.POINTER(dg_merkle_cont), C.c_uint32,
+                                     C.POINTER(dg_merkle_cont), P64, C.c_uint64, P64, P64,
+                                     C.POINTER(C.c_int)]),
+    "dg_merkle_truncate": (C.c_int, [C.c_void_p, C.POINTER(dg_merkle), C.POINTER(dg_merkle_cont),
+                                     C.c_uint64]),
+    "dg_merkle_fold_roots": (C.c_int, [P64, C.c_uint32, P64]),
 }
 
 

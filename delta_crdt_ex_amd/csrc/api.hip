@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/deltagpu.h"
+#include "dg_hash.h"
 #include "dg_launch.h"
 
 using namespace dg;
@@ -777,40 +778,232 @@ int dg_read_lww(dg_engine* e, const dg_store* s, const uint64_t* keys, uint64_t 
   return DG_OK;
 }
 
-int dg_merkle_build(dg_engine* e, const dg_store* s, dg_merkle* t) {
+}  // extern "C"
+
+namespace {
+
+MerkleT merkle_of(const dg_merkle* t) {
+  MerkleT m;
+  m.depth = t->depth;
+  m.sb = t->shard_bits;
+  m.shard = t->shard;
+  m.nodes = t->nodes;
+  return m;
+}
+
+int check_merkle(const dg_merkle* t, const char* what) {
+  if (!t || !t->nodes) return fail(DG_E_INVAL, "%s: null tree", what);
+  if (t->depth < 1 || t->depth > 28) return fail(DG_E_INVAL, "%s: depth %u not in 1..28", what, t->depth);
+  if (t->shard_bits > 16 || t->depth + t->shard_bits > 44)
+    return fail(DG_E_INVAL, "%s: shard_bits %u (depth %u)", what, t->shard_bits, t->depth);
+  if (t->shard_bits ? (t->shard >> t->shard_bits) != 0 : t->shard != 0)
+    return fail(DG_E_INVAL, "%s: shard %llu >= 2^%u", what, (unsigned long long)t->shard, t->shard_bits);
+  return DG_OK;
+}
+
+int same_tree_shape(const dg_merkle* a, const dg_merkle* b, const char* what) {
+  if (a->depth != b->depth || a->shard_bits != b->shard_bits || a->shard != b->shard)
+    return fail(DG_E_INVAL, "%s: trees of different shape (depth %u/%u, shard %llu/%llu)", what,
+                a->depth, b->depth, (unsigned long long)a->shard, (unsigned long long)b->shard);
+  return DG_OK;
+}
+
+// The input-error word (ticket[3]) after a synchronizing read; bit 1: key outside shard.
+int input_error(dg_engine* e, const char* what) {
+  u32 bad = 0;
+  HIP_TRY(hipMemcpyAsync(&e->h_counts[11], e->ticket + 3, sizeof(u32), hipMemcpyDeviceToHost,
+                         e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  memcpy(&bad, &e->h_counts[11], sizeof(u32));
+  if (bad & 2u) return fail(DG_E_INVAL, "%s: a key outside the tree's shard", what);
+  return DG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dg_merkle_build_async(dg_engine* e, const dg_store* s, dg_merkle* t, uint64_t* d_n_keys) {
   if (!e) return fail(DG_E_INVAL, "null engine");
   TRY(check_store(s, "dg_merkle_build"));
-  if (!t || !t->nodes || !t->bucket_off || (s->n && (!t->leaf_key || !t->leaf_hash)))
-    return fail(DG_E_INVAL, "dg_merkle_build: null tree array");
-  if (t->depth < 1 || t->depth > 26) return fail(DG_E_INVAL, "dg_merkle_build: depth %u", t->depth);
-  if (t->cap_keys < s->n) return fail(DG_E_CAPACITY, "dg_merkle_build: cap_keys < rows");
+  TRY(check_merkle(t, "dg_merkle_build"));
+  if (!d_n_keys) return fail(DG_E_INVAL, "dg_merkle_build: null d_n_keys");
   TRY(set_device(e));
-  TRY(ensure_state(e, 2 * seg_tiles(s->n) + 2));  // raw per-tile counts and offsets
-  HIP_TRY(launch_merkle_leaves(rows_of(s), t->depth, t->leaf_key, t->leaf_hash, t->bucket_off,
-                               e->state, e->d_counts, e->stream));
-  HIP_TRY(launch_merkle_levels(t->depth, t->leaf_hash, t->bucket_off, t->nodes, e->stream));
+  HIP_TRY(hipMemsetAsync(e->ticket + 3, 0, sizeof(u32), e->stream));
+  HIP_TRY(launch_merkle_build(rows_of(s), merkle_of(t), d_n_keys, e->ticket, e->ticket + 3,
+                              e->stream));
+  return DG_OK;
+}
+
+int dg_merkle_build(dg_engine* e, const dg_store* s, dg_merkle* t) {
+  TRY(dg_merkle_build_async(e, s, t, e ? e->d_counts : nullptr));
   TRY(read_counts(e, 1));
+  TRY(input_error(e, "dg_merkle_build"));
   t->n_keys = e->h_counts[0];
   return DG_OK;
 }
 
-int dg_merkle_diff(dg_engine* e, const dg_merkle* a, const dg_merkle* b, uint64_t* out_keys,
-                   uint64_t cap, uint64_t* n_out) {
+int dg_merkle_update(dg_engine* e, dg_merkle* t, const dg_store* old_s, const dg_store* new_s,
+                     const uint64_t* keys, uint64_t n_keys) {
   if (!e) return fail(DG_E_INVAL, "null engine");
-  if (!a || !b || !n_out) return fail(DG_E_INVAL, "dg_merkle_diff: null argument");
-  if (a->depth != b->depth) return fail(DG_E_INVAL, "dg_merkle_diff: depth %u != %u", a->depth, b->depth);
-  if (a->depth < 1 || a->depth > 26) return fail(DG_E_INVAL, "dg_merkle_diff: depth %u", a->depth);
+  TRY(check_merkle(t, "dg_merkle_update"));
+  TRY(check_store(old_s, "dg_merkle_update old"));
+  TRY(check_store(new_s, "dg_merkle_update new"));
+  if (n_keys && !keys) return fail(DG_E_INVAL, "dg_merkle_update: null keys");
+  TRY(set_device(e));
+  const u64 chunks = merkle_chunks(t->depth);
+  TRY(ensure_tmp(e, chunks * sizeof(u32)));
+  u32* dirty = (u32*)e->tmp;
+  HIP_TRY(hipMemsetAsync(dirty, 0, chunks * sizeof(u32), e->stream));
+  HIP_TRY(hipMemsetAsync(e->ticket + 3, 0, sizeof(u32), e->stream));
+  HIP_TRY(hipMemsetAsync(e->d_counts, 0, sizeof(u64), e->stream));
+  HIP_TRY(launch_merkle_update(merkle_of(t), rows_of(old_s), rows_of(new_s), keys, n_keys, dirty,
+                               e->d_counts, e->ticket, e->ticket + 3, e->stream));
+  TRY(read_counts(e, 1));
+  TRY(input_error(e, "dg_merkle_update"));
+  t->n_keys += e->h_counts[0];  // a signed change, two's complement
+  return DG_OK;
+}
+
+int dg_merkle_diff(dg_engine* e, const dg_merkle* a, const dg_store* sa, const dg_merkle* b,
+                   const dg_store* sb, uint64_t* out_keys, uint64_t cap, uint64_t* n_out,
+                   uint64_t* n_total) {
+  if (!e) return fail(DG_E_INVAL, "null engine");
+  TRY(check_merkle(a, "dg_merkle_diff a"));
+  TRY(check_merkle(b, "dg_merkle_diff b"));
+  TRY(same_tree_shape(a, b, "dg_merkle_diff"));
+  TRY(check_store(sa, "dg_merkle_diff sa"));
+  TRY(check_store(sb, "dg_merkle_diff sb"));
+  if (!n_out) return fail(DG_E_INVAL, "dg_merkle_diff: null n_out");
   if (cap && !out_keys) return fail(DG_E_INVAL, "dg_merkle_diff: null out_keys");
   TRY(set_device(e));
   TRY(ensure_state(e, diff_scratch_words(a->depth) + 2));  // tile counts, offsets, bucket counts
-  HIP_TRY(launch_merkle_diff(a->depth, a->nodes, a->leaf_key, a->leaf_hash, a->bucket_off, b->nodes,
-                             b->leaf_key, b->leaf_hash, b->bucket_off, out_keys, cap, e->state,
-                             e->d_counts, e->stream));
+  HIP_TRY(launch_merkle_diff(merkle_of(a), rows_of(sa), merkle_of(b), rows_of(sb), out_keys, cap,
+                             e->state, e->d_counts, e->stream));
   TRY(read_counts(e, 1));
-  *n_out = e->h_counts[0];
-  if (*n_out > cap)
-    return fail(DG_E_CAPACITY, "dg_merkle_diff: %llu differing keys > cap %llu",
-                (unsigned long long)*n_out, (unsigned long long)cap);
+  const u64 total = e->h_counts[0];
+  *n_out = std::min<u64>(total, cap);
+  if (n_total) *n_total = total;
+  return DG_OK;
+}
+
+int dg_merkle_prepare(dg_engine* e, const dg_merkle* t, uint32_t levels, dg_merkle_cont* out) {
+  if (!e) return fail(DG_E_INVAL, "null engine");
+  TRY(check_merkle(t, "dg_merkle_prepare"));
+  if (!out || levels < 1) return fail(DG_E_INVAL, "dg_merkle_prepare: bad arguments");
+  const u32 L = std::min<u32>(levels, t->depth);
+  const u64 n = 1ull << L;
+  out->level = L;
+  out->n = n;
+  out->n_buckets = 0;
+  if (out->cap < n || !out->pos || !out->hash)
+    return fail(DG_E_CAPACITY, "dg_merkle_prepare: %llu entries needed", (unsigned long long)n);
+  TRY(set_device(e));
+  TRY(ensure_state(e, 2));
+  HIP_TRY(hipMemsetAsync(e->state, 0, sizeof(u64), e->stream));  // the root's position, 0
+  HIP_TRY(launch_cont_expand(merkle_of(t), 0, L, e->state, 1, out->pos, out->hash, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return DG_OK;
+}
+
+int dg_merkle_continue(dg_engine* e, const dg_merkle* t, const dg_store* s, const dg_merkle_cont* in,
+                       uint32_t levels, dg_merkle_cont* out, uint64_t* keys, uint64_t cap,
+                       uint64_t* n_keys, uint64_t* n_total, int* status) {
+  if (!e) return fail(DG_E_INVAL, "null engine");
+  TRY(check_merkle(t, "dg_merkle_continue"));
+  TRY(check_store(s, "dg_merkle_continue"));
+  if (!in || !status || !n_keys || levels < 1 || (cap && !keys))
+    return fail(DG_E_INVAL, "dg_merkle_continue: bad arguments");
+  if (in->n && (!in->pos || !in->hash)) return fail(DG_E_INVAL, "dg_merkle_continue: null input");
+  *n_keys = 0;
+  if (n_total) *n_total = 0;
+  *status = 0;
+  TRY(set_device(e));
+  const u32 depth = t->depth;
+  const MerkleT m = merkle_of(t);
+  if (in->level == depth + 1) {  // leaf form: the keys
+    if (in->n_buckets && !in->bucket) return fail(DG_E_INVAL, "dg_merkle_continue: null buckets");
+    TRY(ensure_state(e, 2 * cont_tiles(in->n_buckets) + 2));
+    HIP_TRY(launch_leafdiff(m, rows_of(s), in->bucket, in->n_buckets, in->pos, in->hash, in->n, keys,
+                            cap, e->state, e->d_counts, e->stream));
+    TRY(read_counts(e, 1));
+    const u64 total = e->h_counts[0];
+    *n_keys = std::min<u64>(total, cap);
+    if (n_total) *n_total = total;
+    return DG_OK;
+  }
+  if (in->level > depth) return fail(DG_E_INVAL, "dg_merkle_continue: level %u > depth %u", in->level, depth);
+  if (!out) return fail(DG_E_INVAL, "dg_merkle_continue: null out");
+  const u32 L = in->level;
+  TRY(ensure_state(e, 2 * cont_tiles(in->n) + 2));
+  TRY(ensure_tmp(e, std::max<u64>(in->n, 1) * sizeof(u64)));
+  u64* dpos = (u64*)e->tmp;
+  HIP_TRY(launch_cont_compare(m, L, in->pos, in->hash, in->n, e->state, dpos, e->d_counts, e->stream));
+  TRY(read_counts(e, 1));
+  const u64 nd = e->h_counts[0];
+  if (nd == 0) return DG_OK;  // {:ok, []}
+  if (L < depth) {
+    const u32 k = std::min<u32>(levels, depth - L);
+    const u64 need = nd << k;
+    out->level = L + k;
+    out->n = need;
+    out->n_buckets = 0;
+    if (out->cap < need || !out->pos || !out->hash)
+      return fail(DG_E_CAPACITY, "dg_merkle_continue: %llu entries needed", (unsigned long long)need);
+    HIP_TRY(launch_cont_expand(m, L, k, dpos, nd, out->pos, out->hash, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    *status = 1;
+    return DG_OK;
+  }
+  // the differing buckets -> leaf form
+  out->level = depth + 1;
+  out->n_buckets = nd;
+  if (out->cap_buckets < nd || !out->bucket)
+    return fail(DG_E_CAPACITY, "dg_merkle_continue: %llu buckets needed", (unsigned long long)nd);
+  HIP_TRY(hipMemcpyAsync(out->bucket, dpos, nd * sizeof(u64), hipMemcpyDeviceToDevice, e->stream));
+  TRY(ensure_state(e, 2 * cont_tiles(nd) + 2));
+  HIP_TRY(launch_leaves_count(m, rows_of(s), out->bucket, nd, e->state, e->d_counts, e->stream));
+  TRY(read_counts(e, 1));
+  const u64 np = e->h_counts[0];
+  out->n = np;
+  if (out->cap < np || (np && (!out->pos || !out->hash)))
+    return fail(DG_E_CAPACITY, "dg_merkle_continue: %llu leaf pairs needed", (unsigned long long)np);
+  HIP_TRY(launch_leaves_write(m, rows_of(s), out->bucket, nd, e->state, out->pos, out->hash, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  *status = 1;
+  return DG_OK;
+}
+
+int dg_merkle_truncate(dg_engine* e, const dg_merkle* t, dg_merkle_cont* cont, uint64_t max) {
+  if (!e || !cont) return fail(DG_E_INVAL, "dg_merkle_truncate: null argument");
+  TRY(check_merkle(t, "dg_merkle_truncate"));
+  if (cont->n_buckets == 0 || cont->bucket == nullptr) {  // node form (or an empty leaf form)
+    cont->n = std::min<u64>(cont->n, max);
+    return DG_OK;
+  }
+  if (cont->n_buckets <= max) return DG_OK;
+  // leaf form: the pairs of the first `max` buckets are those whose key sorts before
+  // the first pair of bucket[max]; pairs carry keys, buckets carry bucket numbers, so
+  // count the pairs of the dropped buckets by their bucket's first pair
+  TRY(set_device(e));
+  TRY(ensure_state(e, 2));
+  HIP_TRY(launch_pairs_before_bucket(merkle_of(t), cont->pos, cont->n, cont->bucket + max,
+                                     e->d_counts, e->stream));
+  TRY(read_counts(e, 1));
+  cont->n = e->h_counts[0];
+  cont->n_buckets = max;
+  return DG_OK;
+}
+
+int dg_merkle_fold_roots(const uint64_t* roots, uint32_t shard_bits, uint64_t* root) {
+  if (!roots || !root || shard_bits > 16) return fail(DG_E_INVAL, "dg_merkle_fold_roots: bad arguments");
+  std::vector<u64> lvl(roots, roots + (1ull << shard_bits));
+  while (lvl.size() > 1) {
+    std::vector<u64> up(lvl.size() / 2);
+    for (size_t i = 0; i < up.size(); i++) up[i] = node_hash(lvl[2 * i], lvl[2 * i + 1]);
+    lvl.swap(up);
+  }
+  *root = lvl[0];
   return DG_OK;
 }
 

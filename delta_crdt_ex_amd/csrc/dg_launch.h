@@ -139,9 +139,6 @@ inline u64 seg_tiles(u64 n) { return (n + SEG_TILE - 1) / SEG_TILE; }
 // scratch: 2 * seg_tiles(n) u64 (per-tile counts and offsets).
 hipError_t launch_read_lww(const Rows& s, const u64* keys, u64 n_keys, u64* out_key, u64* out_val,
                            u64* scratch, u64* d_count, hipStream_t st);
-// Merkle leaves: (key, Σ row hashes) per key + bucket_off[b] = first leaf of bucket >= b.
-hipError_t launch_merkle_leaves(const Rows& s, u32 depth, u64* leaf_key, u64* leaf_hash,
-                                u64* bucket_off, u64* scratch, u64* d_count, hipStream_t st);
 // Sortedness check: sets *d_bad to nonzero if rows are not strictly ascending.
 hipError_t launch_store_check(const Rows& s, u32* d_bad, hipStream_t st);
 
@@ -151,17 +148,45 @@ hipError_t launch_store_check(const Rows& s, u32* d_bad, hipStream_t st);
 hipError_t launch_remap_values(u64* val, u64 n, const u64* old_ids, const u64* new_ids, u64 n_ids,
                                u32* err, hipStream_t st);
 
-// ---- merkle.hip
-hipError_t launch_merkle_levels(u32 depth, const u64* leaf_hash, const u64* bucket_off,
-                                u64* nodes, hipStream_t st);
+// ---- merkle.hip (see the file header)
+struct MerkleT {
+  u32 depth, sb;  // buckets 2^depth; the tree covers keys whose top sb bits == shard
+  u64 shard;
+  u64* nodes;     // heap, 2^(depth+1) - 1
+};
+constexpr u32 MERKLE_UPL = 11;  // levels reduced per upsweep workgroup
+inline u64 merkle_chunks(u32 depth) { return 1ull << (depth - (depth < MERKLE_UPL ? depth : MERKLE_UPL)); }
+// bucket level zeroed, rows hashed into it, fused upsweep; *d_keys = distinct keys;
+// ctr: a device word left at 0; err bit 1: a row outside the tree's shard.
+hipError_t launch_merkle_build(const Rows& s, const MerkleT& t, u64* d_keys, u32* ctr, u32* err,
+                               hipStream_t st);
+// put/delete of the changed keys + update_hashes; dirty: merkle_chunks(depth) u32, zero
+// on entry and left zero; *d_keys += the change in distinct keys.
+hipError_t launch_merkle_update(const MerkleT& t, const Rows& olds, const Rows& news, const u64* keys,
+                                u64 n_keys, u32* dirty, u64* d_keys, u32* ctr, u32* err,
+                                hipStream_t st);
 constexpr int DIFF_BLOCK = 256;
 inline u64 diff_tiles(u32 depth) { return depth >= 8 ? (1ull << (depth - 8)) : 1ull; }
 // per-tile counts and offsets, then one u32 count per bucket
 inline u64 diff_scratch_words(u32 depth) { return 2 * diff_tiles(depth) + ((1ull << depth) + 1) / 2; }
-hipError_t launch_merkle_diff(u32 depth, const u64* nodes_a, const u64* leaf_key_a,
-                              const u64* leaf_hash_a, const u64* off_a, const u64* nodes_b,
-                              const u64* leaf_key_b, const u64* leaf_hash_b, const u64* off_b,
-                              u64* out_keys, u64 cap, u64* scratch, u64* d_count,
-                              hipStream_t st);  // scratch: diff_scratch_words(depth) u64
+// differing keys, ascending; the first min(total, cap) written; *d_count = total.
+hipError_t launch_merkle_diff(const MerkleT& a, const Rows& sa, const MerkleT& b, const Rows& sb,
+                              u64* out_keys, u64 cap, u64* scratch, u64* d_count, hipStream_t st);
+// partial diff.  scratch: 2 * ceil(n / 256) u64.
+inline u64 cont_tiles(u64 n) { return (n + 255) / 256; }
+hipError_t launch_cont_compare(const MerkleT& t, u32 L, const u64* pos, const u64* hash, u64 n,
+                               u64* scratch, u64* dpos, u64* d_count, hipStream_t st);
+hipError_t launch_cont_expand(const MerkleT& t, u32 L, u32 k, const u64* dpos, u64 nd, u64* opos,
+                              u64* ohash, hipStream_t st);
+hipError_t launch_leaves_count(const MerkleT& t, const Rows& s, const u64* buckets, u64 nb,
+                               u64* scratch, u64* d_count, hipStream_t st);
+hipError_t launch_leaves_write(const MerkleT& t, const Rows& s, const u64* buckets, u64 nb,
+                               const u64* scratch, u64* ok, u64* oh, hipStream_t st);
+// d_count[0] = the number of keys[0, n) (ascending) before bucket[0]'s first key
+hipError_t launch_pairs_before_bucket(const MerkleT& t, const u64* keys, u64 n, const u64* bucket,
+                                     u64* d_count, hipStream_t st);
+hipError_t launch_leafdiff(const MerkleT& t, const Rows& s, const u64* buckets, u64 nb, const u64* pk,
+                           const u64* ph, u64 np, u64* out, u64 cap, u64* scratch, u64* d_count,
+                           hipStream_t st);
 
 }  // namespace dg

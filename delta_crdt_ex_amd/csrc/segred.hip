@@ -218,26 +218,6 @@ hipError_t launch_read_lww(const Rows& s, const u64* keys, u64 n_keys, u64* out_
   return launch_seg<SegOp::Read>(p, st);
 }
 
-hipError_t launch_merkle_leaves(const Rows& s, u32 depth, u64* leaf_key, u64* leaf_hash,
-                                u64* bucket_off, u64* scratch, u64* d_count, hipStream_t st) {
-  SegArgs p{};
-  p.s = s;
-  p.out_a = leaf_key;
-  p.out_b = leaf_hash;
-  p.bucket_off = bucket_off;
-  p.depth = depth;
-  p.ntiles = seg_tiles(s.n);
-  p.cnt = scratch;
-  p.off = scratch + p.ntiles;
-  p.d_count = d_count;
-  if (p.ntiles == 0) {
-    hipLaunchKernelGGL(fill_u64_kernel, dim3(256), dim3(256), 0, st, bucket_off,
-                       (1ull << depth) + 1, 0ull);
-    return hipMemsetAsync(d_count, 0, sizeof(u64), st);
-  }
-  return launch_seg<SegOp::Leaves>(p, st);
-}
-
 hipError_t launch_store_check(const Rows& s, u32* d_bad, hipStream_t st) {
   if (s.n < 2) return hipSuccess;
   u64 blocks = (s.n + 255) / 256;

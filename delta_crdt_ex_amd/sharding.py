@@ -8,9 +8,11 @@ shard with no data exchange.  The only cross-rank steps are tiny:
 * the causal context: every shard carries the replica's full VV, so the union is
   computed redundantly on every rank; `vv_allreduce_max` is the RCCL (or gloo)
   all-reduce that keeps them identical when shards were updated independently;
-* the Merkle tree: each rank builds the tree of its shard; `merkle_roots` all-gathers
-  the N shard roots (8 bytes each) and folds them into the replica's root; a diff
-  descends only into shards whose roots differ (`differing_shards`).
+* the Merkle tree: each rank builds the tree of its shard's key range (a level-log2(N)
+  subtree of the unsharded tree); `merkle_roots` all-gathers the N shard roots (8 bytes
+  each) and folds them into the replica's root -- the unsharded tree's root, so roots
+  compare across shard counts; a diff descends only into shards whose roots differ
+  (`differing_shards`).
 
 One process per GPU (torch.distributed: "nccl" = RCCL over xGMI on MI355X; "gloo" in
 the CPU tests).  Nothing here moves rows between GPUs.
@@ -66,33 +68,40 @@ def vv_merge_max(parts):
     return (np.array([a for a, _ in items], np.uint32), np.array([b for _, b in items], np.uint64))
 
 
-def vv_allreduce_max(node: np.ndarray, cnt: np.ndarray, group=None):
-    """All-reduce(max) of a version vector across the ranks of `group`.
+def _coll_device(group):
+    import torch
+    import torch.distributed as dist
+    if dist.get_backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
 
-    VVs of different ranks may name different nodes, so this all-gathers the (padded)
-    node/counter arrays and merges them: a few KB at most (one entry per replica)."""
+
+def vv_allreduce_max(node: np.ndarray, cnt: np.ndarray, group=None):
+    """All-reduce(max) of a version vector across the ranks of `group`
+    (Dots.union/2 of VVs, aw_lww_map.ex:39-52, across key-hash shards).
+
+    Node ids are dense interned ids (interning.py), so a VV is a dense counter vector
+    indexed by node id: one all-reduce(MAX) of the vector lengths, then one
+    all-reduce(MAX) of the vectors (counter + 1, 0 = absent node).  On RCCL these are
+    two latency-bound all-reduces of a few hundred bytes."""
     import torch
     import torch.distributed as dist
 
-    world = dist.get_world_size(group)
-    backend = dist.get_backend(group)
-    dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
-    n = torch.tensor([len(node)], dtype=torch.int64, device=dev)
-    sizes = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(sizes, n, group=group)
-    m = int(max(int(x.item()) for x in sizes))
-    buf = torch.zeros((max(m, 1), 2), dtype=torch.int64, device=dev)
-    if len(node):
-        buf[: len(node), 0] = torch.from_numpy(np.asarray(node, np.int64))
-        buf[: len(node), 1] = torch.from_numpy(np.asarray(cnt, np.uint64).view(np.int64))
-    outs = [torch.zeros_like(buf) for _ in range(world)]
-    dist.all_gather(outs, buf, group=group)
-    parts = []
-    for r, o in enumerate(outs):
-        k = int(sizes[r].item())
-        a = o[:k].cpu().numpy()
-        parts.append((a[:, 0].astype(np.uint32), a[:, 1].view(np.uint64)))
-    return vv_merge_max(parts)
+    dev = _coll_device(group)
+    node = np.asarray(node, np.int64)
+    n = torch.tensor([int(node.max()) + 1 if len(node) else 0], dtype=torch.int64, device=dev)
+    dist.all_reduce(n, op=dist.ReduceOp.MAX, group=group)
+    m = int(n.item())
+    dense = np.zeros(max(m, 1), np.int64)
+    c = np.asarray(cnt, np.uint64)
+    if np.any(c >= np.uint64((1 << 63) - 1)):
+        raise OverflowError("a counter >= 2^63 - 1 does not fit the int64 all-reduce")
+    dense[node] = c.astype(np.int64) + 1
+    t = torch.from_numpy(dense).to(dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    out = t.cpu().numpy()[:m]
+    have = np.flatnonzero(out)
+    return have.astype(np.uint32), (out[have] - 1).astype(np.uint64)
 
 
 def _mix64(x: int) -> int:
@@ -110,11 +119,13 @@ def node_hash(left: int, right: int) -> int:
 
 
 def fold_roots(roots) -> int:
-    """Replica root over the shard roots: a binary tree over the N roots (padded with
-    0 to a power of two), parents = node_hash(left, right)."""
+    """Replica root over the 2^b shard roots (shard order): the top b levels of the
+    unsharded tree (dg_merkle_fold_roots), parents = node_hash(left, right).  A shard's
+    tree covers exactly its key range (dg_merkle shard_bits/shard), so the result equals
+    the root of the unsharded tree of depth b + the shard depth."""
     level = [int(r) & MASK64 for r in roots]
-    while len(level) & (len(level) - 1):
-        level.append(0)
+    if len(level) & (len(level) - 1):
+        raise ValueError("Merkle shard roots fold only for a power-of-two shard count")
     while len(level) > 1:
         level = [node_hash(level[i], level[i + 1]) for i in range(0, len(level), 2)]
     return level[0]
@@ -126,14 +137,21 @@ def merkle_roots(local_root: int, group=None):
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
-    backend = dist.get_backend(group)
-    dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+    dev = _coll_device(group)
     t = torch.tensor([int(np.array([local_root], np.uint64).view(np.int64)[0])], dtype=torch.int64,
                      device=dev)
     outs = [torch.zeros_like(t) for _ in range(world)]
     dist.all_gather(outs, t, group=group)
     roots = [int(np.array([o.item()], np.int64).view(np.uint64)[0]) for o in outs]
     return roots, fold_roots(roots)
+
+
+def shard_bits(n_shards: int) -> int:
+    """log2 of a power-of-two shard count (the Merkle shard trees need one)."""
+    b = int(n_shards).bit_length() - 1
+    if n_shards != 1 << b:
+        raise ValueError(f"{n_shards} shards: Merkle shard trees need a power of two")
+    return b
 
 
 def differing_shards(roots_a, roots_b):

@@ -31,7 +31,7 @@ def _np_to_dev(a: np.ndarray, dtype_view, device) -> torch.Tensor:
     return torch.from_numpy(a.copy()).to(device, non_blocking=False)
 
 
-@dataclass
+@dataclass(eq=False)  # identity semantics: a Universe tracks stores in a WeakSet
 class Store:
     """SoA dot rows on the device: key u64, val u64, ts i64, node u32, cnt u64."""
 
@@ -139,37 +139,88 @@ class Context:
         return c
 
 
-@dataclass
+@dataclass(eq=False)
 class MerkleTree:
+    """A device Merkle tree (include/deltagpu.h dg_merkle) and the store it indexes (the
+    diff recomputes key leaves from the store's rows)."""
+
     depth: int
     nodes: torch.Tensor
-    bucket_off: torch.Tensor
-    leaf_key: torch.Tensor
-    leaf_hash: torch.Tensor
-    n_keys: int
+    n_keys: int = 0
+    shard_bits: int = 0
+    shard: int = 0
+    store: Store | None = None
 
     @staticmethod
-    def empty(depth: int, cap_keys: int, device) -> "MerkleTree":
-        nb = 1 << depth
-        cap_keys = max(int(cap_keys), 1)
-        return MerkleTree(depth, torch.empty(2 * nb - 1, dtype=_I64, device=device),
-                          torch.empty(nb + 1, dtype=_I64, device=device),
-                          torch.empty(cap_keys, dtype=_I64, device=device),
-                          torch.empty(cap_keys, dtype=_I64, device=device), 0)
+    def empty(depth: int, device, shard_bits: int = 0, shard: int = 0) -> "MerkleTree":
+        return MerkleTree(depth, torch.empty(2 * (1 << depth) - 1, dtype=_I64, device=device), 0,
+                          shard_bits, shard)
 
     def abi(self) -> _abi.dg_merkle:
         t = _abi.dg_merkle()
         t.depth = self.depth
+        t.shard_bits = self.shard_bits
+        t.shard = self.shard
         t.nodes = _ptr(self.nodes, _abi.P64)
-        t.bucket_off = _ptr(self.bucket_off, _abi.P64)
-        t.leaf_key = _ptr(self.leaf_key, _abi.P64)
-        t.leaf_hash = _ptr(self.leaf_hash, _abi.P64)
         t.n_keys = self.n_keys
-        t.cap_keys = int(self.leaf_key.numel())
         return t
 
     def root(self) -> int:
         return int(self.nodes[0].item()) & ((1 << 64) - 1)
+
+    def level(self, lv: int) -> np.ndarray:
+        return self.nodes[(1 << lv) - 1: (1 << (lv + 1)) - 1].cpu().numpy().view(np.uint64)
+
+
+@dataclass(eq=False)
+class MerkleCont:
+    """A partial-diff continuation (dg_merkle_cont): node form (level <= depth) or leaf
+    form (level == depth + 1, with the buckets its (key, leaf) pairs cover)."""
+
+    level: int
+    pos: torch.Tensor
+    hash: torch.Tensor
+    n: int
+    bucket: torch.Tensor | None = None
+    n_buckets: int = 0
+
+    @staticmethod
+    def empty(cap: int, cap_buckets: int, device) -> "MerkleCont":
+        cap, cap_buckets = max(int(cap), 1), max(int(cap_buckets), 1)
+        return MerkleCont(0, torch.empty(cap, dtype=_I64, device=device),
+                          torch.empty(cap, dtype=_I64, device=device), 0,
+                          torch.empty(cap_buckets, dtype=_I64, device=device), 0)
+
+    @property
+    def leaf(self) -> bool:
+        return self.n_buckets > 0
+
+    def abi(self) -> _abi.dg_merkle_cont:
+        c = _abi.dg_merkle_cont()
+        c.level = self.level
+        c.pos = _ptr(self.pos, _abi.P64)
+        c.hash = _ptr(self.hash, _abi.P64)
+        c.n = self.n
+        c.cap = int(self.pos.numel())
+        c.bucket = _ptr(self.bucket, _abi.P64) if self.bucket is not None else None
+        c.n_buckets = self.n_buckets
+        c.cap_buckets = int(self.bucket.numel()) if self.bucket is not None else 0
+        return c
+
+    def _set(self, c: _abi.dg_merkle_cont):
+        self.level, self.n, self.n_buckets = int(c.level), int(c.n), int(c.n_buckets)
+
+
+def fold_roots(roots) -> int:
+    """dg_merkle_fold_roots: the unsharded root from the 2^b shard roots (shard order)."""
+    lib = _abi.load()
+    r = np.ascontiguousarray(np.asarray(roots, dtype=np.uint64))
+    b = int(len(r)).bit_length() - 1
+    if len(r) != 1 << b:
+        raise ValueError("fold_roots needs a power-of-two number of shard roots")
+    out = C.c_uint64()
+    check(lib.dg_merkle_fold_roots(r.ctypes.data_as(_abi.P64), b, C.byref(out)))
+    return int(out.value)
 
 
 class Engine:
@@ -456,27 +507,107 @@ class Engine:
         return ok[: n.value], ov[: n.value]
 
     # ---------------------------------------------------------------- merkle
-    def merkle_build(self, s: Store, depth: int, tree: MerkleTree | None = None) -> MerkleTree:
+    def merkle_build(self, s: Store, depth: int, tree: MerkleTree | None = None,
+                     shard_bits: int = 0, shard: int = 0) -> MerkleTree:
+        """MerkleMap over every key of `s` (or of its key-hash shard)."""
         self._order()
-        if tree is None or tree.depth != depth or tree.leaf_key.numel() < s.n:
-            tree = MerkleTree.empty(depth, s.n, self.device)
+        if tree is None or tree.depth != depth:
+            tree = MerkleTree.empty(depth, self.device, shard_bits, shard)
+        tree.shard_bits, tree.shard = shard_bits, shard
         t = tree.abi()
         ss = s.abi()
         check(self.lib.dg_merkle_build(self.h, C.byref(ss), C.byref(t)))
         tree.n_keys = int(t.n_keys)
+        tree.store = s
         return tree
 
-    def merkle_diff(self, a: MerkleTree, b: MerkleTree, cap: int | None = None) -> torch.Tensor:
+    def prepare_merkle_build(self, s: Store, tree: MerkleTree, d_counts: torch.Tensor):
+        """Pre-marshal one dg_merkle_build_async (benchmark loops): a zero-argument
+        callable that enqueues the build on the engine stream."""
+        args = [s.abi(), tree.abi()]
+        refs = [C.byref(x) for x in args]
+        dp = _ptr(d_counts, _abi.P64)
+        f, h = self.lib.dg_merkle_build_async, self.h
+
+        def launch():
+            check(f(h, refs[0], refs[1], dp))
+
+        launch._keep = (args, d_counts, s, tree)
+        tree.store = s
+        return launch
+
+    def merkle_update(self, tree: MerkleTree, new: Store, keys: torch.Tensor) -> MerkleTree:
+        """MerkleMap.put/delete of the changed `keys` + update_hashes: `tree` indexed
+        tree.store; afterwards it indexes `new` (causal_crdt.ex:383-394)."""
+        self._order()
+        t = tree.abi()
+        so, sn = tree.store.abi(), new.abi()
+        kp, nk = self._keys(keys)
+        check(self.lib.dg_merkle_update(self.h, C.byref(t), C.byref(so), C.byref(sn), kp, nk))
+        tree.n_keys = int(t.n_keys) & ((1 << 64) - 1)
+        tree.store = new
+        return tree
+
+    def merkle_diff(self, a: MerkleTree, b: MerkleTree, cap: int | None = None,
+                    with_total: bool = False):
+        """The differing keys of the two indexed stores, ascending; with `cap` only the
+        first cap (Enum.take(keys, max_sync_size)).  with_total: (keys, total)."""
         self._order()
         if cap is None:
             cap = a.n_keys + b.n_keys
-        cap = max(int(cap), 1)
-        out = torch.empty(cap, dtype=_I64, device=self.device)
-        n = C.c_uint64()
-        ta, tb = a.abi(), b.abi()
-        check(self.lib.dg_merkle_diff(self.h, C.byref(ta), C.byref(tb), _ptr(out, _abi.P64), cap,
-                                      C.byref(n)))
-        return out[: n.value]
+        cap = int(cap)
+        out = torch.empty(max(cap, 1), dtype=_I64, device=self.device)
+        n, tot = C.c_uint64(), C.c_uint64()
+        ta, tb, sa, sb = a.abi(), b.abi(), a.store.abi(), b.store.abi()
+        check(self.lib.dg_merkle_diff(self.h, C.byref(ta), C.byref(sa), C.byref(tb), C.byref(sb),
+                                      _ptr(out, _abi.P64), cap, C.byref(n), C.byref(tot)))
+        keys = out[: n.value]
+        return (keys, int(tot.value)) if with_total else keys
+
+    def merkle_prepare(self, tree: MerkleTree, levels: int = 8) -> MerkleCont:
+        """MerkleMap.prepare_partial_diff(mm, levels) (causal_crdt.ex:255)."""
+        self._order()
+        L = min(levels, tree.depth)
+        cont = MerkleCont.empty(1 << L, 1, self.device)
+        c = cont.abi()
+        check(self.lib.dg_merkle_prepare(self.h, C.byref(tree.abi()), levels, C.byref(c)))
+        cont._set(c)
+        return cont
+
+    def merkle_continue(self, tree: MerkleTree, cont: MerkleCont, levels: int = 8,
+                        cap: int | None = None):
+        """MerkleMap.continue_partial_diff(cont, mm, levels) (causal_crdt.ex:96) on this
+        replica's tree: ("continue", MerkleCont) or ("ok", keys, total)."""
+        self._order()
+        s = tree.store
+        if cap is None:
+            cap = max(cont.n, 1) + s.n
+        keys = torch.empty(max(int(cap), 1), dtype=_I64, device=self.device)
+        cin = cont.abi()
+        t, ss = tree.abi(), s.abi()
+        out_cap, out_bcap = 4 * max(cont.n, 1), max(cont.n, 1)
+        for _ in range(3):  # grow the output continuation to the sizes the call reports
+            out = MerkleCont.empty(out_cap, out_bcap, self.device)
+            co = out.abi()
+            nk, tot, st = C.c_uint64(), C.c_uint64(), C.c_int()
+            rc = self.lib.dg_merkle_continue(self.h, C.byref(t), C.byref(ss), C.byref(cin), levels,
+                                             C.byref(co), _ptr(keys, _abi.P64), int(cap),
+                                             C.byref(nk), C.byref(tot), C.byref(st))
+            if rc != _abi.DG_E_CAPACITY:
+                break
+            out_cap, out_bcap = max(int(co.n), out_cap), max(int(co.n_buckets), out_bcap)
+        check(rc)
+        if st.value == 1:
+            out._set(co)
+            return ("continue", out)
+        return ("ok", keys[: nk.value], int(tot.value))
+
+    def merkle_truncate(self, tree: MerkleTree, cont: MerkleCont, max_entries: int) -> MerkleCont:
+        """MerkleMap.truncate_diff(cont, max_sync_size) (causal_crdt.ex:98,212-214)."""
+        c = cont.abi()
+        check(self.lib.dg_merkle_truncate(self.h, C.byref(tree.abi()), C.byref(c), int(max_entries)))
+        cont._set(c)
+        return cont
 
     # ---------------------------------------------------------------- interning
     def remap_values(self, s: Store, old_ids: np.ndarray, new_ids: np.ndarray):
@@ -500,4 +631,5 @@ def u64(t: torch.Tensor) -> np.ndarray:
     return t.cpu().numpy().view(np.uint64)
 
 
-__all__ = ["Store", "Context", "MerkleTree", "Engine", "u64", "DG_CTX_VV", "DG_CTX_DOTS"]
+__all__ = ["Store", "Context", "MerkleTree", "MerkleCont", "Engine", "fold_roots", "u64",
+           "DG_CTX_VV", "DG_CTX_DOTS"]

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define DG_ABI_VERSION 1
+#define DG_ABI_VERSION 2
 
 enum dg_status {
   DG_OK = 0,
@@ -76,20 +76,40 @@ typedef struct dg_context {
   uint64_t cap;
 } dg_context;
 
-/* Merkle index over a store (the MerkleMap role, causal_crdt.ex:21,94,96,254,255,392-393).
- * Leaves: one (key, hash) per distinct key, ascending by key.  Buckets: 2^depth,
- * bucket(key) = key >> (64 - depth).  `nodes` is a heap in level order: level l
- * (root l = 0) occupies [2^l - 1, 2^(l+1) - 1); the buckets are level `depth`. */
+/* Merkle index over a store (the MerkleMap role, causal_crdt.ex:21,94,96,254,255,390-394).
+ * The tree covers the keys whose top `shard_bits` bits equal `shard` (a key-hash shard,
+ * SURVEY.md §8(e); shard_bits = 0: every key) in 2^depth buckets by the next `depth`
+ * bits: bucket(key) = (key << shard_bits) >> (64 - depth).
+ *   bucket hash = Σ row_hash over the bucket's rows (mod 2^64; a key's leaf is the sum
+ *                 over its own rows: its raw value map, causal_crdt.ex:392)
+ *   parent      = node_hash(left, right)                       (dg_hash.h)
+ * `nodes` is a heap in level order: level l (root l = 0) occupies [2^l - 1, 2^(l+1) - 1);
+ * level `depth` holds the buckets.  The tree keeps no per-key leaves: a diff recomputes
+ * them from the store the tree indexes, so the diff entry points take the stores too.
+ * The 2^b shard trees (shard_bits = b, depth d - b) are exactly the level-b subtrees of
+ * the unsharded depth-d tree; dg_merkle_fold_roots recombines their roots. */
 typedef struct dg_merkle {
-  uint32_t depth;       /* 1..26 */
-  uint32_t reserved;
-  uint64_t* nodes;      /* 2^(depth+1) - 1 entries (caller-allocated) */
-  uint64_t* bucket_off; /* 2^depth + 1 entries: first leaf index of each bucket */
-  uint64_t* leaf_key;   /* cap_keys entries */
-  uint64_t* leaf_hash;
-  uint64_t n_keys;
-  uint64_t cap_keys;    /* must be >= the indexed store's row count */
+  uint32_t depth;      /* 1..28; shard_bits + depth <= 44 */
+  uint32_t shard_bits; /* 0..16 */
+  uint64_t shard;      /* < 2^shard_bits */
+  uint64_t* nodes;     /* 2^(depth+1) - 1 entries (caller-allocated, device) */
+  uint64_t n_keys;     /* distinct keys indexed (set by build / update) */
 } dg_merkle;
+
+/* A partial-diff continuation (the `continuation` of CausalCrdt's %Diff{},
+ * causal_crdt.ex:29,96,255): either NODE form -- the sender's hashes of the nodes
+ * pos[0, n) of tree level `level` -- or LEAF form (level == depth + 1) -- the sender's
+ * (key, leaf hash) pairs pos/hash[0, n) of the buckets bucket[0, n_buckets), all
+ * ascending.  Device arrays, caller-allocated with capacities. */
+typedef struct dg_merkle_cont {
+  uint32_t level;
+  uint32_t reserved;
+  uint64_t* pos;       /* node positions (node form) or keys (leaf form) */
+  uint64_t* hash;
+  uint64_t n, cap;
+  uint64_t* bucket;    /* leaf form: the differing buckets the pairs cover */
+  uint64_t n_buckets, cap_buckets;
+} dg_merkle_cont;
 
 typedef struct dg_engine dg_engine;
 
@@ -224,15 +244,62 @@ int dg_remap_values(dg_engine* e, dg_store* s, const uint64_t* old_ids, const ui
                     uint64_t n_ids);
 
 /* ---- Merkle anti-entropy (MerkleMap role) --------------------------------- */
-/* Build leaves + level-wise bucket hashes for `s` (MerkleMap.put/update_hashes,
- * causal_crdt.ex:94,254,390-394).  t->depth and capacities set by the caller. */
+/* Build the tree of `s` (MerkleMap.new + put of every key, causal_crdt.ex:21,390-394):
+ * t->depth, shard_bits, shard and nodes set by the caller; sets t->n_keys.  DG_E_INVAL
+ * if a row's key is outside the tree's shard.  Synchronous. */
 int dg_merkle_build(dg_engine* e, const dg_store* s, dg_merkle* t);
-/* Keys whose raw value maps differ between the two indexed stores (present in one
- * only, or with different rows), ascending — the role of
- * MerkleMap.prepare_partial_diff/continue_partial_diff (causal_crdt.ex:96,255).
- * Both trees must have the same depth. */
-int dg_merkle_diff(dg_engine* e, const dg_merkle* a, const dg_merkle* b, uint64_t* out_keys,
-                   uint64_t cap, uint64_t* n_out);
+/* Same, asynchronous on the engine stream: the distinct-key count goes to d_n_keys[0]
+ * (device); t->n_keys is not updated and a key outside the shard is not reported. */
+int dg_merkle_build_async(dg_engine* e, const dg_store* s, dg_merkle* t, uint64_t* d_n_keys);
+
+/* MerkleMap.put/delete of the keys a join changed plus update_hashes
+ * (update_state_with_delta, causal_crdt.ex:383-394; update_hashes :94,254): `t` indexes
+ * `old_s`; afterwards it indexes `new_s`, bit-identical to dg_merkle_build(new_s), having
+ * re-hashed only `keys` (device, ascending unique: every key whose rows differ between
+ * the stores, e.g. dg_join2_changes's output; extra keys are harmless) and the 2^11-bucket
+ * chunks they touch.  Synchronous. */
+int dg_merkle_update(dg_engine* e, dg_merkle* t, const dg_store* old_s, const dg_store* new_s,
+                     const uint64_t* keys, uint64_t n_keys);
+
+/* The keys whose raw value maps differ between two indexed stores (present in one only,
+ * or with different rows), ascending -- the key list MerkleMap.continue_partial_diff ends
+ * with (causal_crdt.ex:96,104-105), here with both trees at hand.  The first
+ * min(total, cap) keys are written to out_keys, *n_out = that number and *n_total = the
+ * total: a total above cap is the reference's truncate(keys, max_sync_size)
+ * (Enum.take, causal_crdt.ex:105,206-210), not an error.  Trees: same depth and shard. */
+int dg_merkle_diff(dg_engine* e, const dg_merkle* a, const dg_store* sa, const dg_merkle* b,
+                   const dg_store* sb, uint64_t* out_keys, uint64_t cap, uint64_t* n_out,
+                   uint64_t* n_total);
+
+/* MerkleMap.prepare_partial_diff(mm, levels) (causal_crdt.ex:255): a node-form
+ * continuation of the tree's level min(levels, depth), every node of it.  Synchronous. */
+int dg_merkle_prepare(dg_engine* e, const dg_merkle* t, uint32_t levels, dg_merkle_cont* out);
+
+/* MerkleMap.continue_partial_diff(cont, mm, levels) (causal_crdt.ex:96) on the receiving
+ * replica's tree `t` over its store `s`:
+ *   node form, level < depth : the entries whose node differs, expanded `levels` levels
+ *                              down (at most to the buckets) -> *status = 1 (:continue),
+ *                              `out` holds this tree's hashes of those nodes;
+ *   node form, level == depth: the differing buckets -> *status = 1, `out` in leaf form
+ *                              (this store's (key, leaf) pairs of those buckets);
+ *   leaf form                : the keys of the listed buckets whose leaves differ from
+ *                              this store's -> *status = 0 (:ok), keys as dg_merkle_diff
+ *                              (first min(total, cap) in keys, *n_keys, *n_total).
+ * No differing entry -> *status = 0 with *n_keys = *n_total = 0 ({:ok, []}).  DG_E_CAPACITY
+ * if `out` is too small (out->n / out->n_buckets then hold the sizes needed). */
+int dg_merkle_continue(dg_engine* e, const dg_merkle* t, const dg_store* s, const dg_merkle_cont* in,
+                       uint32_t levels, dg_merkle_cont* out, uint64_t* keys, uint64_t cap,
+                       uint64_t* n_keys, uint64_t* n_total, int* status);
+
+/* MerkleMap.truncate_diff(cont, max) (causal_crdt.ex:98,212-214): keep the first `max`
+ * entries of a node-form continuation, or the pairs of the first `max` buckets of a
+ * leaf-form one (`t`: the tree that produced it; a leaf form needs one device
+ * lower-bound to count the pairs it keeps). */
+int dg_merkle_truncate(dg_engine* e, const dg_merkle* t, dg_merkle_cont* cont, uint64_t max);
+
+/* The root of the unsharded tree from the 2^shard_bits shard roots (shard order), as the
+ * RCCL all-gather of per-GPU roots needs it.  Host only. */
+int dg_merkle_fold_roots(const uint64_t* roots, uint32_t shard_bits, uint64_t* root);
 
 #ifdef __cplusplus
 }

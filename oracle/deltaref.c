@@ -363,70 +363,33 @@ uint64_t ref_node_hash(uint64_t left, uint64_t right) {
   return mix64(left ^ mix64(right ^ 0xD6E8FEB86659FD93ULL));
 }
 
-/* Leaves = Σ row hashes per key (the raw per-key value map, causal_crdt.ex:392);
- * buckets = Σ leaves per bucket; parents = ref_node_hash(children). */
-int ref_merkle_build(const dg_store* s, dg_merkle* t) {
-  if (t->depth < 1 || t->depth > 26) REF_E(DG_E_INVAL);
-  uint64_t nb = 1ULL << t->depth;
+/* The MerkleMap role (csrc/merkle.hip, include/deltagpu.h dg_merkle): the tree over the
+ * keys whose top `sb` bits equal `shard`, 2^depth buckets by the next depth bits;
+ * bucket = Σ row hashes of its rows (a key's leaf = Σ over its rows, the raw per-key
+ * value map, causal_crdt.ex:392), parents = ref_node_hash(children).  `nodes` holds
+ * 2^(depth+1) - 1 entries in level order.  DG_E_INVAL for a key outside the shard. */
+int ref_merkle_build(const dg_store* s, uint32_t depth, uint32_t sb, uint64_t shard,
+                     uint64_t* nodes, uint64_t* n_keys) {
+  if (depth < 1 || depth > 28 || sb > 16 || depth + sb > 44) REF_E(DG_E_INVAL);
+  uint64_t nb = 1ULL << depth;
   uint64_t base = nb - 1;
-  memset(t->nodes, 0, (2 * nb - 1) * 8);
-  uint64_t o = 0, i = 0;
-  while (i < s->n) {
-    uint64_t key = s->key[i], h = 0;
-    while (i < s->n && s->key[i] == key) {
-      h += ref_row_hash(s->key[i], s->val[i], s->ts[i], s->node[i], s->cnt[i]);
-      i++;
-    }
-    if (o >= t->cap_keys) REF_E(DG_E_CAPACITY);
-    t->leaf_key[o] = key;
-    t->leaf_hash[o++] = h;
-    t->nodes[base + (key >> (64 - t->depth))] += h;
+  memset(nodes, 0, (2 * nb - 1) * 8);
+  uint64_t keys = 0;
+  for (uint64_t i = 0; i < s->n; i++) {
+    uint64_t key = s->key[i];
+    if (sb && (key >> (64 - sb)) != shard) REF_E(DG_E_INVAL);
+    if (i == 0 || s->key[i - 1] != key) keys++;
+    nodes[base + ((key << sb) >> (64 - depth))] +=
+        ref_row_hash(key, s->val[i], s->ts[i], s->node[i], s->cnt[i]);
   }
-  t->n_keys = o;
-  /* bucket_off[b] = first leaf whose bucket >= b (b = 0 .. 2^depth) */
-  {
-    uint64_t x = 0;
-    for (uint64_t bk = 0; bk <= nb; bk++) {
-      while (x < o && (t->leaf_key[x] >> (64 - t->depth)) < bk) x++;
-      t->bucket_off[bk] = x;
-    }
-  }
-  for (int l = (int)t->depth - 1; l >= 0; l--) {
+  for (int l = (int)depth - 1; l >= 0; l--) {
     uint64_t first = (1ULL << l) - 1;
     for (uint64_t x = 0; x < (1ULL << l); x++) {
       uint64_t idx = first + x;
-      t->nodes[idx] = ref_node_hash(t->nodes[2 * idx + 1], t->nodes[2 * idx + 2]);
+      nodes[idx] = ref_node_hash(nodes[2 * idx + 1], nodes[2 * idx + 2]);
     }
   }
-  return DG_OK;
-}
-
-/* Keys whose leaves differ (present on one side only, or different hash). */
-int ref_merkle_diff(const dg_merkle* a, const dg_merkle* b, uint64_t* out, uint64_t cap,
-                    uint64_t* n_out) {
-  if (a->depth != b->depth) REF_E(DG_E_INVAL);
-  uint64_t i = 0, j = 0, o = 0;
-  while (i < a->n_keys || j < b->n_keys) {
-    uint64_t k;
-    int d;
-    if (j >= b->n_keys || (i < a->n_keys && a->leaf_key[i] < b->leaf_key[j])) {
-      k = a->leaf_key[i++];
-      d = 1;
-    } else if (i >= a->n_keys || b->leaf_key[j] < a->leaf_key[i]) {
-      k = b->leaf_key[j++];
-      d = 1;
-    } else {
-      k = a->leaf_key[i];
-      d = a->leaf_hash[i] != b->leaf_hash[j];
-      i++;
-      j++;
-    }
-    if (d) {
-      if (o >= cap) REF_E(DG_E_CAPACITY);
-      out[o++] = k;
-    }
-  }
-  *n_out = o;
+  if (n_keys) *n_keys = keys;
   return DG_OK;
 }
 

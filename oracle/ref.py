@@ -34,7 +34,7 @@ def lib():
     if _lib is None:
         build()  # make: a no-op when libdeltaref.so is newer than its sources
         L = C.CDLL(LIB)
-        S, X, M = C.POINTER(_abi.dg_store), C.POINTER(_abi.dg_context), C.POINTER(_abi.dg_merkle)
+        S, X = C.POINTER(_abi.dg_store), C.POINTER(_abi.dg_context)
         L.ref_join2.argtypes = [S, X, S, X, _abi.P64, C.c_uint64, S, X]
         L.ref_joink.argtypes = [C.c_int, S, X, S, X]
         L.ref_join2_mt.argtypes = [S, X, S, X, _abi.P64, C.c_uint64, S, X, S, C.c_int]
@@ -42,8 +42,7 @@ def lib():
         L.ref_compress_dots.argtypes = [X, X]
         L.ref_read_lww.argtypes = [S, _abi.P64, C.c_uint64, _abi.P64, _abi.P64, C.c_uint64,
                                    _abi.P64]
-        L.ref_merkle_build.argtypes = [S, M]
-        L.ref_merkle_diff.argtypes = [M, M, _abi.P64, C.c_uint64, _abi.P64]
+        L.ref_merkle_build.argtypes = [S, C.c_uint32, C.c_uint32, C.c_uint64, _abi.P64, _abi.P64]
         L.ref_store_diff.argtypes = [S, S, _abi.P64, C.c_uint64, _abi.P64]
         L.ref_store_check.argtypes = [S]
         L.ref_row_hash.argtypes = [C.c_uint64, C.c_uint64, C.c_int64, C.c_uint32, C.c_uint64]
@@ -225,44 +224,93 @@ def read_lww(rows, keys=None):
 
 
 class Tree:
-    def __init__(self, depth, cap):
-        nb = 1 << depth
-        self.depth = depth
-        self.nodes = np.zeros(2 * nb - 1, np.uint64)
-        self.bucket_off = np.zeros(nb + 1, np.uint64)
-        self.leaf_key = np.zeros(max(cap, 1), np.uint64)
-        self.leaf_hash = np.zeros(max(cap, 1), np.uint64)
+    """The oracle's Merkle tree (deltaref.c ref_merkle_build): `nodes` in level order."""
+
+    def __init__(self, depth, shard_bits=0, shard=0):
+        self.depth, self.shard_bits, self.shard = depth, shard_bits, shard
+        self.nodes = np.zeros(2 * (1 << depth) - 1, np.uint64)
         self.n_keys = 0
 
-    def abi(self):
-        t = _abi.dg_merkle()
-        t.depth = self.depth
-        t.nodes = _p(self.nodes, _abi.P64)
-        t.bucket_off = _p(self.bucket_off, _abi.P64)
-        t.leaf_key = _p(self.leaf_key, _abi.P64)
-        t.leaf_hash = _p(self.leaf_hash, _abi.P64)
-        t.n_keys = self.n_keys
-        t.cap_keys = len(self.leaf_key)
-        return t
+    def level(self, lv):
+        return self.nodes[(1 << lv) - 1: (1 << (lv + 1)) - 1]
+
+    def bucket_of(self, keys):
+        k = np.asarray(keys, np.uint64)
+        with np.errstate(over="ignore"):
+            return ((k << np.uint64(self.shard_bits)) >> np.uint64(64 - self.depth)).astype(np.int64)
 
 
-def merkle_build(rows, depth):
+def merkle_build(rows, depth, shard_bits=0, shard=0):
     s, rows = _store(rows)
-    t = Tree(depth, len(rows[0]))
-    ta = t.abi()
-    _check(lib().ref_merkle_build(C.byref(s), C.byref(ta)), "ref_merkle_build")
-    t.n_keys = ta.n_keys
+    t = Tree(depth, shard_bits, shard)
+    nk = np.zeros(1, np.uint64)
+    _check(lib().ref_merkle_build(C.byref(s), depth, shard_bits, shard, _p(t.nodes, _abi.P64),
+                                  _p(nk, _abi.P64)), "ref_merkle_build")
+    t.n_keys = int(nk[0])
     return t
 
 
-def merkle_diff(ta: Tree, tb: Tree):
-    cap = ta.n_keys + tb.n_keys + 1
-    out = np.zeros(cap, np.uint64)
-    n = np.zeros(1, np.uint64)
-    a, b = ta.abi(), tb.abi()
-    _check(lib().ref_merkle_diff(C.byref(a), C.byref(b), _p(out, _abi.P64), cap, _p(n, _abi.P64)),
-           "ref_merkle_diff")
-    return out[: int(n[0])]
+def merkle_diff(ta: Tree, ra, tb: Tree, rb, cap=None):
+    """The keys whose raw value maps differ (hash trees agree with the exact row-set diff
+    barring a 64-bit collision), ascending; with `cap`: (first cap keys, total) -- the
+    reference's Enum.take(keys, max_sync_size), causal_crdt.ex:105,206-210."""
+    assert (ta.depth, ta.shard_bits, ta.shard) == (tb.depth, tb.shard_bits, tb.shard)
+    d = store_diff(ra, rb)
+    return d if cap is None else (d[:cap], len(d))
+
+
+def fold_roots(roots):
+    """The unsharded root from 2^b shard roots (shard order)."""
+    lv = [int(x) for x in roots]
+    while len(lv) > 1:
+        lv = [int(lib().ref_node_hash(lv[2 * i], lv[2 * i + 1])) for i in range(len(lv) // 2)]
+    return lv[0]
+
+
+def leaf_pairs(rows, tree: Tree, buckets):
+    """(key, Σ row hash) of every key of `rows` in the given buckets, ascending."""
+    k = rows[0]
+    b = tree.bucket_of(k)
+    m = np.isin(b, np.asarray(buckets, np.int64))
+    keys, hs = [], []
+    for i in np.flatnonzero(m):
+        h = int(lib().ref_row_hash(int(k[i]), int(rows[1][i]), int(rows[2][i]), int(rows[3][i]),
+                                   int(rows[4][i])))
+        if keys and keys[-1] == int(k[i]):
+            hs[-1] = (hs[-1] + h) & ((1 << 64) - 1)
+        else:
+            keys.append(int(k[i]))
+            hs.append(h)
+    return np.array(keys, np.uint64), np.array(hs, np.uint64)
+
+
+def merkle_prepare(t: Tree, levels):
+    """prepare_partial_diff: ("node", level, positions, hashes) of level min(levels, depth)."""
+    L = min(levels, t.depth)
+    return ("node", L, np.arange(1 << L, dtype=np.uint64), t.level(L).copy())
+
+
+def merkle_continue(t: Tree, rows, cont, levels):
+    """continue_partial_diff on the receiver (tree t over rows) -- the protocol
+    include/deltagpu.h documents: ("ok", keys) or ("continue", cont')."""
+    if cont[0] == "leaf":
+        _, buckets, pk, ph = cont
+        own_k, own_h = leaf_pairs(rows, t, buckets)
+        mine = dict(zip(own_k.tolist(), own_h.tolist()))
+        theirs = dict(zip(np.asarray(pk).tolist(), np.asarray(ph).tolist()))
+        keys = sorted(k for k in set(mine) | set(theirs) if mine.get(k) != theirs.get(k))
+        return ("ok", np.array(keys, np.uint64))
+    _, L, pos, hs = cont
+    own = t.level(L)[np.asarray(pos, np.int64)]
+    dpos = np.asarray(pos, np.uint64)[own != np.asarray(hs, np.uint64)]
+    if len(dpos) == 0:
+        return ("ok", np.zeros(0, np.uint64))
+    if L < t.depth:
+        k = min(levels, t.depth - L)
+        child = ((dpos[:, None] << np.uint64(k)) | np.arange(1 << k, dtype=np.uint64)[None, :]).ravel()
+        return ("continue", ("node", L + k, child, t.level(L + k)[child.astype(np.int64)].copy()))
+    pk, ph = leaf_pairs(rows, t, dpos)
+    return ("continue", ("leaf", dpos, pk, ph))
 
 
 def store_diff(ra, rb):

@@ -30,7 +30,7 @@ def test_every_header_function_is_exported(lib):
 
 
 def test_abi_version(lib):
-    assert lib.dg_abi_version() == 1
+    assert lib.dg_abi_version() == 2
 
 
 LAYOUT_C = r"""
@@ -45,8 +45,12 @@ int main(void) {
   printf("dg_context %zu\n", sizeof(dg_context));
   F(dg_context, kind) F(dg_context, node) F(dg_context, cnt) F(dg_context, n) F(dg_context, cap)
   printf("dg_merkle %zu\n", sizeof(dg_merkle));
-  F(dg_merkle, depth) F(dg_merkle, nodes) F(dg_merkle, bucket_off) F(dg_merkle, leaf_key)
-  F(dg_merkle, leaf_hash) F(dg_merkle, n_keys) F(dg_merkle, cap_keys)
+  F(dg_merkle, depth) F(dg_merkle, shard_bits) F(dg_merkle, shard) F(dg_merkle, nodes)
+  F(dg_merkle, n_keys)
+  printf("dg_merkle_cont %zu\n", sizeof(dg_merkle_cont));
+  F(dg_merkle_cont, level) F(dg_merkle_cont, pos) F(dg_merkle_cont, hash) F(dg_merkle_cont, n)
+  F(dg_merkle_cont, cap) F(dg_merkle_cont, bucket) F(dg_merkle_cont, n_buckets)
+  F(dg_merkle_cont, cap_buckets)
   return 0;
 }
 """
@@ -63,7 +67,7 @@ def test_struct_layout_matches_header():
     for line in out.strip().splitlines():
         name, v = line.split()
         want[name] = int(v)
-    for cls in (_abi.dg_store, _abi.dg_context, _abi.dg_merkle):
+    for cls in (_abi.dg_store, _abi.dg_context, _abi.dg_merkle, _abi.dg_merkle_cont):
         assert C.sizeof(cls) == want[cls.__name__]
         for fname, _ in cls._fields_:
             key = f"{cls.__name__}.{fname}"

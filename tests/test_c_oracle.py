@@ -130,17 +130,60 @@ def test_joink_is_left_fold(seed):
 
 
 @pytest.mark.parametrize("seed", range(5))
-def test_merkle_diff_is_exact_store_diff(seed):
+def test_merkle_tree_differs_exactly_above_differing_keys(seed):
     rng = np.random.default_rng(seed)
     a, b = W.random_pair(rng, n_keys=300, ts_range=1 << 30)
+    d = R.store_diff(a["rows"], b["rows"])
     for depth in (1, 3, 8, 12):
         ta, tb = R.merkle_build(a["rows"], depth), R.merkle_build(b["rows"], depth)
-        d = R.merkle_diff(ta, tb)
-        assert np.array_equal(d, R.store_diff(a["rows"], b["rows"]))
-        same = R.merkle_diff(ta, R.merkle_build(a["rows"], depth))
-        assert len(same) == 0
-        # roots differ iff the stores differ
+        # the differing buckets are exactly the buckets of the differing keys
+        diff_b = np.flatnonzero(ta.level(depth) != tb.level(depth))
+        assert np.array_equal(diff_b, np.unique(ta.bucket_of(d)))
+        assert np.array_equal(R.merkle_diff(ta, a["rows"], tb, b["rows"]), d)
+        same = R.merkle_build(a["rows"], depth)
+        assert np.array_equal(same.nodes, ta.nodes)
         assert (ta.nodes[0] != tb.nodes[0]) == (len(d) > 0)
+        assert ta.n_keys == len(np.unique(a["rows"][0]))
+        keys, total = R.merkle_diff(ta, a["rows"], tb, b["rows"], cap=7)
+        assert total == len(d) and np.array_equal(keys, d[:7])
+
+
+@pytest.mark.parametrize("bits", [1, 2, 3])
+def test_merkle_shard_trees_fold_to_the_unsharded_root(bits):
+    from delta_crdt_ex_amd.sharding import shard_of
+    a, _ = W.merkle_pair(n_keys=4000, seed=bits)
+    depth = 10
+    whole = R.merkle_build(a["rows"], depth)
+    roots = []
+    for s in range(1 << bits):
+        m = shard_of(a["rows"][0], 1 << bits) == s
+        t = R.merkle_build(tuple(c[m] for c in a["rows"]), depth - bits, bits, s)
+        assert np.array_equal(t.nodes[0:1], whole.level(bits)[s:s + 1])
+        roots.append(int(t.nodes[0]))
+    assert R.fold_roots(roots) == int(whole.nodes[0])
+    with pytest.raises(RuntimeError):  # a row outside the shard
+        R.merkle_build(a["rows"], depth - bits, bits, 0)
+
+
+@pytest.mark.parametrize("levels", [1, 3, 8])
+def test_merkle_partial_diff_protocol_ends_in_the_diff(levels):
+    a, b = W.merkle_pair(n_keys=3000, diff_frac=0.02, seed=levels)
+    d = R.store_diff(a["rows"], b["rows"])
+    depth = 9
+    ta, tb = R.merkle_build(a["rows"], depth), R.merkle_build(b["rows"], depth)
+    # A prepares, B continues, A continues, ... (the ping-pong of causal_crdt.ex:91-110)
+    cont = R.merkle_prepare(ta, levels)
+    side = [(tb, b["rows"]), (ta, a["rows"])]
+    hops = 0
+    while True:
+        t, rows = side[hops % 2]
+        res = R.merkle_continue(t, rows, cont, levels)
+        hops += 1
+        if res[0] == "ok":
+            break
+        cont = res[1]
+    assert np.array_equal(res[1], d)
+    assert hops == -(-depth // levels) + 1  # node hops down to the buckets, then the leaf hop
 
 
 # ------------------------------------------------------------- generators vs term replay

@@ -156,7 +156,7 @@ def test_config4_shard_anti_entropy_round(rank):
     a, b = W.config4_shard(rank, 4, keys_per_rank=600, diff_frac=0.05)
     diff = R.store_diff(a["rows"], b["rows"])
     ta, tb = R.merkle_build(a["rows"], 8), R.merkle_build(b["rows"], 8)
-    assert np.array_equal(R.merkle_diff(ta, tb), diff)
+    assert np.array_equal(R.merkle_diff(ta, a["rows"], tb, b["rows"]), diff)
     d = W.sync_delta(b, diff)
     rows, ctx = R.apply_deltas(a["rows"], a["ctx"], [d["rows"]], [d["ctx"]], [d["keys"]])
     frows, fctx = R.join2(a["rows"], a["ctx"], b["rows"], b["ctx"])

@@ -114,7 +114,8 @@ def test_config4_shard_round(engine, rank):
     a, b = W.config4_shard(rank, 8, keys_per_rank=50_000, diff_frac=0.01)
     sa, ca = up(a)
     sb, cb = up(b)
-    ta, tb = engine.merkle_build(sa, 14), engine.merkle_build(sb, 14)
+    ta = engine.merkle_build(sa, 11, shard_bits=3, shard=rank)
+    tb = engine.merkle_build(sb, 11, shard_bits=3, shard=rank)
     diff = engine.merkle_diff(ta, tb)
     want = R.store_diff(a["rows"], b["rows"])
     assert np.array_equal(u64(diff), want)
@@ -150,7 +151,8 @@ def test_config4_round_device_resident(engine, rank):
     a, b = W.config4_shard(rank, 8, keys_per_rank=80_000, diff_frac=0.01)
     sa, ca = up(a)
     sb, cb = up(b)
-    diff = engine.merkle_diff(engine.merkle_build(sa, 14), engine.merkle_build(sb, 14))
+    diff = engine.merkle_diff(engine.merkle_build(sa, 11, shard_bits=3, shard=rank),
+                              engine.merkle_build(sb, 11, shard_bits=3, shard=rank))
     delta = engine.take_keys(sb, diff)
     out, octx = engine.join2(sa, ca, delta, cb, keys=diff)
     wr, wc = R.join2(a["rows"], a["ctx"], b["rows"], b["ctx"])

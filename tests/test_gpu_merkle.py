@@ -1,0 +1,202 @@
+"""The MerkleMap role on the GPU (csrc/merkle.hip) against the C oracle
+(oracle/deltaref.c ref_merkle_build, oracle/ref.py): build, incremental
+put/delete + update_hashes from a join's changed keys (causal_crdt.ex:383-394),
+the truncating diff (max_sync_size, :98,105,206-214), the partial-diff ping-pong
+(prepare_partial_diff / continue_partial_diff / truncate_diff, :91-110,252-289) and
+key-hash shard trees that fold to the unsharded root.  The hash itself
+is "parity unpinned" (merkle_map 0.2.0 is not vendored); the GPU tree is bit-exact
+against the C restatement of the same hash, and the differing keys are exactly the
+keys whose raw value maps differ."""
+import numpy as np
+import pytest
+import torch
+
+from delta_crdt_ex_amd import workloads as W
+from delta_crdt_ex_amd._abi import DeltaGpuError
+from delta_crdt_ex_amd.sharding import shard_of
+from delta_crdt_ex_amd.store import Context, Store, fold_roots, u64
+from oracle import ref as R
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def up(rep):
+    rows, ctx = rep["rows"], rep["ctx"]
+    return Store.from_numpy(*rows, device=DEV), Context.from_numpy(ctx[0], ctx[1], ctx[2], DEV)
+
+
+def nodes(t):
+    return t.nodes.cpu().numpy().view(np.uint64)
+
+
+def keys_dev(k):
+    return torch.from_numpy(np.ascontiguousarray(np.asarray(k, np.uint64)).view(np.int64)).to(DEV)
+
+
+@pytest.mark.parametrize("depth", [1, 5, 8, 11, 12, 16, 20])
+def test_build_and_diff(engine, depth):
+    a, b = W.merkle_pair(n_keys=20000, diff_frac=0.01, seed=depth)
+    sa, _ = up(a)
+    sb, _ = up(b)
+    ta, tb = engine.merkle_build(sa, depth), engine.merkle_build(sb, depth)
+    ra, rb = R.merkle_build(a["rows"], depth), R.merkle_build(b["rows"], depth)
+    for t, r in ((ta, ra), (tb, rb)):
+        assert t.n_keys == r.n_keys
+        assert np.array_equal(nodes(t), r.nodes)
+    d = engine.merkle_diff(ta, tb)
+    assert np.array_equal(u64(d), R.store_diff(a["rows"], b["rows"]))
+    assert engine.merkle_diff(ta, ta).numel() == 0
+
+
+def test_build_edges(engine):
+    # empty store, one row, every row in one bucket, rows at both ends of the key space
+    for rows in (tuple(np.zeros(0, dt) for dt in (np.uint64, np.uint64, np.int64, np.uint32, np.uint64)),
+                 (np.array([5], np.uint64), np.array([1], np.uint64), np.array([-3], np.int64),
+                  np.array([2], np.uint32), np.array([9], np.uint64))):
+        s = Store.from_numpy(*rows, device=DEV)
+        s.n = len(rows[0])
+        for depth in (1, 9):
+            t = engine.merkle_build(s, depth)
+            assert np.array_equal(nodes(t), R.merkle_build(rows, depth).nodes)
+    k = np.array([0, 1, 2, 3, (1 << 64) - 2, (1 << 64) - 1], np.uint64)
+    rows = (k, k, k.view(np.int64), (k & np.uint64(7)).astype(np.uint32), k)
+    s = Store.from_numpy(*rows, device=DEV)
+    for depth in (1, 4, 20):
+        assert np.array_equal(nodes(engine.merkle_build(s, depth)), R.merkle_build(rows, depth).nodes)
+    # runs of one bucket across many 64-row chunks (the atomic-add path)
+    a, _ = W.merkle_pair(n_keys=50000, seed=9)
+    sa, _ = up(a)
+    for depth in (2, 6):
+        assert np.array_equal(nodes(engine.merkle_build(sa, depth)), R.merkle_build(a["rows"], depth).nodes)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_update_after_join_equals_fresh_build(engine, seed):
+    """put/delete + update_hashes of dg_join2_changes's changed keys == dg_merkle_build
+    of the joined store, bit for bit."""
+    rng = np.random.default_rng(seed)
+    a, b = W.random_pair(rng, n_keys=3000, ts_range=8, dense_ctx=bool(seed % 2))
+    keys = None
+    if seed >= 2:  # a keyed sync delta: {VV, Map.take(value, keys)}, keys (causal_crdt.ex:324-335)
+        ks = np.unique(np.concatenate([a["rows"][0], b["rows"][0]]))
+        sel = ks[rng.random(len(ks)) < 0.5]
+        b = W.sync_delta(b, sel)
+        keys = keys_dev(sel)
+    sa, ca = up(a)
+    sb, cb = up(b)
+    for depth in (6, 12):
+        t = engine.merkle_build(sa, depth)
+        out, octx, changed = engine.join2_changes(sa, ca, sb, cb, keys=keys)
+        engine.merkle_update(t, out, changed)
+        fresh = engine.merkle_build(out, depth)
+        assert np.array_equal(nodes(t), nodes(fresh))
+        assert t.n_keys == fresh.n_keys
+        assert t.store is out
+
+
+def test_update_config2_scale(engine):
+    a, b = W.config2(n_keys=400_000, seed=11)
+    sa, ca = up(a)
+    sb, cb = up(b)
+    t = engine.merkle_build(sa, 17)
+    out, octx, changed = engine.join2_changes(sa, ca, sb, cb)
+    engine.merkle_update(t, out, changed)
+    assert np.array_equal(nodes(t), nodes(engine.merkle_build(out, 17)))
+    # no change: an update with no keys leaves the tree as it is
+    before = nodes(t).copy()
+    engine.merkle_update(t, out, keys_dev(np.zeros(0, np.uint64)))
+    assert np.array_equal(before, nodes(t))
+
+
+@pytest.mark.parametrize("cap", [0, 1, 5, 100, 10**6])
+def test_truncated_diff_is_the_prefix(engine, cap):
+    a, b = W.merkle_pair(n_keys=30000, diff_frac=0.05, seed=3)
+    sa, _ = up(a)
+    sb, _ = up(b)
+    ta, tb = engine.merkle_build(sa, 12), engine.merkle_build(sb, 12)
+    full = R.store_diff(a["rows"], b["rows"])
+    got, total = engine.merkle_diff(ta, tb, cap=cap, with_total=True)
+    assert total == len(full)
+    assert np.array_equal(u64(got), full[:cap])
+
+
+@pytest.mark.parametrize("levels,depth", [(8, 18), (3, 10), (1, 4), (8, 8)])
+def test_partial_diff_ping_pong(engine, levels, depth):
+    """A.prepare -> B.continue -> A.continue -> ... ends with the differing keys, hop
+    for hop equal to the oracle's continuations."""
+    a, b = W.merkle_pair(n_keys=40000, diff_frac=0.005, seed=levels)
+    sa, _ = up(a)
+    sb, _ = up(b)
+    ta, tb = engine.merkle_build(sa, depth), engine.merkle_build(sb, depth)
+    ra, rb = R.merkle_build(a["rows"], depth), R.merkle_build(b["rows"], depth)
+    cont = engine.merkle_prepare(ta, levels)
+    rc = R.merkle_prepare(ra, levels)
+    side = [(tb, rb, b["rows"]), (ta, ra, a["rows"])]
+    hops = 0
+    while True:
+        t, r, rows = side[hops % 2]
+        res = engine.merkle_continue(t, cont, levels)
+        rres = R.merkle_continue(r, rows, rc, levels)
+        hops += 1
+        assert res[0] == rres[0]
+        if res[0] == "ok":
+            break
+        cont, rc = res[1], rres[1]
+        if rc[0] == "node":
+            assert cont.level == rc[1] and not cont.leaf
+            assert np.array_equal(u64(cont.pos[: cont.n]), rc[2])
+            assert np.array_equal(u64(cont.hash[: cont.n]), rc[3])
+        else:
+            assert cont.level == depth + 1
+            assert np.array_equal(u64(cont.bucket[: cont.n_buckets]), rc[1])
+            assert np.array_equal(u64(cont.pos[: cont.n]), rc[2])
+            assert np.array_equal(u64(cont.hash[: cont.n]), rc[3])
+    full = R.store_diff(a["rows"], b["rows"])
+    assert np.array_equal(u64(res[1]), full) and res[2] == len(full)
+    assert np.array_equal(rres[1], full)
+
+
+def test_partial_diff_equal_trees_and_truncation(engine):
+    a, b = W.merkle_pair(n_keys=20000, diff_frac=0.02, seed=5)
+    sa, _ = up(a)
+    sb, _ = up(b)
+    ta, tb = engine.merkle_build(sa, 10), engine.merkle_build(sb, 10)
+    # identical trees: {:ok, []} on the first hop
+    res = engine.merkle_continue(engine.merkle_build(sa, 10), engine.merkle_prepare(ta, 8), 8)
+    assert res[0] == "ok" and res[1].numel() == 0
+    # truncate_diff of a node-form continuation keeps its first entries
+    c = engine.merkle_continue(tb, engine.merkle_prepare(ta, 4), 4)[1]
+    n0 = c.n
+    engine.merkle_truncate(tb, c, 3)
+    assert c.n == min(3, n0)
+    # leaf form: only the pairs of the first buckets are kept, and the keys that come
+    # out are the differing keys of those buckets
+    c = engine.merkle_continue(tb, engine.merkle_prepare(ta, 10), 10)[1]
+    assert c.leaf
+    bk = u64(c.bucket[: c.n_buckets])
+    engine.merkle_truncate(tb, c, 4)
+    assert c.n_buckets == 4
+    res = engine.merkle_continue(ta, c, 10)
+    full = R.store_diff(a["rows"], b["rows"])
+    want = full[np.isin(R.Tree(10).bucket_of(full), bk[:4].astype(np.int64))]
+    assert res[0] == "ok" and np.array_equal(u64(res[1]), want)
+
+
+@pytest.mark.parametrize("bits", [1, 3])
+def test_shard_trees_fold_to_the_unsharded_root(engine, bits):
+    a, _ = W.merkle_pair(n_keys=60000, seed=bits)
+    depth = 14
+    whole = engine.merkle_build(up(a)[0], depth)
+    roots = []
+    for s in range(1 << bits):
+        m = shard_of(a["rows"][0], 1 << bits) == s
+        rows = tuple(c[m] for c in a["rows"])
+        t = engine.merkle_build(Store.from_numpy(*rows, device=DEV), depth - bits, shard_bits=bits,
+                                shard=s)
+        assert np.array_equal(nodes(t), R.merkle_build(rows, depth - bits, bits, s).nodes)
+        roots.append(t.root())
+    assert fold_roots(roots) == whole.root()
+    with pytest.raises(DeltaGpuError):  # rows outside the tree's shard
+        engine.merkle_build(up(a)[0], depth - bits, shard_bits=bits, shard=0)

@@ -193,34 +193,6 @@ def test_large_dot_set_union(engine):
     ctx_eq(engine.compress_dots(cx), R.compress_dots(x))
 
 
-@pytest.mark.parametrize("depth", [1, 5, 8, 12, 16])
-def test_merkle_build_and_diff(engine, depth):
-    a, b = W.merkle_pair(n_keys=20000, diff_frac=0.01, seed=depth)
-    sa, _ = up(a)
-    sb, _ = up(b)
-    ta, tb = engine.merkle_build(sa, depth), engine.merkle_build(sb, depth)
-    ra, rb = R.merkle_build(a["rows"], depth), R.merkle_build(b["rows"], depth)
-    for t, r in ((ta, ra), (tb, rb)):
-        assert t.n_keys == r.n_keys
-        assert np.array_equal(u64(t.leaf_key[: t.n_keys]), r.leaf_key[: r.n_keys])
-        assert np.array_equal(u64(t.leaf_hash[: t.n_keys]), r.leaf_hash[: r.n_keys])
-        assert np.array_equal(u64(t.bucket_off), r.bucket_off)
-        assert np.array_equal(u64(t.nodes), r.nodes)
-    d = engine.merkle_diff(ta, tb)
-    assert np.array_equal(u64(d), R.merkle_diff(ra, rb))
-    assert np.array_equal(u64(d), R.store_diff(a["rows"], b["rows"]))
-    assert engine.merkle_diff(ta, ta).numel() == 0
-
-
-def test_merkle_diff_capacity(engine):
-    a, b = W.merkle_pair(n_keys=5000, diff_frac=0.1, seed=1)
-    sa, _ = up(a)
-    sb, _ = up(b)
-    ta, tb = engine.merkle_build(sa, 10), engine.merkle_build(sb, 10)
-    with pytest.raises(CapacityError):
-        engine.merkle_diff(ta, tb, cap=5)
-
-
 @pytest.mark.parametrize("seed", range(3))
 def test_joink(engine, seed):
     rng = np.random.default_rng(50 + seed)

@@ -115,3 +115,16 @@ def test_workload_node_ids_are_real_30bit_terms_interned_dense():
     # config 3: 65 replicas -> dense ids 0..64, inside the one-pass fold's node tables
     base, deltas = W.config3(n_keys=5000, n_replicas=64, touch=0.01, seed=3)
     assert max(int(d["ctx"][1].max()) for d in deltas) == 64
+
+
+def test_universe_tracks_device_stores_weakly():
+    import gc
+
+    from delta_crdt_ex_amd.store import Store
+    U = Universe()
+    s = Store.empty(4, "cpu")
+    U.track(s)
+    assert U.tracked() == [s]
+    del s
+    gc.collect()
+    assert U.tracked() == []

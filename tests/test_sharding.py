@@ -44,7 +44,9 @@ def test_fold_roots_matches_c_tree():
     a, _ = W.merkle_pair(n_keys=3000, seed=3)
     t = R.merkle_build(a["rows"], 3)
     lvl3 = t.nodes[7:15]
-    assert S.fold_roots(lvl3.tolist()) == int(t.nodes[0])
+    assert S.fold_roots(lvl3.tolist()) == int(t.nodes[0]) == R.fold_roots(lvl3)
+    with pytest.raises(ValueError):
+        S.fold_roots([1, 2, 3])
 
 
 def _worker(rank, world, port, q):
@@ -69,12 +71,16 @@ def _worker(rank, world, port, q):
             want_mine = S.split_rows(want_rows, world)[rank]
             for x, y in zip(rows, want_mine):
                 assert np.array_equal(x, y)
-            # Merkle: shard roots, replica root, and the diff restricted to differing shards
-            depth = 8
-            ta, tb = R.merkle_build(mine_a, depth), R.merkle_build(mine_b, depth)
+            # Merkle: shard trees over the shard's key range, roots, the replica root
+            # (== the unsharded tree's root), and the diff restricted to differing shards
+            depth, sb = 8, S.shard_bits(world)
+            ta = R.merkle_build(mine_a, depth - sb, sb, rank)
+            tb = R.merkle_build(mine_b, depth - sb, sb, rank)
             ra, root_a = S.merkle_roots(int(ta.nodes[0]))
             rb, root_b = S.merkle_roots(int(tb.nodes[0]))
-            diff_local = R.merkle_diff(ta, tb)
+            assert root_a == int(R.merkle_build(A["rows"], depth).nodes[0])
+            assert root_b == int(R.merkle_build(B["rows"], depth).nodes[0])
+            diff_local = R.merkle_diff(ta, mine_a, tb, mine_b)
             full = R.store_diff(A["rows"], B["rows"])
             assert np.array_equal(diff_local, S.split_rows((full,) * 5, world)[rank][0])
             assert (root_a != root_b) == (len(full) > 0)
