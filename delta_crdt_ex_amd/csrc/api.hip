@@ -829,8 +829,9 @@ int dg_merkle_build_async(dg_engine* e, const dg_store* s, dg_merkle* t, uint64_
   TRY(check_merkle(t, "dg_merkle_build"));
   if (!d_n_keys) return fail(DG_E_INVAL, "dg_merkle_build: null d_n_keys");
   TRY(set_device(e));
+  TRY(ensure_tmp(e, merkle_ctr_words(t->depth) * sizeof(u32)));
   HIP_TRY(hipMemsetAsync(e->ticket + 3, 0, sizeof(u32), e->stream));
-  HIP_TRY(launch_merkle_build(rows_of(s), merkle_of(t), d_n_keys, e->ticket, e->ticket + 3,
+  HIP_TRY(launch_merkle_build(rows_of(s), merkle_of(t), d_n_keys, (u32*)e->tmp, e->ticket + 3,
                               e->stream));
   return DG_OK;
 }
@@ -851,17 +852,18 @@ int dg_merkle_update(dg_engine* e, dg_merkle* t, const dg_store* old_s, const dg
   TRY(check_store(new_s, "dg_merkle_update new"));
   if (n_keys && !keys) return fail(DG_E_INVAL, "dg_merkle_update: null keys");
   TRY(set_device(e));
-  const u64 chunks = merkle_chunks(t->depth);
-  TRY(ensure_tmp(e, chunks * sizeof(u32)));
-  u32* dirty = (u32*)e->tmp;
+  const u64 chunks = merkle_chunks(t->depth), cw = merkle_ctr_words(t->depth);
+  TRY(ensure_tmp(e, (cw + chunks) * sizeof(u32)));
+  u32* ctr = (u32*)e->tmp;
+  u32* dirty = ctr + cw;
   HIP_TRY(hipMemsetAsync(dirty, 0, chunks * sizeof(u32), e->stream));
   HIP_TRY(hipMemsetAsync(e->ticket + 3, 0, sizeof(u32), e->stream));
-  HIP_TRY(hipMemsetAsync(e->d_counts, 0, sizeof(u64), e->stream));
+  HIP_TRY(hipMemsetAsync(e->d_counts, 0, 8 * sizeof(u64), e->stream));
   HIP_TRY(launch_merkle_update(merkle_of(t), rows_of(old_s), rows_of(new_s), keys, n_keys, dirty,
-                               e->d_counts, e->ticket, e->ticket + 3, e->stream));
-  TRY(read_counts(e, 1));
+                               e->d_counts, ctr, e->ticket + 3, e->stream));
+  TRY(read_counts(e, 8));
   TRY(input_error(e, "dg_merkle_update"));
-  t->n_keys += e->h_counts[0];  // a signed change, two's complement
+  for (int i = 0; i < 8; i++) t->n_keys += e->h_counts[i];  // signed changes, two's complement
   return DG_OK;
 }
 
@@ -877,9 +879,9 @@ int dg_merkle_diff(dg_engine* e, const dg_merkle* a, const dg_store* sa, const d
   if (!n_out) return fail(DG_E_INVAL, "dg_merkle_diff: null n_out");
   if (cap && !out_keys) return fail(DG_E_INVAL, "dg_merkle_diff: null out_keys");
   TRY(set_device(e));
-  TRY(ensure_state(e, diff_scratch_words(a->depth) + 2));  // tile counts, offsets, bucket counts
+  TRY(ensure_tmp(e, diff_scratch_words(a->depth, sa->n, sb->n) * sizeof(u64)));
   HIP_TRY(launch_merkle_diff(merkle_of(a), rows_of(sa), merkle_of(b), rows_of(sb), out_keys, cap,
-                             e->state, e->d_counts, e->stream));
+                             (u64*)e->tmp, e->d_counts, e->stream));
   TRY(read_counts(e, 1));
   const u64 total = e->h_counts[0];
   *n_out = std::min<u64>(total, cap);

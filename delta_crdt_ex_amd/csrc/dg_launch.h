@@ -156,19 +156,26 @@ struct MerkleT {
 };
 constexpr u32 MERKLE_UPL = 11;  // levels reduced per upsweep workgroup
 inline u64 merkle_chunks(u32 depth) { return 1ull << (depth - (depth < MERKLE_UPL ? depth : MERKLE_UPL)); }
-// bucket level zeroed, rows hashed into it, fused upsweep; *d_keys = distinct keys;
-// ctr: a device word left at 0; err bit 1: a row outside the tree's shard.
+// scratch u32 words of a build / update: the arrival counter (16 words) + a u64 chunk
+// root and a u64 key count per chunk (the in-launch hand-off)
+inline u64 merkle_ctr_words(u32 depth) { return 16 + 4 * merkle_chunks(depth); }
+// one fused launch: rows hashed into LDS bucket sums per chunk, levels reduced, the last
+// chunk reduces to the root; *d_keys = distinct keys; ctr: merkle_ctr_words(depth) u32
+// of scratch; err bit 1: a row outside the tree's shard.
 hipError_t launch_merkle_build(const Rows& s, const MerkleT& t, u64* d_keys, u32* ctr, u32* err,
                                hipStream_t st);
 // put/delete of the changed keys + update_hashes; dirty: merkle_chunks(depth) u32, zero
-// on entry and left zero; *d_keys += the change in distinct keys.
+// on entry; d_keys[0, 8) (zero on entry) sum to the change in distinct keys.
 hipError_t launch_merkle_update(const MerkleT& t, const Rows& olds, const Rows& news, const u64* keys,
                                 u64 n_keys, u32* dirty, u64* d_keys, u32* ctr, u32* err,
                                 hipStream_t st);
 constexpr int DIFF_BLOCK = 256;
 inline u64 diff_tiles(u32 depth) { return depth >= 8 ? (1ull << (depth - 8)) : 1ull; }
-// per-tile counts and offsets, then one u32 count per bucket
-inline u64 diff_scratch_words(u32 depth) { return 2 * diff_tiles(depth) + ((1ull << depth) + 1) / 2; }
+// tile boundaries in both stores, per-tile counts and offsets, then the differing keys
+// staged per tile (at most one per row of either store)
+inline u64 diff_scratch_words(u32 depth, u64 na, u64 nb) {
+  return 2 * (diff_tiles(depth) + 1) + 2 * diff_tiles(depth) + na + nb + 1;
+}
 // differing keys, ascending; the first min(total, cap) written; *d_count = total.
 hipError_t launch_merkle_diff(const MerkleT& a, const Rows& sa, const MerkleT& b, const Rows& sb,
                               u64* out_keys, u64 cap, u64* scratch, u64* d_count, hipStream_t st);

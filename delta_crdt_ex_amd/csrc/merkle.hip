@@ -78,83 +78,72 @@ __device__ __forceinline__ u64 rh(const Rows& s, u64 i) {
   return row_hash(s.key[i], s.val[i], s.ts[i], s.node[i], s.cnt[i]);
 }
 
-// ---------------------------------------------------------------- build
-constexpr int BB = 256;  // threads per build workgroup
-constexpr int BK = 4;    // 64-row chunks per wave
-
-// Wave-level segmented sum of (bucket, h) over the 64 lanes (lanes ordered by row).
-// Returns, in the LAST lane of each run, the run's sum.
-__device__ __forceinline__ u64 seg_sum(u64 b, u64 h, int lane) {
-#pragma unroll
-  for (int d = 1; d < WAVE; d <<= 1) {
-    const u64 ob = __shfl_up(b, d, WAVE);
-    const u64 oh = __shfl_up(h, d, WAVE);
-    if (lane >= d && ob == b) h += oh;
-  }
-  return h;
-}
-
-__global__ __launch_bounds__(BB) void merkle_build_kernel(Rows s, MT t, u64* d_keys, u32* err) {
+// ---------------------------------------------------------------- lower bounds
+// First index of keys[0, n) (ascending) that is >= x, by ONE wave: a 64-ary search
+// (every step probes 64 positions, one dependent load round: 12.5M rows in 4 rounds
+// instead of a 24-load binary-search chain).  Every lane returns the same value.
+__device__ __forceinline__ u64 wave_lower_bound(const u64* k, u64 n, u64 x) {
   const int lane = threadIdx.x & (WAVE - 1);
-  const u64 wave = ((u64)blockIdx.x * BB + threadIdx.x) / WAVE;
-  u64* lvl = t.nodes + ((1ull << t.depth) - 1);
-  u32 heads = 0;
-  bool bad = false;
-#pragma unroll
-  for (int k = 0; k < BK; k++) {
-    const u64 base = (wave * BK + k) * WAVE;
-    if (base >= s.n) break;
-    const u64 i = base + lane;
-    const bool valid = i < s.n;
-    u64 key = valid ? s.key[i] : ~0ull, h = 0;
-    if (valid) {
-      h = row_hash(key, s.val[i], s.ts[i], s.node[i], s.cnt[i]);
-      if (t.sb && (key >> (64 - t.sb)) != t.shard) bad = true;
-    }
-    // (every shuffle runs in all lanes: a shuffle from an inactive lane is undefined)
-    const u64 up = __shfl_up(key, 1, WAVE);
-    const u64 prev_key = lane ? up : (i > 0 && valid ? s.key[i - 1] : ~key);
-    heads += (valid && (i == 0 || prev_key != key)) ? 1u : 0u;
-    const u64 b = valid ? bucket_of(t, key) : ~0ull;
-    const u64 sum = seg_sum(b, h, lane);
-    const u64 nb = __shfl_down(b, 1, WAVE);
-    const u64 first_b = __shfl(b, 0, WAVE);
-    const u64 end_b = __shfl(b, WAVE - 1, WAVE);
-    const bool last = valid && (lane == WAVE - 1 || nb != b);  // last lane of its run
-    if (last) {
-      // a run that touches the chunk's first or last row may share its bucket with the
-      // neighbouring chunk: atomic add (the level was zeroed); an inner run owns it
-      const bool shared = b == first_b || b == end_b || i + 1 == s.n;
-      if (shared)
-        atomicAdd((unsigned long long*)&lvl[b], (unsigned long long)sum);
-      else
-        lvl[b] = sum;
-    }
+  u64 lo = 0, hi = n;
+  while (hi - lo > WAVE) {
+    const u64 span = hi - lo;
+    const u64 p = lo + span * (u64)(lane + 1) / (WAVE + 1);
+    const u64 m = __ballot(k[p] < x);  // true on a prefix of the lanes
+    const int c = __popcll(m);
+    const u64 nlo = c ? lo + span * (u64)c / (WAVE + 1) + 1 : lo;
+    const u64 nhi = c < WAVE ? lo + span * (u64)(c + 1) / (WAVE + 1) : hi;
+    lo = nlo;
+    hi = nhi;
   }
-  // distinct keys: wave sum of heads -> one atomic per wave
-  u32 c = heads;
-#pragma unroll
-  for (int d = WAVE / 2; d >= 1; d >>= 1) c += __shfl_xor(c, d, WAVE);
-  if (lane == 0 && c) atomicAdd((unsigned long long*)d_keys, (unsigned long long)c);
-  if (__ballot(bad) && lane == 0) atomicOr(err, 2u);
+  const bool lt = lo + lane < hi && k[lo + lane] < x;
+  return lo + (u64)__popcll(__ballot(lt));
 }
 
-// ---------------------------------------------------------------- upsweep
-constexpr int UPB = 512;   // threads per upsweep workgroup
-constexpr int UPL = 11;    // levels reduced per workgroup (2048 nodes in LDS)
+// wave_lower_bound of bucket b's first key (b may be 2^depth: the end of the range).
+__device__ __forceinline__ u64 wave_bucket_start(const MT& t, const u64* keys, u64 n, u64 b) {
+  if (b >> t.depth) {
+    if (t.sb == 0 || t.shard == (1ull << t.sb) - 1) return n;
+    return wave_lower_bound(keys, n, (t.shard + 1) << (64 - t.sb));
+  }
+  const u64 base = t.sb ? (t.shard << (64 - t.sb)) : 0ull;
+  return wave_lower_bound(keys, n, base + (b << (64 - t.sb - t.depth)));
+}
+
+// ---------------------------------------------------------------- build / upsweep
+// One workgroup per chunk of 2^L1 buckets (L1 = min(UPL, depth)).  BUILD: the chunk's
+// rows (a contiguous range: two wave lower bounds) are hashed into LDS bucket sums
+// (LDS atomic adds; no global atomics), UPDATE: the chunk's bucket level is read back
+// (merkle_update_kernel has added the changed keys' deltas) -- only where the chunk is
+// dirty.  Then L1 levels are reduced in LDS and written.  The last workgroup to finish
+// reduces the chunk roots to the root and, for BUILD, sums the per-chunk distinct-key
+// counts.  Hand-off (MI355X_MICROARCH.md "Valid forms", hand-off table row 1): ONE lane
+// per workgroup stores the chunk's root and key count write-through (sc1), waits for
+// them, then adds to ONE arrival counter; the workgroup whose add returns last reads the
+// roots and counts with sc1 loads.  No release fence per workgroup: an agent release
+// in each of 2048 workgroups cost 75 us of a 219 us build (rocprofv3 A/B).
+constexpr int UPB = 512;   // threads per chunk workgroup
+constexpr int UPL = MERKLE_UPL;  // levels reduced per workgroup (2048 nodes in LDS)
 constexpr u32 UPW = 1u << UPL;
 
-// Reduce `width` (power of two, <= UPW) nodes of level `hi` starting at node index g0
-// (within the level) by log2(width) levels in LDS, writing every produced level.
-__device__ void upsweep_chunk(u64* nodes, u32 hi, u64 g0, u32 width, u64* s) {
-  const u64* src = nodes + ((1ull << hi) - 1) + g0;
-  for (u32 x = threadIdx.x; x < width; x += UPB) s[x] = src[x];
-  __syncthreads();
+__device__ __forceinline__ void wait_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ void st_sc1(u64* p, u64 v) {
+  __hip_atomic_store((__attribute__((address_space(1))) u64*)p, v, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ u64 ld_sc1(const u64* p) {
+  return __hip_atomic_load((__attribute__((address_space(1))) u64*)p, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// s[0, width) holds level `hi` nodes g0 .. g0+width-1; reduce log2(width) levels in LDS
+// and write every produced level (s ends with the subtree root in s[0]).
+__device__ void lds_upsweep(u64* nodes, u32 hi, u64 g0, u32 width, u64* s) {
   u32 l = 0;
   for (u32 cnt = width >> 1; cnt >= 1; cnt >>= 1) {
     l++;
     u64* dst = nodes + ((1ull << (hi - l)) - 1) + (g0 >> l);
-    u64 v[UPW / UPB / 2 > 0 ? UPW / UPB / 2 : 1];
+    u64 v[UPW / UPB / 2];
     int nv = 0;
     for (u32 x = threadIdx.x; x < cnt; x += UPB) v[nv++] = node_hash(s[2 * x], s[2 * x + 1]);
     __syncthreads();
@@ -167,40 +156,132 @@ __device__ void upsweep_chunk(u64* nodes, u32 hi, u64 g0, u32 width, u64* s) {
   }
 }
 
-// Workgroup g reduces buckets [g * 2^L1, (g+1) * 2^L1) (L1 = min(UPL, depth)) when its
-// chunk is dirty (dirty == nullptr: every chunk); the last workgroup to finish reduces
-// the 2^(depth - L1) chunk roots to the root.  ctr is left at 0.
-__global__ __launch_bounds__(UPB) void merkle_upsweep_kernel(u64* nodes, u32 depth, u32* dirty,
-                                                             u32* ctr) {
+// scratch: ctr[0] the arrival counter (zeroed before the launch), then per chunk its
+// root and its distinct-key count (u64 each, at hand[0, G) and hand[G, 2G)).
+template <bool BUILD>
+__global__ __launch_bounds__(UPB) void merkle_chunk_kernel(Rows rows, MT t, const u32* dirty,
+                                                           u32* ctr, u64* hand, u64* d_keys,
+                                                           u32* err) {
   __shared__ u64 s[UPW];
+  __shared__ u64 s_rng[2];
+  __shared__ u32 s_red[UPB / WAVE];
   __shared__ u32 s_last;
-  const u32 L1 = depth < (u32)UPL ? depth : (u32)UPL;
-  const u64 g = blockIdx.x;
-  const bool work = dirty == nullptr || dirty[g] != 0;
-  if (work) upsweep_chunk(nodes, depth, g << L1, 1u << L1, s);
-  __threadfence();  // every thread's node stores complete before the block signals
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    if (dirty) dirty[g] = 0;
-    const u32 done = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = done == gridDim.x - 1;
+  const u32 L1 = t.depth < (u32)UPL ? t.depth : (u32)UPL;
+  const u32 width = 1u << L1;
+  const u64 g = blockIdx.x, g0 = g << L1, G = gridDim.x;
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
+  u64* lvl = t.nodes + ((1ull << t.depth) - 1);
+  u64 chunk_root = 0, chunk_keys = 0;
+  if (BUILD) {
+    for (u32 x = tid; x < width; x += UPB) s[x] = 0;
+    if (w < 2) {
+#ifdef MK_INTERP  // timing experiment only: interpolated (inexact) chunk bounds
+      const u64 r = (u64)((double)rows.n * (double)(g + w) / (double)gridDim.x);
+#else
+      const u64 r = wave_bucket_start(t, rows.key, rows.n, g0 + (w ? width : 0));
+#endif
+      if (lane == 0) s_rng[w] = r;
+    }
+    __syncthreads();
+    const u64 lo = s_rng[0], hi = s_rng[1];
+    u32 heads = 0;
+    // rows outside the tree's key range (before the first chunk, after the last one)
+    bool bad = tid == 0 && ((g == 0 && lo > 0) || (g == G - 1 && hi < rows.n));
+    for (u64 i0 = lo; i0 < hi; i0 += 4 * UPB) {
+      u64 key[4], h[4];
+      bool head[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {  // four rows in flight per thread
+        const u64 i = i0 + (u64)q * UPB + tid;
+        key[q] = 0;
+        h[q] = 0;
+        head[q] = false;
+        if (i < hi) {
+          key[q] = rows.key[i];
+          h[q] = row_hash(key[q], rows.val[i], rows.ts[i], rows.node[i], rows.cnt[i]);
+          head[q] = i == lo || rows.key[i - 1] != key[q];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const u64 i = i0 + (u64)q * UPB + tid;
+        if (i < hi) {
+          if (t.sb && (key[q] >> (64 - t.sb)) != t.shard) bad = true;
+          const u64 b = bucket_of(t, key[q]) - g0;
+          if (b < width) atomicAdd((unsigned long long*)&s[b], (unsigned long long)h[q]);
+          heads += head[q] ? 1u : 0u;
+        }
+      }
+    }
+    // distinct keys of the chunk (keys of different chunks differ: a key fixes its bucket)
+    u32 c = heads;
+#pragma unroll
+    for (int d = WAVE / 2; d >= 1; d >>= 1) c += __shfl_xor(c, d, WAVE);
+    if (lane == 0) s_red[w] = c;
+    if (__ballot(bad) && lane == 0) atomicOr(err, 2u);
+    __syncthreads();
+    if (tid == 0)
+      for (int q = 0; q < UPB / WAVE; q++) chunk_keys += s_red[q];
+    for (u32 x = tid; x < width; x += UPB) lvl[g0 + x] = s[x];
+#ifndef MK_NO_UPSWEEP  // timing experiment only
+    lds_upsweep(t.nodes, t.depth, g0, width, s);
+#endif
+    chunk_root = s[0];
+  } else if (dirty[g]) {
+    for (u32 x = tid; x < width; x += UPB) s[x] = lvl[g0 + x];
+    __syncthreads();
+    lds_upsweep(t.nodes, t.depth, g0, width, s);
+    chunk_root = s[0];
+  } else if (tid == 0) {  // unchanged: its root as the previous kernels left it
+    chunk_root = t.nodes[((1ull << (t.depth - L1)) - 1) + g];
+  }
+  // ---- hand the chunk root (and key count) to the last workgroup
+  if (tid == 0) {
+    st_sc1(hand + g, chunk_root);
+    if (BUILD) st_sc1(hand + G + g, chunk_keys);
+    wait_vmem();
+    s_last = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1;
   }
   __syncthreads();
   if (!s_last) return;
-  __threadfence();
-  // the remaining levels: depth - L1 -> 0, UPL levels per round
-  u32 hi = depth - L1;
-  while (hi > 0) {
-    const u32 nlev = hi < (u32)UPL ? hi : (u32)UPL;
-    const u64 chunks = 1ull << (hi - nlev);
-    for (u64 c = 0; c < chunks; c++) upsweep_chunk(nodes, hi, c << nlev, 1u << nlev, s);
-    hi -= nlev;
+  // ---- the last workgroup: levels depth - L1 .. 0, UPL levels per round; the first
+  // round's inputs are the handed-off chunk roots (sc1 loads)
+  u32 hl = t.depth - L1;
+  bool first = true;
+  while (hl > 0) {
+    const u32 nlev = hl < (u32)UPL ? hl : (u32)UPL;
+    const u64 chunks = 1ull << (hl - nlev);
+    const u64* src = t.nodes + ((1ull << hl) - 1);
+    wait_vmem();  // this workgroup's own stores of level hl (depth > 2 * UPL) are complete
+    __syncthreads();
+    for (u64 c = 0; c < chunks; c++) {
+      for (u32 x = tid; x < (1u << nlev); x += UPB)
+        s[x] = first ? ld_sc1(hand + (c << nlev) + x) : src[(c << nlev) + x];
+      __syncthreads();
+      lds_upsweep(t.nodes, hl, c << nlev, 1u << nlev, s);
+    }
+    hl -= nlev;
+    first = false;
   }
-  if (threadIdx.x == 0) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (BUILD) {
+    u64 sum = 0;
+    for (u64 x = tid; x < G; x += UPB) sum += ld_sc1(hand + G + x);
+#pragma unroll
+    for (int d = WAVE / 2; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, WAVE);
+    __syncthreads();
+    if (lane == 0) s[w] = sum;
+    __syncthreads();
+    if (tid == 0) {
+      u64 tot = 0;
+      for (int q = 0; q < UPB / WAVE; q++) tot += s[q];
+      *d_keys = tot;
+    }
+  }
 }
 
 // ---------------------------------------------------------------- update
 constexpr int UB = 256;
+
 
 // Σ row_hash of key x's rows in s (0 if absent); *present = x has rows.
 __device__ __forceinline__ u64 key_leaf(const Rows& s, u64 x, bool* present) {
@@ -237,8 +318,10 @@ __global__ __launch_bounds__(UB) void merkle_update_kernel(MT t, Rows olds, Rows
   int c = dk;
 #pragma unroll
   for (int d = WAVE / 2; d >= 1; d >>= 1) c += __shfl_xor(c, d, WAVE);
+  // 8 count shards (one word takes ~88 same-address atomics per us): d_keys[0, 8)
   if ((threadIdx.x & (WAVE - 1)) == 0 && c)
-    atomicAdd((unsigned long long*)d_keys, (unsigned long long)(long long)c);
+    atomicAdd((unsigned long long*)&d_keys[(blockIdx.x * (UB / WAVE) + threadIdx.x / WAVE) & 7],
+              (unsigned long long)(long long)c);
   if (__ballot(bad) && (threadIdx.x & (WAVE - 1)) == 0) atomicOr(err, 2u);
 }
 
@@ -275,52 +358,166 @@ __device__ u32 merge_bucket(const Rows& A, u64 ia, u64 ie, const Rows& B, const 
 }
 
 // ---------------------------------------------------------------- full diff
+// Tiles of 256 buckets, one thread per bucket.
+//  1. bounds: one wave per tile boundary finds the boundary's first row in both stores
+//     (a 64-ary wave lower bound: 4 dependent load rounds at 12.5M rows).
+//  2. count: a tile whose level-(depth-8) subtree root matches in both trees is
+//     skipped.  Otherwise the tile's key columns are staged in LDS, each thread finds its
+//     bucket's rows there, the rows of the DIFFERING buckets are listed and hashed by
+//     all threads at once (one round of independent loads instead of a dependent chain
+//     per bucket), and each differing bucket merges its keys' leaves from LDS.  The
+//     tile's differing keys go to scratch at (A start + B start) of the tile, which is
+//     unique and increasing across tiles.
+//  3. scan of the per-tile counts; 4. copy: each tile's keys to their output offset,
+//     the keys past `cap` counted, not written (truncation to max_sync_size).
+// A tile whose rows do not fit the LDS stage (far fewer buckets than keys/3) falls back
+// to per-bucket merges over global memory.
 constexpr int DB = DIFF_BLOCK;
+constexpr u32 DCAP = 1024;  // rows per store staged in LDS
 
 struct DiffArgs {
   MT ta, tb;
   Rows sa, sb;
   u64* out;
   u64 cap;
-  u64* cnt;  // differing keys per tile
-  u64* off;  // their output offset
-  u32* bc;   // differing keys per bucket (the count pass's walk, reused by the write pass)
+  u64* bnd;   // ntiles + 1 boundaries x 2 stores: first row of each tile in A, then in B
+  u64* cnt;   // differing keys per tile
+  u64* off;   // their output offset
+  u64* keys;  // scratch: nA + nB keys
   u64 ntiles;
   u64* d_count;
 };
 
 __device__ __forceinline__ u64 diff_bpt(u32 depth) { return depth >= 8 ? 256ull : (1ull << depth); }
 
-__device__ __forceinline__ u64 diff_bucket_of(const DiffArgs& p, u64 tile, int tid, bool* walk) {
-  const u32 depth = p.ta.depth;
-  const u32 rl = depth >= 8 ? depth - 8 : 0;  // subtree root level
-  const u64 root = ((1ull << rl) - 1) + tile;
-  const u64 nbk = 1ull << depth;
-  const u64 b = tile * diff_bpt(depth) + tid;
-  *walk = false;
-  if ((u64)tid < diff_bpt(depth) && p.ta.nodes[root] != p.tb.nodes[root]) {
-    const u64 leaf = (nbk - 1) + b;
-    *walk = p.ta.nodes[leaf] != p.tb.nodes[leaf];
+// lower bound of x in keys[0, n) (LDS or global; n small)
+__device__ __forceinline__ u32 lb_small(const u64* k, u32 n, u64 x) {
+  u32 lo = 0, hi = n;
+  while (lo < hi) {
+    const u32 mid = (lo + hi) >> 1;
+    if (k[mid] < x)
+      lo = mid + 1;
+    else
+      hi = mid;
   }
-  return b;
+  return lo;
 }
 
-template <bool WRITE>
-__device__ __forceinline__ u32 diff_walk(const DiffArgs& p, u64 b, u64 o) {
-  const u64 ia = bucket_start(p.ta, p.sa.key, p.sa.n, b), ie = bucket_start(p.ta, p.sa.key, p.sa.n, b + 1);
-  const u64 jb = bucket_start(p.tb, p.sb.key, p.sb.n, b), je = bucket_start(p.tb, p.sb.key, p.sb.n, b + 1);
-  return merge_bucket<false, WRITE>(p.sa, ia, ie, p.sb, nullptr, nullptr, jb, je, p.out, o, p.cap);
+__device__ __forceinline__ u64 bucket_first_key(const MT& t, u64 b) {
+  const u64 base = t.sb ? (t.shard << (64 - t.sb)) : 0ull;
+  return base + (b << (64 - t.sb - t.depth));
+}
+
+__global__ __launch_bounds__(256) void merkle_diff_bounds_kernel(DiffArgs p) {
+  const u64 i = ((u64)blockIdx.x * 256 + threadIdx.x) / WAVE;  // one wave per boundary
+  const u64 nbnd = p.ntiles + 1;
+  if (i >= 2 * nbnd) return;  // uniform per wave
+  const bool B = i >= nbnd;
+  const u64 t = B ? i - nbnd : i;
+  const Rows& r = B ? p.sb : p.sa;
+  const u64 x = wave_bucket_start(p.ta, r.key, r.n, t * diff_bpt(p.ta.depth));
+  if ((threadIdx.x & (WAVE - 1)) == 0) p.bnd[i] = x;
 }
 
 __global__ __launch_bounds__(DB) void merkle_diff_count_kernel(DiffArgs p) {
+  __shared__ u64 s_ka[DCAP], s_kb[DCAP], s_ha[DCAP], s_hb[DCAP];
+  __shared__ uint16_t s_list[2 * DCAP];  // rows to hash: bit 15 = store B
   __shared__ u32 s_wave[DB / WAVE + 1];
-  bool walk;
-  const u64 b = diff_bucket_of(p, blockIdx.x, threadIdx.x, &walk);
-  const u32 c = walk ? diff_walk<false>(p, b, 0) : 0u;
-  if ((u64)threadIdx.x < diff_bpt(p.ta.depth)) p.bc[b] = c;
-  u32 tot;
-  block_excl_scan<DB>(c, s_wave, &tot);
-  if (threadIdx.x == 0) p.cnt[blockIdx.x] = tot;
+  const u32 depth = p.ta.depth;
+  const u64 tile = blockIdx.x, bpt = diff_bpt(depth), b0 = tile * bpt;
+  const int tid = threadIdx.x;
+  const u32 rl = depth >= 8 ? depth - 8 : 0;
+  const u64 root = ((1ull << rl) - 1) + tile;
+  if (p.ta.nodes[root] == p.tb.nodes[root]) {  // uniform: the whole tile matches
+    if (tid == 0) p.cnt[tile] = 0;
+    return;
+  }
+  const u64 nbnd = p.ntiles + 1;
+  const u64 a0 = p.bnd[tile], a1 = p.bnd[tile + 1], c0 = p.bnd[nbnd + tile], c1 = p.bnd[nbnd + tile + 1];
+  const u64 base = a0 + c0;
+  const bool lds = a1 - a0 <= DCAP && c1 - c0 <= DCAP;  // uniform
+  const u32 na = (u32)(a1 - a0), nc = (u32)(c1 - c0);
+  const bool in = (u64)tid < bpt;
+  const u64 b = b0 + tid;
+  const u64 leaf = ((1ull << depth) - 1) + b;
+  const bool walk = in && p.ta.nodes[leaf] != p.tb.nodes[leaf];
+  const bool last = (u64)tid == bpt - 1;
+  const u64 lk = bucket_first_key(p.ta, b), hk = last ? 0 : bucket_first_key(p.ta, b + 1);
+  if (!lds) {  // fallback: per-bucket merges over global memory
+    u32 ia = 0, ie = 0, jb = 0, je = 0, c = 0;
+    if (walk) {
+      const u64* ka = p.sa.key + a0;
+      const u64* kb = p.sb.key + c0;
+      ia = (b == b0) ? 0u : lb_small(ka, na, lk);
+      ie = last ? na : lb_small(ka, na, hk);
+      jb = (b == b0) ? 0u : lb_small(kb, nc, lk);
+      je = last ? nc : lb_small(kb, nc, hk);
+      c = merge_bucket<false, false>(p.sa, a0 + ia, a0 + ie, p.sb, nullptr, nullptr, c0 + jb, c0 + je,
+                                     nullptr, 0, 0);
+    }
+    u32 tot;
+    const u32 ex = block_excl_scan<DB>(c, s_wave, &tot);
+    if (c)
+      merge_bucket<false, true>(p.sa, a0 + ia, a0 + ie, p.sb, nullptr, nullptr, c0 + jb, c0 + je,
+                                p.keys + base, ex, ~0ull);
+    if (tid == 0) p.cnt[tile] = tot;
+    return;
+  }
+  for (u32 x = tid; x < na; x += DB) s_ka[x] = p.sa.key[a0 + x];
+  for (u32 x = tid; x < nc; x += DB) s_kb[x] = p.sb.key[c0 + x];
+  __syncthreads();
+  u32 ia = 0, ie = 0, jb = 0, je = 0;
+  if (walk) {
+    ia = (b == b0) ? 0u : lb_small(s_ka, na, lk);
+    ie = last ? na : lb_small(s_ka, na, hk);
+    jb = (b == b0) ? 0u : lb_small(s_kb, nc, lk);
+    je = last ? nc : lb_small(s_kb, nc, hk);
+  }
+  // list the differing buckets' rows, then hash them all at once
+  u32 tot_rows;
+  const u32 r0 = block_excl_scan<DB>((ie - ia) + (je - jb), s_wave, &tot_rows);
+  {
+    u32 o = r0;
+    for (u32 x = ia; x < ie; x++) s_list[o++] = (uint16_t)x;
+    for (u32 x = jb; x < je; x++) s_list[o++] = (uint16_t)(x | 0x8000u);
+  }
+  __syncthreads();
+  for (u32 q = tid; q < tot_rows; q += DB) {
+    const u32 e = s_list[q];
+    const bool isb = e & 0x8000u;
+    const u32 r = e & 0x7FFFu;
+    if (isb)
+      s_hb[r] = rh(p.sb, c0 + r);
+    else
+      s_ha[r] = rh(p.sa, a0 + r);
+  }
+  __syncthreads();
+  // merge the differing buckets' keys from LDS: count, then write at the scanned offset
+  u32 c = 0;
+  for (int pass = 0; pass < 2; pass++) {
+    u32 o = 0;
+    if (pass == 1) {
+      u32 tot;
+      o = block_excl_scan<DB>(c, s_wave, &tot);
+      if (tid == 0) p.cnt[tile] = tot;
+    }
+    if (walk) {
+      u32 i = ia, j = jb, k2 = 0;
+      while (i < ie || j < je) {
+        const u64 ka = i < ie ? s_ka[i] : ~0ull, kb = j < je ? s_kb[j] : ~0ull;
+        const u64 k = ka < kb ? ka : kb;
+        u64 ha = 0, hb = 0;
+        const bool pa = ka == k, pb = kb == k;
+        for (; i < ie && s_ka[i] == k; i++) ha += s_ha[i];
+        for (; j < je && s_kb[j] == k; j++) hb += s_hb[j];
+        if (!(pa && pb) || ha != hb) {
+          if (pass == 1) p.keys[base + o + k2] = k;
+          k2++;
+        }
+      }
+      c = k2;
+    }
+  }
 }
 
 constexpr int DSB = 1024;
@@ -331,15 +528,13 @@ __global__ __launch_bounds__(DSB) void tile_scan_kernel(const u64* cnt, u64* off
   scan_tile_counts<DSB>(cnt, off, ntiles, d_count, s_wave, &s_carry);
 }
 
+// each tile's keys from scratch to the output, below cap
 __global__ __launch_bounds__(DB) void merkle_diff_write_kernel(DiffArgs p) {
-  __shared__ u32 s_wave[DB / WAVE + 1];
-  const u64 bpt = diff_bpt(p.ta.depth);
-  const u64 b = blockIdx.x * bpt + threadIdx.x;
-  const u32 c = (u64)threadIdx.x < bpt ? p.bc[b] : 0u;
-  u32 tot;
-  const u32 ex = block_excl_scan<DB>(c, s_wave, &tot);
-  const u64 o = p.off[blockIdx.x] + ex;
-  if (c && o < p.cap) diff_walk<true>(p, b, o);
+  const u64 tile = blockIdx.x;
+  const u64 n = p.cnt[tile], o = p.off[tile];
+  if (n == 0 || o >= p.cap) return;
+  const u64 base = p.bnd[tile] + p.bnd[p.ntiles + 1 + tile];
+  for (u64 x = threadIdx.x; x < n && o + x < p.cap; x += DB) p.out[o + x] = p.keys[base + x];
 }
 
 // ---------------------------------------------------------------- partial diff
@@ -458,19 +653,12 @@ inline unsigned grid_of(u64 n, int b) { return (unsigned)((n + b - 1) / b); }
 hipError_t launch_merkle_build(const Rows& s, const MerkleT& m, u64* d_keys, u32* ctr, u32* err,
                                hipStream_t st) {
   const MT t = mt_of(m);
-  const u64 nb = 1ull << t.depth;
-  hipError_t e = hipMemsetAsync(t.nodes + (nb - 1), 0, nb * sizeof(u64), st);
+  const u64 G = merkle_chunks(t.depth);
+  // scratch: the arrival counter (zeroed before EVERY launch), then the hand-off words
+  hipError_t e = hipMemsetAsync(ctr, 0, 16 * sizeof(u32), st);
   if (e != hipSuccess) return e;
-  e = hipMemsetAsync(d_keys, 0, sizeof(u64), st);
-  if (e != hipSuccess) return e;
-  if (s.n) {
-    const u64 rows_per_block = (u64)BB * BK;
-    hipLaunchKernelGGL(merkle_build_kernel, dim3(grid_of(s.n, (int)rows_per_block)), dim3(BB), 0, st,
-                       s, t, d_keys, err);
-  }
-  const u32 L1 = t.depth < (u32)UPL ? t.depth : (u32)UPL;
-  hipLaunchKernelGGL(merkle_upsweep_kernel, dim3((unsigned)(1ull << (t.depth - L1))), dim3(UPB), 0, st,
-                     t.nodes, t.depth, (u32*)nullptr, ctr);
+  hipLaunchKernelGGL(merkle_chunk_kernel<true>, dim3((unsigned)G), dim3(UPB), 0, st, s, t,
+                     (const u32*)nullptr, ctr, (u64*)(ctr + 16), d_keys, err);
   return hipGetLastError();
 }
 
@@ -478,13 +666,14 @@ hipError_t launch_merkle_update(const MerkleT& m, const Rows& olds, const Rows& 
                                 u64 n_keys, u32* dirty, u64* d_keys, u32* ctr, u32* err,
                                 hipStream_t st) {
   const MT t = mt_of(m);
-  const u32 L1 = t.depth < (u32)UPL ? t.depth : (u32)UPL;
-  const u64 chunks = 1ull << (t.depth - L1);
+  const u64 G = merkle_chunks(t.depth);
+  hipError_t e = hipMemsetAsync(ctr, 0, 16 * sizeof(u32), st);
+  if (e != hipSuccess) return e;
   if (n_keys)
     hipLaunchKernelGGL(merkle_update_kernel, dim3(grid_of(n_keys, UB)), dim3(UB), 0, st, t, olds, news,
                        keys, n_keys, dirty, d_keys, err);
-  hipLaunchKernelGGL(merkle_upsweep_kernel, dim3((unsigned)chunks), dim3(UPB), 0, st, t.nodes, t.depth,
-                     dirty, ctr);
+  hipLaunchKernelGGL(merkle_chunk_kernel<false>, dim3((unsigned)G), dim3(UPB), 0, st, news, t, dirty,
+                     ctr, (u64*)(ctr + 16), (u64*)nullptr, err);
   return hipGetLastError();
 }
 
@@ -498,10 +687,13 @@ hipError_t launch_merkle_diff(const MerkleT& a, const Rows& sa, const MerkleT& b
   p.out = out_keys;
   p.cap = cap;
   p.ntiles = diff_tiles(a.depth);
-  p.cnt = scratch;
-  p.off = scratch + p.ntiles;
-  p.bc = (u32*)(scratch + 2 * p.ntiles);
+  p.bnd = scratch;
+  p.cnt = scratch + 2 * (p.ntiles + 1);
+  p.off = p.cnt + p.ntiles;
+  p.keys = p.off + p.ntiles;
   p.d_count = d_count;
+  const u64 waves = 2 * (p.ntiles + 1);
+  hipLaunchKernelGGL(merkle_diff_bounds_kernel, dim3(grid_of(waves * WAVE, 256)), dim3(256), 0, st, p);
   hipLaunchKernelGGL(merkle_diff_count_kernel, dim3((unsigned)p.ntiles), dim3(DB), 0, st, p);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(DSB), 0, st, p.cnt, p.off, p.ntiles, d_count);
   hipLaunchKernelGGL(merkle_diff_write_kernel, dim3((unsigned)p.ntiles), dim3(DB), 0, st, p);

@@ -5,8 +5,6 @@
 //    ({val, ts}, dot), i.e. the flatmap order the BEAM iterates, so "first maximum
 //    in iteration order" (Enum.max_by) == the first row whose ts is strictly
 //    greater than every earlier one.
-//  * merkle_leaves: per key Σ row_hash (the MerkleMap leaf of the key's raw value
-//    map, causal_crdt.ex:392) plus the bucket -> first-leaf offsets the diff uses.
 //  * store_check: the sorted+unique precondition.
 //
 // Shape: one tile = 1024 rows = 256 threads x 4 consecutive rows; a thread owning a
@@ -15,7 +13,6 @@
 // three passes -- count per tile (key column only), one-workgroup offset scan, write
 // -- not by a decoupled look-back: thousands of tiles finishing in lock-step rounds
 // made every tile walk back a whole round of predecessors.
-#include "dg_hash.h"
 #include "dg_launch.h"
 
 namespace dg {
@@ -26,16 +23,14 @@ constexpr int SB = SEG_BLOCK;
 constexpr int SI = SEG_ITEMS;
 constexpr int ST = SEG_TILE;
 
-enum class SegOp { Read, Leaves };
+enum class SegOp { Read };
 
 struct SegArgs {
   Rows s;
   const u64* keys;
   u64 n_keys;
   u64* out_a;  // key
-  u64* out_b;  // value id / leaf hash
-  u64* bucket_off;
-  u32 depth;
+  u64* out_b;  // value id
   u64* cnt;    // heads per tile
   u64* off;    // output offset per tile
   u64 ntiles;
@@ -74,15 +69,14 @@ __global__ __launch_bounds__(SSB) void seg_scan_kernel(SegArgs p) {
   scan_tile_counts<SSB>(p.cnt, p.off, p.ntiles, p.d_count, s_wave, &s_carry);
 }
 
-// Pass 3: one output per head at the tile's offset -- (key, read value) or (key, leaf
-// hash).  The tile's rows are staged in LDS by coalesced loads (Read: key, val, ts;
-// Leaves: key and the row's hash, computed while loading); each thread then reduces
-// the key runs that start among its SI consecutive rows from LDS (a run that leaves
-// the tile continues from global memory), and the heads are compacted in LDS and
-// written coalesced.
+// Pass 3: one output per head at the tile's offset: (key, read value).  The tile's key,
+// val and ts are staged in LDS by coalesced loads; each thread then reduces the key
+// runs that start among its SI consecutive rows from LDS (a run that leaves the tile
+// continues from global memory), and the heads are compacted in LDS and written
+// coalesced.
 template <SegOp OP>
 __global__ __launch_bounds__(SB) void seg_write_kernel(SegArgs p) {
-  __shared__ u64 s_key[ST + 1], s_x[ST], s_y[ST];  // Read: val, ts.  Leaves: hash, row
+  __shared__ u64 s_key[ST + 1], s_x[ST], s_y[ST];  // key, val, ts
   __shared__ u32 s_wave[SB / WAVE + 1];
   const int tid = threadIdx.x;
   const u64 n = p.s.n, tile = blockIdx.x, t0 = tile * ST;
@@ -92,14 +86,9 @@ __global__ __launch_bounds__(SB) void seg_write_kernel(SegArgs p) {
     const u32 j = k * SB + tid;
     if (j < nt) {
       const u64 i = t0 + j;
-      const u64 key = p.s.key[i];
-      s_key[j + 1] = key;
-      if (OP == SegOp::Read) {
-        s_x[j] = p.s.val[i];
-        s_y[j] = (u64)p.s.ts[i];
-      } else {
-        s_x[j] = row_hash(key, p.s.val[i], p.s.ts[i], p.s.node[i], p.s.cnt[i]);
-      }
+      s_key[j + 1] = p.s.key[i];
+      s_x[j] = p.s.val[i];
+      s_y[j] = (u64)p.s.ts[i];
     }
   }
   if (tid == 0) s_key[0] = t0 > 0 ? p.s.key[t0 - 1] : ~p.s.key[0];
@@ -114,35 +103,27 @@ __global__ __launch_bounds__(SB) void seg_write_kernel(SegArgs p) {
     if (j >= nt) continue;
     const u64 key = s_key[j + 1];
     if (key == s_key[j]) continue;  // not a head
-    if (OP == SegOp::Read && p.keys != nullptr && !keyset_has(p.keys, p.n_keys, key)) continue;
+    if (p.keys != nullptr && !keyset_has(p.keys, p.n_keys, key)) continue;
     heads |= 1u << k;
     oa[k] = key;
     u32 e = j + 1;
-    if (OP == SegOp::Read) {
-      i64 best_ts = (i64)s_y[j];
-      u64 best_val = s_x[j];
-      for (; e < nt && s_key[e + 1] == key; e++) {
-        const i64 ts = (i64)s_y[e];
-        if (ts > best_ts) {
-          best_ts = ts;
-          best_val = s_x[e];
-        }
+    i64 best_ts = (i64)s_y[j];
+    u64 best_val = s_x[j];
+    for (; e < nt && s_key[e + 1] == key; e++) {
+      const i64 ts = (i64)s_y[e];
+      if (ts > best_ts) {
+        best_ts = ts;
+        best_val = s_x[e];
       }
-      for (u64 g = t0 + e; e == nt && g < n && p.s.key[g] == key; g++) {
-        const i64 ts = p.s.ts[g];
-        if (ts > best_ts) {
-          best_ts = ts;
-          best_val = p.s.val[g];
-        }
-      }
-      ob[k] = best_val;
-    } else {
-      u64 h = s_x[j];
-      for (; e < nt && s_key[e + 1] == key; e++) h += s_x[e];
-      for (u64 g = t0 + e; e == nt && g < n && p.s.key[g] == key; g++)
-        h += row_hash(key, p.s.val[g], p.s.ts[g], p.s.node[g], p.s.cnt[g]);
-      ob[k] = h;
     }
+    for (u64 g = t0 + e; e == nt && g < n && p.s.key[g] == key; g++) {
+      const i64 ts = p.s.ts[g];
+      if (ts > best_ts) {
+        best_ts = ts;
+        best_val = p.s.val[g];
+      }
+    }
+    ob[k] = best_val;
   }
   u32 tile_total;
   u32 pos = block_excl_scan<SB>(__popc(heads), s_wave, &tile_total);
@@ -152,31 +133,13 @@ __global__ __launch_bounds__(SB) void seg_write_kernel(SegArgs p) {
     if (heads & (1u << k)) {
       s_x[pos] = oa[k];
       s_y[pos] = ob[k];
-      s_key[pos] = t0 + j0 + k;  // the head's row
       pos++;
     }
   __syncthreads();
   const u64 base = p.off[tile];
   for (u32 q = tid; q < tile_total; q += SB) {
-    const u64 o = base + q;
-    p.out_a[o] = s_x[q];
-    p.out_b[o] = s_y[q];
-    if (OP == SegOp::Leaves) {
-      // bucket_off[b] = index of the first leaf whose bucket >= b, for every bucket
-      // strictly after the previous key's bucket and up to this key's bucket.
-      const u32 sh = 64 - p.depth;
-      const u64 row = s_key[q], key = s_x[q];
-      const u64 bk = key >> sh;
-      const u64 bstart = row == 0 ? 0 : (p.s.key[row - 1] >> sh) + 1;
-      for (u64 b = bstart; b <= bk; b++) p.bucket_off[b] = o;
-      // after the store's last key: the trailing buckets (and the end sentinel)
-      u64 e = row + 1;
-      while (e < n && p.s.key[e] == key) e++;
-      if (e == n) {
-        const u64 nbk = 1ull << p.depth;
-        for (u64 b = bk + 1; b <= nbk; b++) p.bucket_off[b] = o + 1;
-      }
-    }
+    p.out_a[base + q] = s_x[q];
+    p.out_b[base + q] = s_y[q];
   }
 }
 
@@ -193,11 +156,6 @@ __global__ void store_check_kernel(Rows s, u32* bad) {
        i += (u64)gridDim.x * blockDim.x) {
     if (row_cmp(load_row(s, i - 1), load_row(s, i)) >= 0) atomicOr(bad, 1u);
   }
-}
-
-__global__ void fill_u64_kernel(u64* p, u64 n, u64 v) {
-  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x)
-    p[i] = v;
 }
 
 }  // namespace
