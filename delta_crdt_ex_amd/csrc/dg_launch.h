@@ -174,7 +174,7 @@ inline u64 diff_tiles(u32 depth) { return depth >= 8 ? (1ull << (depth - 8)) : 1
 // tile boundaries in both stores, per-tile counts and offsets, then the differing keys
 // staged per tile (at most one per row of either store)
 inline u64 diff_scratch_words(u32 depth, u64 na, u64 nb) {
-  return 2 * (diff_tiles(depth) + 1) + 2 * diff_tiles(depth) + na + nb + 1;
+  return 2 * (diff_tiles(depth) + 1) + 2 * diff_tiles(depth) + na + nb + 1 + diff_tiles(depth) / 256 + 1;
 }
 // differing keys, ascending; the first min(total, cap) written; *d_count = total.
 hipError_t launch_merkle_diff(const MerkleT& a, const Rows& sa, const MerkleT& b, const Rows& sb,

@@ -374,6 +374,7 @@ __device__ u32 merge_bucket(const Rows& A, u64 ia, u64 ie, const Rows& B, const 
 // to per-bucket merges over global memory.
 constexpr int DB = DIFF_BLOCK;
 constexpr u32 DCAP = 1024;  // rows per store staged in LDS
+constexpr u32 LCAP = 512;   // rows of a tile's differing buckets hashed through LDS
 
 struct DiffArgs {
   MT ta, tb;
@@ -384,6 +385,7 @@ struct DiffArgs {
   u64* cnt;   // differing keys per tile
   u64* off;   // their output offset
   u64* keys;  // scratch: nA + nB keys
+  u64* bsum;  // per DB tiles: the sum of their counts (zeroed before the count kernel)
   u64 ntiles;
   u64* d_count;
 };
@@ -420,31 +422,76 @@ __global__ __launch_bounds__(256) void merkle_diff_bounds_kernel(DiffArgs p) {
 }
 
 __global__ __launch_bounds__(DB) void merkle_diff_count_kernel(DiffArgs p) {
-  __shared__ u64 s_ka[DCAP], s_kb[DCAP], s_ha[DCAP], s_hb[DCAP];
-  __shared__ uint16_t s_list[2 * DCAP];  // rows to hash: bit 15 = store B
+  __shared__ u64 s_ka[DCAP], s_kb[DCAP];
+  __shared__ u64 s_h[LCAP];            // hashes of the listed rows, in list order
+  __shared__ uint16_t s_list[LCAP];    // the differing buckets' rows: bit 15 = store B
   __shared__ u32 s_wave[DB / WAVE + 1];
   const u32 depth = p.ta.depth;
   const u64 tile = blockIdx.x, bpt = diff_bpt(depth), b0 = tile * bpt;
   const int tid = threadIdx.x;
   const u32 rl = depth >= 8 ? depth - 8 : 0;
   const u64 root = ((1ull << rl) - 1) + tile;
-  if (p.ta.nodes[root] == p.tb.nodes[root]) {  // uniform: the whole tile matches
-    if (tid == 0) p.cnt[tile] = 0;
-    return;
-  }
   const u64 nbnd = p.ntiles + 1;
-  const u64 a0 = p.bnd[tile], a1 = p.bnd[tile + 1], c0 = p.bnd[nbnd + tile], c1 = p.bnd[nbnd + tile + 1];
-  const u64 base = a0 + c0;
-  const bool lds = a1 - a0 <= DCAP && c1 - c0 <= DCAP;  // uniform
-  const u32 na = (u32)(a1 - a0), nc = (u32)(c1 - c0);
   const bool in = (u64)tid < bpt;
   const u64 b = b0 + tid;
   const u64 leaf = ((1ull << depth) - 1) + b;
-  const bool walk = in && p.ta.nodes[leaf] != p.tb.nodes[leaf];
+  // one round of independent loads: the subtree roots, the tile's row bounds, the leaves
+  const u64 root_a = p.ta.nodes[root], root_b = p.tb.nodes[root];
+  const u64 a0 = p.bnd[tile], a1 = p.bnd[tile + 1], c0 = p.bnd[nbnd + tile], c1 = p.bnd[nbnd + tile + 1];
+  const u64 leaf_a = in ? p.ta.nodes[leaf] : 0, leaf_b = in ? p.tb.nodes[leaf] : 0;
+  if (root_a == root_b) {  // uniform: the whole tile matches
+    if (tid == 0) p.cnt[tile] = 0;
+    return;
+  }
+  const u64 base = a0 + c0;
+  const u32 na = (u32)(a1 - a0), nc = (u32)(c1 - c0);
+  const bool walk = in && leaf_a != leaf_b;
   const bool last = (u64)tid == bpt - 1;
   const u64 lk = bucket_first_key(p.ta, b), hk = last ? 0 : bucket_first_key(p.ta, b + 1);
+  bool lds = a1 - a0 <= DCAP && c1 - c0 <= DCAP;  // uniform
+  u32 ia = 0, ie = 0, jb = 0, je = 0, r0 = 0;
+  if (lds) {
+    {  // every staging load in flight at once (DCAP / DB = 4 per store per thread)
+      constexpr int Q = DCAP / DB;
+      u64 ka[Q], kb[Q];
+#pragma unroll
+      for (int q = 0; q < Q; q++) {
+        const u32 x = q * DB + tid;
+        ka[q] = x < na ? p.sa.key[a0 + x] : 0;
+        kb[q] = x < nc ? p.sb.key[c0 + x] : 0;
+      }
+#pragma unroll
+      for (int q = 0; q < Q; q++) {
+        const u32 x = q * DB + tid;
+        if (x < na) s_ka[x] = ka[q];
+        if (x < nc) s_kb[x] = kb[q];
+      }
+    }
+    __syncthreads();
+    if (walk) {
+      ia = (b == b0) ? 0u : lb_small(s_ka, na, lk);
+      ie = last ? na : lb_small(s_ka, na, hk);
+      jb = (b == b0) ? 0u : lb_small(s_kb, nc, lk);
+      je = last ? nc : lb_small(s_kb, nc, hk);
+    }
+    // list the differing buckets' rows, then hash them all at once
+    u32 tot_rows;
+    r0 = block_excl_scan<DB>((ie - ia) + (je - jb), s_wave, &tot_rows);
+    lds = tot_rows <= LCAP;  // uniform
+    if (lds) {
+      u32 o = r0;
+      for (u32 x = ia; x < ie; x++) s_list[o++] = (uint16_t)x;
+      for (u32 x = jb; x < je; x++) s_list[o++] = (uint16_t)(x | 0x8000u);
+      __syncthreads();
+      for (u32 q = tid; q < tot_rows; q += DB) {
+        const u32 e = s_list[q];
+        s_h[q] = (e & 0x8000u) ? rh(p.sb, c0 + (e & 0x7FFFu)) : rh(p.sa, a0 + e);
+      }
+      __syncthreads();
+    }
+  }
   if (!lds) {  // fallback: per-bucket merges over global memory
-    u32 ia = 0, ie = 0, jb = 0, je = 0, c = 0;
+    u32 c = 0;
     if (walk) {
       const u64* ka = p.sa.key + a0;
       const u64* kb = p.sb.key + c0;
@@ -460,46 +507,25 @@ __global__ __launch_bounds__(DB) void merkle_diff_count_kernel(DiffArgs p) {
     if (c)
       merge_bucket<false, true>(p.sa, a0 + ia, a0 + ie, p.sb, nullptr, nullptr, c0 + jb, c0 + je,
                                 p.keys + base, ex, ~0ull);
-    if (tid == 0) p.cnt[tile] = tot;
+    if (tid == 0) {
+      p.cnt[tile] = tot;
+      if (tot) atomicAdd((unsigned long long*)&p.bsum[tile / DB], (unsigned long long)tot);
+    }
     return;
   }
-  for (u32 x = tid; x < na; x += DB) s_ka[x] = p.sa.key[a0 + x];
-  for (u32 x = tid; x < nc; x += DB) s_kb[x] = p.sb.key[c0 + x];
-  __syncthreads();
-  u32 ia = 0, ie = 0, jb = 0, je = 0;
-  if (walk) {
-    ia = (b == b0) ? 0u : lb_small(s_ka, na, lk);
-    ie = last ? na : lb_small(s_ka, na, hk);
-    jb = (b == b0) ? 0u : lb_small(s_kb, nc, lk);
-    je = last ? nc : lb_small(s_kb, nc, hk);
-  }
-  // list the differing buckets' rows, then hash them all at once
-  u32 tot_rows;
-  const u32 r0 = block_excl_scan<DB>((ie - ia) + (je - jb), s_wave, &tot_rows);
-  {
-    u32 o = r0;
-    for (u32 x = ia; x < ie; x++) s_list[o++] = (uint16_t)x;
-    for (u32 x = jb; x < je; x++) s_list[o++] = (uint16_t)(x | 0x8000u);
-  }
-  __syncthreads();
-  for (u32 q = tid; q < tot_rows; q += DB) {
-    const u32 e = s_list[q];
-    const bool isb = e & 0x8000u;
-    const u32 r = e & 0x7FFFu;
-    if (isb)
-      s_hb[r] = rh(p.sb, c0 + r);
-    else
-      s_ha[r] = rh(p.sa, a0 + r);
-  }
-  __syncthreads();
-  // merge the differing buckets' keys from LDS: count, then write at the scanned offset
+  // merge the differing buckets' keys from LDS: count, then write at the scanned offset.
+  // This bucket's A rows' hashes sit at s_h[r0 + (x - ia)], its B rows' after them.
+  const u32 hb0 = r0 + (ie - ia) - jb;
   u32 c = 0;
   for (int pass = 0; pass < 2; pass++) {
     u32 o = 0;
     if (pass == 1) {
       u32 tot;
       o = block_excl_scan<DB>(c, s_wave, &tot);
-      if (tid == 0) p.cnt[tile] = tot;
+      if (tid == 0) {
+        p.cnt[tile] = tot;
+        if (tot) atomicAdd((unsigned long long*)&p.bsum[tile / DB], (unsigned long long)tot);
+      }
     }
     if (walk) {
       u32 i = ia, j = jb, k2 = 0;
@@ -508,8 +534,8 @@ __global__ __launch_bounds__(DB) void merkle_diff_count_kernel(DiffArgs p) {
         const u64 k = ka < kb ? ka : kb;
         u64 ha = 0, hb = 0;
         const bool pa = ka == k, pb = kb == k;
-        for (; i < ie && s_ka[i] == k; i++) ha += s_ha[i];
-        for (; j < je && s_kb[j] == k; j++) hb += s_hb[j];
+        for (; i < ie && s_ka[i] == k; i++) ha += s_h[r0 + (i - ia)];
+        for (; j < je && s_kb[j] == k; j++) hb += s_h[hb0 + j];
         if (!(pa && pb) || ha != hb) {
           if (pass == 1) p.keys[base + o + k2] = k;
           k2++;
@@ -528,13 +554,27 @@ __global__ __launch_bounds__(DSB) void tile_scan_kernel(const u64* cnt, u64* off
   scan_tile_counts<DSB>(cnt, off, ntiles, d_count, s_wave, &s_carry);
 }
 
-// each tile's keys from scratch to the output, below cap
-__global__ __launch_bounds__(DB) void merkle_diff_write_kernel(DiffArgs p) {
-  const u64 tile = blockIdx.x;
-  const u64 n = p.cnt[tile], o = p.off[tile];
-  if (n == 0 || o >= p.cap) return;
-  const u64 base = p.bnd[tile] + p.bnd[p.ntiles + 1 + tile];
-  for (u64 x = threadIdx.x; x < n && o + x < p.cap; x += DB) p.out[o + x] = p.keys[base + x];
+// Scan and copy in one pass, one wave per tile: the tile's output offset is the sum of
+// the earlier groups' tile sums (bsum, added by the count kernel: 256 same-word adds per
+// group, no scan launch) plus the counts of the earlier tiles of its own group -- at
+// most 255 + ntiles / 256 words, loaded by the 64 lanes at once -- then the lanes copy
+// the tile's keys from scratch to the output below cap.  The last tile's wave writes
+// the total.
+__global__ __launch_bounds__(WAVE) void merkle_diff_write_kernel(DiffArgs p) {
+  const int lane = threadIdx.x;
+  const u64 tile = blockIdx.x, grp = tile / DB;
+  const u64 n = p.cnt[tile];
+  const bool last = tile + 1 == p.ntiles;
+  if (n == 0 && !last) return;  // uniform
+  u64 before = 0;
+  for (u64 x = lane; x < grp; x += WAVE) before += p.bsum[x];
+  for (u64 x = grp * DB + lane; x < tile; x += WAVE) before += p.cnt[x];
+#pragma unroll
+  for (int d = WAVE / 2; d >= 1; d >>= 1) before += __shfl_xor(before, d, WAVE);
+  if (last && lane == 0) *p.d_count = before + n;
+  if (n == 0 || before >= p.cap) return;
+  const u64 src = p.bnd[tile] + p.bnd[p.ntiles + 1 + tile];
+  for (u64 x = lane; x < n && before + x < p.cap; x += WAVE) p.out[before + x] = p.keys[src + x];
 }
 
 // ---------------------------------------------------------------- partial diff
@@ -691,12 +731,14 @@ hipError_t launch_merkle_diff(const MerkleT& a, const Rows& sa, const MerkleT& b
   p.cnt = scratch + 2 * (p.ntiles + 1);
   p.off = p.cnt + p.ntiles;
   p.keys = p.off + p.ntiles;
+  p.bsum = p.keys + sa.n + sb.n + 1;
   p.d_count = d_count;
   const u64 waves = 2 * (p.ntiles + 1);
+  hipError_t e = hipMemsetAsync(p.bsum, 0, grid_of(p.ntiles, DB) * sizeof(u64), st);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(merkle_diff_bounds_kernel, dim3(grid_of(waves * WAVE, 256)), dim3(256), 0, st, p);
   hipLaunchKernelGGL(merkle_diff_count_kernel, dim3((unsigned)p.ntiles), dim3(DB), 0, st, p);
-  hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(DSB), 0, st, p.cnt, p.off, p.ntiles, d_count);
-  hipLaunchKernelGGL(merkle_diff_write_kernel, dim3((unsigned)p.ntiles), dim3(DB), 0, st, p);
+  hipLaunchKernelGGL(merkle_diff_write_kernel, dim3((unsigned)p.ntiles), dim3(WAVE), 0, st, p);
   return hipGetLastError();
 }
 
