@@ -4,8 +4,8 @@ lib/delta_crdt/storage.ex:12-16, written by causal_crdt.ex:238-250 after every d
 and read back at start-up by :216-234) -- stored as the device-resident dot store
 itself instead of the term tree.
 
-    storage.write(path, node_id, sequence_number, state)      # AWLWWMap mirror state
-    node_id, sequence_number, state = storage.read(path)
+    storage.write(path, node_id, sequence_number, state, tree)   # AWLWWMap mirror state
+    node_id, sequence_number, state, tree = storage.read(path)
 
 File layout (little-endian), one self-describing file per replica:
 
@@ -15,10 +15,10 @@ The header holds node_id, sequence_number, the row and context counts, the conte
 kind, the byte length and xxh64 of each column, and the exact interning tables of
 the state's Universe (keys, values and nodes as tagged terms), so `read` restores the
 same terms, ids and rows.  Columns are the raw SoA arrays (key, val, ts, node, cnt,
-ctx node, ctx cnt): 36 B per dot + 12 B per context entry, copied device -> host by
-one D2H copy each.  The MerkleMap is not stored: it is a function of the rows
-(dg_merkle_build rebuilds it, which is how the reference's read_from_storage path
-treats a missing map too).  A checksum mismatch raises.
+ctx node, ctx cnt, and the Merkle tree's nodes when one is persisted): 36 B per dot +
+12 B per context entry + 8 B per tree node, copied device -> host by one D2H copy
+each.  The header names the tree's depth and key-hash shard.  A checksum mismatch
+raises; the file is written to a temporary name, fsynced and renamed over the old one.
 """
 from __future__ import annotations
 
@@ -116,18 +116,23 @@ def _universe_from(tables) -> interning.Universe:
     return U
 
 
-def write(path, node_id, sequence_number: int, state) -> None:
-    """Storage.write/2's payload for an AWLWWMap mirror state (aw_lww_map.AWLWWMap)."""
-    cols = list(state.rows.to_numpy()) + list(state.ctx.to_numpy())
-    blobs = [np.ascontiguousarray(c).tobytes() for c in cols]
+def write_arrays(path, node_id, sequence_number: int, rows, ctx, universe, merkle=None) -> None:
+    """The snapshot file from host arrays: rows = (key, val, ts, node, cnt) numpy columns,
+    ctx = (kind, node, cnt), merkle = None or (depth, shard_bits, shard, nodes uint64)."""
+    cols = [np.ascontiguousarray(c, dt) for c, (_, dt) in zip(rows, _COLS)]
+    cols += [np.ascontiguousarray(ctx[1], np.uint32), np.ascontiguousarray(ctx[2], np.uint64)]
+    if merkle is not None:
+        cols.append(np.ascontiguousarray(merkle[3], np.uint64))
+    blobs = [c.tobytes() for c in cols]
     header = {
         "node_id": _pack(node_id),
         "sequence_number": int(sequence_number),
-        "rows": int(state.rows.n),
-        "ctx_kind": int(state.ctx.kind),
-        "ctx_n": int(state.ctx.n),
+        "rows": int(len(cols[0])),
+        "ctx_kind": int(ctx[0]),
+        "ctx_n": int(len(cols[5])),
+        "merkle": None if merkle is None else [int(merkle[0]), int(merkle[1]), str(int(merkle[2]))],
         "columns": [[len(b), xxhash.xxh64_intdigest(b)] for b in blobs],
-        "universe": _universe_tables(state.universe),
+        "universe": _universe_tables(universe),
     }
     h = msgpack.packb(header, use_bin_type=True)
     # write-then-rename: a crash mid-write leaves the previous snapshot intact
@@ -143,12 +148,9 @@ def write(path, node_id, sequence_number: int, state) -> None:
     os.replace(tmp, path)
 
 
-def read(path, device=None):
-    """Storage.read/1: (node_id, sequence_number, state) or None if `path` is absent."""
-    import os
-
-    from . import aw_lww_map as M
-    from .store import Context, Store
+def read_arrays(path):
+    """(node_id, sequence_number, rows, ctx, universe, merkle) from a snapshot file as
+    host arrays (merkle: None or (depth, shard_bits, shard, nodes)); None if absent."""
     if not os.path.exists(path):
         return None
     with open(path, "rb") as f:
@@ -157,17 +159,53 @@ def read(path, device=None):
         (hl,) = struct.unpack("<Q", f.read(8))
         header = msgpack.unpackb(f.read(hl), raw=False, strict_map_key=False)
         arrays = []
-        dtypes = [d for _, d in _COLS] + [np.uint32, np.uint64]
+        dtypes = [d for _, d in _COLS] + [np.uint32, np.uint64, np.uint64]
         for (nbytes, digest), dt in zip(header["columns"], dtypes):
             b = f.read(nbytes)
             if len(b) != nbytes or xxhash.xxh64_intdigest(b) != digest:
                 raise ValueError(f"{path}: column checksum mismatch")
             arrays.append(np.frombuffer(b, dtype=dt).copy())
+    m = header.get("merkle")
+    merkle = None if m is None else (int(m[0]), int(m[1]), int(m[2]), arrays[7])
+    return (_unpack(header["node_id"]), header["sequence_number"], tuple(arrays[:5]),
+            (header["ctx_kind"], arrays[5], arrays[6]), _universe_from(header["universe"]), merkle)
+
+
+def write(path, node_id, sequence_number: int, state, merkle_map=None) -> None:
+    """Storage.write/2's payload {node_id, sequence_number, crdt_state, merkle_map}
+    (causal_crdt.ex:242-250) for an AWLWWMap mirror state and its device MerkleTree
+    (store.MerkleTree; None: not persisted, rebuilt on read)."""
+    m = None
+    if merkle_map is not None:
+        m = (merkle_map.depth, merkle_map.shard_bits, merkle_map.shard,
+             merkle_map.nodes.cpu().numpy().view(np.uint64))
+    write_arrays(path, node_id, sequence_number, state.rows.to_numpy(),
+                 (state.ctx.kind,) + tuple(state.ctx.to_numpy()), state.universe, m)
+
+
+def read(path, device=None):
+    """Storage.read/1 (causal_crdt.ex:220-230): {node_id, sequence_number, crdt_state,
+    merkle_map} or None if `path` is absent.  The merkle_map is the persisted device tree
+    (indexing the restored rows), or a fresh dg_merkle_build when none was persisted."""
+    import torch
+
+    from . import aw_lww_map as M
+    from .store import Context, MerkleTree, Store
+    got = read_arrays(path)
+    if got is None:
+        return None
+    node_id, seq, rows, ctx, U, merkle = got
     dev = device or M._dev()
-    rows = Store.from_numpy(*arrays[:5], device=dev)
-    ctx = Context.from_numpy(header["ctx_kind"], arrays[5], arrays[6], dev)
-    state = M.AWLWWMap(rows, ctx, _universe_from(header["universe"]))
-    return _unpack(header["node_id"]), header["sequence_number"], state
+    st = Store.from_numpy(*rows, device=dev)
+    state = M.AWLWWMap(st, Context.from_numpy(ctx[0], ctx[1], ctx[2], dev), U)
+    if merkle is None:
+        tree = None
+    else:
+        depth, sb, shard, nodes = merkle
+        tree = MerkleTree(depth, torch.from_numpy(nodes.view(np.int64).copy()).to(dev), 0, sb, shard,
+                          st)
+        tree.n_keys = int(len(np.unique(rows[0])))
+    return node_id, seq, state, tree
 
 
-__all__ = ["write", "read", "MAGIC"]
+__all__ = ["write", "read", "write_arrays", "read_arrays", "MAGIC"]

@@ -30,7 +30,23 @@ sys.path.insert(0, ROOT)
 from delta_crdt_ex_amd.interning import Universe  # noqa: E402
 from oracle import awlww_term as T  # noqa: E402
 from oracle import convert as CV  # noqa: E402
-from oracle.erlterm import Atom  # noqa: E402
+from delta_crdt_ex_amd import storage  # noqa: E402
+from oracle import ref as R  # noqa: E402
+from oracle.erlterm import Atom, EList  # noqa: E402
+
+
+def snapshot_case():
+    """tests/golden/snapshot_terms.dgsnap: what Storage.write persists after a delta,
+    {node_id, sequence_number, crdt_state, merkle_map} (causal_crdt.ex:242-250), for a
+    term-valued replica of history("terms", seed 7): its SoA rows and context through a
+    fresh Universe, and the depth-6 Merkle tree of the C oracle."""
+    U = Universe()
+    A = history(7, U, values=TERM_VALUES)[0]
+    rows, ctx = CV.state_to_soa(A, U)
+    tree = R.merkle_build(rows, 6)
+    storage.write_arrays(os.path.join(HERE, "snapshot_terms.dgsnap"), Atom("replica_a"), 3, rows,
+                         ctx, U, (6, 0, 0, tree.nodes))
+    return A
 
 
 def soa(state, U):
@@ -92,7 +108,11 @@ def kats(U):
     write_case("kat_resolve_conflicts", add1, chg, [1], U, "aw_lww_map_test.exs:31-49")
 
 
-def history(seed, U, n_keys=40, n_rep=3, steps=200, ts_ties=True):
+TERM_VALUES = ["a", "b", "ab", Atom("x"), Atom("nil_not"), (1,), (1, "z"), 2.5, 7, -1.5,
+               EList([2]), b"\x00"]
+
+
+def history(seed, U, n_keys=40, n_rep=3, steps=200, ts_ties=True, values=None):
     rnd = random.Random(seed)
     c = Clock()
     reps = [T.compress_dots(T.new()) for _ in range(n_rep)]
@@ -119,7 +139,8 @@ def history(seed, U, n_keys=40, n_rep=3, steps=200, ts_ties=True):
         i = rnd.randrange(n_rep)
         r = rnd.random()
         if r < 0.55:
-            mutate(i, "add", rnd.randrange(n_keys), rnd.randrange(6))
+            mutate(i, "add", rnd.randrange(n_keys),
+                   rnd.randrange(6) if values is None else rnd.choice(values))
         elif r < 0.8:
             mutate(i, "remove", rnd.randrange(n_keys), None)
         else:
@@ -143,6 +164,15 @@ def main():
         delta = T.AW(A.dots, {k: A.value[k] for k in keys if k in A.value})
         write_case(f"history_{seed}_sync", B, delta, keys or [0], U,
                    f"random history seed {seed}, sync delta (causal_crdt.ex:324-335)")
+    # term-valued histories: LWW ties between strings, atoms, tuples, floats, lists
+    for seed in range(2):
+        V = Universe()
+        reps = history(100 + seed, V, values=TERM_VALUES)
+        A, B = reps[0], reps[1]
+        allk = sorted(set(A.value) | set(B.value))
+        write_case(f"history_terms_{seed}_full", A, B, allk, V,
+                   f"term-valued random history seed {100 + seed}, full join")
+    snapshot_case()
     # config-1 shape, small
     A = T.compress_dots(T.new())
     n = 500
@@ -156,7 +186,7 @@ def main():
             B = T.join(B, T.add(k, k + 1, 2, B, n * 1000 + k), [k])
     write_case("config1_small", A, B, sorted(set(A.value) | set(B.value)), U,
                "config 1 shape (bench/basic_operations.exs), 500 keys")
-    print("wrote", sorted(f for f in os.listdir(HERE) if f.endswith(".npz")))
+    print("wrote", sorted(f for f in os.listdir(HERE) if f.endswith((".npz", ".dgsnap"))))
 
 
 if __name__ == "__main__":

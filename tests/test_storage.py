@@ -1,11 +1,30 @@
 """SoA snapshots (delta_crdt_ex_amd/storage.py): the term codec and the
-interning tables round-trip exactly on the CPU; a device state round-trips through a
-file on the GPU (rows, context, terms, read/1), and a damaged file is refused."""
+interning tables round-trip exactly on the CPU; the committed golden snapshot
+(tests/golden/snapshot_terms.dgsnap, made by tests/golden/make_golden.py from the term
+oracle) holds exactly the oracle's rows, context, read/1 and Merkle tree; a device state
+and its Merkle tree round-trip through a file on the GPU as the reference's 4-tuple
+{node_id, sequence_number, crdt_state, merkle_map} (causal_crdt.ex:242-250, read back
+at :220-230), and a damaged file is refused."""
+import os
+
 import numpy as np
 import pytest
 
 from delta_crdt_ex_amd import interning, storage
 from delta_crdt_ex_amd.terms import Atom, EList, EMap
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "snapshot_terms.dgsnap")
+
+
+def _oracle_replica():
+    """The replica the golden snapshot was made from (make_golden.snapshot_case)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(GOLDEN))
+    import make_golden as G
+    from oracle import convert as CV
+    U = interning.Universe()
+    A = G.history(7, U, values=G.TERM_VALUES)[0]
+    return A
 
 
 TERMS = [None, True, False, Atom("ok"), 0, -5, 1 << 70, 2.5, "txt", b"\x00\xff",
@@ -29,6 +48,58 @@ def test_universe_tables_round_trip():
     assert V.value("new") == U.value("new")
 
 
+def test_golden_snapshot_matches_the_oracle():
+    from oracle import awlww_term as T
+    from oracle import convert as CV
+    from oracle import ref as R
+    A = _oracle_replica()
+    node_id, seq, rows, ctx, U, merkle = storage.read_arrays(GOLDEN)
+    assert node_id == Atom("replica_a") and seq == 3
+    # the rows, read back into terms through the snapshot's own Universe, are the oracle's
+    assert CV.soa_canon(rows, ctx, U) == CV.term_canon(A)
+    # read/1 on those rows (C oracle, ids) equals the term oracle's read/1
+    ok, ov = R.read_lww(rows)
+    got = {U.key_term(int(k)): U.value_term(int(v)) for k, v in zip(ok, ov)}
+    assert {k: repr(v) for k, v in got.items()} == {k: repr(v) for k, v in T.read(A).items()}
+    depth, sb, shard, nodes = merkle
+    assert (depth, sb, shard) == (6, 0, 0)
+    assert np.array_equal(nodes, R.merkle_build(rows, 6).nodes)
+
+
+def test_snapshot_write_is_atomic(tmp_path):
+    """A crash mid-write (simulated: the temporary file is left half written) never
+    damages the previous snapshot (write-then-rename)."""
+    p = tmp_path / "r.dgsnap"
+    U = interning.Universe()
+    rows = tuple(np.zeros(0, dt) for dt in (np.uint64, np.uint64, np.int64, np.uint32, np.uint64))
+    storage.write_arrays(p, 1, 1, rows, (0, np.zeros(0, np.uint32), np.zeros(0, np.uint64)), U)
+    good = p.read_bytes()
+    (tmp_path / "r.dgsnap.tmp").write_bytes(good[: len(good) // 2])
+    assert storage.read_arrays(p)[1] == 1
+    storage.write_arrays(p, 1, 2, rows, (0, np.zeros(0, np.uint32), np.zeros(0, np.uint64)), U)
+    assert storage.read_arrays(p)[1] == 2 and not (tmp_path / "r.dgsnap.tmp").exists()
+
+
+@pytest.mark.gpu
+def test_golden_snapshot_on_the_device():
+    """The golden snapshot read into device state: rows, context and read/1 equal the
+    term oracle's; the persisted Merkle tree equals dg_merkle_build of the restored rows
+    and diffs against it to nothing."""
+    from delta_crdt_ex_amd import aw_lww_map as M
+    from oracle import awlww_term as T
+    from oracle import convert as CV
+    A = _oracle_replica()
+    node_id, seq, st, tree = storage.read(GOLDEN)
+    assert node_id == Atom("replica_a") and seq == 3
+    rows = st.rows.to_numpy()
+    ctx = (st.ctx.kind,) + tuple(st.ctx.to_numpy())
+    assert CV.soa_canon(rows, ctx, st.universe) == CV.term_canon(A)
+    assert {k: repr(v) for k, v in M.read(st).items()} == {k: repr(v) for k, v in T.read(A).items()}
+    fresh = M.engine().merkle_build(st.rows, tree.depth)
+    assert np.array_equal(tree.nodes.cpu().numpy(), fresh.nodes.cpu().numpy())
+    assert M.engine().merkle_diff(tree, fresh).numel() == 0
+
+
 @pytest.mark.gpu
 def test_snapshot_round_trip(tmp_path):
     from delta_crdt_ex_amd import aw_lww_map as M
@@ -37,9 +108,13 @@ def test_snapshot_round_trip(tmp_path):
         st = M.join(st, M.add(k, v, Atom("node1"), st, ts=100 + i), [k])
     st = M.join(st, M.remove(Atom("b"), Atom("node1"), st), [Atom("b")])
     p = tmp_path / "replica.dgsnap"
-    storage.write(p, Atom("node1"), 7, st)
-    node, seq, back = storage.read(p)
+    tree = M.engine().merkle_build(st.rows, 5)
+    storage.write(p, Atom("node1"), 7, st, tree)
+    node, seq, back, back_tree = storage.read(p)
     assert node == Atom("node1") and seq == 7
+    assert back_tree.depth == 5 and back_tree.root() == tree.root()
+    assert np.array_equal(back_tree.nodes.cpu().numpy(),
+                          M.engine().merkle_build(back.rows, 5).nodes.cpu().numpy())
     for x, y in zip(st.rows.to_numpy(), back.rows.to_numpy()):
         assert np.array_equal(x, y)
     for x, y in zip(st.ctx.to_numpy(), back.ctx.to_numpy()):
