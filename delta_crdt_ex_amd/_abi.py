@@ -126,6 +126,8 @@ _SIGS = {
     "dg_compress_dots": (C.c_int, [C.c_void_p, C.POINTER(dg_context), C.POINTER(dg_context)]),
     "dg_read_lww": (C.c_int, [C.c_void_p, C.POINTER(dg_store), P64, C.c_uint64, P64, P64,
                               C.c_uint64, P64]),
+    "dg_sort_store": (C.c_int, [C.c_void_p, C.POINTER(dg_store), C.POINTER(dg_store)]),
+    "dg_sort_context": (C.c_int, [C.c_void_p, C.POINTER(dg_context), C.POINTER(dg_context)]),
     "dg_remap_values": (C.c_int, [C.c_void_p, C.POINTER(dg_store), P64, P64, C.c_uint64]),
     "dg_merkle_build": (C.c_int, [C.c_void_p, C.POINTER(dg_store), C.POINTER(dg_merkle)]),
     "dg_merkle_build_async": (C.c_int, [C.c_void_p, C.POINTER(dg_store), C.POINTER(dg_merkle),

@@ -189,6 +189,41 @@ def join_all(delta1: AWLWWMap, delta2: AWLWWMap) -> AWLWWMap:
     return AWLWWMap(out, octx, delta1.universe)
 
 
+def from_terms(value: dict, dots, universe: interning.Universe | None = None) -> AWLWWMap:
+    """Marshal a term-level `%AWLWWMap{dots, value}` (aw_lww_map.ex:2-3) onto the device,
+    as the NIF's marshal_state does (c_src/marshal.c): walk value = %{key => %{{v, ts} =>
+    MapSet[{node, counter}]}} in map iteration order, intern every term, upload the rows
+    and the context unsorted and order them on the device (dg_sort_store /
+    dg_sort_context).  `dots` is a set of (node, counter) dots or a {node: max} VV."""
+    U = universe or interning.DEFAULT
+    for entries in value.values():  # values first: a relabel re-spaces value ids
+        for (v, _t) in entries:
+            U.value(v)
+    ks, vs, ts, ns, cs = [], [], [], [], []
+    for key, entries in value.items():
+        kid = U.key(key)
+        for (v, t), ds in entries.items():
+            vid = U.value(v)
+            for (nd, c) in ds:
+                ks.append(kid)
+                vs.append(vid)
+                ts.append(t)
+                ns.append(U.node(nd))
+                cs.append(c)
+    dev = _dev()
+    raw = Store.from_numpy(np.array(ks, np.uint64), np.array(vs, np.uint64), np.array(ts, np.int64),
+                           np.array(ns, np.uint32), np.array(cs, np.uint64), dev)
+    if isinstance(dots, dict):
+        kind, pairs = DG_CTX_VV, [(U.node(nd), c) for nd, c in dots.items()]
+    else:
+        kind, pairs = DG_CTX_DOTS, [(U.node(nd), c) for nd, c in dots]
+    ctx = Context.from_numpy(kind, np.array([p[0] for p in pairs], np.uint32),
+                             np.array([p[1] for p in pairs], np.uint64), dev)
+    eng = engine()
+    rows = eng.sort_store(raw) if raw.n else _empty_rows()
+    return AWLWWMap(rows, eng.sort_context(ctx) if ctx.n else ctx, U)
+
+
 def read(state: AWLWWMap, keys=None) -> dict:
     """aw_lww_map.ex:211-224 (read/1, read/2 with a list, read/3 with one key)."""
     U = state.universe
@@ -242,4 +277,4 @@ def mutate_batch(ops, node_id, state: AWLWWMap):
 
 
 __all__ = ["AWLWWMap", "new", "compress_dots", "add", "remove", "clear", "join", "join_all", "read",
-           "mutate_batch", "DG_CTX_VV", "DG_CTX_DOTS"]
+           "mutate_batch", "from_terms", "DG_CTX_VV", "DG_CTX_DOTS"]

@@ -106,6 +106,19 @@ int ensure_tmp(dg_engine* e, size_t bytes) {
   return DG_OK;
 }
 
+// pinned host staging (kernel descriptors, digit histograms), grown on demand
+int ensure_stage(dg_engine* e, size_t bytes) {
+  if (bytes <= e->h_stage_cap) return DG_OK;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (e->h_stage) HIP_TRY(hipHostFree(e->h_stage));
+  e->h_stage = nullptr;
+  e->h_stage_cap = 0;
+  if (hipHostMalloc(&e->h_stage, bytes, 0) != hipSuccess)
+    return fail(DG_E_NOMEM, "pinned staging of %zu bytes failed", bytes);
+  e->h_stage_cap = bytes;
+  return DG_OK;
+}
+
 int ensure_counts(dg_engine* e, u64 tiles) {
   if (tiles <= e->counts_cap) return DG_OK;
   HIP_TRY(hipStreamSynchronize(e->stream));
@@ -1024,6 +1037,44 @@ int dg_remap_values(dg_engine* e, dg_store* s, const uint64_t* old_ids, const ui
   HIP_TRY(hipStreamSynchronize(e->stream));
   memcpy(&bad, &e->h_counts[11], sizeof(u32));
   if (bad) return fail(DG_E_INVAL, "dg_remap_values: a row's value id is not in old_ids");
+  return DG_OK;
+}
+
+int dg_sort_store(dg_engine* e, const dg_store* in, dg_store* out) {
+  if (!e) return fail(DG_E_INVAL, "null engine");
+  TRY(check_store(in, "dg_sort_store"));
+  if (!out) return fail(DG_E_INVAL, "dg_sort_store: null out");
+  if (out->cap < in->n)
+    return fail(DG_E_CAPACITY, "dg_sort_store: out cap %llu < %llu rows", (unsigned long long)out->cap,
+                (unsigned long long)in->n);
+  if (in->n && (!out->key || !out->val || !out->ts || !out->node || !out->cnt))
+    return fail(DG_E_INVAL, "dg_sort_store: null output column");
+  if (in->n >= (1ull << 32)) return fail(DG_E_INVAL, "dg_sort_store: more than 2^32 - 1 rows");
+  TRY(set_device(e));
+  TRY(ensure_tmp(e, sort_tmp_bytes(in->n)));
+  TRY(ensure_stage(e, 8 * 256 * sizeof(u32)));
+  HIP_TRY(launch_sort_store(rows_of(in), rows_out_of(out), e->tmp, (u32*)e->h_stage, e->d_counts,
+                            e->stream));
+  TRY(read_counts(e, 1));
+  out->n = e->h_counts[0];
+  return DG_OK;
+}
+
+int dg_sort_context(dg_engine* e, const dg_context* in, dg_context* out) {
+  if (!e) return fail(DG_E_INVAL, "null engine");
+  TRY(check_ctx(in, "dg_sort_context"));
+  if (!out) return fail(DG_E_INVAL, "dg_sort_context: null out");
+  if (out->cap < in->n) return fail(DG_E_CAPACITY, "dg_sort_context: out cap too small");
+  if (in->n && (!out->node || !out->cnt)) return fail(DG_E_INVAL, "dg_sort_context: null output");
+  if (in->n >= (1ull << 32)) return fail(DG_E_INVAL, "dg_sort_context: more than 2^32 - 1 entries");
+  TRY(set_device(e));
+  TRY(ensure_tmp(e, sort_tmp_bytes(in->n)));
+  TRY(ensure_stage(e, 8 * 256 * sizeof(u32)));
+  HIP_TRY(launch_sort_context(in->kind, in->node, in->cnt, in->n, out->node, out->cnt, e->tmp,
+                              (u32*)e->h_stage, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  out->n = in->n;
+  out->kind = in->kind;
   return DG_OK;
 }
 

@@ -142,6 +142,23 @@ hipError_t launch_read_lww(const Rows& s, const u64* keys, u64 n_keys, u64* out_
 // Sortedness check: sets *d_bad to nonzero if rows are not strictly ascending.
 hipError_t launch_store_check(const Rows& s, u32* d_bad, hipStream_t st);
 
+// ---- sort.hip (rows and contexts marshalled in map order -> the sorted forms)
+struct SortField {  // one column of the sort tuple
+  const void* p;
+  int width;      // 4 (u32) or 8 (u64 / i64)
+  int is_signed;  // i64: order by the sign-flipped bits
+};
+u64 sort_tiles(u64 n);
+size_t sort_tmp_bytes(u64 n);
+// rows sorted by (key, val, ts, node, cnt), exact duplicates dropped; *d_count = rows out.
+// h_hist8: 8 KB of pinned host memory (a digit pass whose byte is constant is skipped,
+// decided per field on the host: synchronizes once per field).
+hipError_t launch_sort_store(const Rows& in, const RowsOut& out, void* tmp, u32* h_hist8,
+                             u64* d_count, hipStream_t st);
+// context entries sorted by node (kind 0, a VV) or (node, cnt) (kind 1, a dot set)
+hipError_t launch_sort_context(int kind, const u32* node, const u64* cnt, u64 n, u32* out_node,
+                               u64* out_cnt, void* tmp, u32* h_hist8, hipStream_t st);
+
 // ---- remap.hip (value ids after a host relabel)
 // val[i] <- new_ids[j] where old_ids[j] == val[i] (old_ids ascending); err bit 0 if a
 // value is not in old_ids.

@@ -609,6 +609,28 @@ class Engine:
         cont._set(c)
         return cont
 
+    # ---------------------------------------------------------------- marshalling
+    def sort_store(self, s: Store, out: Store | None = None) -> Store:
+        """dg_sort_store: rows in any order (e.g. a map walk) -> sorted by (key, val, ts,
+        node, cnt), duplicates dropped."""
+        self._order()
+        if out is None:
+            out = Store.empty(max(s.n, 1), self.device)
+        si, so = s.abi(), out.abi()
+        check(self.lib.dg_sort_store(self.h, C.byref(si), C.byref(so)))
+        out.n = int(so.n)
+        return out
+
+    def sort_context(self, c: Context, out: Context | None = None) -> Context:
+        """dg_sort_context: a VV by node, a dot set by (node, cnt)."""
+        self._order()
+        if out is None:
+            out = Context.empty(c.kind, max(c.n, 1), self.device)
+        ci, co = c.abi(), out.abi()
+        check(self.lib.dg_sort_context(self.h, C.byref(ci), C.byref(co)))
+        out.n, out.kind = int(co.n), int(co.kind)
+        return out
+
     # ---------------------------------------------------------------- interning
     def remap_values(self, s: Store, old_ids: np.ndarray, new_ids: np.ndarray):
         """Rewrite s.val in place after a value relabel (dg_remap_values): old_ids /

@@ -233,6 +233,18 @@ int dg_compress_dots(dg_engine* e, const dg_context* dots, dg_context* out_vv);
 int dg_read_lww(dg_engine* e, const dg_store* s, const uint64_t* keys, uint64_t n_keys,
                 uint64_t* out_key, uint64_t* out_val, uint64_t cap, uint64_t* n_out);
 
+/* ---- marshalling ------------------------------------------------------------ */
+/* Order rows produced by walking %AWLWWMap{value: %{key => %{{v, ts} => MapSet}}}
+ * (aw_lww_map.ex:2-3) in map iteration order: `out` = the rows of `in` sorted by
+ * (key, val, ts [signed], node, cnt) with exact duplicates dropped -- the precondition
+ * of every other entry point.  A hand-written LSD radix sort on the device (csrc/
+ * sort.hip).  in and out: device columns, out->cap >= in->n, distinct from in.
+ * Synchronous. */
+int dg_sort_store(dg_engine* e, const dg_store* in, dg_store* out);
+/* The same for a context: a VV by node (kind DG_CTX_VV), a dot set by (node, cnt)
+ * (DG_CTX_DOTS).  Entries are assumed distinct (a map / MapSet).  out->cap >= in->n. */
+int dg_sort_context(dg_engine* e, const dg_context* in, dg_context* out);
+
 /* ---- interning maintenance -------------------------------------------------- */
 /* Value ids are order-preserving ranks in Erlang term order with gaps (the read
  * tie-break, aw_lww_map.ex:211-216).  When the host's value table runs out of room

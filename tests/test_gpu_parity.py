@@ -217,3 +217,77 @@ def test_store_check_detects_unsorted(engine):
     bad = Store.from_numpy(*rows, device=DEV)
     with pytest.raises(Exception):
         engine.store_check(bad)
+
+
+# ------------------------------------------------------------------ dg_sort_store (marshalling)
+
+def _np_sorted_unique(rows):
+    k, v, t, n, c = (np.asarray(x) for x in rows)
+    o = np.lexsort((c, n, t, v, k))
+    cols = [x[o] for x in (k, v, t, n, c)]
+    if len(cols[0]) > 1:
+        keep = np.ones(len(cols[0]), bool)
+        keep[1:] = ~np.all([x[1:] == x[:-1] for x in cols], axis=0)
+        cols = [x[keep] for x in cols]
+    return tuple(cols)
+
+
+def _shuffled(rows, rng, dup_frac=0.0):
+    n = len(rows[0])
+    order = rng.permutation(n)
+    if dup_frac and n:
+        order = np.concatenate([order, rng.choice(n, int(n * dup_frac))])
+        order = rng.permutation(order)
+    return tuple(np.ascontiguousarray(c[order]) for c in rows)
+
+
+@pytest.mark.parametrize("n,seed", [(0, 0), (1, 1), (17, 2), (4095, 3), (4097, 4), (70_000, 5)])
+def test_sort_store_random(engine, n, seed):
+    rng = np.random.default_rng(seed)
+    rows = (rng.integers(0, 1 << 64, n, dtype=np.uint64), rng.integers(0, 1 << 64, n, dtype=np.uint64),
+            rng.integers(-(1 << 63), (1 << 63) - 1, n, dtype=np.int64),
+            rng.integers(0, 1 << 32, n, dtype=np.uint32), rng.integers(0, 1 << 64, n, dtype=np.uint64))
+    rows = _shuffled(rows, rng, dup_frac=0.1)
+    s = Store.from_numpy(*rows, device=DEV)
+    s.n = len(rows[0])
+    rows_eq(engine.sort_store(s), _np_sorted_unique(rows))
+
+
+def test_sort_store_ties_everywhere(engine):
+    """Equal keys with many entries, equal (key, val) with ts ties of both signs, equal
+    (key, val, ts) with several dots: the order falls through every field."""
+    rng = np.random.default_rng(9)
+    n = 50_000
+    rows = (rng.integers(0, 40, n).astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15),
+            rng.integers(0, 5, n).astype(np.uint64), rng.integers(-3, 3, n).astype(np.int64),
+            rng.integers(0, 4, n).astype(np.uint32), rng.integers(0, 1 << 40, n).astype(np.uint64))
+    rows = _shuffled(rows, rng, dup_frac=0.3)
+    s = Store.from_numpy(*rows, device=DEV)
+    got = engine.sort_store(s)
+    rows_eq(got, _np_sorted_unique(rows))
+    engine.store_check(got)
+
+
+def test_sort_then_join_equals_oracle(engine):
+    """Config-2 replicas marshalled in a map-walk order (shuffled), sorted on the device,
+    then joined: bit-exact with the oracle's join of the sorted replicas."""
+    rng = np.random.default_rng(4)
+    a, b = W.config2(n_keys=60_000, seed=4)
+    sa = engine.sort_store(Store.from_numpy(*_shuffled(a["rows"], rng), device=DEV))
+    sb = engine.sort_store(Store.from_numpy(*_shuffled(b["rows"], rng), device=DEV))
+    ca = engine.sort_context(Context.from_numpy(a["ctx"][0], *[x[::-1].copy() for x in a["ctx"][1:]], DEV))
+    cb = engine.sort_context(Context.from_numpy(b["ctx"][0], *[x[::-1].copy() for x in b["ctx"][1:]], DEV))
+    out, octx = engine.join2(sa, ca, sb, cb)
+    wr, wc = R.join2(a["rows"], a["ctx"], b["rows"], b["ctx"])
+    rows_eq(out, wr)
+    ctx_eq(octx, wc)
+
+
+def test_sort_context_dots(engine):
+    rng = np.random.default_rng(2)
+    n = 30_000
+    pairs = np.unique(np.stack([rng.integers(0, 70, n), rng.integers(0, 1 << 50, n)], 1), axis=0)
+    perm = rng.permutation(len(pairs))
+    c = Context.from_numpy(W.DOTS, pairs[perm, 0].astype(np.uint32), pairs[perm, 1].astype(np.uint64), DEV)
+    got = engine.sort_context(c)
+    ctx_eq(got, (W.DOTS, pairs[:, 0].astype(np.uint32), pairs[:, 1].astype(np.uint64)))

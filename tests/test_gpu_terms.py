@@ -120,3 +120,21 @@ def test_30bit_node_ids_are_dense_on_the_device(M):
     assert dev_nodes <= set(range(len(nodes)))
     assert M.read(ms) == T.read(ts)
     assert ms.dots == ts.dots and ms.value == ts.value
+
+
+def test_from_terms_marshals_through_the_device_sort(M):
+    """A term-level state marshalled in map-walk order and sorted on the device
+    (dg_sort_store / dg_sort_context) is the oracle's state, and joins / reads like it."""
+    import sys, os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import make_golden as G
+    U = Universe()
+    reps = G.history(21, U, values=G.TERM_VALUES)
+    A, B = reps[0], reps[1]
+    V = Universe()
+    ma, mb = M.from_terms(A.value, A.dots, V), M.from_terms(B.value, B.dots, V)
+    assert ma.dots == A.dots and ma.value == A.value
+    keys = sorted(set(A.value) | set(B.value))
+    j, tj = M.join(ma, mb, keys), T.join(A, B, keys)
+    assert j.value == tj.value and j.dots == tj.dots
+    assert {k: repr(v) for k, v in M.read(j).items()} == {k: repr(v) for k, v in T.read(tj).items()}
