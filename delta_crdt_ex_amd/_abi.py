@@ -126,6 +126,18 @@ _SIGS = {
     "dg_compress_dots": (C.c_int, [C.c_void_p, C.POINTER(dg_context), C.POINTER(dg_context)]),
     "dg_read_lww": (C.c_int, [C.c_void_p, C.POINTER(dg_store), P64, C.c_uint64, P64, P64,
                               C.c_uint64, P64]),
+    "dg_store_alloc": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(dg_store)]),
+    "dg_store_free": (C.c_int, [C.c_void_p, C.POINTER(dg_store)]),
+    "dg_store_upload": (C.c_int, [C.c_void_p, C.POINTER(dg_store), C.POINTER(dg_store)]),
+    "dg_store_download": (C.c_int, [C.c_void_p, C.POINTER(dg_store), C.POINTER(dg_store)]),
+    "dg_context_alloc": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(dg_context)]),
+    "dg_context_free": (C.c_int, [C.c_void_p, C.POINTER(dg_context)]),
+    "dg_context_upload": (C.c_int, [C.c_void_p, C.POINTER(dg_context), C.POINTER(dg_context)]),
+    "dg_context_download": (C.c_int, [C.c_void_p, C.POINTER(dg_context), C.POINTER(dg_context)]),
+    "dg_buffer_alloc": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),
+    "dg_buffer_free": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "dg_copy_to_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
+    "dg_copy_to_host": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
     "dg_sort_store": (C.c_int, [C.c_void_p, C.POINTER(dg_store), C.POINTER(dg_store)]),
     "dg_sort_context": (C.c_int, [C.c_void_p, C.POINTER(dg_context), C.POINTER(dg_context)]),
     "dg_remap_values": (C.c_int, [C.c_void_p, C.POINTER(dg_store), P64, P64, C.c_uint64]),

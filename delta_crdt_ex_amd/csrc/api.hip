@@ -1078,4 +1078,152 @@ int dg_sort_context(dg_engine* e, const dg_context* in, dg_context* out) {
   return DG_OK;
 }
 
+// ---- device buffers
+int dg_buffer_alloc(dg_engine* e, uint64_t bytes, void** p) {
+  if (!e || !p) return fail(DG_E_INVAL, "dg_buffer_alloc: null argument");
+  *p = nullptr;
+  TRY(set_device(e));
+  if (bytes == 0) return DG_OK;
+  if (hipMalloc(p, bytes) != hipSuccess) {
+    *p = nullptr;
+    return fail(DG_E_NOMEM, "hipMalloc of %llu bytes failed", (unsigned long long)bytes);
+  }
+  return DG_OK;
+}
+
+int dg_buffer_free(dg_engine* e, void* p) {
+  if (!e) return fail(DG_E_INVAL, "null engine");
+  if (!p) return DG_OK;
+  TRY(set_device(e));
+  HIP_TRY(hipStreamSynchronize(e->stream));  // no kernel of this engine still uses it
+  HIP_TRY(hipFree(p));
+  return DG_OK;
+}
+
+int dg_copy_to_device(dg_engine* e, void* dst, const void* src, uint64_t bytes) {
+  if (!e || (bytes && (!dst || !src))) return fail(DG_E_INVAL, "dg_copy_to_device: null argument");
+  if (!bytes) return DG_OK;
+  TRY(set_device(e));
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return DG_OK;
+}
+
+int dg_copy_to_host(dg_engine* e, void* dst, const void* src, uint64_t bytes) {
+  if (!e || (bytes && (!dst || !src))) return fail(DG_E_INVAL, "dg_copy_to_host: null argument");
+  if (!bytes) return DG_OK;
+  TRY(set_device(e));
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return DG_OK;
+}
+
+int dg_store_alloc(dg_engine* e, uint64_t cap, dg_store* s) {
+  if (!e || !s) return fail(DG_E_INVAL, "dg_store_alloc: null argument");
+  memset(s, 0, sizeof *s);
+  const uint64_t c = cap ? cap : 1;
+  void* p[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  const uint64_t w[5] = {8, 8, 8, 4, 8};
+  for (int i = 0; i < 5; i++) {
+    int rc = dg_buffer_alloc(e, c * w[i], &p[i]);
+    if (rc != DG_OK) {
+      for (int j = 0; j < i; j++) hipFree(p[j]);
+      return rc;
+    }
+  }
+  s->key = (uint64_t*)p[0];
+  s->val = (uint64_t*)p[1];
+  s->ts = (int64_t*)p[2];
+  s->node = (uint32_t*)p[3];
+  s->cnt = (uint64_t*)p[4];
+  s->cap = cap;
+  return DG_OK;
+}
+
+int dg_store_free(dg_engine* e, dg_store* s) {
+  if (!e || !s) return fail(DG_E_INVAL, "dg_store_free: null argument");
+  void* p[5] = {s->key, s->val, s->ts, s->node, s->cnt};
+  for (int i = 0; i < 5; i++) TRY(dg_buffer_free(e, p[i]));
+  memset(s, 0, sizeof *s);
+  return DG_OK;
+}
+
+int dg_store_upload(dg_engine* e, const dg_store* host, dg_store* dev) {
+  if (!e || !host || !dev) return fail(DG_E_INVAL, "dg_store_upload: null argument");
+  if (dev->cap < host->n) return fail(DG_E_CAPACITY, "dg_store_upload: device cap too small");
+  TRY(set_device(e));
+  const uint64_t n = host->n;
+  if (n) {
+    HIP_TRY(hipMemcpyAsync(dev->key, host->key, n * 8, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(dev->val, host->val, n * 8, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(dev->ts, host->ts, n * 8, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(dev->node, host->node, n * 4, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(dev->cnt, host->cnt, n * 8, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+  }
+  dev->n = n;
+  return DG_OK;
+}
+
+int dg_store_download(dg_engine* e, const dg_store* dev, dg_store* host) {
+  if (!e || !host || !dev) return fail(DG_E_INVAL, "dg_store_download: null argument");
+  if (host->cap < dev->n) return fail(DG_E_CAPACITY, "dg_store_download: host cap too small");
+  TRY(set_device(e));
+  const uint64_t n = dev->n;
+  if (n) {
+    HIP_TRY(hipMemcpyAsync(host->key, dev->key, n * 8, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipMemcpyAsync(host->val, dev->val, n * 8, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipMemcpyAsync(host->ts, dev->ts, n * 8, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipMemcpyAsync(host->node, dev->node, n * 4, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipMemcpyAsync(host->cnt, dev->cnt, n * 8, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+  }
+  host->n = n;
+  return DG_OK;
+}
+
+int dg_context_alloc(dg_engine* e, uint64_t cap, dg_context* c) {
+  if (!e || !c) return fail(DG_E_INVAL, "dg_context_alloc: null argument");
+  memset(c, 0, sizeof *c);
+  void *pn = nullptr, *pc = nullptr;
+  TRY(dg_buffer_alloc(e, (cap ? cap : 1) * 4, &pn));
+  int rc = dg_buffer_alloc(e, (cap ? cap : 1) * 8, &pc);
+  if (rc != DG_OK) {
+    hipFree(pn);
+    return rc;
+  }
+  c->node = (uint32_t*)pn;
+  c->cnt = (uint64_t*)pc;
+  c->cap = cap;
+  return DG_OK;
+}
+
+int dg_context_free(dg_engine* e, dg_context* c) {
+  if (!e || !c) return fail(DG_E_INVAL, "dg_context_free: null argument");
+  TRY(dg_buffer_free(e, c->node));
+  TRY(dg_buffer_free(e, c->cnt));
+  memset(c, 0, sizeof *c);
+  return DG_OK;
+}
+
+int dg_context_upload(dg_engine* e, const dg_context* host, dg_context* dev) {
+  if (!e || !host || !dev) return fail(DG_E_INVAL, "dg_context_upload: null argument");
+  if (dev->cap < host->n) return fail(DG_E_CAPACITY, "dg_context_upload: device cap too small");
+  TRY(dg_copy_to_device(e, dev->node, host->node, host->n * 4));
+  TRY(dg_copy_to_device(e, dev->cnt, host->cnt, host->n * 8));
+  dev->n = host->n;
+  dev->kind = host->kind;
+  return DG_OK;
+}
+
+int dg_context_download(dg_engine* e, const dg_context* dev, dg_context* host) {
+  if (!e || !host || !dev) return fail(DG_E_INVAL, "dg_context_download: null argument");
+  if (host->cap < dev->n) return fail(DG_E_CAPACITY, "dg_context_download: host cap too small");
+  TRY(dg_copy_to_host(e, host->node, dev->node, dev->n * 4));
+  TRY(dg_copy_to_host(e, host->cnt, dev->cnt, dev->n * 8));
+  host->n = dev->n;
+  host->kind = dev->kind;
+  return DG_OK;
+}
+
 }  // extern "C"

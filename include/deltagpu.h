@@ -124,6 +124,25 @@ int dg_engine_destroy(dg_engine* e);
 void* dg_engine_stream(dg_engine* e);
 int dg_engine_sync(dg_engine* e);
 
+/* ---- device buffers (for callers without a device runtime of their own: the NIF) -- */
+/* Allocate / free a store's device columns (s->cap = cap, s->n = 0). */
+int dg_store_alloc(dg_engine* e, uint64_t cap, dg_store* s);
+int dg_store_free(dg_engine* e, dg_store* s);
+/* Host columns -> device columns (dev->cap >= host->n; dev->n = host->n), and back
+ * (host->cap >= dev->n; host->n = dev->n).  Synchronous. */
+int dg_store_upload(dg_engine* e, const dg_store* host, dg_store* dev);
+int dg_store_download(dg_engine* e, const dg_store* dev, dg_store* host);
+/* The same for contexts (kind copied). */
+int dg_context_alloc(dg_engine* e, uint64_t cap, dg_context* c);
+int dg_context_free(dg_engine* e, dg_context* c);
+int dg_context_upload(dg_engine* e, const dg_context* host, dg_context* dev);
+int dg_context_download(dg_engine* e, const dg_context* dev, dg_context* host);
+/* Raw device memory (key lists, Merkle nodes, continuations) and copies. */
+int dg_buffer_alloc(dg_engine* e, uint64_t bytes, void** p);
+int dg_buffer_free(dg_engine* e, void* p);
+int dg_copy_to_device(dg_engine* e, void* dst, const void* src, uint64_t bytes);
+int dg_copy_to_host(dg_engine* e, void* dst, const void* src, uint64_t bytes);
+
 /* Verify the sorted+unique precondition of a store (DG_E_ORDER if violated). */
 int dg_store_check(dg_engine* e, const dg_store* s);
 
