@@ -1,0 +1,828 @@
+/*
+ * deltagpu_nif.c — the Erlang NIF that binds DeltaCrdt.AWLWWMap (reference
+ * lib/delta_crdt/aw_lww_map.ex) and the MerkleMap role of DeltaCrdt.CausalCrdt
+ * (lib/delta_crdt/causal_crdt.ex) to libdeltagpu (include/deltagpu.h).  Built by the
+ * Elixir project against its OTP's erl_nif.h; this image has no
+ * Erlang/OTP, so this file is not compiled here.  The term-independent half
+ * (c_src/marshal.c: interning tables, host rows, unmarshal order) is, and is tested
+ * from C with the same C-ABI calls this file makes (c_src/test_marshal.c).
+ *
+ * Resources
+ *   engine   one dg_engine (one HIP stream) + the interning universe of this BEAM node
+ *            + a mutex: every NIF below takes it (a dg_engine is not re-entrant, and
+ *            several CausalCrdt processes call in from several dirty schedulers).
+ *   state    a DEVICE-RESIDENT replica state: rows, context and, once built, its Merkle
+ *            tree.  The Elixir struct keeps `dots` and `value` as real terms -- CausalCrdt
+ *            reads them directly (causal_crdt.ex:118,259,331,346) -- and carries the
+ *            state resource beside them, so a join ships only the delta to the device
+ *            and brings back only the keys it changed.
+ *
+ * NIFs (all dirty-CPU scheduled; errors are {:error, reason}, the Elixir side then
+ * runs the reference code instead):
+ *   engine_open(device)                       -> {:ok, engine}
+ *   state_load(engine, dots, value)           -> {:ok, state}          (marshal once)
+ *   join_delta(state, dots, value, keys)      -> {:ok, new_dots, changed}
+ *        join/3 (aw_lww_map.ex:153-158) of the resident state with a delta
+ *        %{dots: dots, value: value} over `keys`, in place on the device
+ *        (dg_join2_changes); changed = [{key, value_map | nil}] for the keys whose raw
+ *        value maps changed (causal_crdt.ex:344-352), so the caller updates its term
+ *        map with Map.merge/Map.drop of those keys only; the Merkle tree, if built,
+ *        gets put/delete + update_hashes of them (dg_merkle_update, :390-394).
+ *   read(state, keys | :all)                  -> %{key => value}       (read/1,2, :211-224)
+ *   take(state, keys)                         -> value map of those keys (Map.take, :118,331)
+ *   merkle_build(state, depth)                -> :ok
+ *   merkle_prepare(state, levels)             -> {:continue, cont}     (:255)
+ *   merkle_continue(state, cont, levels, max) -> {:continue, cont} | {:ok, keys}  (:96-105)
+ *   (a continuation is an opaque binary; `max` is max_sync_size, :98,105,206-214)
+ */
+#include <erl_nif.h>
+#include <string.h>
+
+#include "../include/deltagpu.h"
+#include "marshal.h"
+
+/* ------------------------------------------------------------ term operations */
+/* Exact Erlang term order: enif_compare, with the map-key tie-break between numbers
+ * that compare equal (1 before 1.0), also inside tuples and lists (the order of a
+ * flatmap's keys, which decides read/1's tie-break). */
+static int exact_cmp(ErlNifEnv* env, ERL_NIF_TERM a, ERL_NIF_TERM b) {
+  const int c = enif_compare(a, b);
+  if (c != 0 || enif_is_identical(a, b)) return c;
+  ErlNifSInt64 ia;
+  double fa;
+  if (enif_is_number(env, a)) {
+    const int a_int = enif_get_int64(env, a, &ia) || !enif_get_double(env, a, &fa);
+    ErlNifSInt64 ib;
+    const int b_int = enif_get_int64(env, b, &ib);
+    return a_int == b_int ? 0 : (a_int ? -1 : 1);
+  }
+  int na, nb;
+  const ERL_NIF_TERM *ea, *eb;
+  if (enif_get_tuple(env, a, &na, &ea) && enif_get_tuple(env, b, &nb, &eb)) {
+    for (int i = 0; i < na; i++) {
+      const int x = exact_cmp(env, ea[i], eb[i]);
+      if (x) return x;
+    }
+    return 0;
+  }
+  ERL_NIF_TERM ha, ta, hb, tb;
+  if (enif_get_list_cell(env, a, &ha, &ta) && enif_get_list_cell(env, b, &hb, &tb)) {
+    const int x = exact_cmp(env, ha, hb);
+    return x ? x : exact_cmp(env, ta, tb);
+  }
+  /* maps (and anything else) equal under enif_compare but not identical: the external
+   * term format decides -- deterministic, not the BEAM's own order ("parity unpinned",
+   * INTEGRATION.md §3) */
+  ErlNifBinary ba, bb;
+  enif_term_to_binary(env, a, &ba);
+  enif_term_to_binary(env, b, &bb);
+  const size_t n = ba.size < bb.size ? ba.size : bb.size;
+  int x = memcmp(ba.data, bb.data, n);
+  if (!x) x = ba.size < bb.size ? -1 : ba.size > bb.size;
+  enif_release_binary(&ba);
+  enif_release_binary(&bb);
+  return x < 0 ? -1 : x > 0;
+}
+
+typedef struct {
+  ErlNifEnv* env; /* the universe's own env: retained terms live here */
+} term_ud;
+
+typedef struct {
+  ERL_NIF_TERM t;
+} boxed;
+
+static int op_cmp(const void* a, const void* b, void* ud) {
+  term_ud* u = (term_ud*)ud;
+  return exact_cmp(u->env, ((const boxed*)a)->t, ((const boxed*)b)->t);
+}
+
+/* key ids: integer keys 0 <= k < 2^64 as splitmix64(k) (the synthetic workloads' and the
+ * Python mirror's id), anything else xxh64 of its external term format */
+static uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+static uint64_t op_hash(const void* p, void* ud) {
+  term_ud* u = (term_ud*)ud;
+  const ERL_NIF_TERM t = ((const boxed*)p)->t;
+  ErlNifUInt64 k;
+  if (enif_get_uint64(u->env, t, &k)) return splitmix64(k);
+  ErlNifBinary b;
+  enif_term_to_binary(u->env, t, &b);
+  const uint64_t h = dgm_hash_bytes(b.data, b.size, 0);
+  enif_release_binary(&b);
+  return h;
+}
+
+static void* op_keep(const void* p, void* ud) {
+  term_ud* u = (term_ud*)ud;
+  boxed* c = (boxed*)enif_alloc(sizeof *c);
+  c->t = enif_make_copy(u->env, ((const boxed*)p)->t);
+  return c;
+}
+
+static void op_drop(void* p, void* ud) {
+  (void)ud;
+  enif_free(p);
+}
+
+/* ------------------------------------------------------------ resources */
+typedef struct state_res state_res;
+
+typedef struct {
+  dg_engine* e;
+  dgm_universe* u;
+  term_ud tu;
+  ErlNifMutex* lock;
+  state_res* live; /* every state of this engine (a relabel rewrites them all) */
+} engine_res;
+
+struct state_res {
+  engine_res* eng;
+  dg_store rows;
+  dg_context ctx;
+  dg_merkle tree;
+  int has_tree;
+  state_res *prev, *next;
+};
+
+static ErlNifResourceType* ENGINE_RT;
+static ErlNifResourceType* STATE_RT;
+static ERL_NIF_TERM A_OK, A_ERROR, A_NIL, A_ALL, A_CONTINUE, A_MAP, A_STRUCT, A_MAPSET;
+
+static void engine_dtor(ErlNifEnv* env, void* obj) {
+  (void)env;
+  engine_res* r = (engine_res*)obj;
+  if (r->u) dgm_universe_free(r->u);
+  if (r->tu.env) enif_free_env(r->tu.env);
+  if (r->e) dg_engine_destroy(r->e);
+  if (r->lock) enif_mutex_destroy(r->lock);
+}
+
+static void state_dtor(ErlNifEnv* env, void* obj) {
+  (void)env;
+  state_res* s = (state_res*)obj;
+  engine_res* g = s->eng;
+  enif_mutex_lock(g->lock);
+  if (s->prev) s->prev->next = s->next; else g->live = s->next;
+  if (s->next) s->next->prev = s->prev;
+  dg_store_free(g->e, &s->rows);
+  dg_context_free(g->e, &s->ctx);
+  if (s->has_tree) dg_buffer_free(g->e, s->tree.nodes);
+  enif_mutex_unlock(g->lock);
+  enif_release_resource(g);
+}
+
+static ERL_NIF_TERM error_term(ErlNifEnv* env, int rc) {
+  return enif_make_tuple2(env, A_ERROR,
+                          enif_make_tuple2(env, enif_make_int(env, rc),
+                                           enif_make_string(env, dg_last_error(), ERL_NIF_LATIN1)));
+}
+
+#define TRY(x)                          \
+  do {                                  \
+    int rc_ = (x);                      \
+    if (rc_ != DG_OK) { rc = rc_; goto out; } \
+  } while (0)
+
+/* ------------------------------------------------------------ marshal */
+/* After any dgm_value that relabelled: rewrite every live state's val column. */
+static int remap_live(engine_res* g) {
+  const uint64_t *old_ids, *new_ids;
+  uint64_t n;
+  dgm_last_relabel(g->u, &old_ids, &new_ids, &n);
+  void *dold = NULL, *dnew = NULL;
+  int rc = dg_buffer_alloc(g->e, n * 8, &dold);
+  if (!rc) rc = dg_buffer_alloc(g->e, n * 8, &dnew);
+  if (!rc) rc = dg_copy_to_device(g->e, dold, old_ids, n * 8);
+  if (!rc) rc = dg_copy_to_device(g->e, dnew, new_ids, n * 8);
+  for (state_res* s = g->live; !rc && s; s = s->next) {
+    rc = dg_remap_values(g->e, &s->rows, (const uint64_t*)dold, (const uint64_t*)dnew, n);
+    if (!rc && s->has_tree) rc = dg_merkle_build(g->e, &s->rows, &s->tree);  /* hashes use ids */
+  }
+  dg_buffer_free(g->e, dold);
+  dg_buffer_free(g->e, dnew);
+  return rc;
+}
+
+static int intern_value(ErlNifEnv* env, engine_res* g, ERL_NIF_TERM v, uint64_t* id) {
+  boxed b = {v};
+  (void)env;
+  int relabeled = 0;
+  int rc = dgm_value(g->u, &b, id, &relabeled);
+  if (!rc && relabeled) rc = remap_live(g);
+  return rc;
+}
+
+/* a MapSet's members: %MapSet{map: %{member => []}} (Elixir 1.7+) */
+static int mapset_map(ErlNifEnv* env, ERL_NIF_TERM set, ERL_NIF_TERM* map) {
+  return enif_get_map_value(env, set, A_MAP, map);
+}
+
+/* walk %{key => %{{v, ts} => MapSet[{node, counter}]}} in map order into host rows */
+static int marshal_value(ErlNifEnv* env, engine_res* g, ERL_NIF_TERM value, dgm_rows* out) {
+  ErlNifMapIterator ki, ei, di;
+  ERL_NIF_TERM key, entries, vt, dots, dmap, dot, unused;
+  /* pass 1: intern every value first (a relabel re-spaces ids already handed out) */
+  if (!enif_map_iterator_create(env, value, &ki, ERL_NIF_MAP_ITERATOR_FIRST)) return DG_E_INVAL;
+  for (; enif_map_iterator_get_pair(env, &ki, &key, &entries); enif_map_iterator_next(env, &ki)) {
+    if (!enif_map_iterator_create(env, entries, &ei, ERL_NIF_MAP_ITERATOR_FIRST)) return DG_E_INVAL;
+    for (; enif_map_iterator_get_pair(env, &ei, &vt, &dots); enif_map_iterator_next(env, &ei)) {
+      int ar;
+      const ERL_NIF_TERM* e;
+      uint64_t id;
+      if (!enif_get_tuple(env, vt, &ar, &e) || ar != 2 || intern_value(env, g, e[0], &id)) {
+        enif_map_iterator_destroy(env, &ei);
+        enif_map_iterator_destroy(env, &ki);
+        return DG_E_INVAL;
+      }
+    }
+    enif_map_iterator_destroy(env, &ei);
+  }
+  enif_map_iterator_destroy(env, &ki);
+  /* pass 2: the rows */
+  enif_map_iterator_create(env, value, &ki, ERL_NIF_MAP_ITERATOR_FIRST);
+  for (; enif_map_iterator_get_pair(env, &ki, &key, &entries); enif_map_iterator_next(env, &ki)) {
+    boxed bk = {key};
+    uint64_t kid;
+    if (dgm_key(g->u, &bk, &kid)) goto bad_k;
+    enif_map_iterator_create(env, entries, &ei, ERL_NIF_MAP_ITERATOR_FIRST);
+    for (; enif_map_iterator_get_pair(env, &ei, &vt, &dots); enif_map_iterator_next(env, &ei)) {
+      int ar;
+      const ERL_NIF_TERM* e;
+      ErlNifSInt64 ts;
+      uint64_t vid;
+      int rl = 0;
+      boxed bv;
+      enif_get_tuple(env, vt, &ar, &e);
+      bv.t = e[0];
+      if (dgm_value(g->u, &bv, &vid, &rl) || rl || !enif_get_int64(env, e[1], &ts) ||
+          !mapset_map(env, dots, &dmap) ||
+          !enif_map_iterator_create(env, dmap, &di, ERL_NIF_MAP_ITERATOR_FIRST))
+        goto bad_e;
+      for (; enif_map_iterator_get_pair(env, &di, &dot, &unused); enif_map_iterator_next(env, &di)) {
+        const ERL_NIF_TERM* d;
+        ErlNifUInt64 cnt;
+        uint32_t nid;
+        boxed bn;
+        if (!enif_get_tuple(env, dot, &ar, &d) || ar != 2 || !enif_get_uint64(env, d[1], &cnt)) goto bad_d;
+        bn.t = d[0];
+        if (dgm_node(g->u, &bn, &nid) || dgm_rows_push(out, kid, vid, ts, nid, cnt)) goto bad_d;
+      }
+      enif_map_iterator_destroy(env, &di);
+    }
+    enif_map_iterator_destroy(env, &ei);
+  }
+  enif_map_iterator_destroy(env, &ki);
+  return DG_OK;
+bad_d:
+  enif_map_iterator_destroy(env, &di);
+bad_e:
+  enif_map_iterator_destroy(env, &ei);
+bad_k:
+  enif_map_iterator_destroy(env, &ki);
+  return DG_E_INVAL;
+}
+
+/* a context: a MapSet of dots (DG_CTX_DOTS) or a %{node => max} VV (DG_CTX_VV) */
+static int marshal_dots(ErlNifEnv* env, engine_res* g, ERL_NIF_TERM dots, dgm_rows* out) {
+  ERL_NIF_TERM m, k, v, st;
+  const int is_set = enif_get_map_value(env, dots, A_STRUCT, &st) && enif_is_identical(st, A_MAPSET);
+  out->c.kind = is_set ? DG_CTX_DOTS : DG_CTX_VV;
+  if (is_set) {
+    if (!mapset_map(env, dots, &m)) return DG_E_INVAL;
+  } else {
+    m = dots;
+  }
+  ErlNifMapIterator it;
+  if (!enif_map_iterator_create(env, m, &it, ERL_NIF_MAP_ITERATOR_FIRST)) return DG_E_INVAL;
+  for (; enif_map_iterator_get_pair(env, &it, &k, &v); enif_map_iterator_next(env, &it)) {
+    ERL_NIF_TERM node = k, cnt_t = v;
+    int ar;
+    const ERL_NIF_TERM* d;
+    if (is_set) {
+      if (!enif_get_tuple(env, k, &ar, &d) || ar != 2) goto bad;
+      node = d[0];
+      cnt_t = d[1];
+    }
+    ErlNifUInt64 cnt;
+    uint32_t nid;
+    boxed bn = {node};
+    if (!enif_get_uint64(env, cnt_t, &cnt) || dgm_node(g->u, &bn, &nid) || dgm_ctx_push(out, nid, cnt))
+      goto bad;
+  }
+  enif_map_iterator_destroy(env, &it);
+  return DG_OK;
+bad:
+  enif_map_iterator_destroy(env, &it);
+  return DG_E_INVAL;
+}
+
+/* host rows -> sorted device store + context (dg_sort_store / dg_sort_context) */
+static int upload_sorted(engine_res* g, const dgm_rows* h, dg_store* rows, dg_context* ctx) {
+  dg_store raw;
+  dg_context rawc;
+  int rc = dg_store_alloc(g->e, h->s.n, &raw);
+  if (rc) return rc;
+  if (!(rc = dg_store_alloc(g->e, h->s.n, rows)) && !(rc = dg_store_upload(g->e, &h->s, &raw)))
+    rc = dg_sort_store(g->e, &raw, rows);
+  dg_store_free(g->e, &raw);
+  if (rc) return rc;
+  if ((rc = dg_context_alloc(g->e, h->c.n, &rawc))) return rc;
+  if (!(rc = dg_context_alloc(g->e, h->c.n, ctx)) && !(rc = dg_context_upload(g->e, &h->c, &rawc)))
+    rc = dg_sort_context(g->e, &rawc, ctx);
+  dg_context_free(g->e, &rawc);
+  return rc;
+}
+
+/* a key list -> its ids, ascending unique, on the device */
+static int marshal_keys(ErlNifEnv* env, engine_res* g, ERL_NIF_TERM keys, uint64_t** d_keys,
+                        uint64_t* n_keys) {
+  unsigned len;
+  if (!enif_get_list_length(env, keys, &len)) return DG_E_INVAL;
+  uint64_t* ids = (uint64_t*)enif_alloc((len ? len : 1) * sizeof *ids);
+  ERL_NIF_TERM h, t = keys;
+  unsigned n = 0;
+  while (enif_get_list_cell(env, t, &h, &t)) {
+    boxed b = {h};
+    if (dgm_key(g->u, &b, &ids[n++])) {
+      enif_free(ids);
+      return DG_E_INVAL;
+    }
+  }
+  /* sort + unique (small: the delta's keys) */
+  for (unsigned i = 1; i < n; i++)
+    for (unsigned j = i; j > 0 && ids[j - 1] > ids[j]; j--) {
+      uint64_t x = ids[j];
+      ids[j] = ids[j - 1];
+      ids[j - 1] = x;
+    }
+  unsigned m = 0;
+  for (unsigned i = 0; i < n; i++)
+    if (!m || ids[m - 1] != ids[i]) ids[m++] = ids[i];
+  int rc = dg_buffer_alloc(g->e, (m ? m : 1) * 8, (void**)d_keys);
+  if (!rc) rc = dg_copy_to_device(g->e, *d_keys, ids, m * 8);
+  *n_keys = m;
+  enif_free(ids);
+  return rc;
+}
+
+/* ------------------------------------------------------------ unmarshal */
+typedef struct {
+  ErlNifEnv* env;
+  engine_res* g;
+  ERL_NIF_TERM out;     /* %{key => %{{v, ts} => MapSet}} being built */
+  ERL_NIF_TERM entries; /* the current key's map */
+  ERL_NIF_TERM dots;    /* the current entry's MapSet map */
+  ERL_NIF_TERM key, vt;
+  int open_key, open_entry;
+} unm;
+
+static ERL_NIF_TERM make_mapset(ErlNifEnv* env, ERL_NIF_TERM map) {
+  ERL_NIF_TERM ks[3] = {A_STRUCT, A_MAP, enif_make_atom(env, "version")};
+  ERL_NIF_TERM vs[3] = {A_MAPSET, map, enif_make_int(env, 2)};
+  ERL_NIF_TERM s;
+  enif_make_map_from_arrays(env, ks, vs, 3, &s);
+  return s;
+}
+
+static void close_entry(unm* u) {
+  if (u->open_entry) {
+    enif_make_map_put(u->env, u->entries, u->vt, make_mapset(u->env, u->dots), &u->entries);
+    u->open_entry = 0;
+  }
+}
+static void close_key(unm* u) {
+  close_entry(u);
+  if (u->open_key) {
+    enif_make_map_put(u->env, u->out, u->key, u->entries, &u->out);
+    u->open_key = 0;
+  }
+}
+static int u_key(void* ud, uint64_t key, uint64_t n) {
+  (void)n;
+  unm* u = (unm*)ud;
+  close_key(u);
+  const boxed* b = (const boxed*)dgm_key_term(u->g->u, key);
+  if (!b) return DG_E_INVAL;
+  u->key = enif_make_copy(u->env, b->t);
+  u->entries = enif_make_new_map(u->env);
+  u->open_key = 1;
+  return 0;
+}
+static int u_entry(void* ud, uint64_t val, int64_t ts, uint64_t n) {
+  (void)n;
+  unm* u = (unm*)ud;
+  close_entry(u);
+  const boxed* b = (const boxed*)dgm_value_term(u->g->u, val);
+  if (!b) return DG_E_INVAL;
+  u->vt = enif_make_tuple2(u->env, enif_make_copy(u->env, b->t), enif_make_int64(u->env, ts));
+  u->dots = enif_make_new_map(u->env);
+  u->open_entry = 1;
+  return 0;
+}
+static int u_dot(void* ud, uint32_t node, uint64_t cnt) {
+  unm* u = (unm*)ud;
+  const boxed* b = (const boxed*)dgm_node_term(u->g->u, node);
+  if (!b) return DG_E_INVAL;
+  ERL_NIF_TERM d = enif_make_tuple2(u->env, enif_make_copy(u->env, b->t), enif_make_uint64(u->env, cnt));
+  enif_make_map_put(u->env, u->dots, d, enif_make_list(u->env, 0), &u->dots);
+  return 0;
+}
+
+/* device rows -> %{key => value map} (host copy of just those rows) */
+static int unmarshal_rows(ErlNifEnv* env, engine_res* g, const dg_store* dev, ERL_NIF_TERM* out) {
+  dgm_rows h;
+  int rc = dgm_rows_init(&h, dev->n, 1);
+  if (rc) return rc;
+  if (!(rc = dg_store_download(g->e, dev, &h.s))) {
+    unm u;
+    memset(&u, 0, sizeof u);
+    u.env = env;
+    u.g = g;
+    u.out = enif_make_new_map(env);
+    dgm_walk w = {u_key, u_entry, u_dot};
+    rc = dgm_walk_rows(&h.s, &w, &u);
+    close_key(&u);
+    *out = u.out;
+  }
+  dgm_rows_free(&h);
+  return rc;
+}
+
+static int unmarshal_dots(ErlNifEnv* env, engine_res* g, const dg_context* dev, ERL_NIF_TERM* out) {
+  dgm_rows h;
+  int rc = dgm_rows_init(&h, 1, dev->n);
+  if (rc) return rc;
+  if (!(rc = dg_context_download(g->e, dev, &h.c))) {
+    ERL_NIF_TERM m = enif_make_new_map(env);
+    for (uint64_t i = 0; i < h.c.n; i++) {
+      const boxed* b = (const boxed*)dgm_node_term(g->u, h.c.node[i]);
+      ERL_NIF_TERM n = enif_make_copy(env, b->t), c = enif_make_uint64(env, h.c.cnt[i]);
+      if (dev->kind == DG_CTX_VV)
+        enif_make_map_put(env, m, n, c, &m);
+      else
+        enif_make_map_put(env, m, enif_make_tuple2(env, n, c), enif_make_list(env, 0), &m);
+    }
+    *out = dev->kind == DG_CTX_VV ? m : make_mapset(env, m);
+  }
+  dgm_rows_free(&h);
+  return rc;
+}
+
+/* ------------------------------------------------------------ NIFs */
+static ERL_NIF_TERM engine_open(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  (void)argc;
+  int dev;
+  if (!enif_get_int(env, argv[0], &dev)) return enif_make_badarg(env);
+  engine_res* g = (engine_res*)enif_alloc_resource(ENGINE_RT, sizeof *g);
+  memset(g, 0, sizeof *g);
+  g->lock = enif_mutex_create("deltagpu_engine");
+  g->tu.env = enif_alloc_env();
+  dgm_term_ops ops = {op_cmp, op_hash, op_keep, op_drop, &g->tu};
+  g->u = dgm_universe_new(&ops);
+  const int rc = dg_engine_create(dev, NULL, &g->e);
+  ERL_NIF_TERM r = rc ? error_term(env, rc) : enif_make_tuple2(env, A_OK, enif_make_resource(env, g));
+  enif_release_resource(g);
+  return r;
+}
+
+static state_res* new_state(engine_res* g) {
+  state_res* s = (state_res*)enif_alloc_resource(STATE_RT, sizeof *s);
+  memset(s, 0, sizeof *s);
+  enif_keep_resource(g);
+  s->eng = g;
+  s->next = g->live;
+  if (g->live) g->live->prev = s;
+  g->live = s;
+  return s;
+}
+
+static ERL_NIF_TERM state_load(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  (void)argc;
+  engine_res* g;
+  if (!enif_get_resource(env, argv[0], ENGINE_RT, (void**)&g)) return enif_make_badarg(env);
+  enif_mutex_lock(g->lock);
+  state_res* s = new_state(g);
+  dgm_rows h;
+  int rc = dgm_rows_init(&h, 1024, 64);
+  ERL_NIF_TERM r;
+  if (!rc) rc = marshal_dots(env, g, argv[1], &h);
+  if (!rc) rc = marshal_value(env, g, argv[2], &h);
+  if (!rc) rc = upload_sorted(g, &h, &s->rows, &s->ctx);
+  dgm_rows_free(&h);
+  r = rc ? error_term(env, rc) : enif_make_tuple2(env, A_OK, enif_make_resource(env, s));
+  enif_mutex_unlock(g->lock);
+  enif_release_resource(s);
+  return r;
+}
+
+static ERL_NIF_TERM join_delta(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  (void)argc;
+  state_res* s;
+  if (!enif_get_resource(env, argv[0], STATE_RT, (void**)&s)) return enif_make_badarg(env);
+  engine_res* g = s->eng;
+  enif_mutex_lock(g->lock);
+  int rc = DG_OK;
+  dgm_rows h;
+  dg_store drows, out, taken;
+  dg_context dctx, octx;
+  uint64_t *d_keys = NULL, n_keys = 0, *changed = NULL, n_changed = 0;
+  memset(&drows, 0, sizeof drows);
+  memset(&out, 0, sizeof out);
+  memset(&taken, 0, sizeof taken);
+  memset(&dctx, 0, sizeof dctx);
+  memset(&octx, 0, sizeof octx);
+  ERL_NIF_TERM r, new_dots, changed_terms = enif_make_list(env, 0), values;
+  TRY(dgm_rows_init(&h, 256, 16));
+  TRY(marshal_dots(env, g, argv[1], &h));
+  TRY(marshal_value(env, g, argv[2], &h));
+  TRY(upload_sorted(g, &h, &drows, &dctx));
+  TRY(marshal_keys(env, g, argv[3], &d_keys, &n_keys));
+  TRY(dg_store_alloc(g->e, s->rows.n + drows.n, &out));
+  TRY(dg_context_alloc(g->e, s->ctx.n + dctx.n, &octx));
+  TRY(dg_buffer_alloc(g->e, (n_keys ? n_keys : 1) * 8, (void**)&changed));
+  TRY(dg_join2_changes(g->e, &s->rows, &s->ctx, &drows, &dctx, d_keys, n_keys, &out, &octx, changed,
+                       n_keys, &n_changed));
+  if (s->has_tree) TRY(dg_merkle_update(g->e, &s->tree, &s->rows, &out, changed, n_changed));
+  /* the changed keys' new value maps (dg_take_keys), and the keys that vanished */
+  TRY(dg_store_alloc(g->e, out.n, &taken));
+  TRY(dg_take_keys(g->e, &out, changed, n_changed, &taken));
+  TRY(unmarshal_rows(env, g, &taken, &values));
+  TRY(unmarshal_dots(env, g, &octx, &new_dots));
+  {
+    uint64_t* hk = (uint64_t*)enif_alloc((n_changed ? n_changed : 1) * 8);
+    rc = dg_copy_to_host(g->e, hk, changed, n_changed * 8);
+    for (uint64_t i = n_changed; !rc && i-- > 0;) {
+      const boxed* b = (const boxed*)dgm_key_term(g->u, hk[i]);
+      ERL_NIF_TERM k = enif_make_copy(env, b->t), v;
+      if (!enif_get_map_value(env, values, k, &v)) v = A_NIL;
+      changed_terms = enif_make_list_cell(env, enif_make_tuple2(env, k, v), changed_terms);
+    }
+    enif_free(hk);
+    if (rc) goto out;
+  }
+  /* the resource now holds the joined state */
+  dg_store_free(g->e, &s->rows);
+  dg_context_free(g->e, &s->ctx);
+  s->rows = out;
+  s->ctx = octx;
+  memset(&out, 0, sizeof out);
+  memset(&octx, 0, sizeof octx);
+out:
+  r = rc ? error_term(env, rc) : enif_make_tuple3(env, A_OK, new_dots, changed_terms);
+  dgm_rows_free(&h);
+  dg_store_free(g->e, &drows);
+  dg_store_free(g->e, &out);
+  dg_store_free(g->e, &taken);
+  dg_context_free(g->e, &dctx);
+  dg_context_free(g->e, &octx);
+  dg_buffer_free(g->e, d_keys);
+  dg_buffer_free(g->e, changed);
+  enif_mutex_unlock(g->lock);
+  return r;
+}
+
+static ERL_NIF_TERM read_nif(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  (void)argc;
+  state_res* s;
+  if (!enif_get_resource(env, argv[0], STATE_RT, (void**)&s)) return enif_make_badarg(env);
+  engine_res* g = s->eng;
+  enif_mutex_lock(g->lock);
+  int rc = DG_OK;
+  uint64_t *d_keys = NULL, n_keys = 0, *dk = NULL, *dv = NULL, n_out = 0;
+  uint64_t *hk = NULL, *hv = NULL;
+  ERL_NIF_TERM r, m = enif_make_new_map(env);
+  const int all = enif_is_identical(argv[1], A_ALL);
+  if (!all) TRY(marshal_keys(env, g, argv[1], &d_keys, &n_keys));
+  const uint64_t cap = s->rows.n ? s->rows.n : 1;
+  TRY(dg_buffer_alloc(g->e, cap * 8, (void**)&dk));
+  TRY(dg_buffer_alloc(g->e, cap * 8, (void**)&dv));
+  TRY(dg_read_lww(g->e, &s->rows, all ? NULL : d_keys, n_keys, dk, dv, cap, &n_out));
+  hk = (uint64_t*)enif_alloc((n_out ? n_out : 1) * 8);
+  hv = (uint64_t*)enif_alloc((n_out ? n_out : 1) * 8);
+  TRY(dg_copy_to_host(g->e, hk, dk, n_out * 8));
+  TRY(dg_copy_to_host(g->e, hv, dv, n_out * 8));
+  for (uint64_t i = 0; i < n_out; i++) {
+    const boxed* k = (const boxed*)dgm_key_term(g->u, hk[i]);
+    const boxed* v = (const boxed*)dgm_value_term(g->u, hv[i]);
+    enif_make_map_put(env, m, enif_make_copy(env, k->t), enif_make_copy(env, v->t), &m);
+  }
+out:
+  r = rc ? error_term(env, rc) : m;
+  if (hk) enif_free(hk);
+  if (hv) enif_free(hv);
+  dg_buffer_free(g->e, d_keys);
+  dg_buffer_free(g->e, dk);
+  dg_buffer_free(g->e, dv);
+  enif_mutex_unlock(g->lock);
+  return r;
+}
+
+static ERL_NIF_TERM take_nif(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  (void)argc;
+  state_res* s;
+  if (!enif_get_resource(env, argv[0], STATE_RT, (void**)&s)) return enif_make_badarg(env);
+  engine_res* g = s->eng;
+  enif_mutex_lock(g->lock);
+  int rc = DG_OK;
+  uint64_t* d_keys = NULL;
+  uint64_t n_keys = 0;
+  dg_store taken;
+  memset(&taken, 0, sizeof taken);
+  ERL_NIF_TERM r, values = enif_make_new_map(env);
+  TRY(marshal_keys(env, g, argv[1], &d_keys, &n_keys));
+  TRY(dg_store_alloc(g->e, s->rows.n, &taken));
+  TRY(dg_take_keys(g->e, &s->rows, d_keys, n_keys, &taken));
+  TRY(unmarshal_rows(env, g, &taken, &values));
+out:
+  r = rc ? error_term(env, rc) : values;
+  dg_store_free(g->e, &taken);
+  dg_buffer_free(g->e, d_keys);
+  enif_mutex_unlock(g->lock);
+  return r;
+}
+
+static ERL_NIF_TERM merkle_build_nif(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  (void)argc;
+  state_res* s;
+  unsigned depth;
+  if (!enif_get_resource(env, argv[0], STATE_RT, (void**)&s) || !enif_get_uint(env, argv[1], &depth))
+    return enif_make_badarg(env);
+  engine_res* g = s->eng;
+  enif_mutex_lock(g->lock);
+  int rc = DG_OK;
+  if (s->has_tree) dg_buffer_free(g->e, s->tree.nodes);
+  memset(&s->tree, 0, sizeof s->tree);
+  s->has_tree = 0;
+  s->tree.depth = depth;
+  TRY(dg_buffer_alloc(g->e, ((2ull << depth) - 1) * 8, (void**)&s->tree.nodes));
+  s->has_tree = 1;
+  TRY(dg_merkle_build(g->e, &s->rows, &s->tree));
+out:;
+  ERL_NIF_TERM r = rc ? error_term(env, rc) : A_OK;
+  enif_mutex_unlock(g->lock);
+  return r;
+}
+
+/* continuation <-> binary: u32 level | u64 n | u64 n_buckets | pos[n] | hash[n] | bucket[nb] */
+static int cont_to_binary(ErlNifEnv* env, engine_res* g, const dg_merkle_cont* c, ERL_NIF_TERM* out) {
+  const size_t bytes = 4 + 16 + c->n * 16 + c->n_buckets * 8;
+  ErlNifBinary b;
+  if (!enif_alloc_binary(bytes, &b)) return DG_E_NOMEM;
+  unsigned char* p = b.data;
+  memcpy(p, &c->level, 4);
+  memcpy(p + 4, &c->n, 8);
+  memcpy(p + 12, &c->n_buckets, 8);
+  int rc = dg_copy_to_host(g->e, p + 20, c->pos, c->n * 8);
+  if (!rc) rc = dg_copy_to_host(g->e, p + 20 + c->n * 8, c->hash, c->n * 8);
+  if (!rc && c->n_buckets) rc = dg_copy_to_host(g->e, p + 20 + c->n * 16, c->bucket, c->n_buckets * 8);
+  if (rc) {
+    enif_release_binary(&b);
+    return rc;
+  }
+  *out = enif_make_binary(env, &b);
+  return DG_OK;
+}
+
+static int cont_alloc(engine_res* g, uint64_t cap, uint64_t cap_b, dg_merkle_cont* c) {
+  memset(c, 0, sizeof *c);
+  int rc = dg_buffer_alloc(g->e, (cap ? cap : 1) * 8, (void**)&c->pos);
+  if (!rc) rc = dg_buffer_alloc(g->e, (cap ? cap : 1) * 8, (void**)&c->hash);
+  if (!rc) rc = dg_buffer_alloc(g->e, (cap_b ? cap_b : 1) * 8, (void**)&c->bucket);
+  c->cap = cap;
+  c->cap_buckets = cap_b;
+  return rc;
+}
+
+static void cont_free(engine_res* g, dg_merkle_cont* c) {
+  dg_buffer_free(g->e, c->pos);
+  dg_buffer_free(g->e, c->hash);
+  dg_buffer_free(g->e, c->bucket);
+}
+
+static ERL_NIF_TERM merkle_prepare_nif(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  (void)argc;
+  state_res* s;
+  unsigned levels;
+  if (!enif_get_resource(env, argv[0], STATE_RT, (void**)&s) || !enif_get_uint(env, argv[1], &levels) ||
+      !s->has_tree)
+    return enif_make_badarg(env);
+  engine_res* g = s->eng;
+  enif_mutex_lock(g->lock);
+  int rc = DG_OK;
+  dg_merkle_cont c;
+  ERL_NIF_TERM bin = A_NIL, r;
+  const unsigned L = levels < s->tree.depth ? levels : s->tree.depth;
+  TRY(cont_alloc(g, 1ull << L, 1, &c));
+  TRY(dg_merkle_prepare(g->e, &s->tree, levels, &c));
+  TRY(cont_to_binary(env, g, &c, &bin));
+out:
+  r = rc ? error_term(env, rc) : enif_make_tuple2(env, A_CONTINUE, bin);
+  cont_free(g, &c);
+  enif_mutex_unlock(g->lock);
+  return r;
+}
+
+static ERL_NIF_TERM merkle_continue_nif(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  (void)argc;
+  state_res* s;
+  ErlNifBinary in;
+  unsigned levels;
+  ErlNifUInt64 max_sync;
+  if (!enif_get_resource(env, argv[0], STATE_RT, (void**)&s) || !enif_inspect_binary(env, argv[1], &in) ||
+      !enif_get_uint(env, argv[2], &levels) || !enif_get_uint64(env, argv[3], &max_sync) ||
+      !s->has_tree || in.size < 20)
+    return enif_make_badarg(env);
+  engine_res* g = s->eng;
+  enif_mutex_lock(g->lock);
+  int rc = DG_OK, status = 0;
+  dg_merkle_cont ci, co;
+  memset(&co, 0, sizeof co);
+  uint64_t *keys = NULL, n_keys = 0, n_total = 0;
+  ERL_NIF_TERM r, res = A_NIL;
+  uint32_t level;
+  uint64_t n, nb;
+  memcpy(&level, in.data, 4);
+  memcpy(&n, in.data + 4, 8);
+  memcpy(&nb, in.data + 12, 8);
+  TRY(cont_alloc(g, n, nb, &ci));
+  ci.level = level;
+  ci.n = n;
+  ci.n_buckets = nb;
+  TRY(dg_copy_to_device(g->e, ci.pos, in.data + 20, n * 8));
+  TRY(dg_copy_to_device(g->e, ci.hash, in.data + 20 + n * 8, n * 8));
+  if (nb) TRY(dg_copy_to_device(g->e, ci.bucket, in.data + 20 + n * 16, nb * 8));
+  const uint64_t cap_keys = max_sync ? max_sync : 1;
+  TRY(dg_buffer_alloc(g->e, cap_keys * 8, (void**)&keys));
+  /* the output: grown to the sizes a DG_E_CAPACITY reports */
+  uint64_t cap = 4 * (n ? n : 1), cap_b = n ? n : 1;
+  for (int attempt = 0; attempt < 3; attempt++) {
+    TRY(cont_alloc(g, cap, cap_b, &co));
+    rc = dg_merkle_continue(g->e, &s->tree, &s->rows, &ci, levels, &co, keys, cap_keys, &n_keys,
+                            &n_total, &status);
+    if (rc != DG_E_CAPACITY) break;
+    cap = co.n > cap ? co.n : cap;
+    cap_b = co.n_buckets > cap_b ? co.n_buckets : cap_b;
+    cont_free(g, &co);
+    memset(&co, 0, sizeof co);
+  }
+  if (rc) goto out;
+  if (status == 1) {
+    TRY(dg_merkle_truncate(g->e, &s->tree, &co, max_sync));  /* truncate_diff, :98 */
+    TRY(cont_to_binary(env, g, &co, &res));
+    res = enif_make_tuple2(env, A_CONTINUE, res);
+  } else {
+    /* {:ok, keys}: the first max_sync_size differing keys (Enum.take, :105) */
+    uint64_t* hk = (uint64_t*)enif_alloc((n_keys ? n_keys : 1) * 8);
+    rc = dg_copy_to_host(g->e, hk, keys, n_keys * 8);
+    ERL_NIF_TERM l = enif_make_list(env, 0);
+    for (uint64_t i = n_keys; !rc && i-- > 0;) {
+      const boxed* b = (const boxed*)dgm_key_term(g->u, hk[i]);
+      l = enif_make_list_cell(env, enif_make_copy(env, b->t), l);
+    }
+    enif_free(hk);
+    res = enif_make_tuple2(env, A_OK, l);
+  }
+out:
+  r = rc ? error_term(env, rc) : res;
+  cont_free(g, &ci);
+  cont_free(g, &co);
+  dg_buffer_free(g->e, keys);
+  enif_mutex_unlock(g->lock);
+  return r;
+}
+
+/* ------------------------------------------------------------ load */
+static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
+  (void)priv;
+  (void)info;
+  ENGINE_RT = enif_open_resource_type(env, NULL, "deltagpu_engine", engine_dtor, ERL_NIF_RT_CREATE, NULL);
+  STATE_RT = enif_open_resource_type(env, NULL, "deltagpu_state", state_dtor, ERL_NIF_RT_CREATE, NULL);
+  A_OK = enif_make_atom(env, "ok");
+  A_ERROR = enif_make_atom(env, "error");
+  A_NIL = enif_make_atom(env, "nil");
+  A_ALL = enif_make_atom(env, "all");
+  A_CONTINUE = enif_make_atom(env, "continue");
+  A_MAP = enif_make_atom(env, "map");
+  A_STRUCT = enif_make_atom(env, "__struct__");
+  A_MAPSET = enif_make_atom(env, "Elixir.MapSet");
+  return (ENGINE_RT && STATE_RT) ? 0 : 1;  /* a failed load -> the Elixir code path */
+}
+
+static ErlNifFunc funcs[] = {
+    {"engine_open", 1, engine_open, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"state_load", 3, state_load, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"join_delta", 4, join_delta, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"read", 2, read_nif, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"take", 2, take_nif, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"merkle_build", 2, merkle_build_nif, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"merkle_prepare", 2, merkle_prepare_nif, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"merkle_continue", 4, merkle_continue_nif, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+};
+
+ERL_NIF_INIT(Elixir.DeltaCrdt.GPU, funcs, load, NULL, NULL, NULL)
