@@ -152,32 +152,36 @@ def config2_shard(rank: int, world: int, keys_per_rank: int = 1_000_000, seed: i
 
 
 def merkle_pair(n_keys: int = 1_000_000, diff_frac: float = 0.01, seed: int = 4, keys=None,
-                nodes: NodeTable | None = None):
-    """Config-4-shaped pair: two replicas of the same base (written by replica 0) that
-    differ on ~diff_frac of the keys (one side re-added them as replica 2).  Returns
+                nodes: NodeTable | None = None, n_total: int | None = None):
+    """Config-4-shaped pair: two replicas of the same base (replica 0 wrote key k with
+    counter k, ts = k * 1000) that differ on ~diff_frac of the keys (replica 2 re-added
+    them: counter k, ts past the base, a value drawn from k).  Every choice is a function
+    of the key alone, so the rows of a key-hash shard (`keys`, a subset of 1..n_total) are
+    exactly that shard's slice of the whole replica pair, and each shard carries the
+    replicas' full version vectors ({0: n_total}, {0: n_total, 2: n_total}).  Returns
     (A, B)."""
     N = nodes or NodeTable(3, 4)
     if keys is None:
         k = np.arange(1, n_keys + 1, dtype=np.uint64)
     else:
         k = np.asarray(keys, np.uint64)
+    total = int(n_total if n_total is not None else (int(k.max()) if len(k) else 0))
     n = len(k)
     key = splitmix64_np(k)
     val = encode_int_value(k.astype(np.int64))
     ts = k.astype(np.int64) * 1000
     node = np.full(n, N[0], np.uint32)
-    cnt = np.arange(1, n + 1, dtype=np.uint64)
-    A = {"rows": sort_rows(key, val, ts, node, cnt), "ctx": vv({N[0]: n}), "nodes": N}
-    rng = np.random.default_rng(seed)
-    d = rng.random(n) < diff_frac
-    nd = int(d.sum())
-    val_b, ts_b, node_b, cnt_b = val.copy(), ts.copy(), node.copy(), cnt.copy()
-    val_b[d] = encode_int_value(rng.integers(0, 1 << 62, nd, dtype=np.int64))
-    ts_b[d] = int(ts.max() if n else 0) + 1000 + rng.integers(0, 1_000_000_000, nd, dtype=np.int64)
+    cnt = k.copy()
+    A = {"rows": sort_rows(key, val, ts, node, cnt), "ctx": vv({N[0]: total}), "nodes": N}
+    h = splitmix64_np(k ^ np.uint64(seed * 0x9E3779B97F4A7C15 & ((1 << 64) - 1)))
+    d = (h % np.uint64(1 << 20)).astype(np.float64) < diff_frac * (1 << 20)
+    hv = splitmix64_np(h)
+    val_b, ts_b, node_b = val.copy(), ts.copy(), node.copy()
+    val_b[d] = encode_int_value((hv[d] >> np.uint64(2)).astype(np.int64))
+    ts_b[d] = total * 1000 + 1000 + (hv[d] % np.uint64(1_000_000_000)).astype(np.int64)
     node_b[d] = N[2]
-    cnt_b[d] = np.arange(1, nd + 1, dtype=np.uint64)
-    B = {"rows": sort_rows(key, val_b, ts_b, node_b, cnt_b), "ctx": vv({N[0]: n, N[2]: nd}),
-         "nodes": N}
+    B = {"rows": sort_rows(key, val_b, ts_b, node_b, cnt.copy()),
+         "ctx": vv({N[0]: total, N[2]: total}), "nodes": N}
     return A, B
 
 
@@ -293,10 +297,12 @@ def config3(n_keys: int = 10_000_000, n_replicas: int = 64, touch: float = 0.01,
 def config4_shard(rank: int, world: int, keys_per_rank: int = 12_500_000,
                   diff_frac: float = 0.01, seed: int = 4):
     """Config 4, one key-hash shard: the shard `rank` of a world * keys_per_rank key
-    space of two replicas that differ on ~diff_frac of the keys (merkle_pair)."""
+    space of two replicas that differ on ~diff_frac of the keys (merkle_pair: the
+    shard's exact slice of the whole pair, with the replicas' full version vectors)."""
     k = np.arange(1, world * keys_per_rank + 1, dtype=np.uint64)
     mine = shard_of(splitmix64_np(k), world) == rank
-    return merkle_pair(keys=k[mine], diff_frac=diff_frac, seed=seed + rank, nodes=NodeTable(3, seed))
+    return merkle_pair(keys=k[mine], diff_frac=diff_frac, seed=seed, nodes=NodeTable(3, seed),
+                       n_total=world * keys_per_rank)
 
 
 def sync_delta(rep, keys):

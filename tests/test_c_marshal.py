@@ -31,8 +31,10 @@ def test_marshal_c_cpu():
 
 @pytest.mark.gpu
 def test_marshal_c_gpu():
+    """Runs as an early process of the session (conftest.EARLY_CMDS), started before
+    this process touches the GPU."""
+    from conftest import early_result
     assert os.path.exists(EXE), "c_src/_build/test_marshal is built by __graft_entry__.build()"
-    env = dict(os.environ, DG_REQUIRE_GPU="1")
-    r = subprocess.run([EXE], capture_output=True, text=True, env=env, timeout=120)
-    assert r.returncode == 0, r.stdout + r.stderr
-    assert "gpu marshal/sort/join/read ok" in r.stdout and "gpu relabel remap ok" in r.stdout
+    rc, out = early_result("c_marshal")
+    assert rc == 0, out
+    assert "gpu marshal/sort/join/read ok" in out and "gpu relabel remap ok" in out

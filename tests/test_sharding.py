@@ -107,3 +107,18 @@ def test_two_rank_gloo_sharded_join_and_merkle():
         p.join(timeout=60)
     for rank, msg in sorted(res):
         assert msg == "ok", f"rank {rank}: {msg}"
+
+
+@pytest.mark.gpu
+def test_two_rank_sharded_round_through_libdeltagpu():
+    """tests/sharded_round.py: two processes on cuda:0, one key-hash shard each, run the
+    config-4 round through libdeltagpu (shard Merkle trees whose roots fold to the
+    unsharded root, diff, take, keyed join, VV all-reduce, incremental Merkle update)
+    against the C oracle's unsharded results.  Started at session start, before this
+    process touches the GPU (conftest.EARLY_CMDS).  Unmeasured at 8 GPUs: the driver's
+    SCALE run is the 8-GPU measurement."""
+    from conftest import early_result
+    rc, out = early_result("sharded2")
+    assert rc == 0, out
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 2 and all('"ok": true' in ln for ln in lines), out
