@@ -258,6 +258,7 @@ def config3_rate(eng, torch, dev, n_keys=10_000_000, reps=3):
     return {"metric": "merged dots/s, config 3 (64 keyed sync deltas into a 10M-key state)",
             "value": rows_in / el, "unit": "merged dots/s", "ms_per_batch": el * 1e3,
             "alg_bytes": alg, "alg_GBps": alg / el / 1e9,
+            "alg_frac": alg / el / 1e9 / HBM_PEAK_GBS,  # of the HBM peak, over the whole call
             "state_rows": sb.n, "delta_rows": d_rows, "keyset_entries": n_keys_total,
             "rows_out": res["n"], "stepwise_ms_per_batch": el_fold * 1e3,
             "note": "dg_apply_deltas, synchronous (one host sync), arguments marshalled once "
@@ -285,7 +286,7 @@ def changes_rate(eng, torch, pr, reps=20):
             "note": "synchronous calls (host sync each), median of reps"}
 
 
-def config5_rate(eng, torch, dev, n_keys=12_500_000, reps=5):
+def config5_rate(eng, torch, dev, n_keys=12_500_000, reps=5, steps=20):
     """Config 5 at one GPU's share of 100M keys over 8 GPUs: full-state join of two
     remove-heavy replicas (50 % removes, 64 nodes, ts in [0,16): LWW ties everywhere),
     then read/1 of the result."""
@@ -305,6 +306,15 @@ def config5_rate(eng, torch, dev, n_keys=12_500_000, reps=5):
         eng.sync()
 
     tj = _timed(torch, join, reps)
+    # the kernels alone: `steps` launches back to back, HIP events on the engine stream
+    launch()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(eng.stream)
+    for _ in range(steps):
+        launch()
+    ev1.record(eng.stream)
+    eng.sync()
+    tk = ev0.elapsed_time(ev1) * 1e-3 / steps
     out.n = int(d_counts[0].item())
     octx.n = int(d_counts[1].item())
 
@@ -314,14 +324,22 @@ def config5_rate(eng, torch, dev, n_keys=12_500_000, reps=5):
 
     tr = _timed(torch, read, reps)
     n_in = sa.n + sb.n
+    alg = 36 * (n_in + out.n)
     return {"metric": "merged dots/s, config 5 (remove-heavy, LWW ties), 12.5M keys per GPU",
             "value": n_in / tj, "unit": "merged dots/s", "ms_per_join": tj * 1e3,
-            "join_alg_GBps": 36 * (n_in + out.n) / tj / 1e9,
+            "join_alg_GBps": alg / tj / 1e9,
+            "roofline": {"bound": "hbm", "kernel": "join2_partition_kernel + join2_stream_kernel",
+                         "alg_bytes_per_launch": alg, "avg_launch_us": tk * 1e6,
+                         "achieved": alg / tk / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": alg / tk / 1e9 / HBM_PEAK_GBS,
+                         "launch_timing": f"HIP events on the engine stream around {steps} "
+                                          "back-to-back dg_join2_async launches"},
             "rows_in": n_in, "rows_out": out.n, "ms_per_read": tr * 1e3,
             "read_rows_per_s": out.n / tr, "read_keys_per_s": res["keys"] / tr,
             "read_keys": res["keys"], "read_alg_GBps": (36 * out.n + 16 * res["keys"]) / tr / 1e9,
-            "note": "one dg_join2_async + sync per join (arguments marshalled once); "
-                    "dg_read_lww synchronous"}
+            "note": "value / ms_per_join: one dg_join2_async + host sync per join (arguments "
+                    "marshalled once); roofline: the launches back to back; dg_read_lww "
+                    "synchronous"}
 
 
 def main():

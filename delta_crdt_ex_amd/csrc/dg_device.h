@@ -139,7 +139,19 @@ __device__ __forceinline__ int row_cmp(const Row& a, const Row& b) {
 
 __device__ __forceinline__ bool row_le(const Row& a, const Row& b) { return row_cmp(a, b) <= 0; }
 __device__ __forceinline__ bool row_eq(const Row& a, const Row& b) {
-  return a.key == b.key && a.val == b.val && a.ts == b.ts && a.node == b.node && a.cnt == b.cnt;
+  return (a.key == b.key) & (a.val == b.val) & (a.ts == b.ts) & (a.node == b.node) & (a.cnt == b.cnt);
+}
+
+// Branch-free full-tuple comparison for divergent lanes: every field is compared
+// unconditionally (ten VALU compares) and the lexicographic result is combined with
+// bitwise mask operations, instead of the exec-mask cascade row_cmp's early returns
+// compile to.
+__device__ __forceinline__ void row_cmp_bf(const Row& a, const Row& b, bool& lt, bool& eq) {
+  const bool ke = a.key == b.key, ve = a.val == b.val, te = a.ts == b.ts, ne = a.node == b.node;
+  const bool kl = a.key < b.key, vl = a.val < b.val, tl = a.ts < b.ts, nl = a.node < b.node,
+             cl = a.cnt < b.cnt;
+  lt = kl | (ke & (vl | (ve & (tl | (te & (nl | (ne & cl)))))));
+  eq = ke & ve & te & ne & (a.cnt == b.cnt);
 }
 
 // Dots.member?/2 (aw_lww_map.ex:67-73).  VV: Map.get(vv, node, 0) >= cnt.

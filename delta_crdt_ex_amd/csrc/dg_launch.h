@@ -67,16 +67,23 @@ inline size_t ctx_union_tmp_bytes(u64 na, u64 nb) {
 }
 
 // ---- kfold.hip (dg_apply_deltas in one pass; see the file header)
-constexpr int KFOLD_BLOCK = 512;
-constexpr int KFOLD_CAP_S = 1024;  // LDS capacity per key bucket: state rows,
-constexpr int KFOLD_CAP_D = 512;   //   delta rows,
-constexpr int KFOLD_CAP_M = 512;   //   keyset entries
+#ifndef DG_KFOLD_BLOCK
+#define DG_KFOLD_BLOCK 512
+#endif
+#ifndef DG_KFOLD_SCALE  // bucket capacities and means are 1024 / 512 / 512 (640 / 320 / 320) >> this
+#define DG_KFOLD_SCALE 0
+#endif
+constexpr int KFOLD_BLOCK = DG_KFOLD_BLOCK;
+constexpr int KFOLD_CAP_S = 1024 >> DG_KFOLD_SCALE;  // LDS capacity per key bucket: state rows,
+constexpr int KFOLD_CAP_D = 512 >> DG_KFOLD_SCALE;   //   delta rows,
+constexpr int KFOLD_CAP_M = 512 >> DG_KFOLD_SCALE;   //   keyset entries
 constexpr int KFOLD_MAX_K = 64;    // deltas per pass (delta masks are u64)
 constexpr int KNT = 1024;          // VV tables cover node ids < KNT
 constexpr u32 KF_PREP_FAIL = 1, KF_OVERFLOW = 2;
 constexpr u64 KFOLD_FILL_CHUNK = 256 * 8;  // elements per workgroup of the bucket fill
 // mean fill per bucket the host sizes T for (capacity / mean >= 1.6: > 10 sigma)
-constexpr u64 KFOLD_MEAN_S = 640, KFOLD_MEAN_D = 320, KFOLD_MEAN_M = 320;
+constexpr u64 KFOLD_MEAN_S = 640 >> DG_KFOLD_SCALE, KFOLD_MEAN_D = 320 >> DG_KFOLD_SCALE,
+              KFOLD_MEAN_M = 320 >> DG_KFOLD_SCALE;
 struct KRun {  // delta i: its rows, keyset (keys == nullptr: every key) and context
   Rows rows;
   const u64* keys;

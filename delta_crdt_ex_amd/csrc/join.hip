@@ -495,15 +495,22 @@ __device__ __forceinline__ void merge_items(const Ctx& ca, const Ctx& cb, const 
   int lo = lo0;
 #pragma unroll
   for (int step = STOP; step >= 1; step >>= 1) {
+    // (both reads unconditional at a clamped index, combined bitwise: no exec-mask branch)
     const int m = lo + step;
     const int mc = min(m, hi0);
-    const bool c = m <= hi0 && buf_key(s, mc) <= buf_key(s, offB + 1 + diag - mc);
+    const bool c = (m <= hi0) & (buf_key(s, mc) <= buf_key(s, offB + 1 + diag - mc));
     lo = c ? m : lo;
   }
   // (2) P(i) implies key <=, so the split is <= iq; step down while the full tuples of
-  //     a[i-1] and b[diag-i] (equal keys) say a > b.  Runs of tied keys are short.
+  //     a[i-1] and b[diag-i] (equal keys) say a > b.  Runs of tied keys are short, and
+  //     distinct keys (the common case) settle on the key columns alone.
   int i = lo;
-  while (i > lo0 && !row_le(lds_row(s, i), lds_row(s, offB + 1 + diag - i))) i--;
+  while (i > lo0 && buf_key(s, i) == buf_key(s, offB + 1 + diag - i)) {
+    bool lt, eq;
+    row_cmp_bf(lds_row(s, i), lds_row(s, offB + 1 + diag - i), lt, eq);
+    if (lt | eq) break;
+    i--;
+  }
   int j = diag - i;
   // ra = a[i], rb = b[j] (possibly the neighbour past the tile); xa / xb are the rows
   // after them, read one step ahead so no merge step waits on LDS.  (Reads past a side's
@@ -511,7 +518,7 @@ __device__ __forceinline__ void merge_items(const Ctx& ca, const Ctx& cb, const 
   // equals the last a row merged before it -- ties go to a, so an a row and its equal b
   // row are adjacent and the b row is the MapSet duplicate.
   Row ra = lds_row(s, 1 + i), rb = lds_row(s, offB + 1 + j);
-  bool dup = (a0 + (u64)i) >= 1 && row_eq(lds_row(s, i), rb);
+  bool dup = ((a0 + (u64)i) >= 1) & row_eq(lds_row(s, i), rb);
   Row xa = lds_row(s, 2 + i), xb = lds_row(s, offB + 2 + j);
   keep = 0;
   if (CHG) *ev = 0;
@@ -519,9 +526,10 @@ __device__ __forceinline__ void merge_items(const Ctx& ca, const Ctx& cb, const 
   for (int k = 0; k < JI; k++) {
     const bool valid = diag + k < dend;
     const bool bvalid = (b0 + (u64)j) < nb;  // b[j] exists globally
-    const int c = row_cmp(ra, rb);
-    const bool takeA = i < nat && (j >= nbt || c <= 0);
-    const bool inB = bvalid && c == 0;
+    bool lt, eq;
+    row_cmp_bf(ra, rb, lt, eq);
+    const bool takeA = (i < nat) & ((j >= nbt) | lt | eq);
+    const bool inB = bvalid & eq;
     bool kp;
     bool jn = true;  // the key is joined (in `keys`), not carried right-biased
     if (FAST) {
@@ -820,6 +828,7 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     }
     StripeCounts sc;  // stripe k-1's counts, in flight during the merge
     if (k > 0) stripe_load(cs, t - G - w, G, ntiles, epoch, sc);
+    JSTAMP(t, 7);
     u32 keep, ev = 0;
     unsigned short src[JI];
     merge_items<FAST, CHG>(p.ca, p.cb, s.tab[0], s.tab[1], p.keys, p.n_keys, B.n, s.buf[bi], nat,
@@ -897,10 +906,10 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     if (k > 0) {  // stripe k-1: this workgroup's tile t - G
       u64 below, all;
       stripe_sums(cs, t - G - w, G, ntiles, epoch, w, true, p.scan.err, sc, s.red, &below, &all);
+      JSTAMP(t, 5);
       write_tile(p, s, bi ^ 1, base + below, np);
       base += all;
     }
-    JSTAMP(t, 5);
     JSTAMP(t, 6);
     np = n;
     if (tn >= ntiles) {
@@ -1230,6 +1239,24 @@ static u64 resident_grid(const void* k) {
   return n;
 }
 
+// Launch of the persistent stream kernel.  Its workgroups wait on each other's tile
+// counts, so the whole grid must be resident at once even while other kernels (another
+// engine's join on another stream) compete for the CUs: a cooperative launch, which the
+// runtime only dispatches as one co-resident grid (DG_JOIN_COOP=1; default: a plain
+// launch).
+static hipError_t launch_stream(void (*kern)(JoinArgs), u64 grid, JoinArgs& p, hipStream_t st) {
+  static const bool coop = [] {
+    const char* v = getenv("DG_JOIN_COOP");
+    return v && v[0] == '1';
+  }();
+  if (!coop) {
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(JB), 0, st, p);
+    return hipGetLastError();
+  }
+  void* args[] = {&p};
+  return hipLaunchCooperativeKernel((const void*)kern, dim3((unsigned)grid), dim3(JB), args, 0, st);
+}
+
 static CtxUnionArgs make_cu(const Ctx& a, const Ctx& b, u32* out_node, u64* out_cnt,
                             u64* d_count, void* tmp) {
   CtxUnionArgs p;
@@ -1307,8 +1334,7 @@ hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& 
     const u64 gt = std::min<u64>(std::min<u64>(p.ntiles, gr - 1), (u64)CQ * JB);
     if (!no_fuse && gr >= 2 && p.ntiles <= (u64)FUSE_IT * gt) {
       p.fused = 1;
-      hipLaunchKernelGGL(kern, dim3((unsigned)gt + 1), dim3(JB), 0, st, p);
-      return hipGetLastError();
+      return launch_stream(kern, gt + 1, p, st);
     }
   }
   const u64 nb_part = (p.ntiles + 1 + (PB / WAVE) - 1) / (PB / WAVE);
@@ -1325,8 +1351,7 @@ hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& 
                        p.splits, p.lists, p.counts, p.ntiles, out, d_counts);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(JB), 0, st, p);
-  return hipGetLastError();
+  return launch_stream(kern, g, p, st);
 }
 
 hipError_t launch_join2_changes(u64 na, u64 nb, void* chg_tmp, u64* out, u64 cap, u64* d_count,

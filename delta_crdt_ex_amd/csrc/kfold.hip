@@ -215,7 +215,10 @@ __device__ u64 g_kf_stamps[65536 * 8];
   } while (0)
 #endif
 
-constexpr int NSUB = 512;  // sub-buckets of a bucket's key range (LDS counting sort)
+#ifndef DG_KFOLD_NSUB
+#define DG_KFOLD_NSUB 512
+#endif
+constexpr int NSUB = DG_KFOLD_NSUB;  // sub-buckets of a bucket's key range (LDS counting sort)
 constexpr int PER = 2;     // items per thread in the block scans
 static_assert(CS <= PER * KB && CU <= PER * KB && NSUB <= PER * KB, "scan coverage");
 

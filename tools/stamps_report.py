@@ -1,0 +1,28 @@
+"""Phase shares of the join stream kernel from a saved DG_STAMPS buffer (tools/prof_c5.py
+with C5_STAMPS=<file.npy>).  Stamps (s_memrealtime, 100 MHz, lane 0 of each tile):
+0/1 iteration start, 2 tile committed to LDS, 7 next tile's loads issued, 3 merge done, 4 block scan + compaction
+list (+ change events) done, 5 previous stripe's counts summed, 6 previous tile written.  Only shares
+are meaningful (the stamps add barriers)."""
+import sys
+
+import numpy as np
+
+
+def main(path):
+    st = np.load(path).reshape(65536, 8).astype(np.int64)
+    ntiles = int(np.nonzero(st[:, 0])[0].max()) + 1
+    st = st[:ntiles]
+    t0 = st[:, 0].min()
+    names = ["commit", "issue", "merge", "scan", "sums", "write"]
+    st[st[:, 5] == 0, 5] = st[st[:, 5] == 0, 4]  # first iteration: no previous tile
+    d = np.diff(st[:, [1, 2, 7, 3, 4, 5, 6]], axis=1) * 10 / 1000.0
+    print(f"tiles={ntiles} span={(st[:, 6].max() - t0) * 10 / 1000:.1f} us")
+    for i, nm in enumerate(names):
+        print(f"{nm:11s} median {np.median(d[:, i]):6.2f} us  p90 {np.percentile(d[:, i], 90):6.2f}"
+              f"  mean {d[:, i].mean():6.2f}")
+    it = np.diff(np.sort(st[:, 1]))
+    print("per-tile total median", np.median((st[:, 6] - st[:, 1]) * 10 / 1000))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
