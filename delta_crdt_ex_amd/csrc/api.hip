@@ -1,6 +1,7 @@
 // api.hip — the C-ABI of libdeltagpu (include/deltagpu.h): engine lifecycle,
 // argument validation, scratch management and kernel sequencing.  Errors follow
 // the header's conventions; nothing here falls back to a CPU path.
+#include <mutex>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -47,7 +48,33 @@ struct dg_engine {
   int apply_mode = 0;
   void* h_stage = nullptr;        // pinned staging of kernel descriptors
   size_t h_stage_cap = 0;
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;  // hand-offs to the device's shared join stream
 };
+
+// The single-pass join kernel is persistent: its workgroups wait on each other, so two
+// of its grids must never be in flight on one device at once (each could hold CUs the
+// other's waiting workgroups need).  While a device has one engine, its joins run on
+// the engine's stream.  With several, every engine's join kernels run on one shared
+// stream per device, ordered with the engine's own stream by events
+// (tests/test_gpu_concurrency.py).  Other processes on the same GPU are not covered:
+// deploy one process per GPU (a grid that stays short of residency times out, reports
+// DG_E_DEVICE, and dg_join2 re-runs the join with the two-pass kernels, which never wait).
+struct DevShare {
+  int engines = 0;
+  hipStream_t stream = nullptr;
+};
+std::mutex g_share_mu;
+DevShare g_share[64];
+
+// The device's shared join stream, or nullptr while e is the only engine on its device.
+hipStream_t shared_join_stream(dg_engine* e) {
+  std::lock_guard<std::mutex> g(g_share_mu);
+  DevShare& d = g_share[e->device & 63];
+  if (d.engines < 2) return nullptr;
+  if (!d.stream && hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess)
+    d.stream = nullptr;
+  return d.stream;
+}
 
 namespace {
 
@@ -219,7 +246,8 @@ int check_ctx(const dg_context* c, const char* what) {
 // receives their scratch for launch_join2_changes.
 int join2_enqueue(dg_engine* e, const dg_store* a, const dg_context* ca, const dg_store* b,
                   const dg_context* cb, const uint64_t* keys, uint64_t n_keys, dg_store* out,
-                  dg_context* out_ctx, uint64_t* d_counts, void** chg = nullptr) {
+                  dg_context* out_ctx, uint64_t* d_counts, void** chg = nullptr,
+                  bool force_two_pass = false) {
   TRY(check_store(a, "dg_join2 a"));
   TRY(check_store(b, "dg_join2 b"));
   TRY(check_ctx(ca, "dg_join2 ca"));
@@ -235,8 +263,8 @@ int join2_enqueue(dg_engine* e, const dg_store* a, const dg_context* ca, const d
   if (a->n + b->n && (!out->key || !out->val || !out->ts || !out->node || !out->cnt))
     return fail(DG_E_INVAL, "dg_join2: null output column");
   TRY(set_device(e));
-  TRY(ensure_state(e, 2 * join2_tiles(a->n, b->n) + 2));  // granules + tile splits
-  const bool two_pass = e->join_mode == JOIN_TWO_PASS && !chg;  // changes: single pass
+  TRY(ensure_state(e, 3 * join2_tiles(a->n, b->n) + 3));  // granules + tile + keyset splits
+  const bool two_pass = (force_two_pass || e->join_mode == JOIN_TWO_PASS) && !chg;  // changes: single pass
   if (!two_pass) TRY(ensure_counts(e, join2_tiles(a->n, b->n)));
   const size_t ctx_bytes = (ctx_union_tmp_bytes(ca->n, cb->n) + 255) / 256 * 256;
   const size_t pass_bytes = two_pass ? (join2_pass_tmp_bytes(a->n, b->n) + 255) / 256 * 256 : 0;
@@ -246,10 +274,21 @@ int join2_enqueue(dg_engine* e, const dg_store* a, const dg_context* ca, const d
   if (chg) *chg = chg_tmp;
   Scan sc;
   TRY(next_scan(e, &sc));
+  hipStream_t st = e->stream;
+  hipStream_t ps = two_pass ? nullptr : shared_join_stream(e);
+  if (ps) {
+    HIP_TRY(hipEventRecord(e->ev_in, e->stream));
+    HIP_TRY(hipStreamWaitEvent(ps, e->ev_in, 0));
+    st = ps;
+  }
   HIP_TRY(launch_join2(rows_of(a), ctx_of(ca), rows_of(b), ctx_of(cb), keys, keys ? n_keys : 0,
                        rows_out_of(out), out_ctx->node, out_ctx->cnt, e->tmp,
                        (char*)e->tmp + ctx_bytes, two_pass ? JOIN_TWO_PASS : JOIN_SINGLE_PASS,
-                       sc, e->join_workers, d_counts, e->stream, chg_tmp));
+                       sc, e->join_workers, d_counts, st, chg_tmp));
+  if (ps) {
+    HIP_TRY(hipEventRecord(e->ev_out, ps));
+    HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_out, 0));
+  }
   out_ctx->kind = (ca->kind == DG_CTX_DOTS && cb->kind == DG_CTX_DOTS) ? DG_CTX_DOTS : DG_CTX_VV;
   return DG_OK;
 }
@@ -309,6 +348,18 @@ int dg_engine_create(int device, void* hip_stream, dg_engine** out) {
     dg_engine_destroy(e);
     return rc;
   }
+  if (hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_out, hipEventDisableTiming) != hipSuccess) {
+    dg_engine_destroy(e);
+    return fail(DG_E_DEVICE, "dg_engine_create: hipEventCreate failed");
+  }
+  {
+    std::lock_guard<std::mutex> g(g_share_mu);
+    const int n = ++g_share[device & 63].engines;
+    // the first engine's joins ran on its own stream: let them finish before any join of
+    // this one can start, from here on they share a stream
+    if (n == 2) hipDeviceSynchronize();
+  }
   *out = e;
   return DG_OK;
 }
@@ -325,6 +376,17 @@ int dg_engine_destroy(dg_engine* e) {
   if (e->fold) hipFree(e->fold);
   if (e->h_stage) hipHostFree(e->h_stage);
   if (e->own_stream && e->stream) hipStreamDestroy(e->stream);
+  if (e->ev_in || e->ev_out) {  // a registered engine (creation got past the registry)
+    if (e->ev_in) hipEventDestroy(e->ev_in);
+    if (e->ev_out) hipEventDestroy(e->ev_out);
+    std::lock_guard<std::mutex> g(g_share_mu);
+    DevShare& d = g_share[e->device & 63];
+    if (e->ev_out && --d.engines == 0 && d.stream) {
+      hipStreamSynchronize(d.stream);
+      hipStreamDestroy(d.stream);
+      d.stream = nullptr;
+    }
+  }
   delete e;
   return DG_OK;
 }
@@ -374,7 +436,12 @@ int dg_join2(dg_engine* e, const dg_store* a, const dg_context* ca, const dg_sto
              dg_context* out_ctx) {
   if (!e) return fail(DG_E_INVAL, "null engine");
   TRY(join2_enqueue(e, a, ca, b, cb, keys, n_keys, out, out_ctx, e->d_counts));
-  TRY(read_counts(e, 2));
+  if (read_counts(e, 2) != DG_OK) {
+    // a single-pass grid that could not become resident (another process's persistent
+    // kernels on this GPU) timed out: the two-pass kernels never wait on each other
+    TRY(join2_enqueue(e, a, ca, b, cb, keys, n_keys, out, out_ctx, e->d_counts, nullptr, true));
+    TRY(read_counts(e, 2));
+  }
   out->n = e->h_counts[0];
   out_ctx->n = e->h_counts[1];
   return DG_OK;

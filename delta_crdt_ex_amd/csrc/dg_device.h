@@ -146,12 +146,17 @@ __device__ __forceinline__ bool row_eq(const Row& a, const Row& b) {
 // unconditionally (ten VALU compares) and the lexicographic result is combined with
 // bitwise mask operations, instead of the exec-mask cascade row_cmp's early returns
 // compile to.
+// (Folded from the last field to the first, so only the two running masks stay live.)
 __device__ __forceinline__ void row_cmp_bf(const Row& a, const Row& b, bool& lt, bool& eq) {
-  const bool ke = a.key == b.key, ve = a.val == b.val, te = a.ts == b.ts, ne = a.node == b.node;
-  const bool kl = a.key < b.key, vl = a.val < b.val, tl = a.ts < b.ts, nl = a.node < b.node,
-             cl = a.cnt < b.cnt;
-  lt = kl | (ke & (vl | (ve & (tl | (te & (nl | (ne & cl)))))));
-  eq = ke & ve & te & ne & (a.cnt == b.cnt);
+  bool l = a.cnt < b.cnt, e = a.cnt == b.cnt;
+  l = (a.node < b.node) | ((a.node == b.node) & l);
+  e = (a.node == b.node) & e;
+  l = (a.ts < b.ts) | ((a.ts == b.ts) & l);
+  e = (a.ts == b.ts) & e;
+  l = (a.val < b.val) | ((a.val == b.val) & l);
+  e = (a.val == b.val) & e;
+  lt = (a.key < b.key) | ((a.key == b.key) & l);
+  eq = (a.key == b.key) & e;
 }
 
 // Dots.member?/2 (aw_lww_map.ex:67-73).  VV: Map.get(vv, node, 0) >= cnt.
@@ -180,6 +185,26 @@ __device__ __forceinline__ bool ctx_covers(const u32* node, const u64* cnt, u64 
       hi = mid;
   }
   return lo < n && node[lo] == dn && cnt[lo] == dc;
+}
+
+// First index of keys[0, n) (ascending) that is >= x, by ONE wave: a 64-ary search
+// (every step probes 64 positions, one dependent load round: 12.5M rows in 4 rounds
+// instead of a 24-load binary-search chain).  Every lane returns the same value.
+__device__ __forceinline__ u64 wave_lower_bound(const u64* k, u64 n, u64 x) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  u64 lo = 0, hi = n;
+  while (hi - lo > WAVE) {
+    const u64 span = hi - lo;
+    const u64 p = lo + span * (u64)(lane + 1) / (WAVE + 1);
+    const u64 m = __ballot(k[p] < x);  // true on a prefix of the lanes
+    const int c = __popcll(m);
+    const u64 nlo = c ? lo + span * (u64)c / (WAVE + 1) + 1 : lo;
+    const u64 nhi = c < WAVE ? lo + span * (u64)(c + 1) / (WAVE + 1) : hi;
+    lo = nlo;
+    hi = nhi;
+  }
+  const bool lt = lo + lane < hi && k[lo + lane] < x;
+  return lo + (u64)__popcll(__ballot(lt));
 }
 
 __device__ __forceinline__ bool keyset_has(const u64* keys, u64 n, u64 k) {

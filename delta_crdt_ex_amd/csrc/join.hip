@@ -265,6 +265,7 @@ struct JoinArgs {
   const u64* keys;
   u64 n_keys;
   const u64* splits;  // merge-path split (a index) of every tile boundary (partition pass)
+  u64* ksplits;       // keyed joins: first index of `keys` >= the key at every tile boundary
   u64 ntiles;
   RowsOut out;
   Scan scan;  // look-back granules + tile tickets
@@ -375,8 +376,22 @@ __device__ u64 mp_split(const Rows A, const Rows B, u64 d) {
   return mp_search(A, B, d, lo, hi);
 }
 
+// Keyed joins: the first index of keys[0, n_keys) >= the key at merged position d (split
+// s), by the calling wave.  Tile t's keys lie in [key(t*JT), key((t+1)*JT)], so the
+// keyset entries they can match are [ksplit(t), ksplit(t+1)] (keys are unique).
+__device__ __forceinline__ u64 key_split(const Rows& A, const Rows& B, const u64* keys, u64 n_keys,
+                                         u64 d, u64 s) {
+  const u64 ib = d - s;
+  const bool va = s < A.n, vb = ib < B.n;
+  if (!va && !vb) return n_keys;
+  const u64 ka = va ? A.key[s] : ~0ull, kb = vb ? B.key[ib] : ~0ull;
+  return wave_lower_bound(keys, n_keys, min(ka, kb));
+}
+
 __global__ __launch_bounds__(PB) void join2_partition_kernel(Rows A, Rows B, u64 ntiles,
-                                                             u64* splits, CtxUnionArgs cu) {
+                                                             u64* splits, CtxUnionArgs cu,
+                                                             const u64* keys, u64 n_keys,
+                                                             u64* ksplits) {
   if (blockIdx.x == gridDim.x - 1) {  // extra workgroup: Dots.union(c1, c2) (aw_lww_map.ex:155)
     __shared__ u32 s_wave[PB / WAVE + 1];
     ctx_union_block<PB>(cu, s_wave);
@@ -387,6 +402,10 @@ __global__ __launch_bounds__(PB) void join2_partition_kernel(Rows A, Rows B, u64
   const u64 d = min(q * (u64)JT, A.n + B.n);
   const u64 s = mp_split(A, B, d);
   if ((threadIdx.x & (WAVE - 1)) == 0) splits[q] = s;
+  if (keys) {
+    const u64 kq = key_split(A, B, keys, n_keys, d, s);
+    if ((threadIdx.x & (WAVE - 1)) == 0) ksplits[q] = kq;
+  }
 }
 
 // ------------------------------------------------------------------- coverage
@@ -401,6 +420,32 @@ __device__ __forceinline__ bool covers(const u64* tab, const Ctx& c, u32 dn, u64
     return ctx_covers(c.node, c.cnt, c.n, 0, dn, dc);
   }
   return ctx_covers(c.node, c.cnt, c.n, c.kind, dn, dc);
+}
+
+// The keyset entries a tile's keys can match (keyed joins): keys[kl, kl + km), staged in
+// LDS (lds) when km <= KS -- a sync delta's few keys per tile -- else searched in global
+// memory (lds == nullptr).  Membership replaces a binary search of the whole keyset per
+// merged row.
+constexpr int KS = 64;
+struct KeySlice {
+  const u64* lds;
+  const u64* keys;  // keys + kl
+  u64 km;
+};
+
+__device__ __forceinline__ bool key_in(const KeySlice& ks, u64 x) {
+  if (ks.lds) {  // (uniform per tile) branch-free binary lifting over the staged slice
+    const int km = (int)ks.km;
+    int pos = 0;  // entries < x
+#pragma unroll
+    for (int step = KS; step >= 1; step >>= 1) {
+      const int m = pos + step;
+      const bool c = (m <= km) & (ks.lds[min(m, KS) - 1] < x);
+      pos = c ? m : pos;
+    }
+    return (pos < km) & (ks.lds[min(pos, KS - 1)] == x);
+  }
+  return keyset_has(ks.keys, ks.km, x);
 }
 
 // VV tables: tab_a[node] / tab_b[node] = the VV's counter for node ids < VT (coalesced
@@ -476,9 +521,10 @@ constexpr int STOP = search_top(JT);
 // cost exec-mask SALU work on every path).
 // CHG: also set bit k of `ev` when item k changes its key's rows (diff/3 of
 // causal_crdt.ex:343-351 over `keys`): a dropped a row or a newly kept b row.
-template <bool FAST, bool CHG = false>
+// FAST: both contexts are version vectors (LDS counter tables); KEYED: a `keys` list.
+template <bool FAST, bool KEYED, bool CHG = false>
 __device__ __forceinline__ void merge_items(const Ctx& ca, const Ctx& cb, const u64* tab_a,
-                                            const u64* tab_b, const u64* keys, const u64 n_keys,
+                                            const u64* tab_b, const KeySlice& ks,
                                             const u64 nb, const Buf& s, int nat, int nbt, u64 a0,
                                             u64 b0, u32& keep, unsigned short (&src)[JI],
                                             u32* ev = nullptr) {
@@ -531,7 +577,8 @@ __device__ __forceinline__ void merge_items(const Ctx& ca, const Ctx& cb, const 
     const bool takeA = (i < nat) & ((j >= nbt) | lt | eq);
     const bool inB = bvalid & eq;
     bool kp;
-    bool jn = true;  // the key is joined (in `keys`), not carried right-biased
+    // the key is joined (in `keys`), not carried right-biased
+    const bool jn = KEYED ? key_in(ks, takeA ? ra.key : rb.key) : true;
     if (FAST) {
       // Dots.member?(c_other, dot of the taken row): one LDS table read
       const u32 dn = takeA ? ra.node : rb.node;
@@ -547,9 +594,16 @@ __device__ __forceinline__ void merge_items(const Ctx& ca, const Ctx& cb, const 
         const u64 vnn = takeA ? opaque_val(cb.n) : opaque_val(ca.n);
         cov = ctx_covers(vn, vc, vnn, 0, dn, dc);
       }
-      kp = takeA ? (inB || !cov) : (!dup && !cov);
+      if (KEYED) {
+        // Map.merge(Map.drop(a), Map.drop(b)) for keys outside `keys`: a's rows survive
+        // iff b lacks the key, b's rows always
+        const bool bprev = ((b0 + (u64)j) >= 1) & (buf_key(s, offB + j) == ra.key);
+        const bool bnext = bvalid & (rb.key == ra.key);
+        kp = takeA ? (jn ? (inB | !cov) : !(bprev | bnext)) : (!jn | (!dup & !cov));
+      } else {
+        kp = takeA ? (inB || !cov) : (!dup && !cov);
+      }
     } else if (takeA) {
-      jn = keys == nullptr || keyset_has(keys, n_keys, ra.key);
       if (jn) {
         kp = inB || !covers<FAST>(tab_b, cb, ra.node, ra.cnt);
       } else {
@@ -559,7 +613,6 @@ __device__ __forceinline__ void merge_items(const Ctx& ca, const Ctx& cb, const 
         kp = !(bprev || bnext);
       }
     } else {
-      jn = keys == nullptr || keyset_has(keys, n_keys, rb.key);
       if (jn)
         kp = !dup && !covers<FAST>(tab_a, ca, rb.node, rb.cnt);
       else
@@ -665,10 +718,13 @@ __device__ __forceinline__ void commit_tile(const Staged& r, Buf& s) {
 // before the merge.  Spins stay bounded (scan.err bit 0 on timeout).
 constexpr int FUSE_IT = JB / WAVE / 2;  // fused splits: one wave per boundary, 2 per tile
 
+template <bool KEYED>
 struct StreamLds {
   Buf buf[2];
   unsigned short comp[2][JT];
   u64 tab[2][VT];
+  u64 kslice[2][KEYED ? KS : 1];    // keyed: the tile's keyset slice (<= KS entries)
+  u64 kspl[KEYED ? 2 * FUSE_IT : 1];  // keyed + fused: keyset splits of this workgroup's tiles
   u32 wave[JB / WAVE + 1];
   u64 red[2 * (JB / WAVE)];
   u64 spl[2 * FUSE_IT];  // fused: splits of this workgroup's tiles (start, end per tile)
@@ -704,9 +760,9 @@ __device__ __forceinline__ void stripe_load(const u32* cs, u64 base_t, u64 G, u6
   }
 }
 
-__device__ __forceinline__ void stripe_sums(const u32* cs, u64 base_t, u64 G, u64 ntiles, u32 epoch,
-                                            u64 w, bool need_all, u32* err, StripeCounts& c,
-                                            u64* s_red, u64* below, u64* all) {
+__device__ __forceinline__ void stripe_sums(const u32* cs, u64 base_t, u64 G, u32 epoch, u64 w,
+                                            bool need_all, u32* err, StripeCounts& c, u64* s_red,
+                                            u64* below, u64* all) {
   const int tid = threadIdx.x;
   // counts this workgroup needs: all of the stripe's (for the next stripe's base), or
   // only those of the workgroups below it (its last tile: no next stripe)
@@ -717,7 +773,7 @@ __device__ __forceinline__ void stripe_sums(const u32* cs, u64 base_t, u64 G, u6
     for (int q = 0; q < CQ; q++)
       ready &= (u64)tid + (u64)q * JB >= need || (c.v[q] >> CNT_BITS) == epoch;
     if (ready) break;
-    if (spins > (1u << 22)) {
+    if (spins > (1u << 20)) {  // the grid is not co-resident: report (api.hip re-runs the join)
       atomicOr(err, 1u);
       break;
     }
@@ -760,8 +816,9 @@ __device__ __forceinline__ void stripe_sums(const u32* cs, u64 base_t, u64 G, u6
   *all = tot;
 }
 
-__device__ __forceinline__ void write_tile(const JoinArgs& p, const StreamLds& s, int bi, u64 o0,
-                                           u32 n) {
+template <bool KEYED>
+__device__ __forceinline__ void write_tile(const JoinArgs& p, const StreamLds<KEYED>& s, int bi,
+                                           u64 o0, u32 n) {
   const Buf& b = s.buf[bi];
   for (u32 q = threadIdx.x; q < n; q += JB) {
     const Row x = lds_row(b, s.comp[bi][q]);
@@ -769,9 +826,9 @@ __device__ __forceinline__ void write_tile(const JoinArgs& p, const StreamLds& s
   }
 }
 
-template <bool FAST, bool CHG>
+template <bool FAST, bool KEYED, bool CHG>
 __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void join2_stream_kernel(JoinArgs p) {
-  __shared__ StreamLds s;
+  __shared__ StreamLds<KEYED> s;
   const int tid = threadIdx.x;
   const u64 total = p.a.n + p.b.n, ntiles = p.ntiles, w = blockIdx.x;
   const u64 G = gridDim.x - (p.fused ? 1 : 0);  // tile workgroups
@@ -788,8 +845,13 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     const int wv = tid / WAVE;
     const u64 tk = w + (u64)(wv >> 1) * G;
     if (tk < ntiles) {
-      const u64 sp = mp_split(A, B, min((tk + (wv & 1)) * (u64)JT, total));
+      const u64 d = min((tk + (wv & 1)) * (u64)JT, total);
+      const u64 sp = mp_split(A, B, d);
       if ((tid & (WAVE - 1)) == 0) s.spl[wv] = sp;
+      if (KEYED) {
+        const u64 kq = key_split(A, B, p.keys, p.n_keys, d, sp);
+        if ((tid & (WAVE - 1)) == 0) s.kspl[wv] = kq;
+      }
     }
   }
   if (FAST)
@@ -799,6 +861,14 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   auto split = [&](u64 tile, int k, int side) -> u64 {
     return p.fused ? s.spl[2 * k + side] : p.splits[tile + side];
   };
+  // keyed: the keyset slice [kl, kl + km) of the tile of iteration k; its entries are
+  // staged with the tile's rows (one per lane) when km <= KS
+  auto kslice = [&](u64 tile, int k, u64* kl) -> u64 {
+    const u64 lo = p.fused ? s.kspl[2 * k] : p.ksplits[tile];
+    const u64 hi = p.fused ? s.kspl[2 * k + 1] : p.ksplits[tile + 1];
+    *kl = lo;
+    return min(hi + 1, p.n_keys) - lo;
+  };
   u64 t = w;
   u64 a0 = split(t, 0, 0), a1 = split(t, 0, 1);
   int nat, nbt;
@@ -806,6 +876,11 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   tile_geom(t, a0, a1, total, &nat, &nbt, &b0);
   Staged r;
   issue_tile(A, B, nat, nbt, a0, b0, r);
+  u64 kl = 0, km = 0, kk = 0;
+  if (KEYED) {
+    km = kslice(t, 0, &kl);
+    if (km <= (u64)KS && (u64)tid < km) kk = p.keys[kl + tid];
+  }
   __syncthreads();  // zeroed tables visible
   if (FAST) fill_vv_tables(p.ca, p.cb, s.tab[0], s.tab[1]);  // once per workgroup
   u64 base = 0;  // output offset of the first tile of the current stripe
@@ -815,24 +890,30 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     JSTAMP(t, 0);
     JSTAMP(t, 1);
     commit_tile(r, s.buf[bi]);
+    if (KEYED && km <= (u64)KS && (u64)tid < km) s.kslice[bi][tid] = kk;
     __syncthreads();
     JSTAMP(t, 2);
     const u64 tn = t + G;
-    u64 a0n = 0, a1n = 0, b0n = 0;
+    u64 a0n = 0, a1n = 0, b0n = 0, kln = 0, kmn = 0;
     int natn = 0, nbtn = 0;
     if (tn < ntiles) {
       a0n = split(tn, k + 1, 0);
       a1n = split(tn, k + 1, 1);
       tile_geom(tn, a0n, a1n, total, &natn, &nbtn, &b0n);
       issue_tile(A, B, natn, nbtn, a0n, b0n, r);
+      if (KEYED) {
+        kmn = kslice(tn, k + 1, &kln);
+        if (kmn <= (u64)KS && (u64)tid < kmn) kk = p.keys[kln + tid];
+      }
     }
     StripeCounts sc;  // stripe k-1's counts, in flight during the merge
     if (k > 0) stripe_load(cs, t - G - w, G, ntiles, epoch, sc);
     JSTAMP(t, 7);
     u32 keep, ev = 0;
     unsigned short src[JI];
-    merge_items<FAST, CHG>(p.ca, p.cb, s.tab[0], s.tab[1], p.keys, p.n_keys, B.n, s.buf[bi], nat,
-                           nbt, a0, b0, keep, src, &ev);
+    const KeySlice ks{KEYED && km <= (u64)KS ? s.kslice[bi] : nullptr, p.keys + kl, km};
+    merge_items<FAST, KEYED, CHG>(p.ca, p.cb, s.tab[0], s.tab[1], ks, B.n, s.buf[bi], nat, nbt, a0,
+                                  b0, keep, src, &ev);
     JSTAMP(t, 3);
     u32 n;
     u32 pos = block_excl_scan<JB>(__popc(keep), s.wave, &n);
@@ -905,7 +986,7 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     JSTAMP(t, 4);
     if (k > 0) {  // stripe k-1: this workgroup's tile t - G
       u64 below, all;
-      stripe_sums(cs, t - G - w, G, ntiles, epoch, w, true, p.scan.err, sc, s.red, &below, &all);
+      stripe_sums(cs, t - G - w, G, epoch, w, true, p.scan.err, sc, s.red, &below, &all);
       JSTAMP(t, 5);
       write_tile(p, s, bi ^ 1, base + below, np);
       base += all;
@@ -916,7 +997,7 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       u64 below, all;
       StripeCounts last;
       stripe_load(cs, t - w, G, ntiles, epoch, last);
-      stripe_sums(cs, t - w, G, ntiles, epoch, w, false, p.scan.err, last, s.red, &below, &all);
+      stripe_sums(cs, t - w, G, epoch, w, false, p.scan.err, last, s.red, &below, &all);
       write_tile(p, s, bi, base + below, np);
       if (tid == 0 && t == ntiles - 1) p.d_count[0] = base + below + np;
       break;
@@ -927,6 +1008,8 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     nat = natn;
     nbt = nbtn;
     b0 = b0n;
+    kl = kln;
+    km = kmn;
     __syncthreads();  // buffer bi^1 written out: free for the next commit
   }
 }
@@ -1120,7 +1203,7 @@ __global__ __launch_bounds__(GB) void chg_write_kernel(ChgArgs p) {
 // Pass 2 (join2_compact_kernel): each workgroup sums the counts before its tile and
 // gathers the kept rows from a/b into the output.  No inter-workgroup dependency in
 // either pass.
-template <bool FAST>
+template <bool FAST, bool KEYED>
 __global__ __launch_bounds__(JB) void join2_slot_kernel(JoinArgs p) {
   __shared__ TileLds s;
   const int tid = threadIdx.x;
@@ -1143,8 +1226,9 @@ __global__ __launch_bounds__(JB) void join2_slot_kernel(JoinArgs p) {
   JSTAMP(t, 2);
   u32 keep;
   unsigned short src[JI];
-  merge_items<FAST>(p.ca, p.cb, s.u.tab[0], s.u.tab[1], p.keys, p.n_keys, p.b.n, s.buf, nat, nbt,
-                    a0, b0, keep, src);
+  const KeySlice ks{nullptr, p.keys, p.n_keys};
+  merge_items<FAST, KEYED>(p.ca, p.cb, s.u.tab[0], s.u.tab[1], ks, p.b.n, s.buf, nat, nbt, a0, b0,
+                           keep, src);
   JSTAMP(t, 3);
   u32 n;
   u32 pos = block_excl_scan<JB>(__popc(keep), s.wave, &n);  // barriers: tables dead
@@ -1287,8 +1371,9 @@ hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& 
   p.keys = keys;
   p.n_keys = n_keys;
   p.ntiles = join2_tiles(a.n, b.n);
-  u64* splits = scan.state + p.ntiles;  // look-back granules first, then the splits
-  p.splits = splits;
+  u64* splits = scan.state + p.ntiles;  // look-back granules first, then the splits,
+  p.splits = splits;                    // then the keyset splits (keyed joins)
+  p.ksplits = splits + p.ntiles + 1;
   const CtxUnionArgs cu = make_cu(ca, cb, out_ctx_node, out_ctx_cnt, d_counts + 1, ctx_tmp);
   p.out = out;
   p.scan = scan;
@@ -1312,12 +1397,17 @@ hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& 
     hipLaunchKernelGGL(ctx_union_kernel, dim3(1), dim3(CB), 0, st, cu);
     return hipGetLastError();
   }
-  // full-state join of two version vectors: LDS VV table, no key list
-  const bool fast = keys == nullptr && ca.kind == 0 && cb.kind == 0;
+  // two version vectors: LDS VV tables; a key list: per-tile keyset slices
+  const bool fast = ca.kind == 0 && cb.kind == 0;
+  const bool keyed = keys != nullptr;
   p.fused = 0;
   p.cu = cu;
-  auto kern = fast ? join2_stream_kernel<true, false> : join2_stream_kernel<false, false>;
-  if (chg_tmp) kern = fast ? join2_stream_kernel<true, true> : join2_stream_kernel<false, true>;
+  void (*const kerns[2][2][2])(JoinArgs) = {
+      {{join2_stream_kernel<false, false, false>, join2_stream_kernel<false, false, true>},
+       {join2_stream_kernel<false, true, false>, join2_stream_kernel<false, true, true>}},
+      {{join2_stream_kernel<true, false, false>, join2_stream_kernel<true, false, true>},
+       {join2_stream_kernel<true, true, false>, join2_stream_kernel<true, true, true>}}};
+  auto kern = kerns[fast][keyed][chg_tmp != nullptr];
   const bool stream = mode != JOIN_TWO_PASS || chg_tmp;
   u64 g = 0;
   if (stream) {
@@ -1339,13 +1429,14 @@ hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& 
   }
   const u64 nb_part = (p.ntiles + 1 + (PB / WAVE) - 1) / (PB / WAVE);
   hipLaunchKernelGGL(join2_partition_kernel, dim3((unsigned)nb_part + 1), dim3(PB), 0, st, a, b,
-                     p.ntiles, splits, cu);
+                     p.ntiles, splits, cu, keys, n_keys, p.ksplits);
   if (!stream) {
     char* t = (char*)pass_tmp;
     p.counts = (u32*)t;
     t += ((p.ntiles * 4 + 255) / 256) * 256;
     p.lists = (unsigned short*)t;
-    auto kern = fast ? join2_slot_kernel<true> : join2_slot_kernel<false>;
+    auto kern = fast ? (keyed ? join2_slot_kernel<true, true> : join2_slot_kernel<true, false>)
+                     : (keyed ? join2_slot_kernel<false, true> : join2_slot_kernel<false, false>);
     hipLaunchKernelGGL(kern, dim3((unsigned)p.ntiles), dim3(JB), 0, st, p);
     hipLaunchKernelGGL(join2_compact_kernel, dim3((unsigned)p.ntiles), dim3(CPB), 0, st, a, b,
                        p.splits, p.lists, p.counts, p.ntiles, out, d_counts);

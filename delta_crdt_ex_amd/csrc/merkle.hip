@@ -79,26 +79,6 @@ __device__ __forceinline__ u64 rh(const Rows& s, u64 i) {
 }
 
 // ---------------------------------------------------------------- lower bounds
-// First index of keys[0, n) (ascending) that is >= x, by ONE wave: a 64-ary search
-// (every step probes 64 positions, one dependent load round: 12.5M rows in 4 rounds
-// instead of a 24-load binary-search chain).  Every lane returns the same value.
-__device__ __forceinline__ u64 wave_lower_bound(const u64* k, u64 n, u64 x) {
-  const int lane = threadIdx.x & (WAVE - 1);
-  u64 lo = 0, hi = n;
-  while (hi - lo > WAVE) {
-    const u64 span = hi - lo;
-    const u64 p = lo + span * (u64)(lane + 1) / (WAVE + 1);
-    const u64 m = __ballot(k[p] < x);  // true on a prefix of the lanes
-    const int c = __popcll(m);
-    const u64 nlo = c ? lo + span * (u64)c / (WAVE + 1) + 1 : lo;
-    const u64 nhi = c < WAVE ? lo + span * (u64)(c + 1) / (WAVE + 1) : hi;
-    lo = nlo;
-    hi = nhi;
-  }
-  const bool lt = lo + lane < hi && k[lo + lane] < x;
-  return lo + (u64)__popcll(__ballot(lt));
-}
-
 // wave_lower_bound of bucket b's first key (b may be 2^depth: the end of the range).
 __device__ __forceinline__ u64 wave_bucket_start(const MT& t, const u64* keys, u64 n, u64 b) {
   if (b >> t.depth) {

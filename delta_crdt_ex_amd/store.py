@@ -346,7 +346,8 @@ class Engine:
         def launch():
             check(f(h, refs[0], refs[1], refs[2], refs[3], kp, nk, refs[4], refs[5], dp))
 
-        launch._keep = (args, keys, d_counts)
+        # the device memory the raw pointers name stays alive as long as the callable
+        launch._keep = (a, ca, b, cb, out, out_ctx, args, keys, d_counts)
         return launch
 
     def joink(self, stores, ctxs, out: Store | None = None, out_ctx: Context | None = None):
@@ -392,7 +393,7 @@ class Engine:
             out_ctx.kind = int(co.kind)
             return out, out_ctx
 
-        run._keep = (arr_s, arr_c, kp, kn, keys, ss, xs, so, co, deltas, dctxs)
+        run._keep = (arr_s, arr_c, kp, kn, keys, ss, xs, so, co, state, ctx, deltas, dctxs)
         if keys is not None:
             run._keep += (kn_np,)
         return run
