@@ -67,8 +67,8 @@ inline size_t ctx_union_tmp_bytes(u64 na, u64 nb) {
 }
 
 // ---- kfold.hip (dg_apply_deltas in one pass; see the file header)
-#ifndef DG_KFOLD_BLOCK
-#define DG_KFOLD_BLOCK 512
+#ifndef DG_KFOLD_BLOCK  // 1024 threads at <= 64 VGPRs: 2 buckets x 16 waves per CU
+#define DG_KFOLD_BLOCK 1024  // (config 3: 2.08-2.33 vs 2.25-2.48 ms per call at 512, A/B)
 #endif
 #ifndef DG_KFOLD_SCALE  // bucket capacities and means are 1024 / 512 / 512 (640 / 320 / 320) >> this
 #define DG_KFOLD_SCALE 0

@@ -293,7 +293,8 @@ __device__ __forceinline__ void scan_excl(const V* in, u32 n, unsigned short* pr
   if (threadIdx.x == 0) pre[n] = (unsigned short)tot;
 }
 
-__global__ __launch_bounds__(KB) void kfold_kernel(KFoldArgs p) {
+// two 1024-thread buckets per CU: 8 waves per SIMD, so at most 64 VGPRs
+__global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256, 8))) void kfold_kernel(KFoldArgs p) {
   __shared__ KLds s;
   if (*p.flag & KF_PREP_FAIL) return;  // every workgroup leaves: no ticket is taken
   const int tid = threadIdx.x;

@@ -18,10 +18,10 @@
 // unsharded tree (dg_merkle_fold_roots recombines them).
 //
 // Kernels:
-//  * build: one streaming pass over the rows (36 B/row), a wave segmented sum per
-//    bucket (plain store for a bucket inside the wave's 64-row chunk, an atomic add
-//    for the chunk's first/last run), then ONE fused upsweep launch: every workgroup
-//    reduces 2^11 buckets 11 levels in LDS, the last one to finish reduces the rest.
+//  * build: ONE launch.  A workgroup per chunk of 2^11 buckets streams the chunk's rows
+//    (36 B/row; the row range from two wave lower bounds) into LDS bucket sums, reduces
+//    the chunk's 11 levels in LDS and writes them; the last workgroup to finish (one
+//    arrival counter, write-through hand-off words) reduces the chunk roots to the root.
 //  * update: one thread per changed key re-hashes the key's rows in the old and the
 //    new store and adds the difference to its bucket (put/delete); the upsweep then
 //    re-reduces only the 2^11-bucket chunks an update touched (update_hashes).

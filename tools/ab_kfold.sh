@@ -4,7 +4,7 @@ set -o pipefail
 mkdir -p gpurun_out
 LIBS=$(cd delta_crdt_ex_amd && ls libdeltagpu*.so | grep -v stamps | grep -v JOIN)
 for l in $LIBS; do
-  DG_LIB_PATH=$PWD/delta_crdt_ex_amd/$l timeout -k 10 300 python -u -m pytest tests/test_gpu_kfold.py -x -q --timeout 120 --timeout-method thread -m gpu > gpurun_out/abk_t.log 2>&1 || { echo "$l TESTS_FAILED"; tail -30 gpurun_out/abk_t.log; exit 1; }
+  DG_LIB_PATH=$PWD/delta_crdt_ex_amd/$l timeout -k 10 300 python -u -m pytest tests/test_gpu_kfold.py -q --timeout 120 --timeout-method thread -m gpu > gpurun_out/abk_t.log 2>&1 || echo "$l TESTS_FAILED"
   echo "$l tests: $(tail -1 gpurun_out/abk_t.log)"
 done
 for rep in 1 2; do
