@@ -105,6 +105,34 @@ def test_config5_properties_large(engine):
     engine.store_check(j1)
 
 
+@pytest.mark.timeout(600)
+def test_config5_full_share_parity(engine):
+    """The bench's config-5 workload itself (one GPU's share of 100M keys: 12.5M keys,
+    22.5M rows in), bit-exact against the C oracle's join and read."""
+    a, b = W.config5(n_keys=12_500_000, n_nodes=64, seed=5)
+    sa, ca = up(a)
+    sb, cb = up(b)
+    out, octx = engine.join2(sa, ca, sb, cb)
+    wr, wc = R.join2(a["rows"], a["ctx"], b["rows"], b["ctx"])
+    rows_eq(out, wr)
+    ctx_eq(octx, wc)
+    ok, ov = engine.read_lww(out)
+    wk, wv = R.read_lww(wr)
+    assert np.array_equal(u64(ok), wk) and np.array_equal(u64(ov), wv)
+
+
+@pytest.mark.timeout(600)
+def test_config3_full_size_parity(engine):
+    """The bench's config-3 batch itself (10M keys, 64 keyed deltas) through the one-pass
+    fold, bit-exact against the C oracle's delta-by-delta fold."""
+    base, deltas = W.config3(n_keys=10_000_000, n_replicas=64, touch=0.01, seed=3)
+    out, octx = gpu_apply(engine, base, deltas)
+    wr, wc = R.apply_deltas(base["rows"], base["ctx"], [d["rows"] for d in deltas],
+                            [d["ctx"] for d in deltas], [d["keys"] for d in deltas])
+    rows_eq(out, wr)
+    ctx_eq(octx, wc)
+
+
 # ------------------------------------------------------------------ config 4
 
 @pytest.mark.parametrize("rank", range(8))
