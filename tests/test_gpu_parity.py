@@ -71,6 +71,23 @@ def test_join2_random(engine, case, seed):
         check_join(engine, a, b, keys=np.concatenate([keys[1::3], np.array([12345], np.uint64)]))
 
 
+@pytest.mark.parametrize("n_keys", [200_000, 3_000_000])  # fused splits / partition launch
+def test_join2_keyed_slices(engine, n_keys):
+    """Keyed joins through the per-tile keyset slices: sparse keysets (a few keys per
+    tile: the slice staged in LDS), a clustered run of keys (tiles whose slice is longer
+    than the LDS slice: global search) next to tiles with no key at all, keys absent
+    from both stores, and every key."""
+    a, b = W.config2(n_keys=n_keys, seed=21)
+    keys = np.unique(np.concatenate([a["rows"][0], b["rows"][0]]))
+    rng = np.random.default_rng(n_keys)
+    sparse = np.concatenate([rng.choice(keys, len(keys) // 100, replace=False),
+                             rng.integers(0, 2**63, 50, dtype=np.uint64)])
+    lo = len(keys) // 3
+    clustered = np.concatenate([keys[lo:lo + 5000], keys[::997]])
+    for ks in (sparse, clustered, keys, np.zeros(0, np.uint64)):
+        check_join(engine, a, b, keys=ks)
+
+
 def test_join2_identical_and_subset(engine):
     """Every row duplicated across the stores: dedup at every tile seam."""
     a, b = W.config2(n_keys=20000, seed=9)
