@@ -858,14 +858,23 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     for (int x = tid; x < 2 * VT; x += JB) (&s.tab[0][0])[x] = 0;
   if (p.fused) __syncthreads();
   // split of boundary `side` (0 start, 1 end) of the tile of iteration k
+  // (a uniform branch between an LDS read and a global read: a select between the two
+  // pointers would make it a flat load, whose wait also drains the previous tile's stores)
   auto split = [&](u64 tile, int k, int side) -> u64 {
-    return p.fused ? s.spl[2 * k + side] : p.splits[tile + side];
+    if (p.fused) return s.spl[2 * k + side];
+    return p.splits[tile + side];
   };
   // keyed: the keyset slice [kl, kl + km) of the tile of iteration k; its entries are
   // staged with the tile's rows (one per lane) when km <= KS
   auto kslice = [&](u64 tile, int k, u64* kl) -> u64 {
-    const u64 lo = p.fused ? s.kspl[2 * k] : p.ksplits[tile];
-    const u64 hi = p.fused ? s.kspl[2 * k + 1] : p.ksplits[tile + 1];
+    u64 lo, hi;
+    if (p.fused) {
+      lo = s.kspl[2 * k];
+      hi = s.kspl[2 * k + 1];
+    } else {
+      lo = p.ksplits[tile];
+      hi = p.ksplits[tile + 1];
+    }
     *kl = lo;
     return min(hi + 1, p.n_keys) - lo;
   };

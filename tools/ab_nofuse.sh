@@ -1,0 +1,14 @@
+# A/B with the fused-split path disabled (DG_JOIN_FUSE=0), so every build runs the
+# partition launch: config-2 bench line and the config-5 loop, twice.
+set -o pipefail
+mkdir -p gpurun_out
+BR='import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print(round(d["value"]/1e9,2), "Gdots/s", round(d["roofline"]["avg_launch_us"],2), "us/launch", round(d["roofline"]["frac"],3))'
+LIBS=$(cd delta_crdt_ex_amd && ls libdeltagpu*.so | grep -v stamps)
+for rep in 1 2; do
+for l in $LIBS; do
+  DG_JOIN_FUSE=0 DG_LIB_PATH=$PWD/delta_crdt_ex_amd/$l timeout -k 10 200 python -u bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-merkle --no-configs > gpurun_out/abn_$l.log 2>&1 || { echo "$l FAILED"; tail -5 gpurun_out/abn_$l.log; exit 1; }
+  echo -n "$l c2(nofuse): "; python -c "$BR" < gpurun_out/abn_$l.log
+  DG_JOIN_FUSE=0 DG_LIB_PATH=$PWD/delta_crdt_ex_amd/$l timeout -k 10 200 python -u tools/prof_c5.py > gpurun_out/abn_c5_$l.log 2>&1 || { echo "$l c5 FAILED"; tail -5 gpurun_out/abn_c5_$l.log; exit 1; }
+  echo -n "$l c5: "; tail -1 gpurun_out/abn_c5_$l.log
+done
+done
