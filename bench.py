@@ -286,6 +286,50 @@ def changes_rate(eng, torch, pr, reps=20):
             "note": "synchronous calls (host sync each), median of reps"}
 
 
+def e2e_rate(eng, torch, pr, reps=20):
+    """SURVEY §8(d)'s end-to-end figure on config 2: the two replicas' host SoA columns
+    copied to the device (pinned staging, as a NIF holding its marshalled rows would),
+    joined, and the joined rows + context copied back -- wall time per call.  Not `value`
+    (the bench contract's value is device-resident throughput)."""
+    a, b = pr["a"], pr["b"]
+    sa, sb, ca, cb, out, octx = pr["sa"], pr["sb"], pr["ca"], pr["cb"], pr["out"], pr["octx"]
+    cols = [(np.asarray(x), t) for rows, st in ((a["rows"], sa), (b["rows"], sb))
+            for x, t in zip(rows, (st.key, st.val, st.ts, st.node, st.cnt))]
+    pinned = [torch.from_numpy(x.view(np.int64 if x.dtype.itemsize == 8 else np.int32)).pin_memory()
+              for x, _ in cols]
+    back = [torch.empty(t.shape, dtype=t.dtype).pin_memory() for t in (out.key, out.val, out.ts,
+                                                                       out.node, out.cnt)]
+    n_in = len(a["rows"][0]) + len(b["rows"][0])
+    ph = {}
+
+    def call():
+        t0 = time.perf_counter()
+        for (x, dst), h in zip(cols, pinned):
+            dst[: len(x)].copy_(h, non_blocking=True)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        eng.join2(sa, ca, sb, cb, out=out, out_ctx=octx)
+        t2 = time.perf_counter()
+        n = out.n
+        for src, h in zip((out.key, out.val, out.ts, out.node, out.cnt), back):
+            h[:n].copy_(src[:n], non_blocking=True)
+        node, cnt = octx.to_numpy()
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        ph.setdefault("h2d", []).append(t1 - t0)
+        ph.setdefault("join", []).append(t2 - t1)
+        ph.setdefault("d2h", []).append(t3 - t2)
+
+    el = _timed(torch, call, reps)
+    med = {k: float(np.median(v)) * 1e3 for k, v in ph.items()}
+    return {"metric": "merged dots/s end to end (H2D + join + D2H), config 2",
+            "value": n_in / el, "unit": "merged dots/s", "ms_per_call": el * 1e3,
+            "ms_h2d": med["h2d"], "ms_join": med["join"], "ms_d2h": med["d2h"],
+            "bytes_h2d": 36 * n_in, "bytes_d2h": 36 * out.n,
+            "note": "pinned host staging reused across calls; synchronous join; "
+                    "median of reps"}
+
+
 def config5_rate(eng, torch, dev, n_keys=12_500_000, reps=5, steps=20):
     """Config 5 at one GPU's share of 100M keys over 8 GPUs: full-state join of two
     remove-heavy replicas (50 % removes, 64 nodes, ts in [0,16): LWW ties everywhere),
@@ -505,6 +549,7 @@ def main():
     if rank == 0:
         if not args.no_configs and world == 1:  # per-GPU secondaries: measured at N=1
             res["changes"] = changes_rate(eng, torch, pairs[0])
+            res["end_to_end"] = e2e_rate(eng, torch, pairs[0])
             for r in pairs:  # free the config-2 replicas before the larger configs
                 r.clear()
             res["config3"] = config3_rate(eng, torch, dev)
