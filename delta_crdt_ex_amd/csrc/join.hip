@@ -234,7 +234,6 @@ struct ChgLayout {
   u64* off;
   u32* cnt;
   u32* wu;
-  u32* first_dup;
   u64* fk;
   u64* lk;
 };
@@ -250,8 +249,7 @@ static __host__ ChgLayout chg_layout(void* tmp, u64 ntiles) {
   c += ntiles * 4;
   l.wu = (u32*)c;
   c += ntiles * 4;
-  l.first_dup = (u32*)c;
-  c += ntiles * 4;
+  c += ntiles * 4;  // (spare)
   c = (char*)(((uintptr_t)c + 7) & ~(uintptr_t)7);
   l.fk = (u64*)c;
   c += ntiles * 8;
@@ -932,7 +930,7 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     if (tid == 0) publish_count(cs, t, epoch, n);
     __syncthreads();
     if (CHG) {  // the tile's change events (keys, ascending, repeats allowed) -> chg_tmp,
-                // with the per-tile figures the changed-key scan needs (chg_scan_kernel)
+                // with the per-tile figures the changed-key kernels need (chg_sum/write)
       const Buf& cb = s.buf[bi];
       const int ne = __popc(ev);
       u64 fkey = 0, lkey = 0;
@@ -1029,177 +1027,157 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
 // kernel's per-tile change events (ascending; a key repeats when several of its rows
 // changed, possibly across tiles).  An event is kept where it differs from the event
 // before it: inside its tile, or -- for a tile's first event -- the last event of the
-// nearest non-empty earlier tile.  Every tile of the launch is resident at once, so
-// instead of a look-back (which would spin on the whole launch):
-//   join2_stream_kernel<_, CHG>  per tile: its events, their count, the events that
+// nearest non-empty earlier tile.  Every input is complete when these kernels run (the
+// stream kernel wrote them), so nothing waits on another workgroup:
+//   join2_stream_kernel<_, _, CHG>  per tile: its events, their count, the events that
 //                     differ from their in-tile predecessor, the first and last event
-//   chg_scan_kernel   one workgroup over the tiles: nearest non-empty predecessor
-//                     (max-scan), the first event's repeat flag, exclusive offsets
-//   chg_write_kernel  per tile: the kept events at the tile's offset
-constexpr int GB = 256, GI = (JT + GB - 1) / GB;
-constexpr int SB = 1024;  // chg_scan_kernel threads
+//   chg_sum_kernel    per chunk of CCH tiles: the chunk's summary (below)
+//   chg_write_kernel  per CWT tiles: its offset from the chunk summaries before it and the
+//                     tiles of its own chunk before it, then one wave per tile writes the
+//                     tile's kept events
+// A summary of a run of tiles: the unique events the run would hold on its own, whether
+// it has events, its first and last event.  Summaries combine associatively (the right
+// run's first event repeats the left run's last one, or not), so any prefix is a
+// reduction of a few of them.
+constexpr int CCH = WAVE;  // tiles per chunk summary (one wave's)
+constexpr int CB2 = 256;   // threads of the changed-key kernels
+constexpr int CWT = CB2 / WAVE;  // tiles per chg_write_kernel workgroup: one per wave
+constexpr int CEV = (JT + WAVE - 1) / WAVE;  // events per lane of one tile
+
+struct ChgSum {
+  u64 u;    // unique events of the run on its own
+  u64 has;  // the run has events
+  u64 fk, lk;
+};
+
+__device__ __forceinline__ ChgSum chg_combine(const ChgSum& L, const ChgSum& R) {
+  if (!L.has) return ChgSum{L.u + R.u, R.has, R.fk, R.lk};
+  if (!R.has) return L;
+  return ChgSum{L.u + R.u - (R.fk == L.lk ? 1ull : 0ull), 1ull, L.fk, R.lk};
+}
 
 struct ChgArgs {
-  const u64* tmp;  // JT events per tile
+  const u64* ev;   // JT events per tile
   const u32* cnt;  // events per tile
-  u32* wu;         // events after the first that differ from their predecessor
-  u32* first_dup;  // the tile's first event repeats the previous tile's last one
-  u64* off;        // output offset of the tile
-  u64* fk;         // the tile's first and last event (written when it has any), so the
-  u64* lk;         //   scan needs no dependent load of a predecessor tile's events
+  const u32* wu;   // events after the first that differ from their predecessor
+  const u64* fk;   // the tile's first and last event (written when it has any)
+  const u64* lk;
+  ChgSum* chunk;   // per chunk of CCH tiles
   u64 ntiles;
   u64* out;
   u64 cap;
   u64* d_count;
 };
 
-// One chunk of SB tiles' scan inputs (chg_scan_kernel loads the next chunk's while it
-// scans the current one).
-struct ChgIn {
-  u32 n, wu;
-  u64 fk, lk;
-};
-
-__device__ __forceinline__ ChgIn chg_in(const ChgArgs& p, u64 t) {
-  ChgIn x{0, 0, 0, 0};
-  if (t < p.ntiles) {
-    x.n = p.cnt[t];
-    x.wu = p.wu[t];
-    x.fk = p.fk[t];  // (unwritten for an empty tile, and then unused)
-    x.lk = p.lk[t];
-  }
-  return x;
-}
-
-// Nearest non-empty tile before each tile (a max-scan of t+1 over non-empty tiles that
-// carries that tile's last event along), the first event's repeat flag, and the tiles'
-// exclusive output offsets.  Chunks of SB * ST tiles (ST consecutive tiles per thread,
-// scanned serially), the carry held in LDS; the next chunk's inputs load during a chunk.
-constexpr int ST = 4;  // tiles per chg_scan_kernel thread per chunk
-
-__global__ __launch_bounds__(SB) void chg_scan_kernel(ChgArgs p) {
-  constexpr int NW = SB / WAVE;
-  __shared__ u32 s_wave[NW + 1];
-  __shared__ i64 s_last[NW + 1];
-  __shared__ u64 s_lkey[NW + 1];
-  __shared__ u64 s_carry[3];  // output offset; last non-empty tile (+1; 0 = none); its last event
-  const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
-  if (tid == 0) s_carry[0] = s_carry[1] = s_carry[2] = 0;
-  __syncthreads();
-  ChgIn cur[ST];
-#pragma unroll
-  for (int q = 0; q < ST; q++) cur[q] = chg_in(p, (u64)tid * ST + q);
-  for (u64 c0 = 0; c0 < p.ntiles; c0 += (u64)SB * ST) {
-    const u64 t0 = c0 + (u64)tid * ST;  // this thread's first tile
-    ChgIn nxt[ST];                      // in flight during this chunk
-#pragma unroll
-    for (int q = 0; q < ST; q++) nxt[q] = chg_in(p, t0 + (u64)SB * ST + q);
-    // the thread's own last non-empty tile (+1) and its last event
-    i64 m = 0;
-    u64 mk = 0;
-#pragma unroll
-    for (int q = 0; q < ST; q++)
-      if (cur[q].n > 0) {
-        m = (i64)(t0 + q) + 1;
-        mk = cur[q].lk;
-      }
-    for (int d = 1; d < WAVE; d <<= 1) {  // inclusive max-scan over the wave's threads
-      const i64 o = __shfl_up(m, d, WAVE);
-      const u64 ok = __shfl_up(mk, d, WAVE);
-      if (lane >= d && o > m) {
-        m = o;
-        mk = ok;
-      }
-    }
-    if (lane == WAVE - 1) {
-      s_last[w] = m;
-      s_lkey[w] = mk;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      i64 run = (i64)s_carry[1];
-      u64 rk = s_carry[2];
-      for (int i = 0; i < NW; i++) {
-        const i64 v = s_last[i];
-        const u64 vk = s_lkey[i];
-        s_last[i] = run;  // exclusive over waves
-        s_lkey[i] = rk;
-        if (v > run) {
-          run = v;
-          rk = vk;
-        }
-      }
-      s_last[NW] = run;
-      s_lkey[NW] = rk;
-    }
-    __syncthreads();
-    const i64 bw = s_last[w];
-    const u64 bk = s_lkey[w];
-    const bool own = m > bw;  // nearest non-empty tile up to this thread's last
-    i64 prev = __shfl_up(own ? m : bw, 1, WAVE);  // ... before this thread's first tile
-    u64 pk = __shfl_up(own ? mk : bk, 1, WAVE);
-    if (lane == 0) {
-      prev = bw;
-      pk = bk;
-    }
-    u32 dup[ST], uc[ST], sum = 0;
-#pragma unroll
-    for (int q = 0; q < ST; q++) {
-      dup[q] = 0;
-      uc[q] = 0;
-      if (cur[q].n > 0) {
-        dup[q] = (prev > 0 && cur[q].fk == pk) ? 1u : 0u;
-        uc[q] = cur[q].wu + 1 - dup[q];
-        prev = (i64)(t0 + q) + 1;
-        pk = cur[q].lk;
-      }
-      sum += uc[q];
-    }
-    u32 tot;
-    u64 o = s_carry[0] + block_excl_scan<SB>(sum, s_wave, &tot);
-#pragma unroll
-    for (int q = 0; q < ST; q++)
-      if (t0 + q < p.ntiles) {
-        p.first_dup[t0 + q] = dup[q];
-        p.off[t0 + q] = o;
-        o += uc[q];
-      }
-    __syncthreads();
-    if (tid == 0) {
-      s_carry[0] += tot;
-      s_carry[1] = (u64)s_last[NW];
-      s_carry[2] = s_lkey[NW];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < ST; q++) cur[q] = nxt[q];
-  }
-  if (tid == 0) p.d_count[0] = s_carry[0];
-}
-
-__global__ __launch_bounds__(GB) void chg_write_kernel(ChgArgs p) {
-  __shared__ u32 s_wave[GB / WAVE + 1];
-  const u64 t = blockIdx.x;
+__device__ __forceinline__ ChgSum chg_tile(const ChgArgs& p, u64 t) {
   const u32 n = p.cnt[t];
-  const u64* ev = p.tmp + t * (u64)JT;
-  const bool dup0 = p.first_dup[t] != 0;
-  u64 v[GI];
-  u32 keep = 0;
+  if (n == 0) return ChgSum{0, 0, 0, 0};
+  return ChgSum{(u64)p.wu[t] + 1, 1, p.fk[t], p.lk[t]};
+}
+
+// Ordered reduction of one summary per thread (thread order = tile order) over the block:
+// shuffles down within each wave (lane 0 ends with its wave's run), then the waves in
+// order.  Every thread returns the block's summary.
+__device__ __forceinline__ ChgSum shfl_down_sum(const ChgSum& x, int d) {
+  return ChgSum{__shfl_down(x.u, d, WAVE), __shfl_down(x.has, d, WAVE), __shfl_down(x.fk, d, WAVE),
+                __shfl_down(x.lk, d, WAVE)};
+}
+
+__device__ ChgSum chg_block_reduce(ChgSum x, ChgSum* s_red) {
+  const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
 #pragma unroll
-  for (int q = 0; q < GI; q++) {
-    const u32 i = threadIdx.x * GI + q;
-    v[q] = i < n ? ev[i] : 0;
-    if (i < n && (i > 0 ? ev[i - 1] != v[q] : !dup0)) keep |= 1u << q;
+  for (int d = 1; d < WAVE; d <<= 1) {
+    const ChgSum y = shfl_down_sum(x, d);
+    if (lane + d < WAVE) x = chg_combine(x, y);
   }
-  u32 tot;
-  u32 pos = block_excl_scan<GB>(__popc(keep), s_wave, &tot);
-  const u64 base = p.off[t];
+  if (lane == 0) s_red[wv] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ChgSum r = s_red[0];
+    for (int i = 1; i < CB2 / WAVE; i++) r = chg_combine(r, s_red[i]);
+    s_red[CB2 / WAVE] = r;
+  }
+  __syncthreads();
+  const ChgSum r = s_red[CB2 / WAVE];
+  __syncthreads();
+  return r;
+}
+
+// Summary of [t0, t1) (t1 - t0 <= WAVE) by one wave: one tile per lane, every lane
+// returns it.
+__device__ __forceinline__ ChgSum chg_wave_range(const ChgArgs& p, u64 t0, u64 t1) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  const u64 t = t0 + lane;
+  ChgSum x = t < t1 ? chg_tile(p, t) : ChgSum{0, 0, 0, 0};
 #pragma unroll
-  for (int q = 0; q < GI; q++)
-    if (keep & (1u << q)) {
-      const u64 o = base + pos++;
-      if (o < p.cap) p.out[o] = v[q];
+  for (int d = 1; d < WAVE; d <<= 1) {
+    const ChgSum y = shfl_down_sum(x, d);
+    if (lane + d < WAVE) x = chg_combine(x, y);
+  }
+  return ChgSum{__shfl(x.u, 0, WAVE), __shfl(x.has, 0, WAVE), __shfl(x.fk, 0, WAVE),
+                __shfl(x.lk, 0, WAVE)};  // lane 0's run, to every lane
+}
+
+// one wave per chunk of CCH tiles
+__global__ __launch_bounds__(CB2) void chg_sum_kernel(ChgArgs p, u64 nchunk) {
+  const u64 c = (u64)blockIdx.x * (CB2 / WAVE) + threadIdx.x / WAVE;
+  if (c >= nchunk) return;  // (uniform per wave)
+  const ChgSum r = chg_wave_range(p, c * CCH, min(c * CCH + CCH, p.ntiles));
+  if ((threadIdx.x & (WAVE - 1)) == 0) p.chunk[c] = r;
+}
+
+__global__ __launch_bounds__(CB2) void chg_write_kernel(ChgArgs p) {
+  __shared__ ChgSum s_red[CB2 / WAVE + 1];
+  __shared__ ChgSum s_tile[CWT];
+  __shared__ u64 s_off[CWT];
+  __shared__ u32 s_dup[CWT];
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
+  const u64 t0 = (u64)blockIdx.x * CWT, chunk = t0 / CCH;
+  // the prefix [0, t0): the chunk summaries before this chunk (CB2 at a time), then this
+  // chunk's tiles before t0 (at most CCH - CWT of them)
+  ChgSum acc{0, 0, 0, 0};
+  for (u64 c0 = 0; c0 < chunk; c0 += CB2) {
+    const ChgSum x = c0 + tid < chunk ? p.chunk[c0 + tid] : ChgSum{0, 0, 0, 0};
+    acc = chg_combine(acc, chg_block_reduce(x, s_red));
+  }
+  // (wave 0: this chunk's tiles before t0; the block reduce's barriers above retired s_red)
+  if (wv == 0) {
+    const ChgSum in = chg_wave_range(p, chunk * CCH, t0);
+    if (lane == 0) s_red[0] = chg_combine(acc, in);
+  }
+  if (tid < CWT) s_tile[tid] = t0 + tid < p.ntiles ? chg_tile(p, t0 + tid) : ChgSum{0, 0, 0, 0};
+  __syncthreads();
+  if (tid == 0) {  // this workgroup's tiles: offsets and first-event repeats, in order
+    ChgSum run = s_red[0];
+    for (int i = 0; i < CWT; i++) {
+      const ChgSum x = s_tile[i];
+      const bool dup = x.has && run.has && x.fk == run.lk;
+      s_dup[i] = dup ? 1u : 0u;
+      s_off[i] = run.u;
+      run = chg_combine(run, x);
     }
+    if (t0 + CWT >= p.ntiles) p.d_count[0] = run.u;  // the last workgroup: the total
+  }
+  __syncthreads();
+  // one wave per tile: the tile's kept events at its offset (below cap)
+  {
+    const int i = wv;
+    const u64 t = t0 + i;
+    if (t >= p.ntiles) return;
+    const u32 n = p.cnt[t];
+    const u64* ev = p.ev + t * (u64)JT;
+    u64 o = s_off[i];
+    const bool dup0 = s_dup[i] != 0;
+    for (u32 e0 = 0; e0 < n; e0 += WAVE) {
+      const u32 e = e0 + lane;
+      const u64 k = e < n ? ev[e] : 0;
+      const bool keep = e < n && (e > 0 ? ev[e - 1] != k : !dup0);
+      const u64 m = __ballot(keep);
+      const u64 pos = o + __popcll(m & ((1ull << lane) - 1));
+      if (keep && pos < p.cap) p.out[pos] = k;
+      o += __popcll(m);
+    }
+  }
 }
 
 // ---------------------------------------------------------------- two-pass join
@@ -1460,19 +1438,24 @@ hipError_t launch_join2_changes(u64 na, u64 nb, void* chg_tmp, u64* out, u64 cap
   if (ntiles == 0) return hipMemsetAsync(d_count, 0, sizeof(u64), st);
   const ChgLayout l = chg_layout(chg_tmp, ntiles);
   ChgArgs p;
-  p.tmp = l.ev;
-  p.off = l.off;
+  p.ev = l.ev;
   p.cnt = l.cnt;
   p.wu = l.wu;
-  p.first_dup = l.first_dup;
   p.fk = l.fk;
   p.lk = l.lk;
+  p.chunk = (ChgSum*)l.off;  // (ntiles / CCH + 1) x 32 B <= the ntiles x 8 B + slack region
   p.ntiles = ntiles;
   p.out = out;
   p.cap = cap;
   p.d_count = d_count;
-  hipLaunchKernelGGL(chg_scan_kernel, dim3(1), dim3(SB), 0, st, p);
-  hipLaunchKernelGGL(chg_write_kernel, dim3((unsigned)ntiles), dim3(GB), 0, st, p);
+  const u64 nchunk = (ntiles + CCH - 1) / CCH;
+  if (nchunk > 1) {  // (the last chunk's summary is never read)
+    const u64 nc = nchunk - 1;
+    hipLaunchKernelGGL(chg_sum_kernel, dim3((unsigned)((nc + CB2 / WAVE - 1) / (CB2 / WAVE))),
+                       dim3(CB2), 0, st, p, nc);
+  }
+  hipLaunchKernelGGL(chg_write_kernel, dim3((unsigned)((ntiles + CWT - 1) / CWT)), dim3(CB2), 0,
+                     st, p);
   return hipGetLastError();
 }
 
