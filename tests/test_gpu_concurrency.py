@@ -56,3 +56,37 @@ def test_two_engines_concurrent_joins(n_keys):
                 assert np.array_equal(x, y)
     for eng, *_ in jobs:
         eng.close()
+
+
+def test_join_beside_long_kernels_on_another_stream():
+    """A join while ordinary kernels of another stream hold CUs: the join's
+    grid becomes resident as those workgroups retire; the result is the same as alone."""
+    import torch
+
+    from delta_crdt_ex_amd.store import Context, Engine, Store
+    dev = "cuda:0"
+    eng = Engine(0)
+    sa, ca, sb, cb = _inputs(3_000_000, 61, dev)
+    out = Store.empty(sa.n + sb.n, dev)
+    octx = Context.empty(0, ca.n + cb.n, dev)
+    d = torch.zeros(8, dtype=torch.int64, device=dev)
+    launch = eng.prepare_join2(sa, ca, sb, cb, out, octx, d)
+    torch.cuda.synchronize()
+    launch()
+    eng.sync()
+    out.n = int(d[0].item())
+    want = tuple(c.copy() for c in out.to_numpy())
+    side = torch.cuda.Stream(device=dev)
+    x = torch.randn(64 << 20, device=dev)  # elementwise kernels: many short workgroups
+    torch.cuda.synchronize()
+    for _ in range(3):
+        with torch.cuda.stream(side):
+            for _ in range(16):
+                x = torch.sin(x) * 1.0001
+        launch()
+        eng.sync()
+        side.synchronize()
+        out.n = int(d[0].item())
+        for a, b in zip(out.to_numpy(), want):
+            assert np.array_equal(a, b)
+    eng.close()
