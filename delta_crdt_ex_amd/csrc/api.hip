@@ -25,9 +25,11 @@ struct dg_engine {
   // decoupled look-back scratch
   u64* state = nullptr;
   u64 state_cap = 0;
-  u32* ticket = nullptr;  // [0] ticket, [1] error bits, [2] store_check flag, [3] op order flag
+  u32* ticket = nullptr;  // [0] ticket, [1] error bits, [2] store_check flag, [3] op order flag,
+                          // [4] join abort epoch
                           // (16 words right behind d_counts: one allocation, see below)
   u32* counts = nullptr;  // single-pass join tile-count granules
+  u32* started = nullptr;  // single-pass join start flags (JOIN_MAX_GRID epochs)
   u64 counts_cap = 0;
   // ping-pong intermediate states of dg_joink / dg_apply_deltas
   void* fold = nullptr;
@@ -49,6 +51,19 @@ struct dg_engine {
   void* h_stage = nullptr;        // pinned staging of kernel descriptors
   size_t h_stage_cap = 0;
   hipEvent_t ev_in = nullptr, ev_out = nullptr;  // hand-offs to the device's shared join stream
+  // asynchronous calls since the last dg_engine_sync, replayed there (joins on the
+  // two-pass kernels) when a single-pass join grid aborted for lack of residency
+  struct Pending {
+    int kind;  // 0 dg_join2_async, 1 dg_merkle_build_async
+    dg_store a, b, out;
+    dg_context ca, cb, out_ctx;
+    const uint64_t* keys;
+    uint64_t n_keys;
+    uint64_t* d_counts;
+    dg_merkle t;
+    dg_merkle* tp;
+  };
+  std::vector<Pending> pending;
 };
 
 // The single-pass join kernel is persistent: its workgroups wait on each other, so two
@@ -56,9 +71,9 @@ struct dg_engine {
 // other's waiting workgroups need).  While a device has one engine, its joins run on
 // the engine's stream.  With several, every engine's join kernels run on one shared
 // stream per device, ordered with the engine's own stream by events
-// (tests/test_gpu_concurrency.py).  Other processes on the same GPU are not covered:
-// deploy one process per GPU (a grid that stays short of residency times out, reports
-// DG_E_DEVICE, and dg_join2 re-runs the join with the two-pass kernels, which never wait).
+// (tests/test_gpu_concurrency.py).  Against other streams' and processes' kernels the
+// grid checks its own residency and aborts (join.hip, stripe_sums); the calls then re-run
+// on kernels that do not wait (dg_join2, dg_engine_sync, dg_join2_changes).
 struct DevShare {
   int engines = 0;
   hipStream_t stream = nullptr;
@@ -164,12 +179,15 @@ int next_scan(dg_engine* e, Scan* s) {
   if (++e->epoch >= (1u << 20)) {
     HIP_TRY(hipMemsetAsync(e->state, 0, e->state_cap * sizeof(u64), e->stream));
     if (e->counts) HIP_TRY(hipMemsetAsync(e->counts, 0, e->counts_cap * sizeof(u32), e->stream));
+    HIP_TRY(hipMemsetAsync(e->started, 0, JOIN_MAX_GRID * sizeof(u32), e->stream));
     e->epoch = 1;
   }
   s->counts = e->counts;
   s->state = e->state;
   s->ticket = e->ticket;
   s->err = e->ticket + 1;
+  s->started = e->started;
+  s->abort = e->ticket + 4;
   s->epoch = e->epoch;
   return DG_OK;
 }
@@ -186,7 +204,7 @@ int read_counts(dg_engine* e, int n) {
   if (err) {
     HIP_TRY(hipMemsetAsync(e->ticket, 0, 4 * sizeof(u32), e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
-    return fail(DG_E_DEVICE, "look-back timeout inside a kernel (error bits 0x%x)", err);
+    return fail(DG_E_DEVICE, "a kernel timed out or a join grid aborted (error bits 0x%x)", err);
   }
   return DG_OK;
 }
@@ -334,12 +352,14 @@ int dg_engine_create(int device, void* hip_stream, dg_engine** out) {
     e->own_stream = true;
   }
   if (hipMalloc(&e->d_counts, 8 * sizeof(u64) + 16 * sizeof(u32)) != hipSuccess ||
+      hipMalloc(&e->started, JOIN_MAX_GRID * sizeof(u32)) != hipSuccess ||
       hipHostMalloc(&e->h_counts, 16 * sizeof(u64), 0) != hipSuccess) {
     dg_engine_destroy(e);
     return fail(DG_E_NOMEM, "dg_engine_create: allocation failed");
   }
   e->ticket = (u32*)(e->d_counts + 8);
-  if (hipMemsetAsync(e->d_counts, 0, 8 * sizeof(u64) + 16 * sizeof(u32), e->stream) != hipSuccess) {
+  if (hipMemsetAsync(e->d_counts, 0, 8 * sizeof(u64) + 16 * sizeof(u32), e->stream) != hipSuccess ||
+      hipMemsetAsync(e->started, 0, JOIN_MAX_GRID * sizeof(u32), e->stream) != hipSuccess) {
     dg_engine_destroy(e);
     return fail(DG_E_DEVICE, "dg_engine_create: hipMemsetAsync failed");
   }
@@ -373,6 +393,7 @@ int dg_engine_destroy(dg_engine* e) {
   if (e->h_counts) hipHostFree(e->h_counts);
   if (e->tmp) hipFree(e->tmp);
   if (e->counts) hipFree(e->counts);
+  if (e->started) hipFree(e->started);
   if (e->fold) hipFree(e->fold);
   if (e->h_stage) hipHostFree(e->h_stage);
   if (e->own_stream && e->stream) hipStreamDestroy(e->stream);
@@ -393,19 +414,44 @@ int dg_engine_destroy(dg_engine* e) {
 
 void* dg_engine_stream(dg_engine* e) { return e ? (void*)e->stream : nullptr; }
 
+constexpr int RETRY_WORKERS = 32;  // dg_join2_changes' re-run after an aborted grid
+
+// Error bits of the work on the engine stream so far (synchronizes), cleared.
+static int stream_error(dg_engine* e, u32* err) {
+  HIP_TRY(hipMemcpyAsync(&e->h_counts[12], e->ticket + 1, sizeof(u32), hipMemcpyDeviceToHost,
+                         e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  memcpy(err, &e->h_counts[12], sizeof(u32));
+  if (*err) {
+    HIP_TRY(hipMemsetAsync(e->ticket, 0, 4 * sizeof(u32), e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+  }
+  return DG_OK;
+}
+
 int dg_engine_sync(dg_engine* e) {
   if (!e) return fail(DG_E_INVAL, "null engine");
   TRY(set_device(e));
   u32 err = 0;
-  HIP_TRY(hipMemcpyAsync(&e->h_counts[12], e->ticket + 1, sizeof(u32), hipMemcpyDeviceToHost,
-                         e->stream));
-  HIP_TRY(hipStreamSynchronize(e->stream));
-  memcpy(&err, &e->h_counts[12], sizeof(u32));
-  if (err) {
-    HIP_TRY(hipMemsetAsync(e->ticket, 0, 4 * sizeof(u32), e->stream));
-    HIP_TRY(hipStreamSynchronize(e->stream));
-    return fail(DG_E_DEVICE, "look-back timeout inside a kernel (error bits 0x%x)", err);
+  TRY(stream_error(e, &err));
+  if (err & 3u) {
+    // a single-pass join grid aborted (not co-resident) or timed out: replay the
+    // asynchronous calls since the last sync in order, the joins on the two-pass kernels
+    // (their workgroups never wait on each other)
+    std::vector<dg_engine::Pending> log;
+    log.swap(e->pending);
+    for (dg_engine::Pending& q : log) {
+      if (q.kind == 0)
+        TRY(join2_enqueue(e, &q.a, &q.ca, &q.b, &q.cb, q.keys, q.n_keys, &q.out, &q.out_ctx,
+                          q.d_counts, nullptr, true));
+      else
+        TRY(dg_merkle_build_async(e, &q.a, q.tp, q.d_counts));
+    }
+    e->pending.clear();
+    TRY(stream_error(e, &err));
   }
+  e->pending.clear();
+  if (err) return fail(DG_E_DEVICE, "kernel error bits 0x%x after dg_engine_sync", err);
   return DG_OK;
 }
 
@@ -428,13 +474,27 @@ int dg_join2_async(dg_engine* e, const dg_store* a, const dg_context* ca, const 
                    const dg_context* cb, const uint64_t* keys, uint64_t n_keys, dg_store* out,
                    dg_context* out_ctx, uint64_t* d_counts) {
   if (!e) return fail(DG_E_INVAL, "null engine");
-  return join2_enqueue(e, a, ca, b, cb, keys, n_keys, out, out_ctx, d_counts);
+  TRY(join2_enqueue(e, a, ca, b, cb, keys, n_keys, out, out_ctx, d_counts));
+  dg_engine::Pending q{};
+  q.kind = 0;
+  q.a = *a;
+  q.b = *b;
+  q.out = *out;
+  q.ca = *ca;
+  q.cb = *cb;
+  q.out_ctx = *out_ctx;
+  q.keys = keys;
+  q.n_keys = n_keys;
+  q.d_counts = d_counts;
+  if (e->pending.size() < 4096) e->pending.push_back(q);  // (a bounded log)
+  return DG_OK;
 }
 
 int dg_join2(dg_engine* e, const dg_store* a, const dg_context* ca, const dg_store* b,
              const dg_context* cb, const uint64_t* keys, uint64_t n_keys, dg_store* out,
              dg_context* out_ctx) {
   if (!e) return fail(DG_E_INVAL, "null engine");
+  if (!e->pending.empty()) TRY(dg_engine_sync(e));  // settle earlier asynchronous calls
   TRY(join2_enqueue(e, a, ca, b, cb, keys, n_keys, out, out_ctx, e->d_counts));
   if (read_counts(e, 2) != DG_OK) {
     // a single-pass grid that could not become resident (another process's persistent
@@ -452,10 +512,21 @@ int dg_join2_changes(dg_engine* e, const dg_store* a, const dg_context* ca, cons
                      dg_context* out_ctx, uint64_t* changed, uint64_t cap, uint64_t* n_changed) {
   if (!e) return fail(DG_E_INVAL, "null engine");
   if (!n_changed || (cap && !changed)) return fail(DG_E_INVAL, "dg_join2_changes: null output");
+  if (!e->pending.empty()) TRY(dg_engine_sync(e));
   void* chg = nullptr;
   TRY(join2_enqueue(e, a, ca, b, cb, keys, n_keys, out, out_ctx, e->d_counts, &chg));
   HIP_TRY(launch_join2_changes(a->n, b->n, chg, changed, cap, e->d_counts + 2, e->stream));
-  TRY(read_counts(e, 3));
+  if (read_counts(e, 3) != DG_OK) {
+    // the grid aborted (not co-resident): the change events come from the single-pass
+    // kernel only, so re-run it on a grid small enough to find room beside other work
+    const int workers = e->join_workers;
+    e->join_workers = RETRY_WORKERS;
+    const int rc = join2_enqueue(e, a, ca, b, cb, keys, n_keys, out, out_ctx, e->d_counts, &chg);
+    e->join_workers = workers;
+    TRY(rc);
+    HIP_TRY(launch_join2_changes(a->n, b->n, chg, changed, cap, e->d_counts + 2, e->stream));
+    TRY(read_counts(e, 3));
+  }
   out->n = e->h_counts[0];
   out_ctx->n = e->h_counts[1];
   *n_changed = e->h_counts[2];
@@ -913,6 +984,13 @@ int dg_merkle_build_async(dg_engine* e, const dg_store* s, dg_merkle* t, uint64_
   HIP_TRY(hipMemsetAsync(e->ticket + 3, 0, sizeof(u32), e->stream));
   HIP_TRY(launch_merkle_build(rows_of(s), merkle_of(t), d_n_keys, (u32*)e->tmp, e->ticket + 3,
                               e->stream));
+  dg_engine::Pending q{};
+  q.kind = 1;
+  q.a = *s;
+  q.t = *t;
+  q.tp = t;
+  q.d_counts = d_n_keys;
+  if (e->pending.size() < 4096) e->pending.push_back(q);
   return DG_OK;
 }
 

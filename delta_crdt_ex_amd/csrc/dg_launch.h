@@ -16,7 +16,15 @@ struct Scan {
   u32 epoch;    // granules of other epochs are ignored
   u32* counts;  // per-tile count granules {epoch:20 | count:12} of the single-pass join
                 // (written only by that kernel, zeroed when allocated)
+  // residency check of the persistent join grid: workgroup w stores the epoch to
+  // started[w] (JOIN_MAX_GRID entries, device) at its start.  A workgroup that waits long
+  // on the count of one that has not started sets *abort = epoch; the grid then runs on
+  // without waiting and the caller re-runs the join on the two-pass kernels.
+  u32* started;
+  u32* abort;
 };
+
+constexpr u64 JOIN_MAX_GRID = 2048;  // >= every single-pass join grid (join.hip checks)
 
 // ---- join.hip
 #ifndef DG_JOIN_BLOCK

@@ -733,6 +733,7 @@ struct StreamLds {
 constexpr u32 CNT_BITS = 12;  // count field of a tile-count granule (JT < 4096)
 static_assert(JT < (1 << CNT_BITS), "tile count must fit the granule's count field");
 constexpr int CQ = (1024 + JB - 1) / JB;  // stripe counts per thread (grid <= CQ * JB)
+static_assert((u64)CQ * JB + 1 <= JOIN_MAX_GRID, "start flags cover every join grid");
 
 __device__ __forceinline__ void publish_count(u32* cs, u64 t, u32 epoch, u32 n) {
   __hip_atomic_store(cs + t, (epoch << CNT_BITS) | n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -758,9 +759,54 @@ __device__ __forceinline__ void stripe_load(const u32* cs, u64 base_t, u64 G, u6
   }
 }
 
-__device__ __forceinline__ void stripe_sums(const u32* cs, u64 base_t, u64 G, u32 epoch, u64 w,
-                                            bool need_all, u32* err, StripeCounts& c, u64* s_red,
-                                            u64* below, u64* all) {
+// Waiting is safe only while the whole grid is resident.  Polls that go on for long
+// check the start flags of the workgroups waited on: one that has started stays
+// resident until it finishes, so the wait ends; one that has not (another stream's or
+// process's kernels hold the CUs) makes the waiter raise the abort flag after
+// ABORT_POLLS, and the grid runs on without waiting (err bit 2; the caller re-runs the
+// join on the two-pass kernels).  Each workgroup stores its start flag once: no
+// contended counter at launch.
+constexpr u32 ABORT_POLLS = 1u << 13;
+
+// The check's own arguments are read from the kernel-argument segment where they are
+// used (volatile: not hoisted), so they hold no registers across the tile loop.
+template <class T>
+__device__ __forceinline__ T cold(const T* field) {
+  return *(const volatile T*)field;
+}
+
+__device__ __forceinline__ const Scan* cold_scan() {
+  return &((const JoinArgs*)__builtin_amdgcn_kernarg_segment_ptr())->scan;
+}
+
+// Whether this thread stops waiting: the grid has aborted, or (after ABORT_POLLS) a
+// workgroup whose count it still lacks has not started.
+__device__ __forceinline__ bool grid_check(u32 epoch, u32 spins, u64 need, const StripeCounts& c) {
+  const Scan* sc = cold_scan();
+  u32* abort = cold(&sc->abort);
+  if (__hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch) return true;
+  if (spins <= ABORT_POLLS) return false;
+  const u32* started = cold(&sc->started);
+  bool absent = false;
+#pragma unroll
+  for (int q = 0; q < CQ; q++) {
+    const u64 x = (u64)threadIdx.x + (u64)q * JB;
+    if (x < need && (c.v[q] >> CNT_BITS) != epoch &&
+        __hip_atomic_load(started + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch)
+      absent = true;
+  }
+  if (!absent) return false;
+  __hip_atomic_store(abort, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  atomicOr(cold(&sc->err), 2u);
+  return true;
+}
+
+// After an abort the counts not yet published read as 0, so the rest of the grid runs
+// through its tiles without waiting and writes stay inside the output (whose rows the
+// caller discards).
+__device__ __forceinline__ void stripe_sums(const u32* cs, u32 epoch, u32* err, u64 base_t,
+                                            u64 G, u64 w, bool need_all, StripeCounts& c,
+                                            u64* s_red, u64* below, u64* all) {
   const int tid = threadIdx.x;
   // counts this workgroup needs: all of the stripe's (for the next stripe's base), or
   // only those of the workgroups below it (its last tile: no next stripe)
@@ -771,7 +817,13 @@ __device__ __forceinline__ void stripe_sums(const u32* cs, u64 base_t, u64 G, u3
     for (int q = 0; q < CQ; q++)
       ready &= (u64)tid + (u64)q * JB >= need || (c.v[q] >> CNT_BITS) == epoch;
     if (ready) break;
-    if (spins > (1u << 20)) {  // the grid is not co-resident: report (api.hip re-runs the join)
+    if ((spins & 63) == 63 && grid_check(epoch, spins, need, c)) {
+#pragma unroll
+      for (int q = 0; q < CQ; q++)
+        if ((c.v[q] >> CNT_BITS) != epoch) c.v[q] = epoch << CNT_BITS;
+      break;
+    }
+    if (spins > (1u << 24)) {  // unreachable on a co-resident grid
       atomicOr(err, 1u);
       break;
     }
@@ -834,6 +886,9 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   const u32 epoch = p.scan.epoch;
   const Rows& A = p.a;
   const Rows& B = p.b;
+  if (tid == 0)  // residency check (stripe_sums)
+    __hip_atomic_store(cold(&cold_scan()->started) + w, epoch, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   if (p.fused) {
     if (w == G) {  // Dots.union(c1, c2) (aw_lww_map.ex:155), beside the tiles
       ctx_union_block<JB>(p.cu, s.wave);
@@ -993,7 +1048,7 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     JSTAMP(t, 4);
     if (k > 0) {  // stripe k-1: this workgroup's tile t - G
       u64 below, all;
-      stripe_sums(cs, t - G - w, G, epoch, w, true, p.scan.err, sc, s.red, &below, &all);
+      stripe_sums(cs, epoch, p.scan.err, t - G - w, G, w, true, sc, s.red, &below, &all);
       JSTAMP(t, 5);
       write_tile(p, s, bi ^ 1, base + below, np);
       base += all;
@@ -1004,7 +1059,7 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       u64 below, all;
       StripeCounts last;
       stripe_load(cs, t - w, G, ntiles, epoch, last);
-      stripe_sums(cs, t - w, G, epoch, w, false, p.scan.err, last, s.red, &below, &all);
+      stripe_sums(cs, epoch, p.scan.err, t - w, G, w, false, last, s.red, &below, &all);
       write_tile(p, s, bi, base + below, np);
       if (tid == 0 && t == ntiles - 1) p.d_count[0] = base + below + np;
       break;

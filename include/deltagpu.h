@@ -122,6 +122,12 @@ const char* dg_last_error(void);
 int dg_engine_create(int device, void* hip_stream, dg_engine** out);
 int dg_engine_destroy(dg_engine* e);
 void* dg_engine_stream(dg_engine* e);
+/* Waits for the engine stream.  The single-pass join is a persistent grid; when it
+ * cannot become resident (other kernels hold the CUs) it aborts, and dg_engine_sync then
+ * replays the asynchronous calls made since the last sync (joins on the two-pass
+ * kernels), so their outputs are correct when it returns DG_OK.  Their arguments (and
+ * dg_merkle objects) must stay valid until then; call dg_engine_sync before a
+ * synchronous call that consumes an asynchronous call's output. */
 int dg_engine_sync(dg_engine* e);
 
 /* ---- device buffers (for callers without a device runtime of their own: the NIF) -- */

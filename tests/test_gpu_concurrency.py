@@ -90,3 +90,46 @@ def test_join_beside_long_kernels_on_another_stream():
         for a, b in zip(out.to_numpy(), want):
             assert np.array_equal(a, b)
     eng.close()
+
+
+def test_overscheduled_grid_aborts_and_replays(monkeypatch):
+    """A single-pass join grid twice the resident size (DG_JOIN_WORKERS=1024; 512
+    workgroups fit): the resident half waits on workgroups that cannot start, raises the
+    abort flag and runs on; dg_join2 re-runs on the two-pass kernels, dg_engine_sync
+    replays the asynchronous joins, dg_join2_changes re-runs on a small grid.  Every
+    result equals the one of a co-resident grid."""
+    import torch
+
+    from delta_crdt_ex_amd.store import Context, Engine, Store
+    dev = "cuda:0"
+    sa, ca, sb, cb = _inputs(3_000_000, 71, dev)
+    ref = Engine(0)
+    want_out, want_ctx, want_chg = ref.join2_changes(sa, ca, sb, cb)
+    want = tuple(c.copy() for c in want_out.to_numpy())
+    want_c = tuple(c.copy() for c in want_ctx.to_numpy())
+    want_k = want_chg.cpu().numpy()
+    ref.close()
+    monkeypatch.setenv("DG_JOIN_WORKERS", "1024")
+    eng = Engine(0)
+    out, octx = eng.join2(sa, ca, sb, cb)
+    for x, y in zip(out.to_numpy(), want):
+        assert np.array_equal(x, y)
+    for x, y in zip(octx.to_numpy(), want_c):
+        assert np.array_equal(x, y)
+    out, octx, chg = eng.join2_changes(sa, ca, sb, cb)
+    assert np.array_equal(chg.cpu().numpy(), want_k)
+    for x, y in zip(out.to_numpy(), want):
+        assert np.array_equal(x, y)
+    outs = []
+    for _ in range(2):
+        o = Store.empty(sa.n + sb.n, dev)
+        oc = Context.empty(0, ca.n + cb.n, dev)
+        d = torch.zeros(8, dtype=torch.int64, device=dev)
+        eng.prepare_join2(sa, ca, sb, cb, o, oc, d)()
+        outs.append((o, d))
+    eng.sync()
+    for o, d in outs:
+        o.n = int(d[0].item())
+        for x, y in zip(o.to_numpy(), want):
+            assert np.array_equal(x, y)
+    eng.close()
