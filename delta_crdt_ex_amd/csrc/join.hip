@@ -876,7 +876,7 @@ __device__ __forceinline__ void write_tile(const JoinArgs& p, const StreamLds<KE
   }
 }
 
-template <bool FAST, bool KEYED, bool CHG>
+template <bool FAST, bool KEYED, bool CHG, bool LATE>
 __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void join2_stream_kernel(JoinArgs p) {
   __shared__ StreamLds<KEYED> s;
   const int tid = threadIdx.x;
@@ -958,7 +958,11 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     const u64 tn = t + G;
     u64 a0n = 0, a1n = 0, b0n = 0, kln = 0, kmn = 0;
     int natn = 0, nbtn = 0;
-    if (tn < ntiles) {
+    // the next tile's loads: issued before the merge on long joins (a whole merge to land
+    // in), after it on short fused ones (LATE; A/B: config 2 39 vs 42 us per join, config
+    // 5 0.39 vs 0.38 ms).  A run-time switch between the two placements was slower than
+    // either (43 us, 0.39 ms): the placement is a template parameter.
+    auto issue_next = [&]() {
       a0n = split(tn, k + 1, 0);
       a1n = split(tn, k + 1, 1);
       tile_geom(tn, a0n, a1n, total, &natn, &nbtn, &b0n);
@@ -967,7 +971,8 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         kmn = kslice(tn, k + 1, &kln);
         if (kmn <= (u64)KS && (u64)tid < kmn) kk = p.keys[kln + tid];
       }
-    }
+    };
+    if (!LATE && tn < ntiles) issue_next();
     StripeCounts sc;  // stripe k-1's counts, in flight during the merge
     if (k > 0) stripe_load(cs, t - G - w, G, ntiles, epoch, sc);
     JSTAMP(t, 7);
@@ -983,6 +988,7 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     for (int q = 0; q < JI; q++)
       if (keep & (1u << q)) s.comp[bi][pos++] = src[q];
     if (tid == 0) publish_count(cs, t, epoch, n);
+    if (LATE && tn < ntiles) issue_next();
     __syncthreads();
     if (CHG) {  // the tile's change events (keys, ascending, repeats allowed) -> chg_tmp,
                 // with the per-tile figures the changed-key kernels need (chg_sum/write)
@@ -1444,12 +1450,17 @@ hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& 
   const bool keyed = keys != nullptr;
   p.fused = 0;
   p.cu = cu;
-  void (*const kerns[2][2][2])(JoinArgs) = {
-      {{join2_stream_kernel<false, false, false>, join2_stream_kernel<false, false, true>},
-       {join2_stream_kernel<false, true, false>, join2_stream_kernel<false, true, true>}},
-      {{join2_stream_kernel<true, false, false>, join2_stream_kernel<true, false, true>},
-       {join2_stream_kernel<true, true, false>, join2_stream_kernel<true, true, true>}}};
-  auto kern = kerns[fast][keyed][chg_tmp != nullptr];
+  void (*const kerns[2][2][2][2])(JoinArgs) = {
+      {{{join2_stream_kernel<false, false, false, false>, join2_stream_kernel<false, false, false, true>},
+        {join2_stream_kernel<false, false, true, false>, join2_stream_kernel<false, false, true, true>}},
+       {{join2_stream_kernel<false, true, false, false>, join2_stream_kernel<false, true, false, true>},
+        {join2_stream_kernel<false, true, true, false>, join2_stream_kernel<false, true, true, true>}}},
+      {{{join2_stream_kernel<true, false, false, false>, join2_stream_kernel<true, false, false, true>},
+        {join2_stream_kernel<true, false, true, false>, join2_stream_kernel<true, false, true, true>}},
+       {{join2_stream_kernel<true, true, false, false>, join2_stream_kernel<true, true, false, true>},
+        {join2_stream_kernel<true, true, true, false>, join2_stream_kernel<true, true, true, true>}}}};
+  auto kern = kerns[fast][keyed][chg_tmp != nullptr][0];
+  auto kern_late = kerns[fast][keyed][chg_tmp != nullptr][1];  // the fused launch
   const bool stream = mode != JOIN_TWO_PASS || chg_tmp;
   u64 g = 0;
   if (stream) {
@@ -1462,11 +1473,11 @@ hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& 
       const char* v = getenv("DG_JOIN_FUSE");
       return v && v[0] == '0';
     }();
-    const u64 gr = workers > 0 ? g + 1 : resident_grid((const void*)kern);
+    const u64 gr = workers > 0 ? g + 1 : resident_grid((const void*)kern_late);
     const u64 gt = std::min<u64>(std::min<u64>(p.ntiles, gr - 1), (u64)CQ * JB);
     if (!no_fuse && gr >= 2 && p.ntiles <= (u64)FUSE_IT * gt) {
       p.fused = 1;
-      return launch_stream(kern, gt + 1, p, st);
+      return launch_stream(kern_late, gt + 1, p, st);
     }
   }
   const u64 nb_part = (p.ntiles + 1 + (PB / WAVE) - 1) / (PB / WAVE);
