@@ -386,6 +386,38 @@ def config5_rate(eng, torch, dev, n_keys=12_500_000, reps=5, steps=20):
                     "synchronous"}
 
 
+def read_runs_rate(eng, torch, dev, n_keys=1_000_000, max_entries=32, reps=5):
+    """read/1 over key runs of 1..32 entries (uniform; SURVEY H2's reproducible regime
+    at its widest), the shape where a per-lane serial walk would diverge: the segmented
+    reduction of csrc/segred.hip.  Algorithmic bytes: key column twice (count and write
+    passes) + val + ts per row, 16 B per key out."""
+    from delta_crdt_ex_amd.store import Store
+    rng = np.random.default_rng(32)
+    keys = np.unique(rng.integers(0, 2**63, n_keys, dtype=np.uint64))
+    lens = rng.integers(1, max_entries + 1, len(keys))
+    n = int(lens.sum())
+    starts = np.repeat(np.cumsum(lens) - lens, lens)
+    rank = np.arange(n, dtype=np.int64) - starts
+    rows = (np.repeat(keys, lens),
+            (rank.astype(np.uint64) << np.uint64(20)) | rng.integers(0, 1 << 20, n, dtype=np.uint64),
+            rng.integers(0, 4, n).astype(np.int64),          # ts ties everywhere
+            rng.integers(0, 64, n).astype(np.uint32),
+            np.arange(1, n + 1, dtype=np.uint64))
+    s = Store.from_numpy(*rows, device=dev)
+    res = {}
+
+    def read():
+        k, _ = eng.read_lww(s)
+        res["keys"] = int(k.numel())
+
+    tr = _timed(torch, read, reps)
+    alg = 32 * n + 16 * res["keys"]
+    return {"rows": n, "keys": res["keys"], "entries_per_key": f"uniform 1..{max_entries}",
+            "ms_per_read": tr * 1e3, "alg_GBps": alg / tr / 1e9,
+            "alg_frac": alg / tr / 1e9 / HBM_PEAK_GBS,
+            "note": "dg_read_lww synchronous (three launches + one count readback)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -554,6 +586,7 @@ def main():
                 r.clear()
             res["config3"] = config3_rate(eng, torch, dev)
             res["config5"] = config5_rate(eng, torch, dev)
+            res["read_runs32"] = read_runs_rate(eng, torch, dev)
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(a, b)
         elif not args.no_cpu_baseline:

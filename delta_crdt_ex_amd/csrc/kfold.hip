@@ -479,35 +479,35 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
   __syncthreads();
   KSTAMP(t, 4);
 
-  // ---- output offset of the bucket (decoupled look-back in ticket order)
+  // ---- the bucket's survivor count goes out first (decoupled look-back in ticket
+  //      order), then every survivor's position inside the bucket is ranked while the
+  //      predecessors publish theirs, and only then is the bucket's offset looked up
   const u32 total = (u32)s.x.pre.spre[nS] + s.x.pre.upre[nU];
-  u64 base = 0;
-  if (t == 0) {
-    if (tid == 0) lb_publish(p.scan.state, 0, p.scan.epoch, LB_INC, total);
-  } else {  // block-wide: one round trip reaches a whole launch round of predecessors
-    if (tid == 0) lb_publish(p.scan.state, t, p.scan.epoch, LB_AGG, total);
-    base = lb_lookback_block<KB, 1>(p.scan.state, t, p.scan.epoch, p.scan.err, s.lb);
-    if (tid == 0) lb_publish(p.scan.state, t, p.scan.epoch, LB_INC, base + total);
-  }
-  if (tid == 0 && t == T - 1) p.d_counts[0] = base + total;
-  KSTAMP(t, 5);
+  if (tid == 0) lb_publish(p.scan.state, t, p.scan.epoch, t == 0 ? LB_INC : LB_AGG, total);
 
-  // ---- survivors in tuple order: rank = survivors of smaller keys + of the same key
-  //      with a smaller tuple
+  // survivors in tuple order: rank = survivors of smaller keys + of the same key with a
+  // smaller tuple
+  constexpr int RS = (CS + KB - 1) / KB, RU = (CU + KB - 1) / KB;
+  u32 so[RS], uo[RU];  // in-bucket output position, ~0u: not a survivor of this thread
   const unsigned short* spre = s.x.pre.spre;
   const unsigned short* upre = s.x.pre.upre;
-  for (u32 i = tid; i < nS; i += KB) {
-    if (!s.ssurv[i]) continue;
+#pragma unroll
+  for (int j = 0; j < RS; j++) {
+    const u32 i = tid + j * KB;
+    so[j] = ~0u;
+    if (i >= nS || !s.ssurv[i]) continue;
     const Row r = srow(s, i);
     const u32 lb = s.slbu[i];
     u32 less = 0;
     for (u32 q = lb; q < nU && s.ukey[q] == r.key; q++)
       if (s.usurv[q] && row_cmp(drow(s, s.utag[q] & SLOT), r) < 0) less++;
-    const u64 o = base + spre[i] + upre[lb] + less;
-    store_row_nt(p.out, o, r);
+    so[j] = spre[i] + upre[lb] + less;
   }
-  for (u32 q = tid; q < nU; q += KB) {
-    if (!s.usurv[q]) continue;
+#pragma unroll
+  for (int j = 0; j < RU; j++) {
+    const u32 q = tid + j * KB;
+    uo[j] = ~0u;
+    if (q >= nU || !s.usurv[q]) continue;
     const Row r = drow(s, s.utag[q] & SLOT);
     const u32 sb = sub_of(r.key, T, t);
     u32 gb = s.ustart[sb];
@@ -521,9 +521,24 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
     u32 sl = 0;
     for (u32 i = ls; i < le && s.skey[i] == r.key; i++)
       if (s.ssurv[i] && row_cmp(srow(s, i), r) < 0) sl++;
-    const u64 o = base + spre[ls] + sl + upre[gb] + less;
-    store_row_nt(p.out, o, r);
+    uo[j] = spre[ls] + sl + upre[gb] + less;
   }
+  KSTAMP(t, 5);
+
+  // ---- the bucket's output offset (block-wide: one round trip reaches a whole launch
+  //      round of predecessors), then the rows
+  u64 base = 0;
+  if (t > 0) {
+    base = lb_lookback_block<KB, 1>(p.scan.state, t, p.scan.epoch, p.scan.err, s.lb);
+    if (tid == 0) lb_publish(p.scan.state, t, p.scan.epoch, LB_INC, base + total);
+  }
+  if (tid == 0 && t == T - 1) p.d_counts[0] = base + total;
+#pragma unroll
+  for (int j = 0; j < RS; j++)
+    if (so[j] != ~0u) store_row_nt(p.out, base + so[j], srow(s, tid + j * KB));
+#pragma unroll
+  for (int j = 0; j < RU; j++)
+    if (uo[j] != ~0u) store_row_nt(p.out, base + uo[j], drow(s, s.utag[tid + j * KB] & SLOT));
   KSTAMP(t, 6);
 }
 

@@ -70,15 +70,41 @@ __global__ __launch_bounds__(SSB) void seg_scan_kernel(SegArgs p) {
 }
 
 // Pass 3: one output per head at the tile's offset: (key, read value).  The tile's key,
-// val and ts are staged in LDS by coalesced loads; each thread then reduces the key
-// runs that start among its SI consecutive rows from LDS (a run that leaves the tile
-// continues from global memory), and the heads are compacted in LDS and written
-// coalesced.
+// val and ts are staged in LDS by coalesced loads.  The per-key LWW choice is a
+// segmented reduction with the order-aware operator `lww_join` (the later row wins only
+// on a strictly greater ts: Enum.max_by's first maximum): each thread reduces its SI
+// consecutive rows; the part of a run that crosses thread boundaries is carried by a
+// segmented suffix scan across the wave (DPP/shuffle steps) and the block's waves (LDS),
+// so no lane walks a long run serially.  The run open at the tile's end continues past
+// it: the last wave reduces those rows from global memory, 64 at a time.  Heads are
+// compacted in LDS and written coalesced.
+struct Lww {  // a partial LWW reduction: the chosen row's ts and value; ok = any row
+  i64 ts;
+  u64 val;
+  bool ok;
+};
+
+__device__ __forceinline__ Lww lww_none() { return Lww{0, 0, false}; }
+
+// a covers rows before b's
+__device__ __forceinline__ Lww lww_join(const Lww& a, const Lww& b) {
+  const bool tb = b.ok & (!a.ok | (b.ts > a.ts));
+  return Lww{tb ? b.ts : a.ts, tb ? b.val : a.val, a.ok || b.ok};
+}
+
+__device__ __forceinline__ Lww lww_shfl_down(const Lww& x, int d) {
+  return Lww{__shfl_down(x.ts, d, WAVE), __shfl_down(x.val, d, WAVE),
+             __shfl_down((int)x.ok, d, WAVE) != 0};
+}
+
 template <SegOp OP>
 __global__ __launch_bounds__(SB) void seg_write_kernel(SegArgs p) {
+  constexpr int NW = SB / WAVE;
   __shared__ u64 s_key[ST + 1], s_x[ST], s_y[ST];  // key, val, ts
   __shared__ u32 s_wave[SB / WAVE + 1];
-  const int tid = threadIdx.x;
+  __shared__ Lww s_agg[NW + 1];  // each wave's suffix from its lane 0; [NW]: past the tile
+  __shared__ int s_closed[NW];
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
   const u64 n = p.s.n, tile = blockIdx.x, t0 = tile * ST;
   const u32 nt = (u32)min<u64>(ST, n - t0);
 #pragma unroll
@@ -93,38 +119,84 @@ __global__ __launch_bounds__(SB) void seg_write_kernel(SegArgs p) {
   }
   if (tid == 0) s_key[0] = t0 > 0 ? p.s.key[t0 - 1] : ~p.s.key[0];
   __syncthreads();
+  // the run open at the tile's end: its rows past the tile (last wave, 64 per round)
+  if (wv == NW - 1) {
+    const u64 lastkey = s_key[nt];
+    Lww past = lww_none();
+    for (u64 g0 = t0 + nt; g0 < n; g0 += WAVE) {
+      const u64 g = g0 + lane;
+      const bool in = g < n && p.s.key[g] == lastkey;
+      Lww x = in ? Lww{p.s.ts[g], p.s.val[g], true} : lww_none();
+#pragma unroll
+      for (int d = 1; d < WAVE; d <<= 1) x = lww_join(x, lww_shfl_down(x, d));
+      past = lww_join(past, Lww{__shfl(x.ts, 0, WAVE), __shfl(x.val, 0, WAVE), __shfl((int)x.ok, 0, WAVE) != 0});
+      if (__ballot(in) != ~0ull) break;
+    }
+    if (lane == 0) s_agg[NW] = past;
+  }
+  // this thread's rows: heads (segment starts), the keys it outputs, and `lead`, its rows
+  // before its first head (the tail of a run that started earlier)
   const u32 j0 = tid * SI;
-  u32 heads = 0;
-  u64 oa[SI], ob[SI];
+  u32 hm = 0, om = 0;
+  Lww lead = lww_none();
 #pragma unroll
   for (int k = 0; k < SI; k++) {
     const u32 j = j0 + k;
+    if (j >= nt) break;
+    const u64 key = s_key[j + 1];
+    if (key != s_key[j]) {
+      hm |= 1u << k;
+      if (p.keys == nullptr || keyset_has(p.keys, p.n_keys, key)) om |= 1u << k;
+    }
+    if (!hm) lead = lww_join(lead, Lww{(i64)s_y[j], s_x[j], true});
+  }
+  // segmented suffix scan of (lead, closed = has a head): S_i = lead_i ⊕ lead_{i+1} ⊕ ...
+  // up to and including the first thread with a head
+  Lww sv = lead;
+  bool sc = hm != 0;
+#pragma unroll
+  for (int d = 1; d < WAVE; d <<= 1) {
+    const Lww y = lww_shfl_down(sv, d);
+    const bool yc = __shfl_down((int)sc, d, WAVE) != 0;
+    if (!sc && lane + d < WAVE) {
+      sv = lww_join(sv, y);
+      sc = yc;
+    }
+  }
+  if (lane == 0) {
+    s_agg[wv] = sv;
+    s_closed[wv] = sc;
+  }
+  __syncthreads();
+  // carry into this thread's last run: S_{i+1}, continued across later waves and past
+  // the tile while no head closes it
+  Lww c = lww_shfl_down(sv, 1);
+  bool cc = __shfl_down((int)sc, 1, WAVE) != 0;
+  if (lane == WAVE - 1) {
+    c = lww_none();
+    cc = false;
+  }
+  for (int w2 = wv + 1; w2 < NW && !cc; w2++) {
+    c = lww_join(c, s_agg[w2]);
+    cc = s_closed[w2];
+  }
+  if (!cc) c = lww_join(c, s_agg[NW]);
+  // each head's run: its rows up to the next head, the last one also the carry
+  u64 oa[SI], ob[SI];
+  Lww acc = c;
+#pragma unroll
+  for (int k = SI - 1; k >= 0; k--) {
+    const u32 j = j0 + k;
     oa[k] = ob[k] = 0;
     if (j >= nt) continue;
-    const u64 key = s_key[j + 1];
-    if (key == s_key[j]) continue;  // not a head
-    if (p.keys != nullptr && !keyset_has(p.keys, p.n_keys, key)) continue;
-    heads |= 1u << k;
-    oa[k] = key;
-    u32 e = j + 1;
-    i64 best_ts = (i64)s_y[j];
-    u64 best_val = s_x[j];
-    for (; e < nt && s_key[e + 1] == key; e++) {
-      const i64 ts = (i64)s_y[e];
-      if (ts > best_ts) {
-        best_ts = ts;
-        best_val = s_x[e];
-      }
+    acc = lww_join(Lww{(i64)s_y[j], s_x[j], true}, acc);
+    if (hm & (1u << k)) {
+      oa[k] = s_key[j + 1];
+      ob[k] = acc.val;
+      acc = lww_none();
     }
-    for (u64 g = t0 + e; e == nt && g < n && p.s.key[g] == key; g++) {
-      const i64 ts = p.s.ts[g];
-      if (ts > best_ts) {
-        best_ts = ts;
-        best_val = p.s.val[g];
-      }
-    }
-    ob[k] = best_val;
   }
+  const u32 heads = om;
   u32 tile_total;
   u32 pos = block_excl_scan<SB>(__popc(heads), s_wave, &tile_total);
   __syncthreads();  // the staged rows are read; their arrays take the compacted heads

@@ -168,6 +168,47 @@ def test_read_lww(engine, seed):
     assert np.array_equal(u64(ok), wk) and np.array_equal(u64(ov), wv)
 
 
+def runs_store(rng, lens, ts_range):
+    """A sorted, unique store whose key i has lens[i] rows (values ascending, ts drawn
+    from a small range so LWW ties are common)."""
+    n = int(lens.sum())
+    keys = np.sort(rng.choice(2**62, len(lens), replace=False).astype(np.uint64))
+    key = np.repeat(keys, lens)
+    val = rng.integers(0, 1 << 20, n, dtype=np.uint64)
+    ts = rng.integers(-ts_range, ts_range, n).astype(np.int64)
+    node = rng.integers(0, 64, n).astype(np.uint32)
+    cnt = np.arange(1, n + 1, dtype=np.uint64)
+    o = np.lexsort((cnt, node, ts, val, key))
+    return tuple(c[o] for c in (key, val, ts, node, cnt))
+
+
+@pytest.mark.parametrize("shape", ["short", "up_to_32", "long", "giant", "tile_seams"])
+def test_read_lww_run_lengths(engine, shape):
+    """read/1 over key runs of every length: the segmented reduction carries a run across
+    lanes, waves and tiles (1024 rows), with ts ties broken toward the earlier row."""
+    rng = np.random.default_rng(len(shape))
+    if shape == "short":
+        lens = rng.integers(1, 4, 30000)
+    elif shape == "up_to_32":
+        lens = rng.integers(1, 33, 20000)
+    elif shape == "long":
+        lens = rng.integers(1, 3000, 300)
+    elif shape == "giant":
+        lens = np.array([3, 70000, 1, 5000, 2], np.int64)
+    else:  # runs ending exactly at, and one row past, tile seams
+        lens = np.array([1024, 1023, 2, 1024, 1025, 63, 65, 64, 1, 2048], np.int64)
+    rows = runs_store(rng, lens.astype(np.int64), ts_range=3)
+    s = Store.from_numpy(*rows, device=DEV)
+    ok, ov = engine.read_lww(s)
+    wk, wv = R.read_lww(rows)
+    assert np.array_equal(u64(ok), wk) and np.array_equal(u64(ov), wv)
+    sub = wk[1::2]
+    kt = torch.from_numpy(np.ascontiguousarray(sub).view(np.int64)).to(DEV)
+    ok, ov = engine.read_lww(s, keys=kt)
+    wk, wv = R.read_lww(rows, keys=sub)
+    assert np.array_equal(u64(ok), wk) and np.array_equal(u64(ov), wv)
+
+
 def test_read_lww_config2(engine):
     a, b = W.config2()
     rows, _ = R.join2(a["rows"], a["ctx"], b["rows"], b["ctx"])

@@ -2,7 +2,7 @@
 # config-3 rate (median of KF_REPS synchronous calls) per build, twice.
 set -o pipefail
 mkdir -p gpurun_out
-LIBS=$(cd delta_crdt_ex_amd && ls libdeltagpu*.so | grep -v stamps | grep -v JOIN)
+LIBS=${LIBS:-$(cd delta_crdt_ex_amd && ls libdeltagpu*.so | grep -v stamps | grep -v JOIN)}
 for l in $LIBS; do
   DG_LIB_PATH=$PWD/delta_crdt_ex_amd/$l timeout -k 10 300 python -u -m pytest tests/test_gpu_kfold.py -q --timeout 120 --timeout-method thread -m gpu > gpurun_out/abk_t.log 2>&1 || echo "$l TESTS_FAILED"
   echo "$l tests: $(tail -1 gpurun_out/abk_t.log)"
