@@ -335,9 +335,6 @@ __device__ u64 mp_search(const Rows A, const Rows B, u64 d, u64 lo, u64 hi) {
 // such probes (wave-uniform loads) put the guess within a few rows of the split for
 // hashed keys, then ONE window of 128 consecutive candidates decides it.  If the
 // split is not bracketed by the window, the exact 128-ary search runs instead.
-#ifndef DG_JOIN_PROBES
-#define DG_JOIN_PROBES 2
-#endif
 __device__ u64 mp_split(const Rows A, const Rows B, u64 d) {
   const int lane = threadIdx.x & (WAVE - 1);
   const u64 na = A.n, nb = B.n, total = na + nb;
@@ -347,7 +344,7 @@ __device__ u64 mp_split(const Rows A, const Rows B, u64 d) {
   u64 i = (u64)((double)d * (double)na / (double)total);
   i = min(max(i, lo), hi - 1);
 #pragma unroll
-  for (int r = 0; r < DG_JOIN_PROBES; r++) {
+  for (int r = 0; r < 2; r++) {
     const double gap = (double)B.key[d - 1 - i] - (double)A.key[i];
     double s = gap * scale;
     const double lim = (double)(hi - lo);
