@@ -7,12 +7,13 @@
 //    greater than every earlier one.
 //  * store_check: the sorted+unique precondition.
 //
-// Shape: one tile = 1024 rows = 256 threads x 4 consecutive rows; a thread owning a
-// key head walks the key's run forward (runs are short: one row per dot, <= 32
-// entries per key in the reference's reproducible regime).  Heads are compacted in
-// three passes -- count per tile (key column only), one-workgroup offset scan, write
-// -- not by a decoupled look-back: thousands of tiles finishing in lock-step rounds
-// made every tile walk back a whole round of predecessors.
+// Shape: one tile = 1024 rows = 256 threads x 4 consecutive rows; each key run is
+// reduced by a segmented scan across lanes and waves (seg_write_kernel), so a key with
+// many entries (<= 32 in the reference's reproducible regime, any number here) costs no
+// more than as many single-entry keys.  Heads are compacted in three passes -- count per
+// tile (key column only), one-workgroup offset scan, write -- not by a decoupled
+// look-back: thousands of tiles finishing in lock-step rounds made every tile walk back a
+// whole round of predecessors.
 #include "dg_launch.h"
 
 namespace dg {

@@ -1,6 +1,6 @@
 """Config-5 full-state join loop for rocprofv3 / PMC passes / stamps (12.5M keys per GPU,
 remove-heavy, 64 nodes, LWW ties): `C5_REPS` back-to-back dg_join2_async launches, then
-one sync.  C5_KEYS overrides the size."""
+one sync.  C5_KEYS overrides the size; C5_CONFIG=2 joins the config-2 replicas instead."""
 import os
 import sys
 import time
@@ -14,7 +14,10 @@ from delta_crdt_ex_amd.store import Context, Engine, Store  # noqa: E402
 n_keys = int(os.environ.get("C5_KEYS", 12_500_000))
 reps = int(os.environ.get("C5_REPS", 20))
 dev = "cuda:0"
-a, b = W.config5(n_keys=n_keys, n_nodes=64, seed=5)
+if os.environ.get("C5_CONFIG") == "2":
+    a, b = W.config2()
+else:
+    a, b = W.config5(n_keys=n_keys, n_nodes=64, seed=5)
 sa, sb = Store.from_numpy(*a["rows"], device=dev), Store.from_numpy(*b["rows"], device=dev)
 ca, cb = Context.from_numpy(*a["ctx"], dev), Context.from_numpy(*b["ctx"], dev)
 out = Store.empty(sa.n + sb.n, dev)

@@ -22,6 +22,9 @@ def main(path):
               f"  mean {d[:, i].mean():6.2f}")
     it = np.diff(np.sort(st[:, 1]))
     print("per-tile total median", np.median((st[:, 6] - st[:, 1]) * 10 / 1000))
+    first = (st[:, 1] - t0) * 10 / 1000  # iteration starts relative to the earliest one
+    print("iteration start (us) at deciles:", np.percentile(first, np.arange(0, 101, 10)).round(1))
+    print(f"last write done at {(st[:, 6].max() - t0) * 10 / 1000:.1f} us after the first iteration start")
 
 
 if __name__ == "__main__":
