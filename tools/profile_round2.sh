@@ -54,6 +54,14 @@ if [ -e delta_crdt_ex_amd/libdeltagpu_stamps.so ]; then
   C5_STAMPS=gpurun_out/c5_stamps.npy DG_LIB_PATH=$PWD/delta_crdt_ex_amd/libdeltagpu_stamps.so timeout -k 10 200 python -u tools/prof_c5.py > $OUT/c5_stamps_run.log 2>&1 || { tail -20 $OUT/c5_stamps_run.log; exit 1; }
   python tools/stamps_report.py gpurun_out/c5_stamps.npy > $OUT/c5_stamps.txt
 fi
+# config-2 join stamps (the bench's fused path)
+if [ -e delta_crdt_ex_amd/libdeltagpu_stamps.so ]; then
+  C5_CONFIG=2 C5_STAMPS=gpurun_out/c2_stamps.npy DG_LIB_PATH=$PWD/delta_crdt_ex_amd/libdeltagpu_stamps.so timeout -k 10 200 python -u tools/prof_c5.py > $OUT/c2_stamps_run.log 2>&1 || { tail -20 $OUT/c2_stamps_run.log; exit 1; }
+  python tools/stamps_report.py gpurun_out/c2_stamps.npy > $OUT/c2_stamps.txt
+fi
+# read/1 (segmented reduction) on config 5's joined state + a Merkle build/diff
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_rd -o rd --output-format csv -- python -u tools/prof_read.py > $OUT/read_run.log 2>&1 || { tail -20 $OUT/read_run.log; exit 1; }
+cp gpurun_out/prof_rd/rd_kernel_stats.csv $OUT/read_merkle_kernel_stats.csv
 # the full default bench line (reads profiles/join2_pmc.json for `traffic`)
 timeout -k 10 600 python -u bench.py > $OUT/bench_full.log 2>&1 || { tail -20 $OUT/bench_full.log; exit 1; }
 tail -1 $OUT/bench_full.log
