@@ -889,6 +889,7 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   if (tid == 0)  // residency check (stripe_sums)
     __hip_atomic_store(cold(&cold_scan()->started) + w, epoch, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
+  if (w < G) JSTAMP(w, 0);  // (stamps build: slot 0 of a workgroup's first tile = its entry)
   if (p.fused) {
     if (w == G) {  // Dots.union(c1, c2) (aw_lww_map.ex:155), beside the tiles
       ctx_union_block<JB>(p.cu, s.wave);
@@ -949,7 +950,7 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   u32 np = 0;    // kept rows of this workgroup's tile of the previous stripe
   for (int k = 0;; k++) {
     const int bi = k & 1;
-    JSTAMP(t, 0);
+    if (k > 0) JSTAMP(t, 0);
     JSTAMP(t, 1);
     commit_tile(r, s.buf[bi]);
     if (KEYED && km <= (u64)KS && (u64)tid < km) s.kslice[bi][tid] = kk;

@@ -55,40 +55,55 @@ __device__ __forceinline__ u64 vv_at(const u64* tab, u32 i, u32 node) {
   return node < (u32)KNT ? tab[(u64)i * KNT + node] : 0ull;
 }
 
-// P after the touching deltas (bits of K | R, in delta order); see the header.  Both
-// tables are read for up to PB touching deltas at a time, before P decides which one
-// applies, so those L2 reads overlap instead of waiting on each other.
-constexpr int PB = 4;
-__device__ __forceinline__ bool present(bool P, u64 K, u64 R, u64 M, u32 node, u64 cnt,
-                                        const u64* tabC, const u64* tabP) {
-  u64 bits = K | R;
-  while (bits) {
-    u32 ib[PB];
-    u64 c[PB], q[PB];
-    int nb = 0;
+// P after the touching deltas (bits of K | R, in delta order; see the header), for a
+// thread's two candidates (its state row and its item) at once: the
+// table reads of both are issued before either is evaluated, so the two candidates cost
+// one round trip to the VV tables instead of two.  PB2 touching deltas per candidate per
+// round (one round covers almost every candidate).
+constexpr int PB2 = 2;
+struct Cand {
+  bool P;
+  u64 K, R, M;
+  u32 node;
+  u64 cnt;
+};
+__device__ __forceinline__ void present2(Cand& a, bool da, Cand& b, bool db, const u64* tabC,
+                                         const u64* tabP) {
+  u64 ba = da ? (a.K | a.R) : 0ull, bb = db ? (b.K | b.R) : 0ull;
+  while (ba | bb) {
+    u32 ia[PB2], ib[PB2];
+    u64 ca[PB2], qa[PB2], cb[PB2], qb[PB2];
+    int na = 0, nb = 0;
 #pragma unroll
-    for (int j = 0; j < PB; j++) {
-      ib[j] = bits ? (u32)__builtin_ctzll(bits) : 0u;
-      nb += bits ? 1 : 0;
-      bits &= bits - 1;
+    for (int j = 0; j < PB2; j++) {
+      ia[j] = ba ? (u32)__builtin_ctzll(ba) : 0u;
+      na += ba ? 1 : 0;
+      ba &= ba - 1;
+      ib[j] = bb ? (u32)__builtin_ctzll(bb) : 0u;
+      nb += bb ? 1 : 0;
+      bb &= bb - 1;
     }
 #pragma unroll
-    for (int j = 0; j < PB; j++) {
-      c[j] = j < nb ? vv_at(tabC, ib[j], node) : 0ull;
-      q[j] = j < nb ? vv_at(tabP, ib[j], node) : 0ull;
+    for (int j = 0; j < PB2; j++) {
+      ca[j] = j < na ? vv_at(tabC, ia[j], a.node) : 0ull;
+      qa[j] = j < na ? vv_at(tabP, ia[j], a.node) : 0ull;
+      cb[j] = j < nb ? vv_at(tabC, ib[j], b.node) : 0ull;
+      qb[j] = j < nb ? vv_at(tabP, ib[j], b.node) : 0ull;
     }
 #pragma unroll
-    for (int j = 0; j < PB; j++) {
-      if (j >= nb) break;
-      const u32 i = ib[j];
-      const bool inD = (M >> i) & 1;
-      if ((K >> i) & 1)
-        P = P ? (inD || c[j] < cnt) : (inD && q[j] < cnt);
-      else
-        P = inD;
+    for (int j = 0; j < PB2; j++) {
+      if (j < na) {
+        const u32 i = ia[j];
+        const bool inD = (a.M >> i) & 1;
+        a.P = ((a.K >> i) & 1) ? (a.P ? (inD || ca[j] < a.cnt) : (inD && qa[j] < a.cnt)) : inD;
+      }
+      if (j < nb) {
+        const u32 i = ib[j];
+        const bool inD = (b.M >> i) & 1;
+        b.P = ((b.K >> i) & 1) ? (b.P ? (inD || cb[j] < b.cnt) : (inD && qb[j] < b.cnt)) : inD;
+      }
     }
   }
-  return P;
 }
 
 // ------------------------------------------------------------------------ prep
@@ -202,12 +217,12 @@ __global__ __launch_bounds__(256) void kfold_fill_kernel(KFoldArgs p) {
 #ifdef DG_STAMPS
 // Diagnostic build only (DG_STAMPS=1): per-bucket phase timestamps (s_memrealtime) by
 // lane 0, read back with dg_debug_kfold_stamps (tools/kfold_stamps.py).
-__device__ u64 g_kf_stamps[65536 * 8];
+__device__ u64 g_kf_stamps[65536 * 16];
 #define KSTAMP(tile, k)                                                              \
   do {                                                                               \
     __syncthreads();                                                                 \
     if (threadIdx.x == 0 && (tile) < 65536)                                          \
-      g_kf_stamps[(tile) * 8 + (k)] = __builtin_amdgcn_s_memrealtime();              \
+      g_kf_stamps[(tile) * 16 + (k)] = __builtin_amdgcn_s_memrealtime();             \
   } while (0)
 #else
 #define KSTAMP(tile, k) \
@@ -238,6 +253,10 @@ struct KLds {
     struct {
       unsigned short spre[CS + 1], upre[CU + 1];  // exclusive survivor prefixes
     } pre;
+    struct {                          // while staging: the runs' column pointers
+      RowsOut d[KFOLD_MAX_K];         //   delta rows (read only)
+      const u64* keys[KFOLD_MAX_K];   //   keysets
+    } run;
   } x;
   unsigned short slbu[CS];            // state row -> first sorted item with key >= its key
   unsigned char ssurv[CS], usurv[CU]; // usurv by sorted position
@@ -308,6 +327,12 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
   __syncthreads();
   const u64 t = s.bcast[0];
   KSTAMP(t, 0);
+  if (tid < k) {  // the runs' column pointers (bucket-independent) for the staging below
+    const Rows& R = p.runs[tid].rows;
+    s.x.run.d[tid] = RowsOut{(u64*)R.key, (u64*)R.val, (i64*)R.ts, (u32*)R.node, (u64*)R.cnt};
+  } else if (tid < nr) {
+    s.x.run.keys[tid - k] = p.runs[tid - k].keys;
+  }
   const u64 s0 = p.sstart[t];
   u32 nS = (u32)min<u64>(p.sstart[t + 1] - s0, 0xffffffffull);
   u32 len = 0;
@@ -319,10 +344,17 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
     s.rbeg[tid] = a;
   }
   bad = __syncthreads_or(bad);
+  // the state row's loads go out now (they need only s0 and nS): they fly during the run
+  // offsets' scan and the item loads, so staging costs one round trip, not two
+  static_assert(CS <= KB && CU <= KB, "one state row and one item per thread");
+  const bool hs = !bad && nS <= (u32)CS && (u32)tid < nS;
+  Row sr{};
+  if (hs) sr = load_row(p.s, s0 + tid);
   u32 nU;
   const u32 off = block_excl_scan<KB>(len, s.wave, &nU);
   if (tid < nr) s.roff[tid] = off;
   if (tid == 0) s.roff[nr] = nU;
+  KSTAMP(t, 12);
   __syncthreads();
   u32 nD = s.roff[k];
   if (bad || nS > (u32)CS || nD > (u32)CD || nU - nD > (u32)CM) {
@@ -330,16 +362,12 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
     nS = nU = nD = 0;  // publish an empty bucket so the look-back chain stays live
   }
 
-  // ---- stage: state slice, delta rows (slot = pre-sort index), keyset markers
-  for (u32 i = tid; i < nS; i += KB) {
-    const u64 g = s0 + i;
-    s.skey[i] = p.s.key[g];
-    s.sval[i] = p.s.val[g];
-    s.sts[i] = p.s.ts[g];
-    s.snode[i] = p.s.node[g];
-    s.scnt[i] = p.s.cnt[g];
-  }
-  for (u32 q = tid; q < nU; q += KB) {
+  // ---- stage: state slice, delta rows (slot = pre-sort index), keyset markers; the
+  //      item's loads are issued before either row is written to LDS
+  const u32 q = tid;  // this thread's item
+  Row ir{};
+  u32 itag = 0;
+  if (q < nU) {
     int lo = 0, hi = nr;  // roff[lo] <= q < roff[hi]
     while (hi - lo > 1) {
       const int mid = (lo + hi) >> 1;
@@ -350,22 +378,35 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
     }
     const u64 j = (u64)s.rbeg[lo] + (q - s.roff[lo]);
     if (lo < k) {
-      const Rows& R = p.runs[lo].rows;
-      const u64 key = R.key[j];
-      s.dkey[q] = key;
-      s.dval[q] = R.val[j];
-      s.dts[q] = R.ts[j];
-      s.dnode[q] = R.node[j];
-      s.dcnt[q] = R.cnt[j];
-      s.ukey[q] = key;
-      s.utag[q] = ((u32)lo << 16) | q;
+      const RowsOut& R = s.x.run.d[lo];
+      ir = Row{R.key[j], R.val[j], R.cnt[j], R.ts[j], R.node[j]};
+      itag = ((u32)lo << 16) | q;
     } else {
-      s.ukey[q] = p.runs[lo - k].keys[j];
-      s.utag[q] = ((u32)(lo - k) << 16) | MARK | q;
+      ir.key = s.x.run.keys[lo - k][j];
+      itag = ((u32)(lo - k) << 16) | MARK | q;
     }
   }
-  for (u32 b = tid; b < NSUB; b += KB) s.x.ucnt[b] = 0;
+  if (hs && (u32)tid < nS) {
+    s.skey[tid] = sr.key;
+    s.sval[tid] = sr.val;
+    s.sts[tid] = sr.ts;
+    s.snode[tid] = sr.node;
+    s.scnt[tid] = sr.cnt;
+  }
+  if (q < nU) {
+    s.ukey[q] = ir.key;
+    s.utag[q] = itag;
+    if (!(itag & MARK)) {
+      s.dkey[q] = ir.key;
+      s.dval[q] = ir.val;
+      s.dts[q] = ir.ts;
+      s.dnode[q] = ir.node;
+      s.dcnt[q] = ir.cnt;
+    }
+  }
   KSTAMP(t, 1);
+  __syncthreads();  // (the run pointers in s.x are dead: the histogram takes it)
+  for (u32 b = tid; b < NSUB; b += KB) s.x.ucnt[b] = 0;
   __syncthreads();
 
   // ---- counting sort of the items by sub-bucket, then (key, tag) within one
@@ -379,8 +420,10 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
   }
   if (nS == 0)
     for (u32 b = tid; b <= (u32)NSUB; b += KB) s.sfirst[b] = 0;
+  KSTAMP(t, 8);
   __syncthreads();
   scan_excl(s.x.ucnt, NSUB, s.ustart, s.wave);
+  KSTAMP(t, 9);
   __syncthreads();
   for (u32 b = tid; b < NSUB; b += KB) s.x.ucnt[b] = 0;
   __syncthreads();
@@ -389,6 +432,7 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
     const u32 sb = sub_of(s.ukey[q], T, t);
     bin[s.ustart[sb] + atomicAdd(&s.x.ucnt[sb], 1u)] = (unsigned short)q;
   }
+  KSTAMP(t, 10);
   __syncthreads();
   // rank by (key, tag) within the (small) sub-bucket, then every item moves itself to
   // its sorted position (the items of a thread are read before the barrier, written
@@ -423,55 +467,68 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
   __syncthreads();
 
   // ---- evaluate every candidate (a key's items and state rows share its sub-bucket)
+  // (one state row and one item per thread; both candidates' VV-table reads go out
+  // together in present2)
   const u64 all = p.allmask;
-  for (u32 i = tid; i < nS; i += KB) {
+  Cand cs{true, all, 0, 0, 0, 0}, cu{false, all, 0, 0, 0, 0};
+  const bool ds = (u32)tid < nS;
+  bool du = false;
+  if (ds) {
+    const u32 i = tid;
     const Row r = srow(s, i);
     const u32 sb = sub_of(r.key, T, t);
-    u32 q = s.ustart[sb];
+    u32 e = s.ustart[sb];
     const u32 qe = s.ustart[sb + 1];
-    while (q < qe && s.ukey[q] < r.key) q++;
-    s.slbu[i] = (unsigned short)q;
-    u64 K = all, R = 0, M = 0;
-    for (; q < qe && s.ukey[q] == r.key; q++) {
-      const u32 tg = s.utag[q], src = tg >> 16;
+    while (e < qe && s.ukey[e] < r.key) e++;
+    s.slbu[i] = (unsigned short)e;
+    for (; e < qe && s.ukey[e] == r.key; e++) {
+      const u32 tg = s.utag[e], src = tg >> 16;
       if (tg & MARK) {
-        K |= 1ull << src;
+        cs.K |= 1ull << src;
       } else {
-        R |= 1ull << src;
-        if (row_eq(drow(s, tg & SLOT), r)) M |= 1ull << src;
+        cs.R |= 1ull << src;
+        if (row_eq(drow(s, tg & SLOT), r)) cs.M |= 1ull << src;
       }
     }
-    s.ssurv[i] = present(true, K, R, M, r.node, r.cnt, p.tabC, p.tabP);
+    cs.node = r.node;
+    cs.cnt = r.cnt;
   }
-  for (u32 q = tid; q < nU; q += KB) {
-    const u32 tg = s.utag[q];
-    bool surv = false;
-    if (!(tg & MARK)) {
-      const u32 src = tg >> 16;
-      const Row r = drow(s, tg & SLOT);
-      const u32 sb = sub_of(r.key, T, t);
-      u64 K = all, R = 0, M = 0;
-      bool rep = true;  // the first holder of this tuple: the state, else the lowest delta
-      for (u32 e = s.ustart[sb], ee = s.ustart[sb + 1]; e < ee; e++) {
-        const u32 te = s.utag[e], se = te >> 16;
-        if (s.ukey[e] != r.key) continue;
-        if (te & MARK) {
-          K |= 1ull << se;
-        } else {
-          R |= 1ull << se;
-          if (row_eq(drow(s, te & SLOT), r)) {
-            M |= 1ull << se;
-            if (se < src) rep = false;
-          }
+  if ((u32)tid < nU && !(s.utag[tid] & MARK)) {
+    const u32 tg = s.utag[tid], src = tg >> 16;
+    const Row r = drow(s, tg & SLOT);
+    const u32 sb = sub_of(r.key, T, t);
+    bool first = true;  // the first holder of this tuple: the state, else the lowest delta
+    // (the items are sorted by (key, tag) and this one sits at position tid: its key's
+    // group starts at most a few items before it)
+    u32 e = tid;
+    while (e > 0 && s.ukey[e - 1] == r.key) e--;
+    for (; e < nU && s.ukey[e] == r.key; e++) {
+      const u32 te = s.utag[e], se = te >> 16;
+      if (te & MARK) {
+        cu.K |= 1ull << se;
+      } else {
+        cu.R |= 1ull << se;
+        if (row_eq(drow(s, te & SLOT), r)) {
+          cu.M |= 1ull << se;
+          if (se < src) first = false;
         }
       }
-      // a tuple the state holds is evaluated (and emitted) as the state's row
-      for (u32 i = s.sfirst[sb], ie = s.sfirst[sb + 1]; rep && i < ie; i++)
-        if (row_eq(srow(s, i), r)) rep = false;
-      if (rep) surv = present(false, K, R, M, r.node, r.cnt, p.tabC, p.tabP);
     }
-    s.usurv[q] = surv;
+    // a tuple the state holds is evaluated (and emitted) as the state's row (the state
+    // rows of the sub-bucket are sorted: compare full rows only under the same key)
+    u32 i = s.sfirst[sb];
+    const u32 ie = s.sfirst[sb + 1];
+    while (i < ie && s.skey[i] < r.key) i++;
+    for (; first && i < ie && s.skey[i] == r.key; i++)
+      if (row_eq(srow(s, i), r)) first = false;
+    du = first;
+    cu.node = r.node;
+    cu.cnt = r.cnt;
   }
+  KSTAMP(t, 7);
+  present2(cs, ds, cu, du, p.tabC, p.tabP);
+  if (ds) s.ssurv[tid] = cs.P;
+  if ((u32)tid < nU) s.usurv[tid] = du && cu.P;
   KSTAMP(t, 3);
   __syncthreads();
   scan_excl(s.ssurv, nS, s.x.pre.spre, s.wave);
@@ -510,8 +567,8 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
     if (q >= nU || !s.usurv[q]) continue;
     const Row r = drow(s, s.utag[q] & SLOT);
     const u32 sb = sub_of(r.key, T, t);
-    u32 gb = s.ustart[sb];
-    while (s.ukey[gb] != r.key) gb++;
+    u32 gb = q;  // the first item of its key: a few positions back at most
+    while (gb > 0 && s.ukey[gb - 1] == r.key) gb--;
     u32 less = 0;
     for (u32 e = gb; e < nU && s.ukey[e] == r.key; e++)
       if (s.usurv[e] && row_cmp(drow(s, s.utag[e] & SLOT), r) < 0) less++;
@@ -546,7 +603,7 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
 
 #ifdef DG_STAMPS
 extern "C" int dg_debug_kfold_stamps(unsigned long long* host, size_t n) {
-  if (n > 65536 * 8) n = 65536 * 8;
+  if (n > 65536 * 16) n = 65536 * 16;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_kf_stamps), n * 8) == hipSuccess ? 0 : -3;
 }
 #endif

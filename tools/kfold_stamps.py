@@ -5,8 +5,9 @@ diagnostic build, on config 3 (KF_KEYS keys, 64 keyed deltas).
     python tools/kfold_stamps.py                       # on the GPU box
 
 Stamps (s_memrealtime, 100 MHz) by lane 0 of every bucket at: 0 start (after the
-ticket)  1 slices staged in LDS  2 delta items sorted  3 candidates evaluated
-4 survivor scans done  5 look-back done  6 rows written.  Only SHARES are meaningful
+ticket)  1 slices staged in LDS  2 delta items sorted  7 key masks built  3 candidates
+evaluated (VV tables)  4 survivor scans done  5 survivors ranked  6 offset looked up and
+rows written; 12 run offsets scanned, 8 sub-bucket histogram, 9 its scan, 10 scatter.  Only SHARES are meaningful
 (stamps add barriers)."""
 import ctypes as C
 import os
@@ -38,18 +39,19 @@ def main():
     eng = Engine(0)
     for _ in range(3):
         o, c = eng.apply_deltas(sb, cb, ds, dc, ks)
-    buf = np.zeros(65536 * 8, np.uint64)
+    buf = np.zeros(65536 * 16, np.uint64)
     lib.dg_debug_kfold_stamps.argtypes = [C.c_void_p, C.c_size_t]
     assert lib.dg_debug_kfold_stamps(buf.ctypes.data, len(buf)) == 0
-    st = buf.reshape(65536, 8).astype(np.int64)
+    st = buf.reshape(65536, 16).astype(np.int64)
     nb = int(np.nonzero(st[:, 0])[0].max()) + 1
     st = st[:nb]
     t0 = st[:, 0].min()
-    names = ["stage", "sort", "evaluate", "scans", "lookback", "write"]
-    d = np.diff(st[:, :7], axis=1) * 10 / 1000.0  # us
+    names = ["stage:meta+scan", "stage:rows", "sort:histogram", "sort:scan", "sort:scatter",
+             "sort:rank+move", "masks", "vv-tables", "scans", "rank", "lookback+write"]
+    d = np.diff(st[:, [0, 12, 1, 8, 9, 10, 2, 7, 3, 4, 5, 6]], axis=1) * 10 / 1000.0  # us
     print(f"buckets={nb} kernel span={(st[:, 6].max() - t0) * 10 / 1000:.1f} us")
     for i, nm in enumerate(names):
-        print(f"{nm:9s} median {np.median(d[:, i]):7.2f} us  p90 {np.percentile(d[:, i], 90):7.2f}"
+        print(f"{nm:16s} median {np.median(d[:, i]):7.2f} us  p90 {np.percentile(d[:, i], 90):7.2f}"
               f"  mean {d[:, i].mean():7.2f}")
     tot = (st[:, 6] - st[:, 0]) * 10 / 1000
     print(f"per-bucket total median {np.median(tot):.2f} us  mean {tot.mean():.2f}")

@@ -1,6 +1,6 @@
 """Phase shares of the join stream kernel from a saved DG_STAMPS buffer (tools/prof_c5.py
 with C5_STAMPS=<file.npy>).  Stamps (s_memrealtime, 100 MHz, lane 0 of each tile):
-0/1 iteration start, 2 tile committed to LDS, 7 next tile's loads issued, 3 merge done, 4 block scan + compaction
+0 iteration start (a workgroup's first tile: the workgroup's entry), 1 iteration start, 2 tile committed to LDS, 7 next tile's loads issued, 3 merge done, 4 block scan + compaction
 list (+ change events) done, 5 previous stripe's counts summed, 6 previous tile written.  Only shares
 are meaningful (the stamps add barriers)."""
 import sys
@@ -22,6 +22,13 @@ def main(path):
               f"  mean {d[:, i].mean():6.2f}")
     it = np.diff(np.sort(st[:, 1]))
     print("per-tile total median", np.median((st[:, 6] - st[:, 1]) * 10 / 1000))
+    first = st[:, 0] < st[:, 1]  # first tiles: slot 0 is the workgroup's entry
+    if first.any():
+        pro = (st[first, 1] - st[first, 0]) * 10 / 1000
+        ent = (st[first, 0] - st[first, 0].min()) * 10 / 1000
+        print(f"prologue (entry -> first iteration) median {np.median(pro):.2f} us  p90 "
+              f"{np.percentile(pro, 90):.2f}; entries spread over {ent.max():.2f} us; "
+              f"last write {(st[:, 6].max() - st[first, 0].min()) * 10 / 1000:.1f} us after the first entry")
     first = (st[:, 1] - t0) * 10 / 1000  # iteration starts relative to the earliest one
     print("iteration start (us) at deciles:", np.percentile(first, np.arange(0, 101, 10)).round(1))
     print(f"last write done at {(st[:, 6].max() - t0) * 10 / 1000:.1f} us after the first iteration start")
