@@ -57,12 +57,12 @@ constexpr int VT = 64;      // VV table: node ids below this are looked up direc
 #ifdef DG_STAMPS
 // Diagnostic build only (DG_STAMPS=1): per-tile phase timestamps (s_memrealtime,
 // 100 MHz) written by lane 0 into a buffer no other code reads.
-__device__ u64 g_join_stamps[65536 * 8];
+__device__ u64 g_join_stamps[65536 * 16];
 #define JSTAMP(tile, k)                                                              \
   do {                                                                               \
     __syncthreads();                                                                 \
     __builtin_amdgcn_sched_barrier(0);                                               \
-    if (threadIdx.x == 0 && (tile) < 65536) g_join_stamps[(tile) * 8 + (k)] =        \
+    if (threadIdx.x == 0 && (tile) < 65536) g_join_stamps[(tile) * 16 + (k)] =       \
         __builtin_amdgcn_s_memrealtime();                                            \
     __builtin_amdgcn_sched_barrier(0);                                               \
   } while (0)
@@ -330,11 +330,14 @@ __device__ u64 mp_search(const Rows A, const Rows B, u64 d, u64 lo, u64 hi) {
 }
 
 // Merge-path split of diagonal d (= #A rows among the first d merged rows).
-// Interpolation: at a guess i the key gap B.key[d-1-i] - A.key[i] (in units of the
-// 2^64 key space) converts to a row shift of gap * na*nb / ((na+nb) * 2^64); two
-// such probes (wave-uniform loads) put the guess within a few rows of the split for
-// hashed keys, then ONE window of 128 consecutive candidates decides it.  If the
-// split is not bracketed by the window, the exact 128-ary search runs instead.
+// A window of 128 consecutive candidates is decided in ONE round trip (two per lane,
+// ballots), first around the proportional guess d * na / (na + nb): replicas that share
+// most keys (config 2) split there exactly.  If the window does not bracket the split,
+// the key gap B.key[d-1-c] - A.key[c] at the window's middle c (in units of the 2^64
+// key space; the rows were just loaded, so this is a cache hit) converts to a row shift
+// of gap * na*nb / ((na+nb) * 2^64), which lands within a few rows for hashed keys, and
+// the next window is decided there.  Three windows without a bracket fall back to the
+// exact 128-ary search for any key distribution.
 __device__ u64 mp_split(const Rows A, const Rows B, u64 d) {
   const int lane = threadIdx.x & (WAVE - 1);
   const u64 na = A.n, nb = B.n, total = na + nb;
@@ -343,34 +346,32 @@ __device__ u64 mp_split(const Rows A, const Rows B, u64 d) {
   const double scale = (double)na * (double)nb / ((double)total * 18446744073709551616.0);
   u64 i = (u64)((double)d * (double)na / (double)total);
   i = min(max(i, lo), hi - 1);
-#pragma unroll
-  for (int r = 0; r < 2; r++) {
-    const double gap = (double)B.key[d - 1 - i] - (double)A.key[i];
-    double s = gap * scale;
+  for (int r = 0; r < 3; r++) {
+    u64 wlo = i > lo + PK / 2 ? i - PK / 2 : lo;
+    const u64 whi = min(wlo + (u64)PK, hi);
+    wlo = whi - PK > lo ? whi - PK : lo;
+    const u64 x0 = wlo + 2 * lane, x1 = x0 + 1;
+    const bool f0 = x0 < whi && !mp_pred(A, B, d, x0);
+    const bool f1 = x1 < whi && !mp_pred(A, B, d, x1);
+    const u64 m0 = __ballot(f0), m1 = __ballot(f1);
+    u64 kf = whi - wlo;  // first false candidate in the window (none: whi - wlo)
+    if (m0 | m1) {
+      const int l0 = m0 ? __ffsll((long long)m0) - 1 : 64;
+      const int l1 = m1 ? __ffsll((long long)m1) - 1 : 64;
+      kf = (l0 <= l1) ? 2 * l0 : 2 * l1 + 1;
+    }
+    // bracketed iff the first false is not at the window's low edge (unless that edge is
+    // lo) and some candidate is false (unless the window reaches hi)
+    if ((kf > 0 || wlo == lo) && (kf < whi - wlo || whi == hi)) return wlo + kf;
+    const u64 c = (wlo + whi) / 2;
+    const double gap = (double)B.key[d - 1 - c] - (double)A.key[c];
+    double sft = gap * scale;
     const double lim = (double)(hi - lo);
-    s = s > lim ? lim : (s < -lim ? -lim : s);
-    const i64 si = (i64)s;
-    i64 ni = (i64)i + si;
+    sft = sft > lim ? lim : (sft < -lim ? -lim : sft);
+    i64 ni = (i64)c + (i64)sft;
     ni = ni < (i64)lo ? (i64)lo : (ni > (i64)hi - 1 ? (i64)hi - 1 : ni);
     i = (u64)ni;
   }
-  u64 wlo = i > lo + PK / 2 ? i - PK / 2 : lo;
-  const u64 whi = min(wlo + (u64)PK, hi);
-  wlo = whi - PK > lo ? whi - PK : lo;
-  const u64 x0 = wlo + 2 * lane, x1 = x0 + 1;
-  const bool f0 = x0 < whi && !mp_pred(A, B, d, x0);
-  const bool f1 = x1 < whi && !mp_pred(A, B, d, x1);
-  const u64 m0 = __ballot(f0), m1 = __ballot(f1);
-  u64 kf = whi - wlo;  // first false candidate in the window (none: whi - wlo)
-  if (m0 | m1) {
-    const int l0 = m0 ? __ffsll((long long)m0) - 1 : 64;
-    const int l1 = m1 ? __ffsll((long long)m1) - 1 : 64;
-    kf = (l0 <= l1) ? 2 * l0 : 2 * l1 + 1;
-  }
-  // bracketed iff the first false is not at the window's low edge (unless that edge is
-  // lo) and some candidate is false (unless the window reaches hi)
-  const bool ok = (kf > 0 || wlo == lo) && (kf < whi - wlo || whi == hi);
-  if (ok) return wlo + kf;
   return mp_search(A, B, d, lo, hi);
 }
 
@@ -911,6 +912,7 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   if (FAST)
     for (int x = tid; x < 2 * VT; x += JB) (&s.tab[0][0])[x] = 0;
   if (p.fused) __syncthreads();
+  if (w < G) JSTAMP(w, 8);  // (stamps build: splits searched)
   // split of boundary `side` (0 start, 1 end) of the tile of iteration k
   // (a uniform branch between an LDS read and a global read: a select between the two
   // pointers would make it a flat load, whose wait also drains the previous tile's stores)
@@ -945,6 +947,7 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     if (km <= (u64)KS && (u64)tid < km) kk = p.keys[kl + tid];
   }
   __syncthreads();  // zeroed tables visible
+  if (w < G) JSTAMP(w, 9);  // (stamps build: first tile's loads issued)
   if (FAST) fill_vv_tables(p.ca, p.cb, s.tab[0], s.tab[1]);  // once per workgroup
   u64 base = 0;  // output offset of the first tile of the current stripe
   u32 np = 0;    // kept rows of this workgroup's tile of the previous stripe
@@ -1535,7 +1538,7 @@ hipError_t launch_ctx_union(const Ctx& a, const Ctx& b, u32* out_node, u64* out_
 
 #ifdef DG_STAMPS
 extern "C" int dg_debug_join_stamps(unsigned long long* host, size_t n) {
-  if (n > 65536 * 8) n = 65536 * 8;
+  if (n > 65536 * 16) n = 65536 * 16;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_join_stamps), n * 8) == hipSuccess ? 0 : -3;
 }
 #endif

@@ -40,7 +40,7 @@ if os.environ.get("C5_STAMPS"):
 
     import numpy as np
     lib = eng.lib
-    buf = np.zeros(65536 * 8, np.uint64)
+    buf = np.zeros(65536 * 16, np.uint64)
     lib.dg_debug_join_stamps.argtypes = [C.c_void_p, C.c_size_t]
     assert lib.dg_debug_join_stamps(buf.ctypes.data, len(buf)) == 0
     np.save(os.environ["C5_STAMPS"], buf)

@@ -9,7 +9,7 @@ import numpy as np
 
 
 def main(path):
-    st = np.load(path).reshape(65536, 8).astype(np.int64)
+    st = np.load(path).reshape(65536, 16).astype(np.int64)
     ntiles = int(np.nonzero(st[:, 0])[0].max()) + 1
     st = st[:ntiles]
     t0 = st[:, 0].min()
@@ -22,10 +22,13 @@ def main(path):
               f"  mean {d[:, i].mean():6.2f}")
     it = np.diff(np.sort(st[:, 1]))
     print("per-tile total median", np.median((st[:, 6] - st[:, 1]) * 10 / 1000))
-    first = st[:, 0] < st[:, 1]  # first tiles: slot 0 is the workgroup's entry
+    first = st[:, 8] > 0  # a workgroup's first tile: slot 0 is its entry, 8 and 9 prologue stamps
     if first.any():
         pro = (st[first, 1] - st[first, 0]) * 10 / 1000
         ent = (st[first, 0] - st[first, 0].min()) * 10 / 1000
+        for a, b, nm in ((0, 8, "split search"), (8, 9, "first tile issued"), (9, 1, "VV tables + tile landed")):
+            x = (st[first, b] - st[first, a]) * 10 / 1000
+            print(f"  prologue {nm:24s} median {np.median(x):5.2f} us  p90 {np.percentile(x, 90):5.2f}")
         print(f"prologue (entry -> first iteration) median {np.median(pro):.2f} us  p90 "
               f"{np.percentile(pro, 90):.2f}; entries spread over {ent.max():.2f} us; "
               f"last write {(st[:, 6].max() - st[first, 0].min()) * 10 / 1000:.1f} us after the first entry")
