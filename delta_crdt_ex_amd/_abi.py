@@ -28,15 +28,18 @@ DG_CTX_DOTS = 1
 P64 = C.POINTER(C.c_uint64)
 PI64 = C.POINTER(C.c_int64)
 P32 = C.POINTER(C.c_uint32)
+# struct pointer fields are untyped (same size and offsets as the header's typed pointers):
+# the host mirror sets them from tensor addresses without a ctypes cast per field
+VP = C.c_void_p
 
 
 class dg_store(C.Structure):
     _fields_ = [
-        ("key", P64),
-        ("val", P64),
-        ("ts", PI64),
-        ("node", P32),
-        ("cnt", P64),
+        ("key", VP),
+        ("val", VP),
+        ("ts", VP),
+        ("node", VP),
+        ("cnt", VP),
         ("n", C.c_uint64),
         ("cap", C.c_uint64),
     ]
@@ -46,8 +49,8 @@ class dg_context(C.Structure):
     _fields_ = [
         ("kind", C.c_int32),
         ("reserved", C.c_int32),
-        ("node", P32),
-        ("cnt", P64),
+        ("node", VP),
+        ("cnt", VP),
         ("n", C.c_uint64),
         ("cap", C.c_uint64),
     ]
@@ -58,7 +61,7 @@ class dg_merkle(C.Structure):
         ("depth", C.c_uint32),
         ("shard_bits", C.c_uint32),
         ("shard", C.c_uint64),
-        ("nodes", P64),
+        ("nodes", VP),
         ("n_keys", C.c_uint64),
     ]
 
@@ -67,11 +70,11 @@ class dg_merkle_cont(C.Structure):
     _fields_ = [
         ("level", C.c_uint32),
         ("reserved", C.c_uint32),
-        ("pos", P64),
-        ("hash", P64),
+        ("pos", VP),
+        ("hash", VP),
         ("n", C.c_uint64),
         ("cap", C.c_uint64),
-        ("bucket", P64),
+        ("bucket", VP),
         ("n_buckets", C.c_uint64),
         ("cap_buckets", C.c_uint64),
     ]

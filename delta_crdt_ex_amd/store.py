@@ -87,15 +87,8 @@ class Store:
         )
 
     def abi(self) -> _abi.dg_store:
-        s = _abi.dg_store()
-        s.key = _ptr(self.key, _abi.P64)
-        s.val = _ptr(self.val, _abi.P64)
-        s.ts = _ptr(self.ts, _abi.PI64)
-        s.node = _ptr(self.node, _abi.P32)
-        s.cnt = _ptr(self.cnt, _abi.P64)
-        s.n = self.n
-        s.cap = self.cap
-        return s
+        return _abi.dg_store(self.key.data_ptr(), self.val.data_ptr(), self.ts.data_ptr(),
+                             self.node.data_ptr(), self.cnt.data_ptr(), self.n, self.cap)
 
 
 @dataclass
@@ -130,13 +123,8 @@ class Context:
                 self.cnt[: self.n].cpu().numpy().view(np.uint64))
 
     def abi(self) -> _abi.dg_context:
-        c = _abi.dg_context()
-        c.kind = self.kind
-        c.node = _ptr(self.node, _abi.P32)
-        c.cnt = _ptr(self.cnt, _abi.P64)
-        c.n = self.n
-        c.cap = self.cap
-        return c
+        return _abi.dg_context(self.kind, 0, self.node.data_ptr(), self.cnt.data_ptr(), self.n,
+                               self.cap)
 
 
 @dataclass(eq=False)
@@ -161,7 +149,7 @@ class MerkleTree:
         t.depth = self.depth
         t.shard_bits = self.shard_bits
         t.shard = self.shard
-        t.nodes = _ptr(self.nodes, _abi.P64)
+        t.nodes = self.nodes.data_ptr()
         t.n_keys = self.n_keys
         return t
 
@@ -198,11 +186,11 @@ class MerkleCont:
     def abi(self) -> _abi.dg_merkle_cont:
         c = _abi.dg_merkle_cont()
         c.level = self.level
-        c.pos = _ptr(self.pos, _abi.P64)
-        c.hash = _ptr(self.hash, _abi.P64)
+        c.pos = self.pos.data_ptr()
+        c.hash = self.hash.data_ptr()
         c.n = self.n
         c.cap = int(self.pos.numel())
-        c.bucket = _ptr(self.bucket, _abi.P64) if self.bucket is not None else None
+        c.bucket = self.bucket.data_ptr() if self.bucket is not None else None
         c.n_buckets = self.n_buckets
         c.cap_buckets = int(self.bucket.numel()) if self.bucket is not None else 0
         return c
@@ -248,7 +236,11 @@ class Engine:
         (uploads of the inputs), so a call never reads half-written tensors."""
         cur = torch.cuda.current_stream(self.device)
         if cur.cuda_stream != self.stream.cuda_stream:
-            self.stream.wait_stream(cur)
+            # one reused event (Stream.wait_stream creates a new one per call)
+            if getattr(self, "_order_ev", None) is None:
+                self._order_ev = torch.cuda.Event()
+            self._order_ev.record(cur)
+            self.stream.wait_event(self._order_ev)
 
     def close(self):
         if getattr(self, "h", None):

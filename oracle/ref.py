@@ -72,11 +72,11 @@ def as_rows(rows):
 def _store(rows, cap=None):
     rows = as_rows(rows)
     s = _abi.dg_store()
-    s.key = _p(rows[0], _abi.P64)
-    s.val = _p(rows[1], _abi.P64)
-    s.ts = _p(rows[2], _abi.PI64)
-    s.node = _p(rows[3], _abi.P32)
-    s.cnt = _p(rows[4], _abi.P64)
+    s.key = rows[0].ctypes.data
+    s.val = rows[1].ctypes.data
+    s.ts = rows[2].ctypes.data
+    s.node = rows[3].ctypes.data
+    s.cnt = rows[4].ctypes.data
     s.n = len(rows[0])
     s.cap = len(rows[0]) if cap is None else cap
     return s, rows
@@ -88,8 +88,8 @@ def _ctx(ctx):
     cnt = np.ascontiguousarray(cnt, np.uint64)
     c = _abi.dg_context()
     c.kind = kind
-    c.node = _p(node, _abi.P32)
-    c.cnt = _p(cnt, _abi.P64)
+    c.node = node.ctypes.data
+    c.cnt = cnt.ctypes.data
     c.n = len(node)
     c.cap = len(node)
     return c, (kind, node, cnt)

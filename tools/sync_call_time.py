@@ -58,3 +58,11 @@ eng.sync()
 us_async = (time.perf_counter() - t0) / 200 * 1e6
 print(f"{os.path.basename(eng.lib._name)}: sync dg_join2 {us_sync:.1f} us/call (median), "
       f"async back-to-back {us_async:.1f} us/join")
+
+
+def py_join():
+    eng.join2(sa, ca, sb, cb, out=out, out_ctx=octx)
+
+
+us_py = timed(py_join)
+print(f"{os.path.basename(eng.lib._name)}: sync Engine.join2 (Python mirror) {us_py:.1f} us/call (median)")
