@@ -43,9 +43,10 @@ struct dg_engine {
   u64* h_counts = nullptr;  // pinned, 16 entries (a mirror of the whole block)
   // synchronous calls: a one-wave kernel copies the counts into host-coherent mapped memory
   // and then stores a sequence number there, which the host polls (read_counts)
-  u64* h_pub = nullptr;  // mapped host memory, 16 words: [0..9) the block, [15] the sequence
+  u64* h_pub = nullptr;  // mapped host memory, 24 words: [0..16) the block, [16] the sequence
   u64* d_pub = nullptr;  // its device address
   u64 pub_seq = 0;
+  u32 h_ticket[16] = {};  // the ticket words as of the last synchronous call
   // general scratch
   void* tmp = nullptr;
   size_t tmp_cap = 0;
@@ -203,10 +204,10 @@ int next_scan(dg_engine* e, Scan* s) {
 // number, everything before this kernel on the stream has finished and the copies landed.
 __global__ void publish_counts_kernel(const u64* d, u64* h, u64 seq) {
   const int l = threadIdx.x;
-  if (l < 9) h[l] = d[l];  // d_counts[0..8) and ticket[0..2)
+  if (l < 16) h[l] = d[l];  // d_counts[0..8) and ticket[0..16)
   __threadfence_system();
   __syncthreads();
-  if (l == 0) __hip_atomic_store(h + 15, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (l == 0) __hip_atomic_store(h + 16, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // The first n counts and the error bits (ticket[1]) of a synchronous call: d_counts[0..8)
@@ -214,13 +215,12 @@ __global__ void publish_counts_kernel(const u64* d, u64* h, u64 seq) {
 // D2H copy and a stream synchronize (≈ 14 µs on top of a config-2 join), a one-wave kernel
 // publishes them into mapped host memory and the host polls its sequence word; past 20 ms
 // (a long call) the runtime's synchronize takes over, and it is what reports a fault.
-int read_counts(dg_engine* e, int n) {
-  (void)n;
+int sync_words(dg_engine* e) {
   const u64 seq = ++e->pub_seq;
   hipLaunchKernelGGL(publish_counts_kernel, dim3(1), dim3(WAVE), 0, e->stream, e->d_counts,
                      e->d_pub, seq);
   HIP_TRY(hipGetLastError());
-  const volatile u64* flag = e->h_pub + 15;
+  const volatile u64* flag = e->h_pub + 16;
   const auto t0 = std::chrono::steady_clock::now();
   bool seen = false;
   for (u32 i = 0;; i++) {
@@ -237,6 +237,14 @@ int read_counts(dg_engine* e, int n) {
   }
   __atomic_thread_fence(__ATOMIC_ACQUIRE);
   memcpy(e->h_counts, (const void*)e->h_pub, 8 * sizeof(u64) + 2 * sizeof(u32));
+  memcpy(e->h_ticket, (const void*)(e->h_pub + 8), sizeof(e->h_ticket));
+  return DG_OK;
+}
+
+int read_counts(dg_engine* e, int n) {
+  (void)n;
+  const int rc = sync_words(e);
+  if (rc != DG_OK) return rc;
   u32 err = 0;
   memcpy(&err, (const char*)&e->h_counts[8] + sizeof(u32), sizeof(u32));
   if (err) {
@@ -392,14 +400,14 @@ int dg_engine_create(int device, void* hip_stream, dg_engine** out) {
   if (hipMalloc(&e->d_counts, 8 * sizeof(u64) + 16 * sizeof(u32)) != hipSuccess ||
       hipMalloc(&e->started, JOIN_MAX_GRID * sizeof(u32)) != hipSuccess ||
       hipHostMalloc(&e->h_counts, 16 * sizeof(u64), 0) != hipSuccess ||
-      hipHostMalloc(&e->h_pub, 16 * sizeof(u64), hipHostMallocMapped | hipHostMallocCoherent) !=
+      hipHostMalloc(&e->h_pub, 24 * sizeof(u64), hipHostMallocMapped | hipHostMallocCoherent) !=
           hipSuccess ||
       hipHostGetDevicePointer((void**)&e->d_pub, e->h_pub, 0) != hipSuccess) {
     dg_engine_destroy(e);
     return fail(DG_E_NOMEM, "dg_engine_create: allocation failed");
   }
   e->ticket = (u32*)(e->d_counts + 8);
-  memset(e->h_pub, 0, 16 * sizeof(u64));  // sequence 0: nothing published yet
+  memset(e->h_pub, 0, 24 * sizeof(u64));  // sequence 0: nothing published yet
   if (hipMemsetAsync(e->d_counts, 0, 8 * sizeof(u64) + 16 * sizeof(u32), e->stream) != hipSuccess ||
       hipMemsetAsync(e->started, 0, JOIN_MAX_GRID * sizeof(u32), e->stream) != hipSuccess) {
     dg_engine_destroy(e);
@@ -461,10 +469,8 @@ constexpr int RETRY_WORKERS = 32;  // dg_join2_changes' re-run after an aborted 
 
 // Error bits of the work on the engine stream so far (synchronizes), cleared.
 static int stream_error(dg_engine* e, u32* err) {
-  HIP_TRY(hipMemcpyAsync(&e->h_counts[12], e->ticket + 1, sizeof(u32), hipMemcpyDeviceToHost,
-                         e->stream));
-  HIP_TRY(hipStreamSynchronize(e->stream));
-  memcpy(err, &e->h_counts[12], sizeof(u32));
+  TRY(sync_words(e));
+  *err = e->h_ticket[1];
   if (*err) {
     HIP_TRY(hipMemsetAsync(e->ticket, 0, 4 * sizeof(u32), e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -504,12 +510,8 @@ int dg_store_check(dg_engine* e, const dg_store* s) {
   TRY(set_device(e));
   HIP_TRY(hipMemsetAsync(e->ticket + 2, 0, sizeof(u32), e->stream));
   HIP_TRY(launch_store_check(rows_of(s), e->ticket + 2, e->stream));
-  u32 bad = 0;
-  HIP_TRY(hipMemcpyAsync(&e->h_counts[11], e->ticket + 2, sizeof(u32), hipMemcpyDeviceToHost,
-                         e->stream));
-  HIP_TRY(hipStreamSynchronize(e->stream));
-  memcpy(&bad, &e->h_counts[11], sizeof(u32));
-  if (bad) return fail(DG_E_ORDER, "store rows are not strictly ascending");
+  TRY(sync_words(e));
+  if (e->h_ticket[2]) return fail(DG_E_ORDER, "store rows are not strictly ascending");
   return DG_OK;
 }
 
@@ -1003,13 +1005,9 @@ int same_tree_shape(const dg_merkle* a, const dg_merkle* b, const char* what) {
 }
 
 // The input-error word (ticket[3]) after a synchronizing read; bit 1: key outside shard.
+// (reads the ticket words of the read_counts right before it)
 int input_error(dg_engine* e, const char* what) {
-  u32 bad = 0;
-  HIP_TRY(hipMemcpyAsync(&e->h_counts[11], e->ticket + 3, sizeof(u32), hipMemcpyDeviceToHost,
-                         e->stream));
-  HIP_TRY(hipStreamSynchronize(e->stream));
-  memcpy(&bad, &e->h_counts[11], sizeof(u32));
-  if (bad & 2u) return fail(DG_E_INVAL, "%s: a key outside the tree's shard", what);
+  if (e->h_ticket[3] & 2u) return fail(DG_E_INVAL, "%s: a key outside the tree's shard", what);
   return DG_OK;
 }
 
@@ -1219,12 +1217,8 @@ int dg_remap_values(dg_engine* e, dg_store* s, const uint64_t* old_ids, const ui
   TRY(set_device(e));
   HIP_TRY(hipMemsetAsync(e->ticket + 3, 0, sizeof(u32), e->stream));
   HIP_TRY(launch_remap_values(s->val, s->n, old_ids, new_ids, n_ids, e->ticket + 3, e->stream));
-  u32 bad = 0;
-  HIP_TRY(hipMemcpyAsync(&e->h_counts[11], e->ticket + 3, sizeof(u32), hipMemcpyDeviceToHost,
-                         e->stream));
-  HIP_TRY(hipStreamSynchronize(e->stream));
-  memcpy(&bad, &e->h_counts[11], sizeof(u32));
-  if (bad) return fail(DG_E_INVAL, "dg_remap_values: a row's value id is not in old_ids");
+  TRY(sync_words(e));
+  if (e->h_ticket[3]) return fail(DG_E_INVAL, "dg_remap_values: a row's value id is not in old_ids");
   return DG_OK;
 }
 
