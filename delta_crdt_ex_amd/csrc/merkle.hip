@@ -406,6 +406,7 @@ __global__ __launch_bounds__(DB) void merkle_diff_count_kernel(DiffArgs p) {
   __shared__ u64 s_h[LCAP];            // hashes of the listed rows, in list order
   __shared__ uint16_t s_list[LCAP];    // the differing buckets' rows: bit 15 = store B
   __shared__ u32 s_wave[DB / WAVE + 1];
+  __shared__ u32 s_bc[DB];             // rows per bucket: A in the low, B in the high half
   const u32 depth = p.ta.depth;
   const u64 tile = blockIdx.x, bpt = diff_bpt(depth), b0 = tile * bpt;
   const int tid = threadIdx.x;
@@ -446,13 +447,33 @@ __global__ __launch_bounds__(DB) void merkle_diff_count_kernel(DiffArgs p) {
         if (x < na) s_ka[x] = ka[q];
         if (x < nc) s_kb[x] = kb[q];
       }
+      s_bc[tid] = 0;
+      __syncthreads();
+      // every bucket's row range from a histogram of the staged keys (LDS atomics) and one
+      // scan, instead of four binary searches per differing bucket
+      const u64 kbase = p.ta.sb ? (p.ta.shard << (64 - p.ta.sb)) : 0ull;
+      const u32 sh = 64 - p.ta.sb - depth;
+#pragma unroll
+      for (int q = 0; q < Q; q++) {
+        const u32 x = q * DB + tid;
+        const u64 la = ((ka[q] - kbase) >> sh) - b0, lb = ((kb[q] - kbase) >> sh) - b0;
+        if (x < na && la < bpt) atomicAdd(&s_bc[la], 1u);  // (bounds: the tile's buckets)
+        if (x < nc && lb < bpt) atomicAdd(&s_bc[lb], 1u << 16);
+      }
     }
     __syncthreads();
-    if (walk) {
-      ia = (b == b0) ? 0u : lb_small(s_ka, na, lk);
-      ie = last ? na : lb_small(s_ka, na, hk);
-      jb = (b == b0) ? 0u : lb_small(s_kb, nc, lk);
-      je = last ? nc : lb_small(s_kb, nc, hk);
+    {
+      const u32 bc = in ? s_bc[tid] : 0u;
+      u32 tot_bc;
+      const u32 st = block_excl_scan<DB>(bc, s_wave, &tot_bc);  // (counts <= DCAP: no carry)
+      ia = st & 0xffffu;
+      ie = ia + (bc & 0xffffu);
+      jb = st >> 16;
+      je = jb + (bc >> 16);
+      if (!walk) {  // only the differing buckets' rows are listed and merged
+        ie = ia;
+        je = jb;
+      }
     }
     // list the differing buckets' rows, then hash them all at once
     u32 tot_rows;

@@ -1,0 +1,9 @@
+# GPU suite, then the Merkle kernels A/B (default vs libdeltagpu_base.so) under rocprofv3,
+# then the full bench line.
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/ -q -x --timeout 120 --timeout-method thread -m gpu > gpurun_out/pytest_gpu.log 2>&1 || { echo TESTS_FAILED; tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+tail -1 gpurun_out/pytest_gpu.log
+bash tools/ab_prof_merkle.sh || exit 1
+timeout -k 10 400 python -u bench.py > gpurun_out/bench.log 2>&1 || { echo BENCH_FAILED; tail -20 gpurun_out/bench.log; exit 1; }
+tail -1 gpurun_out/bench.log
