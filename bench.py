@@ -447,10 +447,18 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
+    # rehearsal of the N > 1 path on a one-GPU box: DG_BENCH_BACKEND=gloo and
+    # DG_BENCH_SAME_GPU=1 put every rank on cuda:0 (RCCL refuses two ranks on one GPU)
+    backend = os.environ.get("DG_BENCH_BACKEND", "nccl")
+    if os.environ.get("DG_BENCH_SAME_GPU") == "1":
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     # `--rotate R` distinct replica pairs (different seeds), joined round-robin: R x 112 MB
     # of inputs+outputs exceeds the 256 MB Infinity Cache, so every step streams its
@@ -523,8 +531,9 @@ def main():
         eng.sync()
 
     rows_done = sum(n_in_all[i % R] for i in range(args.steps))  # input rows merged by K steps
-    el_t = torch.tensor([el], dtype=torch.float64, device=dev)
-    tot = torch.tensor([float(rows_done)], dtype=torch.float64, device=dev)
+    cdev = dev if backend == "nccl" else torch.device("cpu")  # the collectives' device
+    el_t = torch.tensor([el], dtype=torch.float64, device=cdev)
+    tot = torch.tensor([float(rows_done)], dtype=torch.float64, device=cdev)
     if world > 1:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
