@@ -357,7 +357,8 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
   KSTAMP(t, 12);
   __syncthreads();
   u32 nD = s.roff[k];
-  if (bad || nS > (u32)CS || nD > (u32)CD || nU - nD > (u32)CM) {
+  if (bad || nS > (u32)CS || nD > (u32)CD || nU > (u32)CU) {  // (keyset entries take
+                                                              // any share of the items)
     if (tid == 0) atomicOr(p.flag, KF_OVERFLOW);
     nS = nU = nD = 0;  // publish an empty bucket so the look-back chain stays live
   }
