@@ -114,6 +114,9 @@ typedef struct dg_merkle_cont {
 typedef struct dg_engine dg_engine;
 
 /* ---- lifecycle ------------------------------------------------------------ */
+/* Synchronous calls (every entry point without _async) return when their work is done:
+ * the calling thread polls a word in host-mapped memory for up to 20 ms (a CPU core
+ * stays busy, as on a BEAM dirty scheduler), then waits on the stream instead. */
 int dg_abi_version(void);
 const char* dg_last_error(void);
 /* `hip_stream` NULL: the engine creates its own stream; otherwise it launches on the
