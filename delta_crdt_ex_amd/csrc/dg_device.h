@@ -219,7 +219,22 @@ __device__ __forceinline__ bool keyset_has(const u64* keys, u64 n, u64 k) {
   return lo < n && keys[lo] == k;
 }
 
-// Inclusive scan of a 32-bit value across the 64 lanes of a wave.
+// Inclusive scan of a 32-bit value across the 64 lanes of a wave, on the DPP network
+// (a few cycles a step) instead of ds_bpermute shuffles (an LDS round trip each): row_shr
+// 1/2/4/8 scans each row of 16 lanes, row_bcast:15 carries row 0 into row 1 (and row 2
+// into row 3), row_bcast:31 carries rows 0-1 into rows 2-3.  Lanes a step does not write
+// add the `old` operand, 0.
+#ifndef DG_SHFL_SCAN
+__device__ __forceinline__ u32 wave_incl_scan(u32 v) {
+  v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return v;
+}
+#else
 __device__ __forceinline__ u32 wave_incl_scan(u32 v) {
   const int lane = threadIdx.x & (WAVE - 1);
 #pragma unroll
@@ -228,6 +243,12 @@ __device__ __forceinline__ u32 wave_incl_scan(u32 v) {
     if (lane >= d) v += t;
   }
   return v;
+}
+#endif
+
+// Sum of a 32-bit value over the wave (every lane gets it).
+__device__ __forceinline__ u32 wave_sum_u32(u32 v) {
+  return (u32)__builtin_amdgcn_readlane((int)wave_incl_scan(v), WAVE - 1);
 }
 
 // Exclusive block scan; returns the exclusive prefix of `v` and the block total in

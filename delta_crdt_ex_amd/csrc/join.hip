@@ -844,11 +844,9 @@ __device__ __forceinline__ void stripe_sums(const u32* cs, u32 epoch, u32* err, 
     tot += n;
     lo += x < w ? n : 0;
   }
-#pragma unroll
-  for (int d = WAVE / 2; d >= 1; d >>= 1) {
-    lo += __shfl_xor(lo, d, WAVE);
-    tot += __shfl_xor(tot, d, WAVE);
-  }
+  // (a wave's sums of <= 2 x 64 twelve-bit counts fit 32 bits: DPP reductions)
+  lo = wave_sum_u32((u32)lo);
+  tot = wave_sum_u32((u32)tot);
   constexpr int NW = JB / WAVE;
   __syncthreads();  // every wave is done reading s_red from the previous call
   if ((tid & (WAVE - 1)) == 0) {
