@@ -246,9 +246,31 @@ __device__ __forceinline__ u32 wave_incl_scan(u32 v) {
 }
 #endif
 
+// Inclusive max-scan of a 32-bit value across the wave (DPP, as wave_incl_scan).
+__device__ __forceinline__ u32 wave_incl_max(u32 v) {
+  v = max(v, (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));
+  v = max(v, (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));
+  v = max(v, (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));
+  v = max(v, (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));
+  v = max(v, (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));
+  v = max(v, (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
+  return v;
+}
+
+// The value of the previous lane (lane 0: 0), DPP wave_shr:1.
+__device__ __forceinline__ u32 wave_prev(u32 v) {
+  return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
+}
+
 // Sum of a 32-bit value over the wave (every lane gets it).
 __device__ __forceinline__ u32 wave_sum_u32(u32 v) {
   return (u32)__builtin_amdgcn_readlane((int)wave_incl_scan(v), WAVE - 1);
+}
+
+// Sum over the wave of values below 2^42 (look-back granules): two 21-bit halves, each
+// summed on the DPP network (64 x 2^21 fits 32 bits).
+__device__ __forceinline__ u64 wave_sum_42(u64 v) {
+  return ((u64)wave_sum_u32((u32)(v >> 21)) << 21) + (u64)wave_sum_u32((u32)(v & 0x1FFFFFull));
 }
 
 // Exclusive block scan; returns the exclusive prefix of `v` and the block total in
@@ -341,13 +363,13 @@ __device__ __forceinline__ u64 lb_lookback(u64* state, u64 tile, u32 epoch, u32*
       if ((zero_mask & upto) == 0) {
         u64 contrib = (lane <= first) ? value : 0;
 #pragma unroll
-        for (int d = WAVE / 2; d >= 1; d >>= 1) contrib += __shfl_xor(contrib, d, WAVE);
+        contrib = wave_sum_42(contrib);
         return prefix + contrib;
       }
     } else if (zero_mask == 0) {
       u64 contrib = value;
 #pragma unroll
-      for (int d = WAVE / 2; d >= 1; d >>= 1) contrib += __shfl_xor(contrib, d, WAVE);
+      contrib = wave_sum_42(contrib);
       prefix += contrib;
       base -= WAVE;
       continue;
@@ -406,7 +428,7 @@ __device__ __forceinline__ u64 lb_lookback_block(u64* state, u64 tile, u32 epoch
     const u64 upto = first >= WAVE - 1 ? ~0ull : ((2ull << first) - 1);
     u64 c = lane <= first ? part : 0;
 #pragma unroll
-    for (int d = WAVE / 2; d >= 1; d >>= 1) c += __shfl_xor(c, d, WAVE);
+    c = wave_sum_42(c);
     if (lane == 0) {
       s_lb[w] = c;
       s_lb[NW + w] = im != 0;

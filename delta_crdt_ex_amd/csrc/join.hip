@@ -1010,24 +1010,19 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         }
       // the event before this thread's first: a max-scan of (lane + 1, last event) over
       // the wave's lanes with events, then the nearest earlier wave with events
+      // (DPP max-scan of the lane tags, then one shuffle for the key of the lane found)
       const int lane = tid & (WAVE - 1), wv = tid / WAVE;
-      int m = ne ? lane + 1 : 0;
-      u64 mk = lkey;
-      for (int d = 1; d < WAVE; d <<= 1) {
-        const int o = __shfl_up(m, d, WAVE);
-        const u64 ok = __shfl_up(mk, d, WAVE);
-        if (lane >= d && o > m) {
-          m = o;
-          mk = ok;
-        }
-      }
+      const u32 mi = wave_incl_max(ne ? (u32)lane + 1 : 0u);  // last lane <= this with events, + 1
+      const u32 mx = wave_prev(mi);                            // ... < this lane
+      const u64 pk = __shfl(lkey, mx > 0 ? (int)mx - 1 : 0, WAVE);
+      const u32 ml = (u32)__builtin_amdgcn_readlane((int)mi, WAVE - 1);  // the wave's last
+      const u64 wk = __shfl(lkey, ml > 0 ? (int)ml - 1 : 0, WAVE);
       if (lane == WAVE - 1) {
-        s.chf[wv] = m;
-        s.chk[wv] = mk;
+        s.chf[wv] = (int)ml;
+        s.chk[wv] = wk;
       }
-      int pm = __shfl_up(m, 1, WAVE);
-      u64 pkey = __shfl_up(mk, 1, WAVE);
-      if (lane == 0) pm = 0;
+      int pm = (int)mx;
+      u64 pkey = pk;
       __syncthreads();
       if (pm == 0)
         for (int w2 = wv - 1; w2 >= 0; w2--)
