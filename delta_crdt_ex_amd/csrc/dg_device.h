@@ -298,6 +298,26 @@ __device__ __forceinline__ u32 block_excl_scan(u32 v, u32* s_wave, u32* total) {
   return s_wave[w] + inc - v;
 }
 
+// The same scan with ONE barrier: every wave reads all BLOCK/64 wave totals and scans them
+// itself on the DPP network (reading its own prefix and the total with readlane), instead
+// of one thread prefixing them between two barriers.  Every wave reads every s_wave entry,
+// so the next write of s_wave (e.g. the next scan on the same scratch) needs a barrier
+// after this call; block_excl_scan above has no such precondition.
+template <int BLOCK>
+__device__ __forceinline__ u32 block_excl_scan1(u32 v, u32* s_wave, u32* total) {
+  constexpr int NW = BLOCK / WAVE;
+  static_assert(NW <= WAVE, "one wave total per lane");
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int w = threadIdx.x / WAVE;
+  const u32 inc = wave_incl_scan(v);
+  if (lane == WAVE - 1) s_wave[w] = inc;
+  __syncthreads();
+  const u32 ws = wave_incl_scan(lane < NW ? s_wave[lane] : 0u);
+  const u32 below = w > 0 ? (u32)__builtin_amdgcn_readlane((int)ws, w - 1) : 0u;
+  *total = (u32)__builtin_amdgcn_readlane((int)ws, NW - 1);
+  return below + inc - v;
+}
+
 // ---------------------------------------------------------------- tile offsets
 // Exclusive offsets of per-tile counts by ONE workgroup of NT threads (the middle pass
 // of count / scan / write compactions, used where every tile of a launch is resident
@@ -362,13 +382,11 @@ __device__ __forceinline__ u64 lb_lookback(u64* state, u64 tile, u32 epoch, u32*
       u64 upto = (first == 63) ? ~0ull : ((2ull << first) - 1);
       if ((zero_mask & upto) == 0) {
         u64 contrib = (lane <= first) ? value : 0;
-#pragma unroll
         contrib = wave_sum_42(contrib);
         return prefix + contrib;
       }
     } else if (zero_mask == 0) {
       u64 contrib = value;
-#pragma unroll
       contrib = wave_sum_42(contrib);
       prefix += contrib;
       base -= WAVE;
@@ -427,7 +445,6 @@ __device__ __forceinline__ u64 lb_lookback_block(u64* state, u64 tile, u32 epoch
     const int first = im ? __ffsll((long long)im) - 1 : WAVE;
     const u64 upto = first >= WAVE - 1 ? ~0ull : ((2ull << first) - 1);
     u64 c = lane <= first ? part : 0;
-#pragma unroll
     c = wave_sum_42(c);
     if (lane == 0) {
       s_lb[w] = c;
