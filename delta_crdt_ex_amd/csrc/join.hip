@@ -985,7 +985,7 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
                                   b0, keep, src, &ev);
     JSTAMP(t, 3);
     u32 n;
-    u32 pos = block_excl_scan<JB>(__popc(keep), s.wave, &n);
+    u32 pos = block_excl_scan1<JB>(__popc(keep), s.wave, &n);  // (barriers before s.wave's next use)
 #pragma unroll
     for (int q = 0; q < JI; q++)
       if (keep & (1u << q)) s.comp[bi][pos++] = src[q];
@@ -1034,7 +1034,7 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       if (ne && pm > 0 && fkey != pkey) diff++;
       // one scan for both: events (low 16 bits) and differing events (high 16 bits)
       u32 tot2;
-      const u32 sc2 = block_excl_scan<JB>((diff << 16) | (u32)ne, s.wave, &tot2);
+      const u32 sc2 = block_excl_scan1<JB>((diff << 16) | (u32)ne, s.wave, &tot2);
       const u32 n2 = tot2 & 0xffffu, p0 = sc2 & 0xffffu;
       u64* dst = p.chg_tmp + t * (u64)JT;
       u32 p2 = p0;
