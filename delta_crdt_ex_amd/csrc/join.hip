@@ -375,6 +375,24 @@ __device__ u64 mp_split(const Rows A, const Rows B, u64 d) {
   return mp_search(A, B, d, lo, hi);
 }
 
+// The proportional split of diagonal d, d * na / (na + nb) clamped to the diagonal's
+// range: exact for replicas that hold the same keys (config 2).
+__device__ __forceinline__ u64 split_guess(u64 na, u64 nb, u64 d) {
+  const u64 lo = d > nb ? d - nb : 0, hi = min(d, na);
+  const u64 i = (u64)((double)d * (double)na / (double)(na + nb));
+  return min(max(i, lo), hi);
+}
+
+// Whether g is diagonal d's split: A[g-1] <= B[d-g] and not A[g] <= B[d-1-g] (full tuples;
+// at the diagonal's ends one side is vacuous).  Uniform indices: scalar loads.
+__device__ __forceinline__ bool guess_exact(const Rows& A, const Rows& B, u64 d, u64 g) {
+  const u64 lo = d > B.n ? d - B.n : 0, hi = min(d, A.n);
+  bool ok = true;
+  if (g > lo) ok = row_le(load_row(A, g - 1), load_row(B, d - g));
+  if (g < hi) ok = ok && !row_le(load_row(A, g), load_row(B, d - 1 - g));
+  return ok;
+}
+
 // Keyed joins: the first index of keys[0, n_keys) >= the key at merged position d (split
 // s), by the calling wave.  Tile t's keys lie in [key(t*JT), key((t+1)*JT)], so the
 // keyset entries they can match are [ksplit(t), ksplit(t+1)] (keys are unique).
@@ -889,17 +907,33 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     __hip_atomic_store(cold(&cold_scan()->started) + w, epoch, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   if (w < G) JSTAMP(w, 0);  // (stamps build: slot 0 of a workgroup's first tile = its entry)
+  Staged r;
+  u64 ga0 = 0, ga1 = 0;  // fused: the first tile's speculative splits
   if (p.fused) {
     if (w == G) {  // Dots.union(c1, c2) (aw_lww_map.ex:155), beside the tiles
       ctx_union_block<JB>(p.cu, s.wave);
       return;
+    }
+    // The first tile's loads go out at the proportional splits d * na / (na + nb) BEFORE
+    // the exact search: replicas that hold the same keys (config 2) split exactly there,
+    // so the tile streams in during the search (checked below; re-issued otherwise).
+    {
+      ga0 = split_guess(A.n, B.n, w * (u64)JT);
+      ga1 = split_guess(A.n, B.n, min((w + 1) * (u64)JT, total));
+      int gnat, gnbt;
+      u64 gb0;
+      tile_geom(w, ga0, ga1, total, &gnat, &gnbt, &gb0);
+      issue_tile(A, B, gnat, gnbt, ga0, gb0, r);
     }
     // merge-path splits of this workgroup's (<= FUSE_IT) tiles, one wave per boundary
     const int wv = tid / WAVE;
     const u64 tk = w + (u64)(wv >> 1) * G;
     if (tk < ntiles) {
       const u64 d = min((tk + (wv & 1)) * (u64)JT, total);
-      const u64 sp = mp_split(A, B, d);
+      // the proportional split is checked first with scalar loads (a counter the tile
+      // loads in flight do not hold up); the search runs only where it is not exact
+      const u64 g = split_guess(A.n, B.n, d);
+      const u64 sp = guess_exact(A, B, d, g) ? g : mp_split(A, B, d);
       if ((tid & (WAVE - 1)) == 0) s.spl[wv] = sp;
       if (KEYED) {
         const u64 kq = key_split(A, B, p.keys, p.n_keys, d, sp);
@@ -937,8 +971,7 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   int nat, nbt;
   u64 b0;
   tile_geom(t, a0, a1, total, &nat, &nbt, &b0);
-  Staged r;
-  issue_tile(A, B, nat, nbt, a0, b0, r);
+  if (!p.fused || a0 != ga0 || a1 != ga1) issue_tile(A, B, nat, nbt, a0, b0, r);  // (uniform)
   u64 kl = 0, km = 0, kk = 0;
   if (KEYED) {
     km = kslice(t, 0, &kl);
