@@ -20,7 +20,7 @@ for lib in delta_crdt_ex_amd/libdeltagpu.so delta_crdt_ex_amd/libdeltagpu_DG*.so
   done
 done
 for mode in ${MODES:-1}; do
-  echo "stamps mode $mode"; DG_JOIN_MODE=$mode timeout -k 10 120 python -u tools/join_stamps.py || exit 1
+  echo "stamps mode $mode"; DG_JOIN_MODE=$mode C5_CONFIG=2 C5_STAMPS=gpurun_out/c2_stamps_$mode.npy DG_LIB_PATH=$PWD/delta_crdt_ex_amd/libdeltagpu_stamps.so timeout -k 10 120 python -u tools/prof_c5.py && python tools/stamps_report.py gpurun_out/c2_stamps_$mode.npy || exit 1
 done
 bash tools/prof_join.sh iter > gpurun_out/prof_iter.txt 2>&1 || { tail -5 gpurun_out/prof_iter.txt; exit 1; }
 head -8 gpurun_out/prof_iter.txt
