@@ -750,7 +750,7 @@ int kfold_pass(dg_engine* e, const dg_store* state, const dg_context* ctx, int k
     p.k = k;
     p.allmask = allmask;
     p.T = T;
-    p.n_fill_chunks = hf[2 * k + 1];
+    p.n_fill_chunks = hf[2 * k];  // the delta runs; the state's starts: kfold_sstart_kernel
     p.out = rows_out_of(out);
     p.out_ctx_node = out_ctx->node;
     p.out_ctx_cnt = out_ctx->cnt;

@@ -112,7 +112,7 @@ struct KFoldArgs {
   u64 T;               // key buckets
   const u64* flat;     // 2k+2 prefix sums of run lengths in KFOLD_FILL_CHUNKs: delta
                        // rows, keysets, state
-  u64 n_fill_chunks;   // flat[2k+1]
+  u64 n_fill_chunks;   // flat[2k]: the delta runs' chunks
   u64* sstart;         // T+1
   u32* dstart;         // (T+1) x 2k
   u64* tabC;           // k x KNT: c_i

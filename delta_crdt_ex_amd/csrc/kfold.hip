@@ -23,9 +23,10 @@
 //                       (node ids < KNT; larger ids in a context -> fallback flag), and
 //                       the output context C_k in node order.
 //   kfold_fill_kernel   key ids are 64-bit hashes, so the key space is cut into T equal
-//                       buckets; for the state and for every delta row run / keyset run,
-//                       start[t][run] = its first element of bucket >= t (one coalesced
-//                       pass over the keys).
+//                       buckets; for every delta row run / keyset run, start[t][run] = its
+//                       first element of bucket >= t (one coalesced pass over the keys);
+//                       the same starts for the state by one wave-wide search per bucket
+//                       (the state is much longer than the deltas and is not scanned).
 //   kfold_kernel        one workgroup per bucket: loads the state slice and the slices
 //                       of all runs into LDS, bitonic-sorts the delta rows + keyset
 //                       markers by key, evaluates every candidate as above, ranks the
@@ -176,16 +177,54 @@ __device__ __forceinline__ const u64* run_keys(const KFoldArgs& p, int r, u64* n
   return p.s.key;
 }
 
-// One workgroup per chunk of FILL_CHUNK elements of ONE run (chunk prefix sums per run
-// in p.flat), so the run's key pointer is uniform and the key loads coalesce.
+// sstart[t] for t in [0, T]: the state's first row whose bucket is >= t, one wave per t
+// (a 64-ary search: 4 dependent load rounds at 10M rows) instead of a pass over all of the
+// state's keys (80 MB at config 3).
+__device__ __forceinline__ void state_start(const KFoldArgs& p, u64 t) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  const u64* k = p.s.key;
+  const u64 T = p.T;
+  u64 lo = 0, hi = p.s.n;
+  while (hi - lo > WAVE) {
+    const u64 span = hi - lo;
+    const u64 q = lo + span * (u64)(lane + 1) / (WAVE + 1);
+    const u64 m = __ballot(bucket_of(k[q], T) < t);  // true on a prefix of the lanes
+    const int c = __popcll(m);
+    const u64 nlo = c ? lo + span * (u64)c / (WAVE + 1) + 1 : lo;
+    const u64 nhi = c < WAVE ? lo + span * (u64)(c + 1) / (WAVE + 1) : hi;
+    lo = nlo;
+    hi = nhi;
+  }
+  const bool lt = lo + lane < hi && bucket_of(k[lo + lane], T) < t;
+  const u64 r = lo + (u64)__popcll(__ballot(lt));
+  if (lane == 0) p.sstart[t] = r;
+}
+
+// Workgroups [0, fill_blocks) walk the delta runs, one chunk of FILL_CHUNK elements of ONE
+// run at a time (chunk prefix sums per run in p.flat), so the run's key pointer is uniform
+// and the key loads coalesce; each thread issues all of its chunk's loads before any
+// store. The workgroups past them search the state's starts, four buckets each.
 constexpr u64 FILL_CHUNK = KFOLD_FILL_CHUNK;
+constexpr int FILL_PER = (int)(FILL_CHUNK / 256);
+static_assert(FILL_CHUNK % 256 == 0, "whole rounds per chunk");
+__host__ __device__ __forceinline__ u32 fill_blocks(u64 n_fill_chunks) {
+  return (u32)(n_fill_chunks < 8192 ? n_fill_chunks : 8192);
+}
+
 __global__ __launch_bounds__(256) void kfold_fill_kernel(KFoldArgs p) {
+  const u32 g = fill_blocks(p.n_fill_chunks);
+  if (blockIdx.x >= g) {  // block-uniform
+    const u64 t = ((u64)(blockIdx.x - g) * 256 + threadIdx.x) / WAVE;  // wave-uniform
+    if (t <= p.T) state_start(p, t);
+    return;
+  }
   __shared__ u64 flat[2 * KFOLD_MAX_K + 2];
-  const int nr = 2 * p.k + 1;  // runs incl. the state
+  const int nr = 2 * p.k;  // the delta runs
   for (int i = threadIdx.x; i <= nr; i += 256) flat[i] = p.flat[i];
   __syncthreads();
   const u64 T = p.T, stride = 2 * (u64)p.k;
-  for (u64 c = blockIdx.x; c < flat[nr]; c += gridDim.x) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  for (u64 c = blockIdx.x; c < p.n_fill_chunks; c += g) {
     int lo = 0, hi = nr;  // flat[lo] <= c < flat[hi]; empty runs are skipped
     while (hi - lo > 1) {
       const int mid = (lo + hi) >> 1;
@@ -198,16 +237,23 @@ __global__ __launch_bounds__(256) void kfold_fill_kernel(KFoldArgs p) {
     u64 n;
     const u64* keys = run_keys(p, r, &n);
     const u64 j0 = (c - flat[r]) * FILL_CHUNK;
-    for (u64 j = j0 + threadIdx.x; j < min<u64>(j0 + FILL_CHUNK, n); j += 256) {
-      const u64 b = bucket_of(keys[j], T);
-      u64 bb = j == 0 ? 0 : bucket_of(keys[j - 1], T) + 1;
-      const u64 end = (j == n - 1) ? T : b;
-      for (; bb <= end; bb++) {
-        const u64 v = bb <= b ? j : n;
-        if (r == nr - 1)
-          p.sstart[bb] = v;
-        else
-          p.dstart[bb * stride + r] = (u32)v;
+    const u64 jend = min<u64>(j0 + FILL_CHUNK, n);
+    u64 kc[FILL_PER], kp[FILL_PER];
+#pragma unroll
+    for (int u = 0; u < FILL_PER; u++) {
+      const u64 j = j0 + (u64)u * 256 + threadIdx.x;
+      kc[u] = j < jend ? keys[j] : 0;
+      kp[u] = (lane == 0 && j > 0 && j < jend) ? keys[j - 1] : 0;  // lanes > 0: DPP
+    }
+#pragma unroll
+    for (int u = 0; u < FILL_PER; u++) {
+      const u64 j = j0 + (u64)u * 256 + threadIdx.x;
+      const u32 b = (u32)bucket_of(kc[u], T);  // every lane, for the DPP shift
+      const u32 pb = wave_prev(b);
+      if (j < jend) {
+        u64 bb = j == 0 ? 0 : (lane ? (u64)pb : bucket_of(kp[u], T)) + 1;
+        const u64 end = (j == n - 1) ? T : b;
+        for (; bb <= end; bb++) p.dstart[bb * stride + r] = (u32)(bb <= b ? j : n);
       }
     }
   }
@@ -611,10 +657,8 @@ extern "C" int dg_debug_kfold_stamps(unsigned long long* host, size_t n) {
 
 hipError_t launch_kfold(const KFoldArgs& p, hipStream_t st) {
   hipLaunchKernelGGL(kfold_prep_kernel, dim3(1), dim3(KNT), 0, st, p);
-  if (p.n_fill_chunks) {
-    const u64 g = std::min<u64>(p.n_fill_chunks, 8192);
-    hipLaunchKernelGGL(kfold_fill_kernel, dim3((u32)g), dim3(256), 0, st, p);
-  }
+  const u64 g = fill_blocks(p.n_fill_chunks) + (p.T + 1 + 3) / 4;  // + the state's starts
+  hipLaunchKernelGGL(kfold_fill_kernel, dim3((u32)g), dim3(256), 0, st, p);
   hipLaunchKernelGGL(kfold_kernel, dim3((u32)p.T), dim3(KB), 0, st, p);
   return hipGetLastError();
 }
