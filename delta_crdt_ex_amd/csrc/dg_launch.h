@@ -88,7 +88,7 @@ constexpr int KFOLD_CAP_M = 512 >> DG_KFOLD_SCALE;   //   keyset entries
 constexpr int KFOLD_MAX_K = 64;    // deltas per pass (delta masks are u64)
 constexpr int KNT = 1024;          // VV tables cover node ids < KNT
 constexpr u32 KF_PREP_FAIL = 1, KF_OVERFLOW = 2;
-constexpr u64 KFOLD_FILL_CHUNK = 256 * 8;  // elements per workgroup of the bucket fill
+constexpr u64 KFOLD_FILL_CHUNK = 1024 * 8;  // elements per workgroup of the bucket fill
 // mean fill per bucket the host sizes T for, each >= 5.5 sigma below its LDS capacity:
 // state rows (cap 1024), delta rows (their payload slots: cap 512) and all items, delta
 // rows + keyset entries (one per thread: cap 1024; a touched key brings a keyset entry and

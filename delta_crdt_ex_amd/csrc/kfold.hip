@@ -19,7 +19,7 @@
 // two VV lookups per touching delta.
 //
 // Kernels (one stream, no host sync until the end):
-//   kfold_prep_kernel   dense VV tables: tabC[i][node] = c_i, tabP[i][node] = C_{i-1}
+//   kfold_prep          dense VV tables: tabC[i][node] = c_i, tabP[i][node] = C_{i-1}
 //                       (node ids < KNT; larger ids in a context -> fallback flag), and
 //                       the output context C_k in node order.
 //   kfold_fill_kernel   key ids are 64-bit hashes, so the key space is cut into T equal
@@ -108,7 +108,9 @@ __device__ __forceinline__ void present2(Cand& a, bool da, Cand& b, bool db, con
 }
 
 // ------------------------------------------------------------------------ prep
-__global__ __launch_bounds__(KNT) void kfold_prep_kernel(KFoldArgs p) {
+// One workgroup of KNT threads (workgroup 0 of the fill launch, so that this single-block
+// latency chain runs beside the fill instead of before it).
+__device__ __forceinline__ void kfold_prep(const KFoldArgs& p) {
   __shared__ u32 pres[KNT];
   __shared__ u32 wave[KNT / WAVE + 1];
   const u32 n = threadIdx.x;
@@ -200,31 +202,39 @@ __device__ __forceinline__ void state_start(const KFoldArgs& p, u64 t) {
   if (lane == 0) p.sstart[t] = r;
 }
 
-// Workgroups [0, fill_blocks) walk the delta runs, one chunk of FILL_CHUNK elements of ONE
-// run at a time (chunk prefix sums per run in p.flat), so the run's key pointer is uniform
-// and the key loads coalesce; each thread issues all of its chunk's loads before any
-// store. The workgroups past them search the state's starts, four buckets each.
+// One launch of KNT-thread workgroups: workgroup 0 builds the VV tables (kfold_prep);
+// workgroups [1, 1 + fill_blocks) walk the delta runs, one chunk of FILL_CHUNK elements of
+// ONE run at a time (chunk prefix sums per run in p.flat), so the run's key pointer is
+// uniform and the key loads coalesce; each thread issues all of its chunk's loads before
+// any store. The workgroups past them search the state's starts, one bucket per wave.
+constexpr int FILL_BLOCK = KNT;
 constexpr u64 FILL_CHUNK = KFOLD_FILL_CHUNK;
-constexpr int FILL_PER = (int)(FILL_CHUNK / 256);
-static_assert(FILL_CHUNK % 256 == 0, "whole rounds per chunk");
+constexpr int FILL_PER = (int)(FILL_CHUNK / FILL_BLOCK);
+static_assert(FILL_CHUNK % FILL_BLOCK == 0, "whole rounds per chunk");
+constexpr int FILL_WAVES = FILL_BLOCK / WAVE;
 __host__ __device__ __forceinline__ u32 fill_blocks(u64 n_fill_chunks) {
-  return (u32)(n_fill_chunks < 8192 ? n_fill_chunks : 8192);
+  return (u32)(n_fill_chunks < 2048 ? n_fill_chunks : 2048);
 }
 
-__global__ __launch_bounds__(256) void kfold_fill_kernel(KFoldArgs p) {
+__global__ __launch_bounds__(FILL_BLOCK) void kfold_fill_kernel(KFoldArgs p) {
+  if (blockIdx.x == 0) {
+    kfold_prep(p);
+    return;
+  }
   const u32 g = fill_blocks(p.n_fill_chunks);
-  if (blockIdx.x >= g) {  // block-uniform
-    const u64 t = ((u64)(blockIdx.x - g) * 256 + threadIdx.x) / WAVE;  // wave-uniform
+  const u32 blk = blockIdx.x - 1;
+  if (blk >= g) {  // block-uniform
+    const u64 t = (u64)(blk - g) * FILL_WAVES + threadIdx.x / WAVE;  // wave-uniform
     if (t <= p.T) state_start(p, t);
     return;
   }
   __shared__ u64 flat[2 * KFOLD_MAX_K + 2];
   const int nr = 2 * p.k;  // the delta runs
-  for (int i = threadIdx.x; i <= nr; i += 256) flat[i] = p.flat[i];
+  for (int i = threadIdx.x; i <= nr; i += FILL_BLOCK) flat[i] = p.flat[i];
   __syncthreads();
   const u64 T = p.T, stride = 2 * (u64)p.k;
   const int lane = threadIdx.x & (WAVE - 1);
-  for (u64 c = blockIdx.x; c < p.n_fill_chunks; c += g) {
+  for (u64 c = blk; c < p.n_fill_chunks; c += g) {
     int lo = 0, hi = nr;  // flat[lo] <= c < flat[hi]; empty runs are skipped
     while (hi - lo > 1) {
       const int mid = (lo + hi) >> 1;
@@ -241,13 +251,13 @@ __global__ __launch_bounds__(256) void kfold_fill_kernel(KFoldArgs p) {
     u64 kc[FILL_PER], kp[FILL_PER];
 #pragma unroll
     for (int u = 0; u < FILL_PER; u++) {
-      const u64 j = j0 + (u64)u * 256 + threadIdx.x;
+      const u64 j = j0 + (u64)u * FILL_BLOCK + threadIdx.x;
       kc[u] = j < jend ? keys[j] : 0;
       kp[u] = (lane == 0 && j > 0 && j < jend) ? keys[j - 1] : 0;  // lanes > 0: DPP
     }
 #pragma unroll
     for (int u = 0; u < FILL_PER; u++) {
-      const u64 j = j0 + (u64)u * 256 + threadIdx.x;
+      const u64 j = j0 + (u64)u * FILL_BLOCK + threadIdx.x;
       const u32 b = (u32)bucket_of(kc[u], T);  // every lane, for the DPP shift
       const u32 pb = wave_prev(b);
       if (j < jend) {
@@ -656,9 +666,9 @@ extern "C" int dg_debug_kfold_stamps(unsigned long long* host, size_t n) {
 #endif
 
 hipError_t launch_kfold(const KFoldArgs& p, hipStream_t st) {
-  hipLaunchKernelGGL(kfold_prep_kernel, dim3(1), dim3(KNT), 0, st, p);
-  const u64 g = fill_blocks(p.n_fill_chunks) + (p.T + 1 + 3) / 4;  // + the state's starts
-  hipLaunchKernelGGL(kfold_fill_kernel, dim3((u32)g), dim3(256), 0, st, p);
+  // prep + delta fill + the state's starts
+  const u64 g = 1 + fill_blocks(p.n_fill_chunks) + (p.T + FILL_WAVES) / FILL_WAVES;
+  hipLaunchKernelGGL(kfold_fill_kernel, dim3((u32)g), dim3(FILL_BLOCK), 0, st, p);
   hipLaunchKernelGGL(kfold_kernel, dim3((u32)p.T), dim3(KB), 0, st, p);
   return hipGetLastError();
 }
