@@ -287,7 +287,7 @@ __device__ u64 g_kf_stamps[65536 * 16];
 #endif
 
 #ifndef DG_KFOLD_NSUB
-#define DG_KFOLD_NSUB 512
+#define DG_KFOLD_NSUB 1024  // (512: 904 us vs 878 us per config-3 fold; 768: 897 us)
 #endif
 constexpr int NSUB = DG_KFOLD_NSUB;  // sub-buckets of a bucket's key range (LDS counting sort)
 constexpr int PER = 2;     // items per thread in the block scans
@@ -322,6 +322,8 @@ struct KLds {
   u64 lb[3 * (KB / WAVE) + 2];
   u64 bcast[1];
 };
+
+static_assert(sizeof(KLds) <= 80 * 1024, "two buckets per CU (160 KB of LDS)");
 
 __device__ __forceinline__ Row srow(const KLds& s, u32 i) {
   Row r;
