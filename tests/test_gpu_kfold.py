@@ -100,6 +100,18 @@ def test_onepass_empty_inputs(strict):
     check(strict, es, ds)
 
 
+@pytest.mark.parametrize("n_keys,keep", [(40, None), (65, None), (130, None), (3000, 1),
+                                         (3000, 63), (3000, 64), (3000, 65)])
+def test_onepass_small_states(strict, n_keys, keep):
+    """States of 0-130 rows: the per-bucket wave search for the state's bucket starts
+    (kfold_fill_kernel) below, at and just above one wave's width, and many buckets with no
+    state row at all."""
+    st, ds = random_fold(30 + n_keys + (keep or 0), n_keys=n_keys, k=5)
+    if keep is not None:
+        st = {"rows": tuple(c[:keep] for c in st["rows"]), "ctx": st["ctx"]}
+    check(strict, st, ds)
+
+
 def test_onepass_large_node_ids_in_rows(strict):
     """Row node ids >= the VV table width that no context names: never covered."""
     st, ds = random_fold(22, n_keys=2000, k=8, n_nodes=40, node_base=1000, ctx_node_max=1024)
