@@ -115,6 +115,16 @@ __device__ __forceinline__ void store_row_nt(const RowsOut& out, u64 o, const Ro
   __builtin_nontemporal_store(x.cnt, out.cnt + o);
 }
 
+// The same through the L2 (a row's columns written in pieces by several waves merge there
+// before they go to HBM).
+__device__ __forceinline__ void store_row(const RowsOut& out, u64 o, const Row& x) {
+  out.key[o] = x.key;
+  out.val[o] = x.val;
+  out.ts[o] = x.ts;
+  out.node[o] = x.node;
+  out.cnt[o] = x.cnt;
+}
+
 // c ? x : y field by field (a conditional on two Row objects selects an ADDRESS and
 // copies through it, which keeps both rows in scratch memory).
 __device__ __forceinline__ Row row_sel(bool c, const Row& x, const Row& y) {

@@ -649,12 +649,15 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
     if (tid == 0) lb_publish(p.scan.state, t, p.scan.epoch, LB_INC, base + total);
   }
   if (tid == 0 && t == T - 1) p.d_counts[0] = base + total;
+// plain stores, not non-temporal: a bucket's state rows and items interleave in the
+// output, so every line is written in pieces by several waves, and the pieces must merge
+// in the L2 (non-temporal: 783 MB written per config-3 fold; plain: 376 MB = the output)
 #pragma unroll
   for (int j = 0; j < RS; j++)
-    if (so[j] != ~0u) store_row_nt(p.out, base + so[j], srow(s, tid + j * KB));
+    if (so[j] != ~0u) store_row(p.out, base + so[j], srow(s, tid + j * KB));
 #pragma unroll
   for (int j = 0; j < RU; j++)
-    if (uo[j] != ~0u) store_row_nt(p.out, base + uo[j], drow(s, s.utag[tid + j * KB] & SLOT));
+    if (uo[j] != ~0u) store_row(p.out, base + uo[j], drow(s, s.utag[tid + j * KB] & SLOT));
   KSTAMP(t, 6);
 }
 
