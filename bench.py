@@ -36,15 +36,10 @@ KEYS_PER_GPU = 1_000_000
 
 
 def kernel_source_digest():
-    """sha256 over the HIP sources of libdeltagpu: ties a PMC summary to the kernels
-    it measured."""
-    import glob
-    import hashlib
-    h = hashlib.sha256()
-    for f in sorted(glob.glob(os.path.join(ROOT, "delta_crdt_ex_amd", "csrc", "*"))):
-        h.update(os.path.basename(f).encode())
-        h.update(open(f, "rb").read())
-    return h.hexdigest()[:16]
+    """The digest of libdeltagpu's sources (the one the library embeds, dg_build_digest):
+    ties a PMC summary to the kernels it measured."""
+    from delta_crdt_ex_amd._abi import source_digest
+    return source_digest()
 
 
 def _traffic_from_profiles(n_in, n_out):
@@ -556,6 +551,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u64",
+            "lib_digest": eng.lib.dg_build_digest().decode(),
             "data": "synthetic (seeded config-2 replicas, SURVEY.md §8(d))",
             "config": {
                 "workload": "config2: 1M-key AWLWWMap full-state join of two replicas, 10% "

@@ -7,12 +7,32 @@ Loading fails loudly: there is no CPU fallback anywhere in the product path.
 from __future__ import annotations
 
 import ctypes as C
+import glob
+import hashlib
 import os
 import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DG_LIB_PATH") or os.path.join(HERE, "libdeltagpu.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "deltagpu.h")
+CSRC = os.path.join(HERE, "csrc")
+
+
+def source_files() -> list[str]:
+    """The sources libdeltagpu.so is built from (the digest's inputs)."""
+    return (sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.h")))
+            + [HEADER])
+
+
+def source_digest() -> str:
+    """sha256 prefix over the library's sources (name + content), as build.py embeds it
+    in the library (dg_build_digest)."""
+    h = hashlib.sha256()
+    for f in source_files():
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 DG_OK = 0
 DG_E_INVAL = -1
@@ -96,6 +116,7 @@ class FunctionClauseError(DeltaGpuError):
 
 _SIGS = {
     "dg_abi_version": (C.c_int, []),
+    "dg_build_digest": (C.c_char_p, []),
     "dg_last_error": (C.c_char_p, []),
     "dg_engine_create": (C.c_int, [C.c_int, C.c_void_p, C.POINTER(C.c_void_p)]),
     "dg_engine_destroy": (C.c_int, [C.c_void_p]),
@@ -188,6 +209,11 @@ def load(path: str = LIB_PATH):
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
+    built = lib.dg_build_digest().decode()
+    if os.path.isdir(CSRC) and built != source_digest():
+        raise RuntimeError(
+            f"{path} is stale: built from sources {built}, the tree's are {source_digest()}; "
+            "rebuild with `python -m delta_crdt_ex_amd.build`")
     _lib = lib
     return lib
 

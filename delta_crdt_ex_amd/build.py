@@ -44,6 +44,26 @@ def _stale(target: str, inputs: list[str]) -> bool:
     return any(os.path.getmtime(i) > t for i in inputs)
 
 
+def _digest_object(hipcc: str, run) -> str:
+    """OBJ/digest.o defining dg_build_digest() = the sources' digest (rewritten, and so
+    relinked, only when the digest changes)."""
+    sys.path.insert(0, HERE)
+    try:
+        from _abi import source_digest  # noqa: E402  (no package import: no torch needed)
+    finally:
+        sys.path.pop(0)
+    d = source_digest()
+    src = os.path.join(OBJ, "digest.c")
+    obj = os.path.join(OBJ, "digest.o")
+    text = f'const char* dg_build_digest(void) {{ return "{d}"; }}\n'
+    if not os.path.exists(src) or open(src).read() != text:
+        with open(src, "w") as f:
+            f.write(text)
+    if _stale(obj, [src]):
+        run([hipcc, "-x", "c", "-O2", "-fPIC", "-c", src, "-o", obj])
+    return obj
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(OBJ, exist_ok=True)
     hipcc = _hipcc()
@@ -68,6 +88,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
     with ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
         list(ex.map(run, jobs))
+    objs.append(_digest_object(hipcc, run))
     if force or jobs or _stale(LIB, objs):
         tmp = LIB + ".tmp"
         run([hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", tmp] + objs)

@@ -306,6 +306,21 @@ int check_ctx(const dg_context* c, const char* what) {
     if (_r != DG_OK) return _r; \
   } while (0)
 
+// Asynchronous calls logged for a replay at dg_engine_sync (a single-pass join grid that
+// aborted for lack of residency).  A full log is settled before the next call is added.
+constexpr size_t MAX_PENDING = 4096;
+
+// Every synchronous entry point settles the asynchronous calls before it enqueues its own
+// work: an aborted grid's error bit is then seen (and its calls replayed) by
+// dg_engine_sync, never by the synchronous call's own error check, which would clear
+// it and leave the aborted join's output unreported.
+int settle(dg_engine* e) {
+  if (!e->pending.empty()) return dg_engine_sync(e);
+  return DG_OK;
+}
+
+int merkle_build_enqueue(dg_engine* e, const dg_store* s, dg_merkle* t, uint64_t* d_n_keys);
+
 // chg (optional): the join also records its change events (dg_join2_changes); *chg
 // receives their scratch for launch_join2_changes.
 int join2_enqueue(dg_engine* e, const dg_store* a, const dg_context* ca, const dg_store* b,
@@ -494,7 +509,7 @@ int dg_engine_sync(dg_engine* e) {
         TRY(join2_enqueue(e, &q.a, &q.ca, &q.b, &q.cb, q.keys, q.n_keys, &q.out, &q.out_ctx,
                           q.d_counts, nullptr, true));
       else
-        TRY(dg_merkle_build_async(e, &q.a, q.tp, q.d_counts));
+        TRY(merkle_build_enqueue(e, &q.a, q.tp, q.d_counts));
     }
     e->pending.clear();
     TRY(stream_error(e, &err));
@@ -508,6 +523,7 @@ int dg_store_check(dg_engine* e, const dg_store* s) {
   if (!e) return fail(DG_E_INVAL, "null engine");
   TRY(check_store(s, "dg_store_check"));
   TRY(set_device(e));
+  TRY(settle(e));
   HIP_TRY(hipMemsetAsync(e->ticket + 2, 0, sizeof(u32), e->stream));
   HIP_TRY(launch_store_check(rows_of(s), e->ticket + 2, e->stream));
   TRY(sync_words(e));
@@ -519,6 +535,7 @@ int dg_join2_async(dg_engine* e, const dg_store* a, const dg_context* ca, const 
                    const dg_context* cb, const uint64_t* keys, uint64_t n_keys, dg_store* out,
                    dg_context* out_ctx, uint64_t* d_counts) {
   if (!e) return fail(DG_E_INVAL, "null engine");
+  if (e->pending.size() >= MAX_PENDING) TRY(dg_engine_sync(e));
   TRY(join2_enqueue(e, a, ca, b, cb, keys, n_keys, out, out_ctx, d_counts));
   dg_engine::Pending q{};
   q.kind = 0;
@@ -531,7 +548,7 @@ int dg_join2_async(dg_engine* e, const dg_store* a, const dg_context* ca, const 
   q.keys = keys;
   q.n_keys = n_keys;
   q.d_counts = d_counts;
-  if (e->pending.size() < 4096) e->pending.push_back(q);  // (a bounded log)
+  e->pending.push_back(q);
   return DG_OK;
 }
 
@@ -539,7 +556,7 @@ int dg_join2(dg_engine* e, const dg_store* a, const dg_context* ca, const dg_sto
              const dg_context* cb, const uint64_t* keys, uint64_t n_keys, dg_store* out,
              dg_context* out_ctx) {
   if (!e) return fail(DG_E_INVAL, "null engine");
-  if (!e->pending.empty()) TRY(dg_engine_sync(e));  // settle earlier asynchronous calls
+  TRY(settle(e));  // earlier asynchronous calls
   TRY(join2_enqueue(e, a, ca, b, cb, keys, n_keys, out, out_ctx, e->d_counts));
   if (read_counts(e, 2) != DG_OK) {
     // a single-pass grid that could not become resident (another process's persistent
@@ -557,7 +574,7 @@ int dg_join2_changes(dg_engine* e, const dg_store* a, const dg_context* ca, cons
                      dg_context* out_ctx, uint64_t* changed, uint64_t cap, uint64_t* n_changed) {
   if (!e) return fail(DG_E_INVAL, "null engine");
   if (!n_changed || (cap && !changed)) return fail(DG_E_INVAL, "dg_join2_changes: null output");
-  if (!e->pending.empty()) TRY(dg_engine_sync(e));
+  TRY(settle(e));
   void* chg = nullptr;
   TRY(join2_enqueue(e, a, ca, b, cb, keys, n_keys, out, out_ctx, e->d_counts, &chg));
   HIP_TRY(launch_join2_changes(a->n, b->n, chg, changed, cap, e->d_counts + 2, e->stream));
@@ -750,7 +767,8 @@ int kfold_pass(dg_engine* e, const dg_store* state, const dg_context* ctx, int k
     p.k = k;
     p.allmask = allmask;
     p.T = T;
-    p.n_fill_chunks = hf[2 * k];  // the delta runs; the state's starts: kfold_sstart_kernel
+    p.n_fill_chunks = hf[2 * k];  // the delta runs; the state's starts: kfold_fill_kernel's
+                                  // trailing workgroups (state_start, one wave per bucket)
     p.out = rows_out_of(out);
     p.out_ctx_node = out_ctx->node;
     p.out_ctx_cnt = out_ctx->cnt;
@@ -830,6 +848,7 @@ int dg_joink(dg_engine* e, int k, const dg_store* stores, const dg_context* ctxs
   if (k <= 0 || !stores || !ctxs || !out || !out_ctx) return fail(DG_E_INVAL, "dg_joink: bad args");
   TRY(check_store(&stores[0], "dg_joink store"));
   TRY(check_ctx(&ctxs[0], "dg_joink ctx"));
+  TRY(settle(e));
   return fold_join(e, &stores[0], &ctxs[0], k - 1, stores + 1, ctxs + 1, nullptr, nullptr, out,
                    out_ctx, "dg_joink");
 }
@@ -844,6 +863,7 @@ int dg_apply_deltas(dg_engine* e, const dg_store* state, const dg_context* ctx, 
   TRY(check_store(state, "dg_apply_deltas state"));
   TRY(check_ctx(ctx, "dg_apply_deltas ctx"));
   if (keys && !n_keys) return fail(DG_E_INVAL, "dg_apply_deltas: keys without n_keys");
+  TRY(settle(e));
   return apply_deltas(e, state, ctx, k, deltas, dctxs, keys, n_keys, out, out_ctx);
 }
 
@@ -855,6 +875,7 @@ int dg_take_keys(dg_engine* e, const dg_store* s, const uint64_t* keys, uint64_t
   if (out->cap && (!out->key || !out->val || !out->ts || !out->node || !out->cnt))
     return fail(DG_E_INVAL, "dg_take_keys: null output column");
   TRY(set_device(e));
+  TRY(settle(e));
   TRY(ensure_state(e, take_tiles(n_keys) + 1));
   Scan sc;
   TRY(next_scan(e, &sc));
@@ -883,6 +904,7 @@ int dg_mutate_batch(dg_engine* e, const dg_store* state, const dg_context* ctx, 
     return fail(DG_E_INVAL, "dg_mutate_batch: null argument");
   if (n_adds > m) return fail(DG_E_INVAL, "dg_mutate_batch: n_adds > m");
   TRY(set_device(e));
+  TRY(settle(e));
   const u64 nt = mutate_tiles(m);
   TRY(ensure_state(e, 6 * nt + 2));  // raw per-tile counts and offsets
   HIP_TRY(hipMemsetAsync(e->ticket + 3, 0, sizeof(u32), e->stream));
@@ -933,6 +955,7 @@ int dg_context_union(dg_engine* e, const dg_context* a, const dg_context* b, dg_
   if (!out) return fail(DG_E_INVAL, "dg_context_union: null out");
   if (out->cap < a->n + b->n) return fail(DG_E_CAPACITY, "dg_context_union: out cap too small");
   TRY(set_device(e));
+  TRY(settle(e));
   TRY(ensure_tmp(e, ctx_union_tmp_bytes(a->n, b->n)));
   HIP_TRY(launch_ctx_union(ctx_of(a), ctx_of(b), out->node, out->cnt, e->d_counts + 1, e->tmp,
                            e->stream));
@@ -966,6 +989,7 @@ int dg_read_lww(dg_engine* e, const dg_store* s, const uint64_t* keys, uint64_t 
     return fail(DG_E_CAPACITY, "dg_read_lww: cap %llu < %llu", (unsigned long long)cap,
                 (unsigned long long)need);
   TRY(set_device(e));
+  TRY(settle(e));
   TRY(ensure_state(e, 2 * seg_tiles(s->n) + 2));  // raw per-tile counts and offsets
   HIP_TRY(launch_read_lww(rows_of(s), keys, keys ? n_keys : 0, out_key, out_val, e->state,
                           e->d_counts, e->stream));
@@ -1015,8 +1039,12 @@ int input_error(dg_engine* e, const char* what) {
 
 extern "C" {
 
-int dg_merkle_build_async(dg_engine* e, const dg_store* s, dg_merkle* t, uint64_t* d_n_keys) {
-  if (!e) return fail(DG_E_INVAL, "null engine");
+}  // extern "C"
+
+namespace {
+
+// The build's launch, shared by the synchronous call, the asynchronous one and the replay.
+int merkle_build_enqueue(dg_engine* e, const dg_store* s, dg_merkle* t, uint64_t* d_n_keys) {
   TRY(check_store(s, "dg_merkle_build"));
   TRY(check_merkle(t, "dg_merkle_build"));
   if (!d_n_keys) return fail(DG_E_INVAL, "dg_merkle_build: null d_n_keys");
@@ -1025,18 +1053,31 @@ int dg_merkle_build_async(dg_engine* e, const dg_store* s, dg_merkle* t, uint64_
   HIP_TRY(hipMemsetAsync(e->ticket + 3, 0, sizeof(u32), e->stream));
   HIP_TRY(launch_merkle_build(rows_of(s), merkle_of(t), d_n_keys, (u32*)e->tmp, e->ticket + 3,
                               e->stream));
+  return DG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dg_merkle_build_async(dg_engine* e, const dg_store* s, dg_merkle* t, uint64_t* d_n_keys) {
+  if (!e) return fail(DG_E_INVAL, "null engine");
+  if (e->pending.size() >= MAX_PENDING) TRY(dg_engine_sync(e));
+  TRY(merkle_build_enqueue(e, s, t, d_n_keys));
   dg_engine::Pending q{};
   q.kind = 1;
   q.a = *s;
   q.t = *t;
   q.tp = t;
   q.d_counts = d_n_keys;
-  if (e->pending.size() < 4096) e->pending.push_back(q);
+  e->pending.push_back(q);
   return DG_OK;
 }
 
 int dg_merkle_build(dg_engine* e, const dg_store* s, dg_merkle* t) {
-  TRY(dg_merkle_build_async(e, s, t, e ? e->d_counts : nullptr));
+  if (!e) return fail(DG_E_INVAL, "null engine");
+  TRY(settle(e));
+  TRY(merkle_build_enqueue(e, s, t, e->d_counts));  // not logged: it is settled right here
   TRY(read_counts(e, 1));
   TRY(input_error(e, "dg_merkle_build"));
   t->n_keys = e->h_counts[0];
@@ -1051,6 +1092,7 @@ int dg_merkle_update(dg_engine* e, dg_merkle* t, const dg_store* old_s, const dg
   TRY(check_store(new_s, "dg_merkle_update new"));
   if (n_keys && !keys) return fail(DG_E_INVAL, "dg_merkle_update: null keys");
   TRY(set_device(e));
+  TRY(settle(e));
   const u64 chunks = merkle_chunks(t->depth), cw = merkle_ctr_words(t->depth);
   TRY(ensure_tmp(e, (cw + chunks) * sizeof(u32)));
   u32* ctr = (u32*)e->tmp;
@@ -1078,6 +1120,7 @@ int dg_merkle_diff(dg_engine* e, const dg_merkle* a, const dg_store* sa, const d
   if (!n_out) return fail(DG_E_INVAL, "dg_merkle_diff: null n_out");
   if (cap && !out_keys) return fail(DG_E_INVAL, "dg_merkle_diff: null out_keys");
   TRY(set_device(e));
+  TRY(settle(e));
   TRY(ensure_tmp(e, diff_scratch_words(a->depth, sa->n, sb->n) * sizeof(u64)));
   HIP_TRY(launch_merkle_diff(merkle_of(a), rows_of(sa), merkle_of(b), rows_of(sb), out_keys, cap,
                              (u64*)e->tmp, e->d_counts, e->stream));
@@ -1100,6 +1143,7 @@ int dg_merkle_prepare(dg_engine* e, const dg_merkle* t, uint32_t levels, dg_merk
   if (out->cap < n || !out->pos || !out->hash)
     return fail(DG_E_CAPACITY, "dg_merkle_prepare: %llu entries needed", (unsigned long long)n);
   TRY(set_device(e));
+  TRY(settle(e));
   TRY(ensure_state(e, 2));
   HIP_TRY(hipMemsetAsync(e->state, 0, sizeof(u64), e->stream));  // the root's position, 0
   HIP_TRY(launch_cont_expand(merkle_of(t), 0, L, e->state, 1, out->pos, out->hash, e->stream));
@@ -1120,6 +1164,7 @@ int dg_merkle_continue(dg_engine* e, const dg_merkle* t, const dg_store* s, cons
   if (n_total) *n_total = 0;
   *status = 0;
   TRY(set_device(e));
+  TRY(settle(e));
   const u32 depth = t->depth;
   const MerkleT m = merkle_of(t);
   if (in->level == depth + 1) {  // leaf form: the keys
@@ -1187,6 +1232,7 @@ int dg_merkle_truncate(dg_engine* e, const dg_merkle* t, dg_merkle_cont* cont, u
   // the first pair of bucket[max]; pairs carry keys, buckets carry bucket numbers, so
   // count the pairs of the dropped buckets by their bucket's first pair
   TRY(set_device(e));
+  TRY(settle(e));
   TRY(ensure_state(e, 2));
   HIP_TRY(launch_pairs_before_bucket(merkle_of(t), cont->pos, cont->n, cont->bucket + max,
                                      e->d_counts, e->stream));
@@ -1215,6 +1261,7 @@ int dg_remap_values(dg_engine* e, dg_store* s, const uint64_t* old_ids, const ui
   if (n_ids && (!old_ids || !new_ids)) return fail(DG_E_INVAL, "dg_remap_values: null id table");
   if (s->n == 0) return DG_OK;
   TRY(set_device(e));
+  TRY(settle(e));
   HIP_TRY(hipMemsetAsync(e->ticket + 3, 0, sizeof(u32), e->stream));
   HIP_TRY(launch_remap_values(s->val, s->n, old_ids, new_ids, n_ids, e->ticket + 3, e->stream));
   TRY(sync_words(e));
@@ -1233,6 +1280,7 @@ int dg_sort_store(dg_engine* e, const dg_store* in, dg_store* out) {
     return fail(DG_E_INVAL, "dg_sort_store: null output column");
   if (in->n >= (1ull << 32)) return fail(DG_E_INVAL, "dg_sort_store: more than 2^32 - 1 rows");
   TRY(set_device(e));
+  TRY(settle(e));
   TRY(ensure_tmp(e, sort_tmp_bytes(in->n)));
   TRY(ensure_stage(e, 8 * 256 * sizeof(u32)));
   HIP_TRY(launch_sort_store(rows_of(in), rows_out_of(out), e->tmp, (u32*)e->h_stage, e->d_counts,
@@ -1250,6 +1298,7 @@ int dg_sort_context(dg_engine* e, const dg_context* in, dg_context* out) {
   if (in->n && (!out->node || !out->cnt)) return fail(DG_E_INVAL, "dg_sort_context: null output");
   if (in->n >= (1ull << 32)) return fail(DG_E_INVAL, "dg_sort_context: more than 2^32 - 1 entries");
   TRY(set_device(e));
+  TRY(settle(e));
   TRY(ensure_tmp(e, sort_tmp_bytes(in->n)));
   TRY(ensure_stage(e, 8 * 256 * sizeof(u32)));
   HIP_TRY(launch_sort_context(in->kind, in->node, in->cnt, in->n, out->node, out->cnt, e->tmp,

@@ -1,35 +1,55 @@
-"""Exact interning of BEAM-style terms to the fixed-width ids of a dot row.
+"""Exact interning of BEAM-style terms to the fixed-width ids of a dot row, and the
+term hashes that make Merkle trees independent of the interning tables.
 
 * key  -> u64 key id.  Integer keys 0 <= k < 2^64 map through splitmix64 (a
-  bijection on u64, so distinct keys never collide); other terms through a 64-bit
-  BLAKE2b of a canonical encoding, with an exact collision check.  Because key ids
-  are hashes, sorting a store by key id also groups it into Merkle buckets and
-  key-hash shards (bucket / shard = the id's high bits).
+  bijection on u64, so distinct keys never collide); other terms to `term_hash(t, 0)`,
+  the xxh64 of the term's canonical encoding (below), with an exact collision check.
+  The NIF computes the same ids (c_src/marshal.c, dgm_key), so key ids agree between
+  BEAM nodes.  Because key ids are hashes, sorting a store by key id also groups it
+  into Merkle buckets and key-hash shards (bucket / shard = the id's high bits).
 * value -> u64 value id, ORDER-PRESERVING over every term (the
-  read tie-break is "smallest {value, ts} in Erlang term order",
-  aw_lww_map.ex:211-216).  A Universe keeps its values sorted by `terms.order_key`
-  and gives each a rank-like id with gaps: a new value takes an id between its two
-  neighbours' (the midpoint; a fixed stride when it lands past either end).  When a
-  gap is used up, every value is RELABELLED with evenly spaced ids -- a monotone map
-  old id -> new id, so stores stay sorted -- and `remap_hook` rewrites the `val`
-  column of every device store the Universe tracks (dg_remap_values).  Ids are
-  therefore per-Universe; the synthetic workloads use the closed-form integer
-  encoding `encode_int_value` (ints only, as bench/basic_operations.exs:4).
+  read tie-break is "smallest {value, ts} in map-key order", aw_lww_map.ex:211-216):
+    - integers v in [CANON_LO, 2^62) have the CLOSED-FORM id v + 2^62, in
+      [2^58, 2^63): the same on every node, no table entry (`encode_int_value`);
+    - the other terms get gapped ids from the Universe's sorted table: integers below
+      CANON_LO in (0, 2^58), everything above the canonical integers (larger integers,
+      floats, atoms, tuples, ...) in [2^63, 2^64).  In map-key order every integer
+      precedes every float and numbers precede every other class, so both regions keep
+      term order.  A new value takes the midpoint of its neighbours' ids in its region
+      (a 2^32 stride past either end); when a gap is used up, the region's values are
+      RELABELLED with evenly spaced ids -- a monotone map old id -> new id, so stores
+      stay sorted -- and `remap_hook` rewrites the `val` column of every device store
+      the Universe tracks (dg_remap_values).
 * node -> u32 node id, DENSE: the Universe's n-th distinct node term gets id n.
   The reference draws node ids from :rand.uniform(1_000_000_000)
   (causal_crdt.ex:65); dense ids keep every context inside the kernels' table
   lookups (the join's LDS VV table, the one-pass fold's KNT-entry tables).  Node
   order carries no meaning in the reference (dots are set members), so any
   bijection is exact.
+
+Canonical encoding (`canon`, the input of every term hash; c_src/marshal.c builds the
+same bytes from a NIF term walk): a tag byte and a little-endian u32 length, then
+
+    a <utf8 text>             atom           f <f64 LE>           float (no length)
+    i <sign byte><magnitude>  integer: sign 0/1, magnitude little-endian, minimal bytes
+    t <n> <elements>          tuple          l <n> <elements>     proper list
+    m <n> <key, value>...     map, pairs in map-key order         b <bytes>  binary
+
+Term hashes of the Merkle rows (dg_term_hashes, include/deltagpu.h): a node's is
+`term_hash(node, NODE_SEED)`, a non-canonical value's `term_hash(value, VAL_SEED)`;
+a canonical integer value hashes as its closed-form id.  Trees built with them are
+bit-identical for equal states whatever order two Universes interned the terms in, so
+two replicas on different BEAM nodes compare their trees directly (causal_crdt.ex:
+390-394, causal_crdt_test.exs:68-78).
 """
 from __future__ import annotations
 
 import bisect
-import hashlib
 import struct
 import weakref
 
 import numpy as np
+import xxhash
 
 from .terms import order_key
 
@@ -56,50 +76,84 @@ def splitmix64_np(x: np.ndarray) -> np.ndarray:
     return x
 
 
+CANON_LO = -(1 << 62) + (1 << 58)   # the canonical integer values: [CANON_LO, CANON_HI)
+CANON_HI = 1 << 62
+CANON_ID_LO = 1 << 58               # their ids: [CANON_ID_LO, CANON_ID_HI)
+CANON_ID_HI = 1 << 63
+NODE_SEED = 0x6E6F6465              # term_hash seeds of node and value terms
+VAL_SEED = 0x76616C75
+
+
 def encode_int_value(v) -> np.ndarray:
-    """Order-preserving value ids for integers in [-2^62, 2^62) (vectorised)."""
+    """Closed-form (canonical) value ids of integers in [CANON_LO, 2^62) (vectorised):
+    v + 2^62.  The Universe hands out exactly these ids for such integers."""
     v = np.asarray(v, dtype=np.int64)
+    if v.size and (int(v.min()) < CANON_LO or int(v.max()) >= CANON_HI):
+        raise ValueError("encode_int_value: integer outside the canonical range")
     return (v.astype(np.uint64) + np.uint64(1 << 62))
 
 
-class _Enc:
-    @staticmethod
-    def enc(t, out: bytearray):
-        # local import keeps the product free of the oracle package
-        from .terms import Atom, EList, EMap
-        if isinstance(t, bool) or t is None or isinstance(t, Atom):
-            s = ("nil" if t is None else "true" if t is True else "false" if t is False
-                 else str.__str__(t)).encode()
-            out += b"a" + struct.pack("<I", len(s)) + s
-        elif isinstance(t, int):
-            s = str(t).encode()
-            out += b"i" + struct.pack("<I", len(s)) + s
-        elif isinstance(t, float):
-            out += b"f" + struct.pack("<d", t)
-        elif isinstance(t, EList):
-            out += b"l" + struct.pack("<I", len(t))
-            for x in t:
-                _Enc.enc(x, out)
-        elif isinstance(t, EMap):
-            out += b"m" + struct.pack("<I", len(t))
-            for k, v in t:
-                _Enc.enc(k, out)
-                _Enc.enc(v, out)
-        elif isinstance(t, tuple):
-            out += b"t" + struct.pack("<I", len(t))
-            for x in t:
-                _Enc.enc(x, out)
-        elif isinstance(t, (str, bytes)):
-            b = t.encode() if isinstance(t, str) else t
-            out += b"b" + struct.pack("<I", len(b)) + b
-        else:
-            raise TypeError(f"cannot intern a {type(t).__name__}")
+def is_canonical_int(t) -> bool:
+    return isinstance(t, int) and not isinstance(t, bool) and CANON_LO <= t < CANON_HI
 
 
-def term_hash64(t) -> int:
-    buf = bytearray()
-    _Enc.enc(t, buf)
-    return int.from_bytes(hashlib.blake2b(bytes(buf), digest_size=8).digest(), "little")
+def canon(t, out: bytearray | None = None) -> bytearray:
+    """The canonical encoding of a term (module docstring)."""
+    from .terms import Atom, EList, EMap
+    if out is None:
+        out = bytearray()
+    if isinstance(t, bool) or t is None or isinstance(t, Atom):
+        b = ("nil" if t is None else "true" if t is True else "false" if t is False
+             else str.__str__(t)).encode()
+        out += b"a" + struct.pack("<I", len(b)) + b
+    elif isinstance(t, int):
+        m = abs(t)
+        mag = m.to_bytes((m.bit_length() + 7) // 8, "little")
+        out += b"i" + struct.pack("<I", len(mag) + 1) + (b"\x01" if t < 0 else b"\x00") + mag
+    elif isinstance(t, float):
+        out += b"f" + struct.pack("<d", t)
+    elif isinstance(t, EList):
+        out += b"l" + struct.pack("<I", len(t))
+        for x in t:
+            canon(x, out)
+    elif isinstance(t, EMap):  # EMap pairs are in map-key order (oracle.erlterm.emap)
+        out += b"m" + struct.pack("<I", len(t))
+        for k, v in t:
+            canon(k, out)
+            canon(v, out)
+    elif isinstance(t, tuple):
+        out += b"t" + struct.pack("<I", len(t))
+        for x in t:
+            canon(x, out)
+    elif isinstance(t, (str, bytes)):
+        b = t.encode() if isinstance(t, str) else t
+        out += b"b" + struct.pack("<I", len(b)) + b
+    else:
+        raise TypeError(f"cannot intern a {type(t).__name__}")
+    return out
+
+
+def term_hash(t, seed: int = 0) -> int:
+    """xxh64 of the canonical encoding (c_src/marshal.c dgm_hash_bytes)."""
+    return xxhash.xxh64_intdigest(bytes(canon(t)), seed)
+
+
+def key_id(t) -> int:
+    """The key id of a key term (dgm_key in c_src/marshal.c computes the same)."""
+    if isinstance(t, int) and not isinstance(t, bool) and 0 <= t <= MASK64:
+        return splitmix64(t)
+    return term_hash(t, 0)
+
+
+def node_hash(t) -> int:
+    return term_hash(t, NODE_SEED)
+
+
+def value_hash(t) -> int:
+    """A value's term in the Merkle row hash: its closed-form id when canonical."""
+    if is_canonical_int(t):
+        return int(t) + (1 << 62)
+    return term_hash(t, VAL_SEED)
 
 
 def _hkey(t):
@@ -108,8 +162,10 @@ def _hkey(t):
     return order_key(t)
 
 
-ID_SPAN = 1 << 64
-VAL_STRIDE = 1 << 32     # id step of a value that lands past either end of the order
+VAL_STRIDE = 1 << 32     # id step of a value that lands past either end of its region
+# the two table regions (exclusive bounds): below and above the canonical integers
+LOW = (0, CANON_ID_LO)
+HIGH = (CANON_ID_HI - 1, 1 << 64)
 
 
 class Universe:
@@ -117,18 +173,22 @@ class Universe:
 
     `remap_hook(old_ids, new_ids)` (uint64 arrays, both ascending) is called after a
     value relabel; the host mirror sets it to rewrite the tracked device stores.
-    `val_epoch` counts relabels (a Merkle tree built before one is stale)."""
+    `val_epoch` counts relabels; `terms_version` changes whenever the term-hash tables
+    (`term_tables`) do: a new node, a new table value or a relabel."""
 
     def __init__(self):
         self._key_id = {}
         self._key_term = {}
-        self._val_id = {}
+        self._val_id = {}        # table values only (canonical integers are closed-form)
         self._val_term = {}
-        self._val_keys = []      # order keys of the values, ascending
+        self._val_keys = []      # order keys of the table values, ascending
         self._val_ids = []       # their ids, ascending (same order)
+        self._val_hash = []      # their term hashes (same order)
         self._node_id = {}
         self._node_term = []     # dense: node id -> term
+        self._node_hash = []
         self.val_epoch = 0
+        self.terms_version = 0
         self.remap_hook = None
         self._tracked = weakref.WeakSet()
 
@@ -138,10 +198,7 @@ class Universe:
         kid = self._key_id.get(hk)
         if kid is not None:
             return kid
-        if isinstance(t, int) and not isinstance(t, bool) and 0 <= t <= MASK64:
-            kid = splitmix64(t)
-        else:
-            kid = term_hash64(t)
+        kid = key_id(t)
         other = self._key_term.get(kid)
         if other is not None and _hkey(other) != hk:
             raise RuntimeError(f"64-bit key id collision between {other!r} and {t!r}")
@@ -154,58 +211,73 @@ class Universe:
 
     # -- values
     def value(self, t) -> int:
+        if is_canonical_int(t):
+            return int(t) + (1 << 62)
         hk = _hkey(t)
         vid = self._val_id.get(hk)
         if vid is not None:
             return vid
+        low = isinstance(t, int) and not isinstance(t, bool) and t < CANON_LO
         p = bisect.bisect_left(self._val_keys, hk)
-        vid = self._gap_id(p)
+        vid = self._gap_id(p, low)
         if vid is None:
-            self.relabel(extra=1)
-            vid = self._gap_id(p)
+            self.relabel(extra=1, low=low)
+            vid = self._gap_id(p, low)
         self._val_keys.insert(p, hk)
         self._val_ids.insert(p, vid)
+        self._val_hash.insert(p, term_hash(t, VAL_SEED))
         self._val_id[hk] = vid
         self._val_term[vid] = t
+        self.terms_version += 1
         return vid
 
-    def _gap_id(self, p: int):
-        """An id strictly between the neighbours of insertion point p, or None."""
-        n = len(self._val_ids)
-        if n == 0:
-            return 1 << 63
-        lo = self._val_ids[p - 1] if p > 0 else 0          # ids are >= 1
-        hi = self._val_ids[p] if p < n else ID_SPAN
-        if hi - lo < 2:
+    def _gap_id(self, p: int, low: bool):
+        """An id strictly between the neighbours of insertion point p inside the value's
+        region (LOW or HIGH, exclusive bounds), or None when the gap is used up."""
+        rlo, rhi = LOW if low else HIGH
+        ids = self._val_ids
+        lo = ids[p - 1] if p > 0 and rlo < ids[p - 1] < rhi else None
+        hi = ids[p] if p < len(ids) and rlo < ids[p] < rhi else None
+        a, b = (lo if lo is not None else rlo), (hi if hi is not None else rhi)
+        if b - a < 2:
             return None
-        if p == n:
-            return lo + min(VAL_STRIDE, (hi - lo) // 2)
-        if p == 0:
-            return hi - min(VAL_STRIDE, (hi - lo) // 2)
-        return lo + (hi - lo) // 2
+        if lo is None and hi is None:
+            return a + (b - a) // 2
+        if hi is None:
+            return a + min(VAL_STRIDE, (b - a) // 2)
+        if lo is None:
+            return b - min(VAL_STRIDE, (b - a) // 2)
+        return a + (b - a) // 2
 
-    def relabel(self, extra: int = 0):
-        """Re-space every value id evenly over the id range (order kept), then let
+    def relabel(self, extra: int = 0, low: bool = False):
+        """Re-space the value ids of one region evenly over it (order kept), then let
         `remap_hook` rewrite the device stores.  Returns (old_ids, new_ids)."""
-        n = len(self._val_ids)
-        step = ID_SPAN // (n + extra + 1)
-        old = np.array(self._val_ids, dtype=np.uint64)
-        new_ids = [(i + 1) * step for i in range(n)]
+        rlo, rhi = LOW if low else HIGH
+        idx = [i for i, v in enumerate(self._val_ids) if rlo < v < rhi]
+        n = len(idx)
+        step = (rhi - rlo) // (n + extra + 1)
+        old = np.array([self._val_ids[i] for i in idx], dtype=np.uint64)
+        new_ids = [rlo + (j + 1) * step for j in range(n)]
         new = np.array(new_ids, dtype=np.uint64)
-        terms = [self._val_term[v] for v in self._val_ids]
-        self._val_ids = new_ids
-        self._val_term = {v: t for v, t in zip(new_ids, terms)}
-        self._val_id = {k: v for k, v in zip(self._val_keys, new_ids)}
+        for j, i in enumerate(idx):
+            t = self._val_term.pop(self._val_ids[i])
+            self._val_ids[i] = new_ids[j]
+            self._val_term[new_ids[j]] = t
+            self._val_id[self._val_keys[i]] = new_ids[j]
         self.val_epoch += 1
+        self.terms_version += 1
         if self.remap_hook is not None and n:
             self.remap_hook(old, new)
         return old, new
 
     def value_term(self, vid: int):
+        if CANON_ID_LO <= vid < CANON_ID_HI:
+            return vid - (1 << 62)
         return self._val_term[vid]
 
     def value_ids(self):
-        """(ids, terms) of every value, ascending (= Erlang term order)."""
+        """(ids, terms) of the table values (every value but the canonical integers),
+        ascending (= term order)."""
         return list(self._val_ids), [self._val_term[v] for v in self._val_ids]
 
     def track(self, store):
@@ -228,6 +300,8 @@ class Universe:
             raise RuntimeError("node id space exhausted")
         self._node_id[hk] = nid
         self._node_term.append(t)
+        self._node_hash.append(node_hash(t))
+        self.terms_version += 1
         return nid
 
     def node_term(self, nid: int):
@@ -242,6 +316,15 @@ class Universe:
         uniq, inv = np.unique(raw, return_inverse=True)
         ids = np.array([self.node(int(u)) for u in uniq], np.uint32)
         return ids[inv].reshape(raw.shape)
+
+    # -- term hashes (dg_term_hashes)
+    def term_tables(self):
+        """(node_hash[n_nodes], val_ids[n], val_hash[n]) as uint64 arrays: the node hash
+        of every dense node id, and the ascending table value ids with their hashes (the
+        canonical integers need no entry)."""
+        return (np.array(self._node_hash, dtype=np.uint64),
+                np.array(self._val_ids, dtype=np.uint64),
+                np.array(self._val_hash, dtype=np.uint64))
 
 
 DEFAULT = Universe()

@@ -9,7 +9,7 @@ itself instead of the term tree.
 
 File layout (little-endian), one self-describing file per replica:
 
-    b"DGSNAP01" | u64 header length | header (msgpack) | column bytes ...
+    b"DGSNAP02" | u64 header length | header (msgpack) | column bytes ...
 
 The header holds node_id, sequence_number, the row and context counts, the context
 kind, the byte length and xxh64 of each column, and the exact interning tables of
@@ -32,7 +32,10 @@ import xxhash
 from . import interning
 from .terms import Atom, EList, EMap
 
-MAGIC = b"DGSNAP01"
+MAGIC = b"DGSNAP02"
+# DGSNAP01 (round 2): [id, term] node pairs and one value-id region; its ids do not carry
+# over to the closed-form integer ids of DGSNAP02, so such a file is refused, not guessed.
+_OLD_MAGICS = (b"DGSNAP01",)
 _COLS = (("key", np.uint64), ("val", np.uint64), ("ts", np.int64), ("node", np.uint32),
          ("cnt", np.uint64))
 
@@ -91,7 +94,7 @@ def _universe_tables(U: interning.Universe):
     ids, terms = U.value_ids()
     return {
         "keys": [[str(k), _pack(t)] for k, t in U._key_term.items()],
-        "vals": [[str(v), _pack(t)] for v, t in zip(ids, terms)],   # ascending ids
+        "vals": [[str(v), _pack(t)] for v, t in zip(ids, terms)],   # table values, ascending ids
         "nodes": [_pack(t) for t in U._node_term],                  # dense ids 0..n-1
         "val_epoch": U.val_epoch,
     }
@@ -110,6 +113,7 @@ def _universe_from(tables) -> interning.Universe:
         U._val_id[hk] = int(v)
         U._val_keys.append(hk)
         U._val_ids.append(int(v))
+        U._val_hash.append(interning.term_hash(term, interning.VAL_SEED))
     for t in tables["nodes"]:
         U.node(_unpack(t))
     U.val_epoch = int(tables.get("val_epoch", 0))
@@ -154,7 +158,11 @@ def read_arrays(path):
     if not os.path.exists(path):
         return None
     with open(path, "rb") as f:
-        if f.read(8) != MAGIC:
+        magic = f.read(8)
+        if magic in _OLD_MAGICS:
+            raise ValueError(f"{path}: a {magic.decode()} snapshot (an older layout whose value "
+                             f"ids {MAGIC.decode()} does not read); re-create it")
+        if magic != MAGIC:
             raise ValueError(f"{path}: not a deltagpu snapshot")
         (hl,) = struct.unpack("<Q", f.read(8))
         header = msgpack.unpackb(f.read(hl), raw=False, strict_map_key=False)

@@ -6,6 +6,8 @@ Used by the host mirror (interning) and shared with the test oracle.
 """
 from __future__ import annotations
 
+import math
+
 
 class Atom(str):
     """An Erlang atom (``:foo``)."""
@@ -62,8 +64,10 @@ def order_key(t):
     flatmap of <= 32 keys iterates in, which decides AWLWWMap.read/1's tie-break,
     reference lib/delta_crdt/aw_lww_map.ex:211-216):
 
-    * numbers compare by value (Python compares int and float exactly); on a value tie
-      an integer sorts before the float (`1` before `1.0`, the map-key order);
+    * numbers in MAP-KEY order (the order a flatmap's `{value, ts}` keys are sorted in):
+      every integer before every float ("in maps key order integers types are considered
+      less than floats types", OTP's term-order rules), then by value; -0.0 before 0.0
+      (distinct keys since OTP 27; the relative order of the two zeros is unpinned);
     * atoms by their text; tuples by size, then element-wise; maps by size, then keys
       in key order, then values; lists element-wise with a proper prefix first;
       bitstrings byte-wise (a ``str`` is its UTF-8 binary).
@@ -71,7 +75,9 @@ def order_key(t):
     Two keys are equal exactly when the terms are `=:=`."""
     c = term_class(t)
     if c == C_NUMBER:
-        return (c, t, 0 if isinstance(t, int) else 1)
+        if isinstance(t, int):
+            return (c, 0, t)
+        return (c, 1, t, 0 if math.copysign(1.0, t) < 0 else 1)
     if c == C_ATOM:
         return (c, atom_text(t))
     if c == C_TUPLE:

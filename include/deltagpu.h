@@ -119,6 +119,11 @@ typedef struct dg_engine dg_engine;
  * stays busy, as on a BEAM dirty scheduler), then waits on the stream instead. */
 int dg_abi_version(void);
 const char* dg_last_error(void);
+/* The sha256 prefix (16 hex digits) of the sources this library was built from
+ * (csrc/*.hip, csrc/*.h and this header, delta_crdt_ex_amd/build.py): the host side
+ * refuses a library whose digest differs from its tree's, so a stale build is never the
+ * one tested or measured. */
+const char* dg_build_digest(void);
 /* `hip_stream` NULL: the engine creates its own stream; otherwise it launches on the
  * given hipStream_t (e.g. torch.cuda.current_stream().cuda_stream) and never
  * destroys it. */
@@ -129,8 +134,10 @@ void* dg_engine_stream(dg_engine* e);
  * cannot become resident (other kernels hold the CUs) it aborts, and dg_engine_sync then
  * replays the asynchronous calls made since the last sync (joins on the two-pass
  * kernels), so their outputs are correct when it returns DG_OK.  Their arguments (and
- * dg_merkle objects) must stay valid until then; call dg_engine_sync before a
- * synchronous call that consumes an asynchronous call's output. */
+ * dg_merkle objects) must stay valid until then.  Every synchronous call first settles
+ * the asynchronous calls made before it, as dg_engine_sync does (an error of theirs is
+ * then that call's error).  At most 4096 asynchronous calls are logged: the next one
+ * settles the log first. */
 int dg_engine_sync(dg_engine* e);
 
 /* ---- device buffers (for callers without a device runtime of their own: the NIF) -- */

@@ -12,9 +12,13 @@ give a value on the device must preserve that order.
 Erlang term order (number < atom < reference < fun < port < pid < tuple < map <
 nil < list < bitstring) restricted to the Python stand-ins used here:
 
-* ``int`` / ``float``           -> number (compared numerically; int before float on a tie,
-                                   which is how map keys 1 and 1.0 are ordered — unpinned,
-                                   the reference tests never mix them)
+* ``int`` / ``float``           -> number, in MAP-KEY order: every integer before every
+                                   float, then by value (OTP: "in maps key order integers
+                                   types are considered less than floats types"; a flatmap
+                                   sorts its {value, ts} keys so, recursively inside
+                                   tuples, lists and maps).  -0.0 sorts before 0.0 (distinct
+                                   keys since OTP 27; their relative order is unpinned).
+                                   The reference's tests never mix ints and floats.
 * ``Atom`` / ``None`` / ``bool``  -> atom (``None`` is ``:nil``; ``True``/``False`` are
                                    ``:true``/``:false``); atoms compare by their text
 * ``tuple``                     -> tuple: by size, then element-wise
@@ -25,6 +29,7 @@ nil < list < bitstring) restricted to the Python stand-ins used here:
 from __future__ import annotations
 
 import functools
+import math
 
 
 from delta_crdt_ex_amd.terms import Atom, EList, EMap  # noqa: E402,F401  (shared stand-ins)
@@ -76,8 +81,8 @@ def tg(t):
                    else str.__str__(t)))
     if isinstance(t, int):
         return Tg(("i", t))
-    if isinstance(t, float):
-        return Tg(("f", t))
+    if isinstance(t, float):  # the sign keeps -0.0 and 0.0 apart (`=:=` since OTP 27)
+        return Tg(("f", t, math.copysign(1.0, t) < 0))
     if isinstance(t, EList):
         return Tg(("l", tuple(tg(x) for x in t)))
     if isinstance(t, EMap):
@@ -93,7 +98,7 @@ def untg(t):
     """Inverse of `tg` (binaries come back as bytes, atoms as Atom)."""
     if not isinstance(t, Tg):
         return t
-    tag, p = t
+    tag, p = t[0], t[1]
     if tag == "a":
         return Atom(p)
     if tag in ("i", "f", "b"):
@@ -113,14 +118,17 @@ def compare(a, b) -> int:
     if ca != cb:
         return -1 if ca < cb else 1
     if ca == 0:
+        ia, ib = isinstance(a, int), isinstance(b, int)
+        if ia != ib:  # map-key order: integers before floats, whatever their values
+            return -1 if ia else 1
         if a < b:
             return -1
         if a > b:
             return 1
-        ia, ib = isinstance(a, int), isinstance(b, int)
-        if ia == ib:
-            return 0
-        return -1 if ia else 1
+        if not ia and a == 0.0:  # -0.0 before 0.0
+            sa, sb = math.copysign(1.0, a), math.copysign(1.0, b)
+            return (sa > sb) - (sa < sb)
+        return 0
     if ca == 1:
         x, y = _atom_text(a), _atom_text(b)
         return (x > y) - (x < y)

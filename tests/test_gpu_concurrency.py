@@ -133,3 +133,36 @@ def test_overscheduled_grid_aborts_and_replays(monkeypatch):
         for x, y in zip(o.to_numpy(), want):
             assert np.array_equal(x, y)
     eng.close()
+
+
+def test_aborted_async_join_then_synchronous_call(monkeypatch):
+    """an asynchronous join whose grid aborts, followed by a synchronous
+    call of another kind (dg_read_lww) before dg_engine_sync.  The synchronous call settles
+    the pending join first (replays it on the two-pass kernels), so the join's output is
+    right and the read sees it; dg_engine_sync afterwards is clean."""
+    import torch
+
+    from delta_crdt_ex_amd.store import Context, Engine, Store
+    dev = "cuda:0"
+    sa, ca, sb, cb = _inputs(3_000_000, 73, dev)
+    ref = Engine(0)
+    want_out, _ = ref.join2(sa, ca, sb, cb)
+    want = tuple(c.copy() for c in want_out.to_numpy())
+    wk, wv = ref.read_lww(want_out)
+    wk, wv = wk.cpu().numpy(), wv.cpu().numpy()
+    ref.close()
+    monkeypatch.setenv("DG_JOIN_WORKERS", "1024")  # over-sized grid: the async join aborts
+    eng = Engine(0)
+    o = Store.empty(sa.n + sb.n, dev)
+    oc = Context.empty(0, ca.n + cb.n, dev)
+    d = torch.zeros(8, dtype=torch.int64, device=dev)
+    eng.prepare_join2(sa, ca, sb, cb, o, oc, d)()
+    o.n = sa.n + sb.n  # unknown until settled: read the count after the read call
+    k0, v0 = eng.read_lww(sb)  # a synchronous call of another kind: settles the join first
+    o.n = int(d[0].item())
+    for x, y in zip(o.to_numpy(), want):
+        assert np.array_equal(x, y)
+    k, v = eng.read_lww(o)
+    assert np.array_equal(k.cpu().numpy(), wk) and np.array_equal(v.cpu().numpy(), wv)
+    eng.sync()
+    eng.close()

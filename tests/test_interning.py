@@ -59,15 +59,33 @@ def test_mixed_classes_rank_as_erlang():
     # 1 and 1.0 (and True) are distinct values, also nested
     assert len({U.value(1), U.value(1.0), U.value(True)}) == 3
     assert U.value((1,)) != U.value((1.0,))
-    assert U.value(1) < U.value(1.0) < U.value(2)  # int before float on a numeric tie
+    # map-key order (OTP: "in maps key order integers types are considered less than
+    # floats types"): every integer before every float, whatever the values
+    assert U.value(1) < U.value(2) < U.value(1 << 70) < U.value(-5.0) < U.value(1.0) < U.value(1.5)
+    assert U.value((2, 0)) < U.value((1.5, 0))
+
+
+def test_canonical_integer_ids_are_universe_independent():
+    from delta_crdt_ex_amd.interning import CANON_LO, CANON_HI, encode_int_value
+    U, V = Universe(), Universe()
+    for t in ("x", 2.5, Atom("a")):
+        V.value(t)  # V's table differs from U's
+    for v in (0, 1, -1, 7, CANON_LO, CANON_HI - 1, (1 << 62) - 5):
+        assert U.value(v) == V.value(v) == int(encode_int_value([v])[0]) == v + (1 << 62)
+        assert U.value_term(U.value(v)) == v
+    # outside the canonical range: table ids, in order around the canonical block
+    big_neg, big_pos = CANON_LO - 1, CANON_HI
+    assert U.value(big_neg) < U.value(CANON_LO) < U.value(CANON_HI - 1) < U.value(big_pos)
+    assert U.value(big_neg) < (1 << 58) and U.value(big_pos) >= (1 << 63)
+    assert U.value_ids()[1] == [big_neg, big_pos]
 
 
 def test_relabel_is_monotone_and_calls_the_hook():
     U = Universe()
     seen = []
     U.remap_hook = lambda old, new: seen.append((old.copy(), new.copy()))
-    U.value(1)
-    U.value(2)
+    U.value(1.0)
+    U.value(2.0)
     lo, hi = 1.0, 2.0
     for _ in range(80):  # every insert lands in the same, halving gap
         lo = (lo + hi) / 2

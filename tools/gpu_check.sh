@@ -1,10 +1,7 @@
-# One GPU call: the GPU test suite, the default bench line, then (optional) the kfold
-# A/B across experiment builds (tools/ab_kfold.sh).  Usage: bash tools/gpu_check.sh [ab]
+# One GPU call: the GPU test suite, then the default bench line.  Usage: bash tools/gpu_check.sh
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests/ -q -x --timeout 120 --timeout-method thread -m gpu > gpurun_out/pytest_gpu.log 2>&1 || { echo TESTS_FAILED; tail -30 gpurun_out/pytest_gpu.log; exit 1; }
 tail -1 gpurun_out/pytest_gpu.log
 timeout -k 10 400 python -u bench.py > gpurun_out/bench.log 2>&1 || { echo BENCH_FAILED; tail -20 gpurun_out/bench.log; exit 1; }
 tail -1 gpurun_out/bench.log
-if [ "$1" = ab ]; then bash tools/ab_kfold.sh; fi
-if [ "$1" = ab ]; then LIBS="libdeltagpu.so $(cd delta_crdt_ex_amd && ls libdeltagpu_*JOIN*.so 2>/dev/null | tr '\n' ' ')" bash tools/ab_quick.sh; fi
