@@ -120,7 +120,7 @@ typedef struct dg_engine dg_engine;
 int dg_abi_version(void);
 const char* dg_last_error(void);
 /* The sha256 prefix (16 hex digits) of the sources this library was built from
- * (csrc/*.hip, csrc/*.h and this header, delta_crdt_ex_amd/build.py): the host side
+ * (the .hip and .h files of csrc/ and this header, delta_crdt_ex_amd/build.py): the host side
  * refuses a library whose digest differs from its tree's, so a stale build is never the
  * one tested or measured. */
 const char* dg_build_digest(void);
