@@ -156,7 +156,7 @@ def config4_round(eng, torch, dev, rank=0, world=1, keys_per_rank=12_500_000, st
         t2 = time.perf_counter()
         out, octx, changed = eng.join2_changes(sa, ca, delta, cb, keys=keys)
         t3 = time.perf_counter()
-        tt = MerkleTree(ta.depth, ta.nodes.clone(), ta.n_keys, ta.shard_bits, ta.shard, sa)
+        tt = ta.clone()
         t4 = time.perf_counter()
         eng.merkle_update(tt, out, changed)
         torch.cuda.synchronize()

@@ -42,46 +42,103 @@
 #include "marshal.h"
 
 /* ------------------------------------------------------------ term operations */
-/* Exact Erlang term order: enif_compare, with the map-key tie-break between numbers
- * that compare equal (1 before 1.0), also inside tuples and lists (the order of a
- * flatmap's keys, which decides read/1's tie-break). */
+/* Exact map-key order (the order a flatmap's {value, ts} keys are sorted in, which decides
+ * read/1's tie-break, aw_lww_map.ex:211-216): the standard term order
+ * number < atom < reference < fun < port < pid < tuple < map < list < bitstring, except
+ * that numbers compare as map keys do -- every integer before every float ("in maps key
+ * order integers types are considered less than floats types") -- recursively inside
+ * tuples, lists and maps.  Leaves of one class other than numbers compare by enif_compare
+ * (exact and arithmetic order agree there). */
+static int term_rank(ErlNifEnv* env, ERL_NIF_TERM t) {
+  switch (enif_term_type(env, t)) {
+    case ERL_NIF_TERM_TYPE_INTEGER:
+    case ERL_NIF_TERM_TYPE_FLOAT: return 0;
+    case ERL_NIF_TERM_TYPE_ATOM: return 1;
+    case ERL_NIF_TERM_TYPE_REFERENCE: return 2;
+    case ERL_NIF_TERM_TYPE_FUN: return 3;
+    case ERL_NIF_TERM_TYPE_PORT: return 4;
+    case ERL_NIF_TERM_TYPE_PID: return 5;
+    case ERL_NIF_TERM_TYPE_TUPLE: return 6;
+    case ERL_NIF_TERM_TYPE_MAP: return 7;
+    case ERL_NIF_TERM_TYPE_LIST: return 8;
+    default: return 9; /* bitstring */
+  }
+}
+
+static int sgn(int x) { return x < 0 ? -1 : x > 0; }
+static int exact_cmp(ErlNifEnv* env, ERL_NIF_TERM a, ERL_NIF_TERM b);
+
+/* a map's keys in map-key order (insertion sort: value maps are small) */
+static ERL_NIF_TERM* sorted_keys(ErlNifEnv* env, ERL_NIF_TERM m, size_t n) {
+  ERL_NIF_TERM* k = (ERL_NIF_TERM*)enif_alloc((n ? n : 1) * sizeof *k);
+  ErlNifMapIterator it;
+  ERL_NIF_TERM key, val;
+  size_t i = 0;
+  enif_map_iterator_create(env, m, &it, ERL_NIF_MAP_ITERATOR_FIRST);
+  for (; i < n && enif_map_iterator_get_pair(env, &it, &key, &val); enif_map_iterator_next(env, &it)) {
+    size_t j = i++;
+    for (; j > 0 && exact_cmp(env, k[j - 1], key) > 0; j--) k[j] = k[j - 1];
+    k[j] = key;
+  }
+  enif_map_iterator_destroy(env, &it);
+  return k;
+}
+
 static int exact_cmp(ErlNifEnv* env, ERL_NIF_TERM a, ERL_NIF_TERM b) {
-  const int c = enif_compare(a, b);
-  if (c != 0 || enif_is_identical(a, b)) return c;
-  ErlNifSInt64 ia;
-  double fa;
-  if (enif_is_number(env, a)) {
-    const int a_int = enif_get_int64(env, a, &ia) || !enif_get_double(env, a, &fa);
-    ErlNifSInt64 ib;
-    const int b_int = enif_get_int64(env, b, &ib);
-    return a_int == b_int ? 0 : (a_int ? -1 : 1);
-  }
-  int na, nb;
-  const ERL_NIF_TERM *ea, *eb;
-  if (enif_get_tuple(env, a, &na, &ea) && enif_get_tuple(env, b, &nb, &eb)) {
-    for (int i = 0; i < na; i++) {
-      const int x = exact_cmp(env, ea[i], eb[i]);
-      if (x) return x;
+  const int ra = term_rank(env, a), rb = term_rank(env, b);
+  if (ra != rb) return ra < rb ? -1 : 1;
+  switch (ra) {
+    case 0: {
+      const int ia = enif_term_type(env, a) == ERL_NIF_TERM_TYPE_INTEGER;
+      const int ib = enif_term_type(env, b) == ERL_NIF_TERM_TYPE_INTEGER;
+      if (ia != ib) return ia ? -1 : 1;
+      return sgn(enif_compare(a, b));
     }
-    return 0;
+    case 6: {
+      int na, nb;
+      const ERL_NIF_TERM *ea, *eb;
+      enif_get_tuple(env, a, &na, &ea);
+      enif_get_tuple(env, b, &nb, &eb);
+      if (na != nb) return na < nb ? -1 : 1;
+      for (int i = 0; i < na; i++) {
+        const int x = exact_cmp(env, ea[i], eb[i]);
+        if (x) return x;
+      }
+      return 0;
+    }
+    case 7: { /* size, then keys in key order, then values in key order */
+      size_t na, nb;
+      enif_get_map_size(env, a, &na);
+      enif_get_map_size(env, b, &nb);
+      if (na != nb) return na < nb ? -1 : 1;
+      ERL_NIF_TERM *ka = sorted_keys(env, a, na), *kb = sorted_keys(env, b, nb);
+      int x = 0;
+      for (size_t i = 0; !x && i < na; i++) x = exact_cmp(env, ka[i], kb[i]);
+      for (size_t i = 0; !x && i < na; i++) {
+        ERL_NIF_TERM va, vb;
+        enif_get_map_value(env, a, ka[i], &va);
+        enif_get_map_value(env, b, kb[i], &vb);
+        x = exact_cmp(env, va, vb);
+      }
+      enif_free(ka);
+      enif_free(kb);
+      return x;
+    }
+    case 8: /* element-wise, [] first; an improper tail compares as a term */
+      for (;;) {
+        const int ea = enif_is_empty_list(env, a), eb = enif_is_empty_list(env, b);
+        if (ea || eb) return (ea && eb) ? 0 : (ea ? -1 : 1);
+        ERL_NIF_TERM ha, ta, hb, tb;
+        if (!enif_get_list_cell(env, a, &ha, &ta) || !enif_get_list_cell(env, b, &hb, &tb))
+          return exact_cmp(env, a, b); /* a tail that is not a list: of another class */
+        const int x = exact_cmp(env, ha, hb);
+        if (x) return x;
+        a = ta;
+        b = tb;
+      }
+    default:
+      return sgn(enif_compare(a, b));
   }
-  ERL_NIF_TERM ha, ta, hb, tb;
-  if (enif_get_list_cell(env, a, &ha, &ta) && enif_get_list_cell(env, b, &hb, &tb)) {
-    const int x = exact_cmp(env, ha, hb);
-    return x ? x : exact_cmp(env, ta, tb);
-  }
-  /* maps (and anything else) equal under enif_compare but not identical: the external
-   * term format decides -- deterministic, not the BEAM's own order ("parity unpinned",
-   * INTEGRATION.md §3) */
-  ErlNifBinary ba, bb;
-  enif_term_to_binary(env, a, &ba);
-  enif_term_to_binary(env, b, &bb);
-  const size_t n = ba.size < bb.size ? ba.size : bb.size;
-  int x = memcmp(ba.data, bb.data, n);
-  if (!x) x = ba.size < bb.size ? -1 : ba.size > bb.size;
-  enif_release_binary(&ba);
-  enif_release_binary(&bb);
-  return x < 0 ? -1 : x > 0;
 }
 
 typedef struct {
@@ -97,25 +154,84 @@ static int op_cmp(const void* a, const void* b, void* ud) {
   return exact_cmp(u->env, ((const boxed*)a)->t, ((const boxed*)b)->t);
 }
 
-/* key ids: integer keys 0 <= k < 2^64 as splitmix64(k) (the synthetic workloads' and the
- * Python mirror's id), anything else xxh64 of its external term format */
-static uint64_t splitmix64(uint64_t x) {
-  x += 0x9E3779B97F4A7C15ull;
-  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-  return x ^ (x >> 31);
+/* The canonical encoding of a term (marshal.h; the Python mirror's interning.canon):
+ * key ids, and the node / value term hashes of Merkle rows, are xxh64 of it, so they are
+ * the same on every node.  Big integers come from the external term format's digits. */
+static int encode_term(ErlNifEnv* env, ERL_NIF_TERM t, dgm_buf* b) {
+  switch (enif_term_type(env, t)) {
+    case ERL_NIF_TERM_TYPE_INTEGER: {
+      ErlNifSInt64 i;
+      ErlNifUInt64 u;
+      if (enif_get_int64(env, t, &i)) return dgm_enc_i64(b, i);
+      if (enif_get_uint64(env, t, &u)) return dgm_enc_u64(b, u);
+      ErlNifBinary e; /* SMALL_BIG_EXT 110: n, sign, n digits LE; LARGE_BIG_EXT 111: u32 n */
+      if (!enif_term_to_binary(env, t, &e)) return DG_E_NOMEM;
+      int rc = DG_E_INVAL;
+      if (e.size > 3 && e.data[1] == 110)
+        rc = dgm_enc_int(b, e.data[3], e.data + 4, e.data[2]);
+      else if (e.size > 6 && e.data[1] == 111)
+        rc = dgm_enc_int(b, e.data[6], e.data + 7,
+                         ((size_t)e.data[2] << 24) | ((size_t)e.data[3] << 16) | ((size_t)e.data[4] << 8) | e.data[5]);
+      enif_release_binary(&e);
+      return rc;
+    }
+    case ERL_NIF_TERM_TYPE_FLOAT: {
+      double d;
+      enif_get_double(env, t, &d);
+      return dgm_enc_float(b, d);
+    }
+    case ERL_NIF_TERM_TYPE_ATOM: {
+      unsigned len;
+      if (!enif_get_atom_length(env, t, &len, ERL_NIF_UTF8)) return DG_E_INVAL;
+      char* s = (char*)enif_alloc(len + 1);
+      enif_get_atom(env, t, s, len + 1, ERL_NIF_UTF8);
+      const int rc = dgm_enc_atom(b, s, len);
+      enif_free(s);
+      return rc;
+    }
+    case ERL_NIF_TERM_TYPE_BITSTRING: {
+      ErlNifBinary bin;
+      if (!enif_inspect_binary(env, t, &bin)) return DG_E_INVAL; /* not byte-aligned */
+      return dgm_enc_binary(b, bin.data, bin.size);
+    }
+    case ERL_NIF_TERM_TYPE_TUPLE: {
+      int n;
+      const ERL_NIF_TERM* e;
+      enif_get_tuple(env, t, &n, &e);
+      int rc = dgm_enc_tuple(b, (uint32_t)n);
+      for (int i = 0; !rc && i < n; i++) rc = encode_term(env, e[i], b);
+      return rc;
+    }
+    case ERL_NIF_TERM_TYPE_LIST: {
+      unsigned n;
+      if (!enif_get_list_length(env, t, &n)) return DG_E_INVAL; /* improper: unsupported */
+      int rc = dgm_enc_list(b, n);
+      ERL_NIF_TERM h;
+      while (!rc && enif_get_list_cell(env, t, &h, &t)) rc = encode_term(env, h, b);
+      return rc;
+    }
+    case ERL_NIF_TERM_TYPE_MAP: {
+      size_t n;
+      enif_get_map_size(env, t, &n);
+      ERL_NIF_TERM* k = sorted_keys(env, t, n);
+      int rc = dgm_enc_map(b, (uint32_t)n);
+      for (size_t i = 0; !rc && i < n; i++) {
+        ERL_NIF_TERM v;
+        enif_get_map_value(env, t, k[i], &v);
+        rc = encode_term(env, k[i], b);
+        if (!rc) rc = encode_term(env, v, b);
+      }
+      enif_free(k);
+      return rc;
+    }
+    default: /* pids, ports, references, funs: node-local terms, not interned */
+      return DG_E_INVAL;
+  }
 }
 
-static uint64_t op_hash(const void* p, void* ud) {
+static int op_encode(const void* p, dgm_buf* b, void* ud) {
   term_ud* u = (term_ud*)ud;
-  const ERL_NIF_TERM t = ((const boxed*)p)->t;
-  ErlNifUInt64 k;
-  if (enif_get_uint64(u->env, t, &k)) return splitmix64(k);
-  ErlNifBinary b;
-  enif_term_to_binary(u->env, t, &b);
-  const uint64_t h = dgm_hash_bytes(b.data, b.size, 0);
-  enif_release_binary(&b);
-  return h;
+  return encode_term(u->env, ((const boxed*)p)->t, b);
 }
 
 static void* op_keep(const void* p, void* ud) {
@@ -139,6 +255,10 @@ typedef struct {
   term_ud tu;
   ErlNifMutex* lock;
   state_res* live; /* every state of this engine (a relabel rewrites them all) */
+  /* the universe's term-hash tables on the device, for the trees (dg_term_hashes) */
+  dg_term_hashes th;
+  uint64_t *d_nh, *d_vid, *d_vh;
+  uint64_t th_nodes, th_vals; /* the table sizes uploaded; a relabel clears th_vals */
 } engine_res;
 
 struct state_res {
@@ -157,6 +277,11 @@ static ERL_NIF_TERM A_OK, A_ERROR, A_NIL, A_ALL, A_CONTINUE, A_MAP, A_STRUCT, A_
 static void engine_dtor(ErlNifEnv* env, void* obj) {
   (void)env;
   engine_res* r = (engine_res*)obj;
+  if (r->e) {
+    dg_buffer_free(r->e, r->d_nh);
+    dg_buffer_free(r->e, r->d_vid);
+    dg_buffer_free(r->e, r->d_vh);
+  }
   if (r->u) dgm_universe_free(r->u);
   if (r->tu.env) enif_free_env(r->tu.env);
   if (r->e) dg_engine_destroy(r->e);
@@ -172,7 +297,10 @@ static void state_dtor(ErlNifEnv* env, void* obj) {
   if (s->next) s->next->prev = s->prev;
   dg_store_free(g->e, &s->rows);
   dg_context_free(g->e, &s->ctx);
-  if (s->has_tree) dg_buffer_free(g->e, s->tree.nodes);
+  if (s->has_tree) {
+    dg_buffer_free(g->e, s->tree.nodes);
+    dg_buffer_free(g->e, s->tree.counts);
+  }
   enif_mutex_unlock(g->lock);
   enif_release_resource(g);
 }
@@ -190,7 +318,42 @@ static ERL_NIF_TERM error_term(ErlNifEnv* env, int rc) {
   } while (0)
 
 /* ------------------------------------------------------------ marshal */
-/* After any dgm_value that relabelled: rewrite every live state's val column. */
+/* The universe's term-hash tables on the device (re-uploaded when they grew or a relabel
+ * changed the value ids); every tree points at g->th. */
+static int refresh_terms(engine_res* g) {
+  const uint64_t *nh, *vid, *vh;
+  uint32_t nn;
+  uint64_t nv;
+  dgm_node_hashes(g->u, &nh, &nn);
+  dgm_value_hashes(g->u, &vid, &vh, &nv);
+  int rc = DG_OK;
+  if (nn != g->th_nodes) {
+    dg_buffer_free(g->e, g->d_nh);
+    g->d_nh = NULL;
+    if (!(rc = dg_buffer_alloc(g->e, (nn ? nn : 1) * 8, (void**)&g->d_nh)))
+      rc = dg_copy_to_device(g->e, g->d_nh, nh, (uint64_t)nn * 8);
+    g->th_nodes = rc ? 0 : nn;
+  }
+  if (!rc && nv != g->th_vals) {
+    dg_buffer_free(g->e, g->d_vid);
+    dg_buffer_free(g->e, g->d_vh);
+    g->d_vid = g->d_vh = NULL;
+    if (!(rc = dg_buffer_alloc(g->e, (nv ? nv : 1) * 8, (void**)&g->d_vid)) &&
+        !(rc = dg_buffer_alloc(g->e, (nv ? nv : 1) * 8, (void**)&g->d_vh)) &&
+        !(rc = dg_copy_to_device(g->e, g->d_vid, vid, nv * 8)))
+      rc = dg_copy_to_device(g->e, g->d_vh, vh, nv * 8);
+    g->th_vals = rc ? UINT64_MAX : nv;
+  }
+  g->th.node_hash = g->d_nh;
+  g->th.n_nodes = g->th_nodes;
+  g->th.val_id = g->d_vid;
+  g->th.val_hash = g->d_vh;
+  g->th.n_vals = g->th_vals == UINT64_MAX ? 0 : g->th_vals;
+  return rc;
+}
+
+/* After any dgm_value that relabelled: rewrite every live state's val column.  Trees hash
+ * terms, so they stay valid; the value table is re-uploaded with the new ids. */
 static int remap_live(engine_res* g) {
   const uint64_t *old_ids, *new_ids;
   uint64_t n;
@@ -200,12 +363,11 @@ static int remap_live(engine_res* g) {
   if (!rc) rc = dg_buffer_alloc(g->e, n * 8, &dnew);
   if (!rc) rc = dg_copy_to_device(g->e, dold, old_ids, n * 8);
   if (!rc) rc = dg_copy_to_device(g->e, dnew, new_ids, n * 8);
-  for (state_res* s = g->live; !rc && s; s = s->next) {
+  for (state_res* s = g->live; !rc && s; s = s->next)
     rc = dg_remap_values(g->e, &s->rows, (const uint64_t*)dold, (const uint64_t*)dnew, n);
-    if (!rc && s->has_tree) rc = dg_merkle_build(g->e, &s->rows, &s->tree);  /* hashes use ids */
-  }
   dg_buffer_free(g->e, dold);
   dg_buffer_free(g->e, dnew);
+  g->th_vals = UINT64_MAX - 1; /* stale: the next refresh_terms re-uploads the value table */
   return rc;
 }
 
@@ -414,13 +576,26 @@ static int u_key(void* ud, uint64_t key, uint64_t n) {
   u->open_key = 1;
   return 0;
 }
+/* the term of a value id: a canonical integer from its closed form, else the table's */
+static int value_term(ErlNifEnv* env, engine_res* g, uint64_t id, ERL_NIF_TERM* out) {
+  int64_t v;
+  if (dgm_value_is_canonical(id, &v)) {
+    *out = enif_make_int64(env, v);
+    return DG_OK;
+  }
+  const boxed* b = (const boxed*)dgm_value_term(g->u, id);
+  if (!b) return DG_E_INVAL;
+  *out = enif_make_copy(env, b->t);
+  return DG_OK;
+}
+
 static int u_entry(void* ud, uint64_t val, int64_t ts, uint64_t n) {
   (void)n;
   unm* u = (unm*)ud;
   close_entry(u);
-  const boxed* b = (const boxed*)dgm_value_term(u->g->u, val);
-  if (!b) return DG_E_INVAL;
-  u->vt = enif_make_tuple2(u->env, enif_make_copy(u->env, b->t), enif_make_int64(u->env, ts));
+  ERL_NIF_TERM vt;
+  if (value_term(u->env, u->g, val, &vt)) return DG_E_INVAL;
+  u->vt = enif_make_tuple2(u->env, vt, enif_make_int64(u->env, ts));
   u->dots = enif_make_new_map(u->env);
   u->open_entry = 1;
   return 0;
@@ -483,7 +658,7 @@ static ERL_NIF_TERM engine_open(ErlNifEnv* env, int argc, const ERL_NIF_TERM arg
   memset(g, 0, sizeof *g);
   g->lock = enif_mutex_create("deltagpu_engine");
   g->tu.env = enif_alloc_env();
-  dgm_term_ops ops = {op_cmp, op_hash, op_keep, op_drop, &g->tu};
+  dgm_term_ops ops = {op_cmp, op_encode, NULL, op_keep, op_drop, &g->tu};
   g->u = dgm_universe_new(&ops);
   const int rc = dg_engine_create(dev, NULL, &g->e);
   ERL_NIF_TERM r = rc ? error_term(env, rc) : enif_make_tuple2(env, A_OK, enif_make_resource(env, g));
@@ -548,7 +723,10 @@ static ERL_NIF_TERM join_delta(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
   TRY(dg_buffer_alloc(g->e, (n_keys ? n_keys : 1) * 8, (void**)&changed));
   TRY(dg_join2_changes(g->e, &s->rows, &s->ctx, &drows, &dctx, d_keys, n_keys, &out, &octx, changed,
                        n_keys, &n_changed));
-  if (s->has_tree) TRY(dg_merkle_update(g->e, &s->tree, &s->rows, &out, changed, n_changed));
+  if (s->has_tree) {
+    TRY(refresh_terms(g));
+    TRY(dg_merkle_update(g->e, &s->tree, &s->rows, &out, changed, n_changed));
+  }
   /* the changed keys' new value maps (dg_take_keys), and the keys that vanished */
   TRY(dg_store_alloc(g->e, out.n, &taken));
   TRY(dg_take_keys(g->e, &out, changed, n_changed, &taken));
@@ -609,8 +787,9 @@ static ERL_NIF_TERM read_nif(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]
   TRY(dg_copy_to_host(g->e, hv, dv, n_out * 8));
   for (uint64_t i = 0; i < n_out; i++) {
     const boxed* k = (const boxed*)dgm_key_term(g->u, hk[i]);
-    const boxed* v = (const boxed*)dgm_value_term(g->u, hv[i]);
-    enif_make_map_put(env, m, enif_make_copy(env, k->t), enif_make_copy(env, v->t), &m);
+    ERL_NIF_TERM v;
+    TRY(value_term(env, g, hv[i], &v));
+    enif_make_map_put(env, m, enif_make_copy(env, k->t), v, &m);
   }
 out:
   r = rc ? error_term(env, rc) : m;
@@ -656,11 +835,17 @@ static ERL_NIF_TERM merkle_build_nif(ErlNifEnv* env, int argc, const ERL_NIF_TER
   engine_res* g = s->eng;
   enif_mutex_lock(g->lock);
   int rc = DG_OK;
-  if (s->has_tree) dg_buffer_free(g->e, s->tree.nodes);
+  if (s->has_tree) {
+    dg_buffer_free(g->e, s->tree.nodes);
+    dg_buffer_free(g->e, s->tree.counts);
+  }
   memset(&s->tree, 0, sizeof s->tree);
   s->has_tree = 0;
   s->tree.depth = depth;
+  TRY(refresh_terms(g));
+  s->tree.terms = &g->th; /* rows hashed through their terms: comparable across nodes */
   TRY(dg_buffer_alloc(g->e, ((2ull << depth) - 1) * 8, (void**)&s->tree.nodes));
+  TRY(dg_buffer_alloc(g->e, ((1ull << depth) > 8 ? (1ull << depth) : 8) * 2, (void**)&s->tree.counts));
   s->has_tree = 1;
   TRY(dg_merkle_build(g->e, &s->rows, &s->tree));
 out:;
@@ -750,6 +935,7 @@ static ERL_NIF_TERM merkle_continue_nif(ErlNifEnv* env, int argc, const ERL_NIF_
   memcpy(&level, in.data, 4);
   memcpy(&n, in.data + 4, 8);
   memcpy(&nb, in.data + 12, 8);
+  TRY(refresh_terms(g));
   TRY(cont_alloc(g, n, nb, &ci));
   ci.level = level;
   ci.n = n;

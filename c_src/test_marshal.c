@@ -12,8 +12,8 @@
  *      smallest {value, ts} in term order) by TERM comparison;
  *   3. (with a GPU) a relabel rewrites a device store with dg_remap_values.
  *
- * Test terms stand in for BEAM terms: integers, floats, atoms and binaries with the
- * Erlang order number < atom < binary (int before float on a numeric tie).
+ * Test terms stand in for BEAM terms: integers, floats, atoms and binaries in map-key
+ * order: integers < floats < atoms < binaries.
  * Exit status 0 = pass.  Without a device part 1 runs and the rest prints SKIP, unless
  * DG_REQUIRE_GPU=1.
  */
@@ -62,34 +62,23 @@ static int tcmp(const void* pa, const void* pb, void* ud) {
   (void)ud;
   const tterm *a = (const tterm*)pa, *b = (const tterm*)pb;
   if (cls(a) != cls(b)) return cls(a) < cls(b) ? -1 : 1;
-  if (cls(a) == 0) {
-    const double x = a->kind == T_INT ? (double)a->i : a->f;
-    const double y = b->kind == T_INT ? (double)b->i : b->f;
-    if (x != y) return x < y ? -1 : 1;
-    if (a->kind != b->kind) return a->kind == T_INT ? -1 : 1; /* 1 before 1.0 */
-    return 0;
+  if (cls(a) == 0) { /* map-key order: every integer before every float */
+    if (a->kind != b->kind) return a->kind == T_INT ? -1 : 1;
+    if (a->kind == T_INT) return a->i < b->i ? -1 : a->i > b->i;
+    return a->f < b->f ? -1 : a->f > b->f;
   }
   return strcmp(a->s, b->s) < 0 ? -1 : strcmp(a->s, b->s) > 0 ? 1 : 0;
 }
 
-static uint64_t thash(const void* p, void* ud) {
+static int tenc(const void* p, dgm_buf* b, void* ud) {
   (void)ud;
   const tterm* t = (const tterm*)p;
-  unsigned char buf[32];
-  size_t n = 0;
-  buf[n++] = (unsigned char)t->kind;
-  if (t->kind == T_INT) {
-    memcpy(buf + n, &t->i, 8);
-    n += 8;
-  } else if (t->kind == T_FLOAT) {
-    memcpy(buf + n, &t->f, 8);
-    n += 8;
-  } else {
-    size_t l = strlen(t->s);
-    memcpy(buf + n, t->s, l);
-    n += l;
+  switch (t->kind) {
+    case T_INT: return dgm_enc_i64(b, t->i);
+    case T_FLOAT: return dgm_enc_float(b, t->f);
+    case T_ATOM: return dgm_enc_atom(b, t->s, strlen(t->s));
+    default: return dgm_enc_binary(b, t->s, strlen(t->s));
   }
-  return dgm_hash_bytes(buf, n, 0);
 }
 
 static void* tkeep(const void* t, void* ud) {
@@ -117,6 +106,18 @@ static tterm tf(double f) {
   t.f = f;
   return t;
 }
+/* the term of a value id: a canonical integer from its closed form, else the table's */
+static const tterm* value_term(const dgm_universe* u, uint64_t id, tterm* scratch) {
+  int64_t v;
+  if (dgm_value_is_canonical(id, &v)) {
+    memset(scratch, 0, sizeof *scratch);
+    scratch->kind = T_INT;
+    scratch->i = v;
+    return scratch;
+  }
+  return (const tterm*)dgm_value_term(u, id);
+}
+
 static tterm ts_(int kind, const char* s) {
   tterm t;
   memset(&t, 0, sizeof t);
@@ -147,7 +148,8 @@ static tterm random_value(void) {
 static dgm_term_ops ops(void) {
   dgm_term_ops o;
   o.cmp = tcmp;
-  o.hash = thash;
+  o.encode = tenc;
+  o.hash = NULL;
   o.keep = tkeep;
   o.drop = tdrop;
   o.ud = NULL;
@@ -200,7 +202,8 @@ static void test_universe(void) {
   for (int i = 0; i < N; i++) {
     uint64_t id;
     CHECK(dgm_value(u, &vals[i], &id, &rl) == DG_OK && !rl);
-    const tterm* back = (const tterm*)dgm_value_term(u, id);
+    tterm sc;
+    const tterm* back = value_term(u, id, &sc);
     CHECK(back && tcmp(back, &vals[i], NULL) == 0);
   }
   for (int j = 0; j < 200000; j++) {
@@ -221,10 +224,29 @@ static void test_universe(void) {
   CHECK(tcmp(dgm_node_term(u, 1), &nb, NULL) == 0);
   dgm_universe_free(u);
 
+  /* canonical integers have closed-form ids; others land in the two regions around them */
+  {
+    dgm_term_ops o2 = ops();
+    dgm_universe* w = dgm_universe_new(&o2);
+    tterm a = ti(7), bneg = ti(INT64_MIN), bpos = ti(INT64_C(1) << 62), f = tf(-1e300);
+    uint64_t ia, in, ip, ifl;
+    int64_t back;
+    CHECK(dgm_value(w, &a, &ia, &rl) == DG_OK && ia == 7 + (1ull << 62));
+    CHECK(dgm_value_is_canonical(ia, &back) && back == 7 && !dgm_value_term(w, ia));
+    CHECK(dgm_value(w, &bneg, &in, &rl) == DG_OK && in > 0 && in < (1ull << 58));
+    CHECK(dgm_value(w, &bpos, &ip, &rl) == DG_OK && ip >= (1ull << 63));
+    CHECK(dgm_value(w, &f, &ifl, &rl) == DG_OK && ifl > ip);  /* every float after every int */
+    const uint64_t *vids, *vh;
+    uint64_t nv;
+    dgm_value_hashes(w, &vids, &vh, &nv);
+    CHECK(nv == 3 && vids[0] == in && vids[1] == ip && vids[2] == ifl);
+    dgm_universe_free(w);
+  }
   /* a key-id collision is refused: every key hashes alike here */
   dgm_term_ops c = ops();
-  c.hash = NULL;
+  c.encode = NULL;
   CHECK(dgm_universe_new(&c) == NULL);
+  c.encode = tenc;
   c.hash = const_hash;
   dgm_universe* v = dgm_universe_new(&c);
   uint64_t k1, k2;
@@ -366,6 +388,7 @@ typedef struct {
   int have;
   int64_t best_ts;
   uint64_t best_val;
+  tterm s1, s2;
 } readst;
 
 static void flush(readst* r) {
@@ -387,7 +410,7 @@ static int w_entry(void* ud, uint64_t val, int64_t ts, uint64_t n_dots) {
   readst* r = (readst*)ud;
   if (!r->have || ts > r->best_ts ||
       (ts == r->best_ts &&
-       tcmp(dgm_value_term(r->u, val), dgm_value_term(r->u, r->best_val), NULL) < 0)) {
+       tcmp(value_term(r->u, val, &r->s1), value_term(r->u, r->best_val, &r->s2), NULL) < 0)) {
     r->best_ts = ts;
     r->best_val = val;
     r->have = 1;

@@ -76,6 +76,16 @@ class dg_context(C.Structure):
     ]
 
 
+class dg_term_hashes(C.Structure):
+    _fields_ = [
+        ("node_hash", VP),
+        ("n_nodes", C.c_uint64),
+        ("val_id", VP),
+        ("val_hash", VP),
+        ("n_vals", C.c_uint64),
+    ]
+
+
 class dg_merkle(C.Structure):
     _fields_ = [
         ("depth", C.c_uint32),
@@ -83,6 +93,8 @@ class dg_merkle(C.Structure):
         ("shard", C.c_uint64),
         ("nodes", VP),
         ("n_keys", C.c_uint64),
+        ("counts", VP),
+        ("terms", C.POINTER(dg_term_hashes)),
     ]
 
 

@@ -24,7 +24,7 @@ import torch
 
 from . import interning
 from ._abi import DG_CTX_DOTS, DG_CTX_VV, FunctionClauseError
-from .store import Context, Engine, Store, u64
+from .store import Context, Engine, MerkleTree, Store, TermHashes, u64
 
 _ENGINE: Engine | None = None
 _LIVE: "weakref.WeakSet[AWLWWMap]" = weakref.WeakSet()  # host row caches to drop on a relabel
@@ -239,6 +239,36 @@ def read(state: AWLWWMap, keys=None) -> dict:
     return {U.key_term(int(k)): U.value_term(int(v)) for k, v in zip(u64(ok), u64(ov))}
 
 
+def merkle_map(state: AWLWWMap, depth: int | None = None, shard_bits: int = 0,
+               shard: int = 0) -> MerkleTree:
+    """The state's MerkleMap (MerkleMap.new + put of every key's raw value map,
+    causal_crdt.ex:21,390-394) on the device.  Rows are hashed through their TERMS
+    (the Universe's term hashes, interning.py), so the tree compares bit for bit with a
+    replica's built through another Universe -- a neighbour on another BEAM node
+    (causal_crdt_test.exs:68-78).  depth: ~3 keys per bucket by default."""
+    if depth is None:
+        n = max(int(np.unique(u64(state.rows.key[: state.rows.n])).size) if state.rows.n else 1, 2)
+        depth = max(1, min(28, int(np.ceil(np.log2(n / 3))) if n > 3 else 1))
+    return engine().merkle_build(state.rows, depth, shard_bits=shard_bits, shard=shard,
+                                 terms=TermHashes.of(state.universe, _dev()))
+
+
+def merkle_diff(a: AWLWWMap, ta: MerkleTree, b: AWLWWMap, tb: MerkleTree, cap: int | None = None):
+    """The keys (terms, ascending by key id) whose raw value maps differ between two
+    replicas, from their trees (continue_partial_diff run to the keys, causal_crdt.ex:96,
+    104-105; Enum.take(keys, max_sync_size) with `cap`).  Key ids are term hashes, so the
+    replicas' Universes may differ."""
+    keys = engine().merkle_diff(ta, tb, cap=cap)
+    out = []
+    for k in u64(keys):
+        k = int(k)
+        try:
+            out.append(a.universe.key_term(k))
+        except KeyError:
+            out.append(b.universe.key_term(k))
+    return out
+
+
 def mutate_batch(ops, node_id, state: AWLWWMap):
     """Many add/4 and remove/3 calls by one node as ONE delta on the GPU
     (dg_mutate_batch): ops = [("add", key, value[, ts]) or ("remove",
@@ -277,4 +307,4 @@ def mutate_batch(ops, node_id, state: AWLWWMap):
 
 
 __all__ = ["AWLWWMap", "new", "compress_dots", "add", "remove", "clear", "join", "join_all", "read",
-           "mutate_batch", "from_terms", "DG_CTX_VV", "DG_CTX_DOTS"]
+           "mutate_batch", "from_terms", "merkle_map", "merkle_diff", "DG_CTX_VV", "DG_CTX_DOTS"]

@@ -1008,11 +1008,23 @@ MerkleT merkle_of(const dg_merkle* t) {
   m.sb = t->shard_bits;
   m.shard = t->shard;
   m.nodes = t->nodes;
+  m.counts = t->counts;
+  m.th = TermH{};
+  if (t->terms) {
+    m.th.nh = t->terms->node_hash;
+    m.th.nn = t->terms->node_hash ? t->terms->n_nodes : 0;
+    m.th.vid = t->terms->val_id;
+    m.th.vh = t->terms->val_hash;
+    m.th.nv = (t->terms->val_id && t->terms->val_hash) ? t->terms->n_vals : 0;
+    m.th.on = 1;
+  }
   return m;
 }
 
 int check_merkle(const dg_merkle* t, const char* what) {
   if (!t || !t->nodes) return fail(DG_E_INVAL, "%s: null tree", what);
+  if (!t->counts || ((uintptr_t)t->counts & 15))
+    return fail(DG_E_INVAL, "%s: the tree's counts must be a 16-byte aligned device array", what);
   if (t->depth < 1 || t->depth > 28) return fail(DG_E_INVAL, "%s: depth %u not in 1..28", what, t->depth);
   if (t->shard_bits > 16 || t->depth + t->shard_bits > 44)
     return fail(DG_E_INVAL, "%s: shard_bits %u (depth %u)", what, t->shard_bits, t->depth);
@@ -1028,10 +1040,12 @@ int same_tree_shape(const dg_merkle* a, const dg_merkle* b, const char* what) {
   return DG_OK;
 }
 
-// The input-error word (ticket[3]) after a synchronizing read; bit 1: key outside shard.
-// (reads the ticket words of the read_counts right before it)
+// The input-error word (ticket[3]) after a synchronizing read; bit 1: key outside shard,
+// bit 2: a bucket over 65535 rows.  (reads the ticket words of the read_counts before it)
 int input_error(dg_engine* e, const char* what) {
   if (e->h_ticket[3] & 2u) return fail(DG_E_INVAL, "%s: a key outside the tree's shard", what);
+  if (e->h_ticket[3] & 4u)
+    return fail(DG_E_CAPACITY, "%s: a bucket holds more than 65535 rows (use a deeper tree)", what);
   return DG_OK;
 }
 

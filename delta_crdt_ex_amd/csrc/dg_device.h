@@ -234,7 +234,6 @@ __device__ __forceinline__ bool keyset_has(const u64* keys, u64 n, u64 k) {
 // 1/2/4/8 scans each row of 16 lanes, row_bcast:15 carries row 0 into row 1 (and row 2
 // into row 3), row_bcast:31 carries rows 0-1 into rows 2-3.  Lanes a step does not write
 // add the `old` operand, 0.
-#ifndef DG_SHFL_SCAN
 __device__ __forceinline__ u32 wave_incl_scan(u32 v) {
   v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
   v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
@@ -244,17 +243,6 @@ __device__ __forceinline__ u32 wave_incl_scan(u32 v) {
   v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
   return v;
 }
-#else
-__device__ __forceinline__ u32 wave_incl_scan(u32 v) {
-  const int lane = threadIdx.x & (WAVE - 1);
-#pragma unroll
-  for (int d = 1; d < WAVE; d <<= 1) {
-    u32 t = __shfl_up(v, d, WAVE);
-    if (lane >= d) v += t;
-  }
-  return v;
-}
-#endif
 
 // Inclusive max-scan of a 32-bit value across the wave (DPP, as wave_incl_scan).
 __device__ __forceinline__ u32 wave_incl_max(u32 v) {

@@ -7,6 +7,7 @@
 // exactly above the keys whose raw value maps differ.
 //
 //   row_hash  = mix(mix(mix(mix(mix(key ^ G) ^ val) ^ ts) ^ node) ^ cnt)
+//               (val / node: the ids, or their term hashes -- dg_term_hashes)
 //   leaf(k)   = Σ row_hash over k's rows                  (mod 2^64, order-free)
 //   bucket(b) = Σ leaf(k) over keys with k >> (64-depth) == b
 //   parent    = mix(left ^ mix(right ^ H))
@@ -31,11 +32,11 @@ DG_HD uint64_t mix64(uint64_t x) {
   return x;
 }
 
-DG_HD uint64_t row_hash(uint64_t key, uint64_t val, int64_t ts, uint32_t node, uint64_t cnt) {
+DG_HD uint64_t row_hash(uint64_t key, uint64_t val, int64_t ts, uint64_t node, uint64_t cnt) {
   uint64_t h = mix64(key ^ 0x9E3779B97F4A7C15ULL);
   h = mix64(h ^ val);
   h = mix64(h ^ (uint64_t)ts);
-  h = mix64(h ^ (uint64_t)node);
+  h = mix64(h ^ node);
   return mix64(h ^ cnt);
 }
 

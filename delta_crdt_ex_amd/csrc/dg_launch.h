@@ -186,10 +186,21 @@ hipError_t launch_remap_values(u64* val, u64 n, const u64* old_ids, const u64* n
                                u32* err, hipStream_t st);
 
 // ---- merkle.hip (see the file header)
+// term hashes of a tree's rows (dg_term_hashes; on = 0: the ids themselves)
+struct TermH {
+  const u64* nh;   // node_hash[node id]
+  u64 nn;
+  const u64* vid;  // ascending non-canonical value ids
+  const u64* vh;   // their hashes
+  u64 nv;
+  u32 on;
+};
 struct MerkleT {
   u32 depth, sb;  // buckets 2^depth; the tree covers keys whose top sb bits == shard
   u64 shard;
   u64* nodes;     // heap, 2^(depth+1) - 1
+  uint16_t* counts;  // rows per bucket, 2^depth
+  TermH th;
 };
 constexpr u32 MERKLE_UPL = 11;  // levels reduced per upsweep workgroup
 inline u64 merkle_chunks(u32 depth) { return 1ull << (depth - (depth < MERKLE_UPL ? depth : MERKLE_UPL)); }
@@ -207,11 +218,13 @@ hipError_t launch_merkle_update(const MerkleT& t, const Rows& olds, const Rows& 
                                 u64 n_keys, u32* dirty, u64* d_keys, u32* ctr, u32* err,
                                 hipStream_t st);
 constexpr int DIFF_BLOCK = 256;
-inline u64 diff_tiles(u32 depth) { return depth >= 8 ? (1ull << (depth - 8)) : 1ull; }
-// tile boundaries in both stores, per-tile counts and offsets, then the differing keys
-// staged per tile (at most one per row of either store)
+constexpr u32 DIFF_SUB = 12;  // levels a diff workgroup descends: subtrees of 4096 buckets
+inline u32 diff_sub(u32 depth) { return depth < DIFF_SUB ? depth : DIFF_SUB; }
+inline u64 diff_tiles(u32 depth) { return 1ull << (depth - diff_sub(depth)); }
+// subtree boundaries in both stores, per-subtree counts, then the differing keys staged
+// per subtree (at most one per row of either store), then the group sums
 inline u64 diff_scratch_words(u32 depth, u64 na, u64 nb) {
-  return 2 * (diff_tiles(depth) + 1) + 2 * diff_tiles(depth) + na + nb + 1 + diff_tiles(depth) / 256 + 1;
+  return 2 * (diff_tiles(depth) + 1) + diff_tiles(depth) + na + nb + 1 + diff_tiles(depth) / 256 + 1;
 }
 // differing keys, ascending; the first min(total, cap) written; *d_count = total.
 hipError_t launch_merkle_diff(const MerkleT& a, const Rows& sa, const MerkleT& b, const Rows& sb,

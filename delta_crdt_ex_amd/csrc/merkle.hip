@@ -17,6 +17,11 @@
 // the shard trees of a 2^sb-way split are exactly the level-sb subtrees of the
 // unsharded tree (dg_merkle_fold_roots recombines them).
 //
+// Row hashes cover term hashes of the value and node when the tree carries them
+// (dg_term_hashes: trees then compare across interning tables and BEAM nodes), the ids
+// otherwise.  The tree also keeps each bucket's row count (u16), maintained by build and
+// update, read by the diff.
+//
 // Kernels:
 //  * build: ONE launch.  A workgroup per chunk of 2^11 buckets streams the chunk's rows
 //    (36 B/row; the row range from two wave lower bounds) into LDS bucket sums, reduces
@@ -25,10 +30,11 @@
 //  * update: one thread per changed key re-hashes the key's rows in the old and the
 //    new store and adds the difference to its bucket (put/delete); the upsweep then
 //    re-reduces only the 2^11-bucket chunks an update touched (update_hashes).
-//  * diff: 256 buckets per workgroup; a workgroup whose level-(depth-8) node matches
-//    is skipped, otherwise each differing bucket merges the two stores' rows of the
-//    bucket key by key.  count / scan / write passes; keys past `cap` are counted,
-//    not written (truncation to max_sync_size).
+//  * diff: a workgroup per subtree of 4096 buckets; a subtree whose root matches is
+//    skipped, otherwise the workgroup descends it level by level through the differing
+//    nodes only (a frontier in LDS), locates each differing bucket's rows from the trees'
+//    per-bucket row counts, hashes just those rows and merges them key by key.  count /
+//    write passes; keys past `cap` are counted, not written (max_sync_size truncation).
 //  * partial diff: node-form continuations (positions + the sender's hashes at one
 //    level) are compared and expanded `levels` levels down; at the bucket level the
 //    reply is a leaf-form continuation (the sender's (key, leaf) pairs of the
@@ -44,7 +50,28 @@ struct MT {
   u32 depth, sb;
   u64 shard;
   u64* nodes;
+  uint16_t* counts;
+  TermH th;
 };
+
+// The value's and the node's terms in a row hash (dg_term_hashes): a canonical integer
+// value id [2^58, 2^63) and ids missing from the tables stand for themselves.
+__device__ __forceinline__ u64 th_val(const TermH& th, u64 v) {
+  if (!th.on || th.nv == 0 || (v >= (1ull << 58) && v < (1ull << 63))) return v;
+  u64 lo = 0, hi = th.nv;
+  while (lo < hi) {
+    const u64 mid = (lo + hi) >> 1;
+    if (th.vid[mid] < v)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return (lo < th.nv && th.vid[lo] == v) ? th.vh[lo] : v;
+}
+
+__device__ __forceinline__ u64 th_node(const TermH& th, u32 n) {
+  return (th.on && (u64)n < th.nn) ? th.nh[n] : (u64)n;
+}
 
 __device__ __forceinline__ u64 bucket_of(const MT& t, u64 key) {
   return (key << t.sb) >> (64 - t.depth);
@@ -74,8 +101,8 @@ __device__ __forceinline__ u64 bucket_start(const MT& t, const u64* keys, u64 n,
   return lower_bound_key(keys, n, base + (b << sh));
 }
 
-__device__ __forceinline__ u64 rh(const Rows& s, u64 i) {
-  return row_hash(s.key[i], s.val[i], s.ts[i], s.node[i], s.cnt[i]);
+__device__ __forceinline__ u64 rh(const Rows& s, u64 i, const TermH& th) {
+  return row_hash(s.key[i], th_val(th, s.val[i]), s.ts[i], th_node(th, s.node[i]), s.cnt[i]);
 }
 
 // ---------------------------------------------------------------- lower bounds
@@ -104,6 +131,9 @@ __device__ __forceinline__ u64 wave_bucket_start(const MT& t, const u64* keys, u
 constexpr int UPB = 512;   // threads per chunk workgroup
 constexpr int UPL = MERKLE_UPL;  // levels reduced per workgroup (2048 nodes in LDS)
 constexpr u32 UPW = 1u << UPL;
+constexpr u32 NHL = 1024;  // node hashes staged in LDS by the build (more: read from global)
+constexpr u32 ERR_SHARD = 2u, ERR_COUNT = 4u;  // input-error bits: key outside the shard,
+                                               // a bucket over 65535 rows
 
 __device__ __forceinline__ void wait_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
@@ -143,6 +173,8 @@ __global__ __launch_bounds__(UPB) void merkle_chunk_kernel(Rows rows, MT t, cons
                                                            u32* ctr, u64* hand, u64* d_keys,
                                                            u32* err) {
   __shared__ u64 s[UPW];
+  __shared__ u32 s_c[BUILD ? UPW : 1];  // rows per bucket
+  __shared__ u64 s_nh[BUILD ? NHL : 1]; // node term hashes
   __shared__ u64 s_rng[2];
   __shared__ u32 s_red[UPB / WAVE];
   __shared__ u32 s_last;
@@ -153,13 +185,15 @@ __global__ __launch_bounds__(UPB) void merkle_chunk_kernel(Rows rows, MT t, cons
   u64* lvl = t.nodes + ((1ull << t.depth) - 1);
   u64 chunk_root = 0, chunk_keys = 0;
   if (BUILD) {
-    for (u32 x = tid; x < width; x += UPB) s[x] = 0;
+    for (u32 x = tid; x < width; x += UPB) {
+      s[x] = 0;
+      s_c[x] = 0;
+    }
+    const bool nh_lds = t.th.on && t.th.nn <= NHL;  // uniform
+    if (nh_lds)
+      for (u32 x = tid; x < (u32)t.th.nn; x += UPB) s_nh[x] = t.th.nh[x];
     if (w < 2) {
-#ifdef MK_INTERP  // timing experiment only: interpolated (inexact) chunk bounds
-      const u64 r = (u64)((double)rows.n * (double)(g + w) / (double)gridDim.x);
-#else
       const u64 r = wave_bucket_start(t, rows.key, rows.n, g0 + (w ? width : 0));
-#endif
       if (lane == 0) s_rng[w] = r;
     }
     __syncthreads();
@@ -178,7 +212,9 @@ __global__ __launch_bounds__(UPB) void merkle_chunk_kernel(Rows rows, MT t, cons
         head[q] = false;
         if (i < hi) {
           key[q] = rows.key[i];
-          h[q] = row_hash(key[q], rows.val[i], rows.ts[i], rows.node[i], rows.cnt[i]);
+          const u32 nd = rows.node[i];
+          const u64 nt = nh_lds ? (nd < (u32)t.th.nn ? s_nh[nd] : (u64)nd) : th_node(t.th, nd);
+          h[q] = row_hash(key[q], th_val(t.th, rows.val[i]), rows.ts[i], nt, rows.cnt[i]);
           head[q] = i == lo || rows.key[i - 1] != key[q];
         }
       }
@@ -188,7 +224,10 @@ __global__ __launch_bounds__(UPB) void merkle_chunk_kernel(Rows rows, MT t, cons
         if (i < hi) {
           if (t.sb && (key[q] >> (64 - t.sb)) != t.shard) bad = true;
           const u64 b = bucket_of(t, key[q]) - g0;
-          if (b < width) atomicAdd((unsigned long long*)&s[b], (unsigned long long)h[q]);
+          if (b < width) {
+            atomicAdd((unsigned long long*)&s[b], (unsigned long long)h[q]);
+            atomicAdd(&s_c[b], 1u);
+          }
           heads += head[q] ? 1u : 0u;
         }
       }
@@ -198,14 +237,19 @@ __global__ __launch_bounds__(UPB) void merkle_chunk_kernel(Rows rows, MT t, cons
 #pragma unroll
     for (int d = WAVE / 2; d >= 1; d >>= 1) c += __shfl_xor(c, d, WAVE);
     if (lane == 0) s_red[w] = c;
-    if (__ballot(bad) && lane == 0) atomicOr(err, 2u);
+    if (__ballot(bad) && lane == 0) atomicOr(err, ERR_SHARD);
     __syncthreads();
     if (tid == 0)
       for (int q = 0; q < UPB / WAVE; q++) chunk_keys += s_red[q];
-    for (u32 x = tid; x < width; x += UPB) lvl[g0 + x] = s[x];
-#ifndef MK_NO_UPSWEEP  // timing experiment only
+    bool over = false;
+    for (u32 x = tid; x < width; x += UPB) {
+      lvl[g0 + x] = s[x];
+      const u32 c = s_c[x];
+      over |= c > 0xFFFFu;
+      t.counts[g0 + x] = (uint16_t)(c > 0xFFFFu ? 0xFFFFu : c);
+    }
+    if (__ballot(over) && lane == 0) atomicOr(err, ERR_COUNT);
     lds_upsweep(t.nodes, t.depth, g0, width, s);
-#endif
     chunk_root = s[0];
   } else if (dirty[g]) {
     for (u32 x = tid; x < width; x += UPB) s[x] = lvl[g0 + x];
@@ -263,12 +307,13 @@ __global__ __launch_bounds__(UPB) void merkle_chunk_kernel(Rows rows, MT t, cons
 constexpr int UB = 256;
 
 
-// Σ row_hash of key x's rows in s (0 if absent); *present = x has rows.
-__device__ __forceinline__ u64 key_leaf(const Rows& s, u64 x, bool* present) {
+// Σ row_hash of key x's rows in s (0 if absent); *rows = their number.
+__device__ __forceinline__ u64 key_leaf(const Rows& s, u64 x, const TermH& th, u32* rows) {
   u64 i = lower_bound_key(s.key, s.n, x);
   u64 h = 0;
-  *present = i < s.n && s.key[i] == x;
-  for (; i < s.n && s.key[i] == x; i++) h += rh(s, i);
+  u32 r = 0;
+  for (; i < s.n && s.key[i] == x; i++, r++) h += rh(s, i, th);
+  *rows = r;
   return h;
 }
 
@@ -277,19 +322,30 @@ __global__ __launch_bounds__(UB) void merkle_update_kernel(MT t, Rows olds, Rows
                                                            u32* err) {
   const u64 i = (u64)blockIdx.x * UB + threadIdx.x;
   int dk = 0;
-  bool bad = false;
+  bool bad = false, over = false;
   if (i < n_keys) {
     const u64 x = keys[i];
-    bool po, pn;
-    const u64 ho = key_leaf(olds, x, &po), hn = key_leaf(news, x, &pn);
-    dk = (int)pn - (int)po;
-    if (ho != hn || po != pn) {
+    u32 ro, rn;
+    const u64 ho = key_leaf(olds, x, t.th, &ro), hn = key_leaf(news, x, t.th, &rn);
+    dk = (int)(rn > 0) - (int)(ro > 0);
+    if (ho != hn || ro != rn) {
       if (t.sb && (x >> (64 - t.sb)) != t.shard) {
         bad = true;
       } else {
         const u64 b = bucket_of(t, x);
         u64* lvl = t.nodes + ((1ull << t.depth) - 1);
         atomicAdd((unsigned long long*)&lvl[b], (unsigned long long)(hn - ho));
+        if (rn != ro) {  // the bucket's row count, in its aligned 32-bit word (counts stay
+                         // in [0, 65535]: no carry or borrow into the neighbour's half)
+          u32* wd = (u32*)t.counts + (b >> 1);
+          const u32 sh = 16u * (u32)(b & 1);
+          if (rn > ro) {
+            const u32 old = atomicAdd(wd, (rn - ro) << sh);
+            over = ((old >> sh) & 0xFFFFu) + (rn - ro) > 0xFFFFu;
+          } else {
+            atomicSub(wd, (ro - rn) << sh);
+          }
+        }
         const u32 L1 = t.depth < (u32)UPL ? t.depth : (u32)UPL;
         dirty[b >> L1] = 1u;
       }
@@ -302,7 +358,8 @@ __global__ __launch_bounds__(UB) void merkle_update_kernel(MT t, Rows olds, Rows
   if ((threadIdx.x & (WAVE - 1)) == 0 && c)
     atomicAdd((unsigned long long*)&d_keys[(blockIdx.x * (UB / WAVE) + threadIdx.x / WAVE) & 7],
               (unsigned long long)(long long)c);
-  if (__ballot(bad) && (threadIdx.x & (WAVE - 1)) == 0) atomicOr(err, 2u);
+  if (__ballot(bad) && (threadIdx.x & (WAVE - 1)) == 0) atomicOr(err, ERR_SHARD);
+  if (__ballot(over) && (threadIdx.x & (WAVE - 1)) == 0) atomicOr(err, ERR_COUNT);
 }
 
 // ---------------------------------------------------------------- key-level merge
@@ -310,8 +367,9 @@ __global__ __launch_bounds__(UB) void merkle_update_kernel(MT t, Rows olds, Rows
 // list of (key, leaf) pairs; emit the keys present on one side only or with different
 // leaves.  WRITE: store them at out[o..) (only below cap); returns the count.
 template <bool B_LEAVES, bool WRITE>
-__device__ u32 merge_bucket(const Rows& A, u64 ia, u64 ie, const Rows& B, const u64* bk,
-                            const u64* bh, u64 jb, u64 je, u64* out, u64 o, u64 cap) {
+__device__ u32 merge_bucket(const Rows& A, const TermH& tha, u64 ia, u64 ie, const Rows& B,
+                            const TermH& thb, const u64* bk, const u64* bh, u64 jb, u64 je,
+                            u64* out, u64 o, u64 cap) {
   u32 c = 0;
   while (ia < ie || jb < je) {
     const u64 ka = ia < ie ? A.key[ia] : ~0ull;
@@ -321,12 +379,12 @@ __device__ u32 merge_bucket(const Rows& A, u64 ia, u64 ie, const Rows& B, const 
     const u64 k = has_a ? ka : kb;
     u64 ha = 0, hb = 0;
     if (has_a)
-      for (; ia < ie && A.key[ia] == k; ia++) ha += rh(A, ia);
+      for (; ia < ie && A.key[ia] == k; ia++) ha += rh(A, ia, tha);
     if (has_b) {
       if (B_LEAVES) {
         hb = bh[jb++];
       } else {
-        for (; jb < je && B.key[jb] == k; jb++) hb += rh(B, jb);
+        for (; jb < je && B.key[jb] == k; jb++) hb += rh(B, jb, thb);
       }
     }
     if (!(has_a && has_b) || ha != hb) {
@@ -338,57 +396,42 @@ __device__ u32 merge_bucket(const Rows& A, u64 ia, u64 ie, const Rows& B, const 
 }
 
 // ---------------------------------------------------------------- full diff
-// Tiles of 256 buckets, one thread per bucket.
-//  1. bounds: one wave per tile boundary finds the boundary's first row in both stores
+// One workgroup per subtree of 2^sub buckets (sub = min(depth, 12)), whose root sits at
+// level Ls = depth - sub.
+//  1. bounds: one wave per subtree boundary finds the boundary's first row in both stores
 //     (a 64-ary wave lower bound: 4 dependent load rounds at 12.5M rows).
-//  2. count: a tile whose level-(depth-8) subtree root matches in both trees is
-//     skipped.  Otherwise the tile's key columns are staged in LDS, each thread finds its
-//     bucket's rows there, the rows of the DIFFERING buckets are listed and hashed by
-//     all threads at once (one round of independent loads instead of a dependent chain
-//     per bucket), and each differing bucket merges its keys' leaves from LDS.  The
-//     tile's differing keys go to scratch at (A start + B start) of the tile, which is
-//     unique and increasing across tiles.
-//  3. scan of the per-tile counts; 4. copy: each tile's keys to their output offset,
-//     the keys past `cap` counted, not written (truncation to max_sync_size).
-// A tile whose rows do not fit the LDS stage (far fewer buckets than keys/3) falls back
-// to per-bucket merges over global memory.
+//  2. count: a subtree whose roots match is skipped.  Otherwise the workgroup descends it
+//     level by level: the frontier (differing nodes of one level, ascending) lives in
+//     LDS, and only the children of differing nodes are loaded and compared -- about
+//     2 x (differing nodes) per level, one round trip each.  The last level's frontier
+//     is the differing buckets.  Each thread owns 16 consecutive buckets: it loads their
+//     row counts in both trees (u16), and a block scan turns them into row ranges.  The
+//     differing buckets' rows are listed and hashed by all threads at once (one round of
+//     independent loads), and each thread merges its differing buckets' keys from LDS.
+//     The subtree's differing keys go to scratch at (A start + B start) of the subtree,
+//     unique and increasing across subtrees.  More rows than the LDS stage holds: each
+//     thread merges its differing buckets over global memory instead.
+//  3. write: each subtree's keys to their output offset, the keys past `cap` counted,
+//     not written (truncation to max_sync_size).
 constexpr int DB = DIFF_BLOCK;
-constexpr u32 DCAP = 1024;  // rows per store staged in LDS
-constexpr u32 LCAP = 512;   // rows of a tile's differing buckets hashed through LDS
+constexpr u32 XSUB = 1u << DIFF_SUB;  // buckets per subtree (at most)
+constexpr u32 OWN = XSUB / DB;        // buckets per thread
+constexpr u32 RCAP = 2048;            // rows of the differing buckets staged in LDS
+static_assert(OWN == 16, "a thread owns 16 buckets: two 16-byte count loads per tree");
 
 struct DiffArgs {
   MT ta, tb;
   Rows sa, sb;
   u64* out;
   u64 cap;
-  u64* bnd;   // ntiles + 1 boundaries x 2 stores: first row of each tile in A, then in B
-  u64* cnt;   // differing keys per tile
-  u64* off;   // their output offset
+  u64* bnd;   // ntiles + 1 boundaries x 2 stores: first row of each subtree in A, then in B
+  u64* cnt;   // differing keys per subtree
   u64* keys;  // scratch: nA + nB keys
-  u64* bsum;  // per DB tiles: the sum of their counts (zeroed before the count kernel)
+  u64* bsum;  // per DB subtrees: the sum of their counts (zeroed before the count kernel)
   u64 ntiles;
+  u32 sub;
   u64* d_count;
 };
-
-__device__ __forceinline__ u64 diff_bpt(u32 depth) { return depth >= 8 ? 256ull : (1ull << depth); }
-
-// lower bound of x in keys[0, n) (LDS or global; n small)
-__device__ __forceinline__ u32 lb_small(const u64* k, u32 n, u64 x) {
-  u32 lo = 0, hi = n;
-  while (lo < hi) {
-    const u32 mid = (lo + hi) >> 1;
-    if (k[mid] < x)
-      lo = mid + 1;
-    else
-      hi = mid;
-  }
-  return lo;
-}
-
-__device__ __forceinline__ u64 bucket_first_key(const MT& t, u64 b) {
-  const u64 base = t.sb ? (t.shard << (64 - t.sb)) : 0ull;
-  return base + (b << (64 - t.sb - t.depth));
-}
 
 __global__ __launch_bounds__(256) void merkle_diff_bounds_kernel(DiffArgs p) {
   const u64 i = ((u64)blockIdx.x * 256 + threadIdx.x) / WAVE;  // one wave per boundary
@@ -397,153 +440,190 @@ __global__ __launch_bounds__(256) void merkle_diff_bounds_kernel(DiffArgs p) {
   const bool B = i >= nbnd;
   const u64 t = B ? i - nbnd : i;
   const Rows& r = B ? p.sb : p.sa;
-  const u64 x = wave_bucket_start(p.ta, r.key, r.n, t * diff_bpt(p.ta.depth));
+  const u64 x = wave_bucket_start(p.ta, r.key, r.n, t << p.sub);
   if ((threadIdx.x & (WAVE - 1)) == 0) p.bnd[i] = x;
 }
 
+// the counts of a thread's 16 buckets (u16) as 8 words of two halves
+__device__ __forceinline__ void load_counts16(const uint16_t* c, u32 nb, u32 first, u32 w[8]) {
+  if (nb >= OWN) {  // aligned: 32 bytes per thread
+    const uint4* v = (const uint4*)(c + first);
+    const uint4 x = v[0], y = v[1];
+    w[0] = x.x, w[1] = x.y, w[2] = x.z, w[3] = x.w, w[4] = y.x, w[5] = y.y, w[6] = y.z, w[7] = y.w;
+  } else {  // a subtree of fewer than 16 buckets (depth < 4): thread 0 only
+#pragma unroll
+    for (u32 q = 0; q < 8; q++) {
+      const u32 lo = 2 * q < nb ? c[first + 2 * q] : 0u, hi = 2 * q + 1 < nb ? c[first + 2 * q + 1] : 0u;
+      w[q] = lo | (hi << 16);
+    }
+  }
+}
+
+__device__ __forceinline__ u32 half16(const u32 w[8], u32 i) { return (w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu; }
+
 __global__ __launch_bounds__(DB) void merkle_diff_count_kernel(DiffArgs p) {
-  __shared__ u64 s_ka[DCAP], s_kb[DCAP];
-  __shared__ u64 s_h[LCAP];            // hashes of the listed rows, in list order
-  __shared__ uint16_t s_list[LCAP];    // the differing buckets' rows: bit 15 = store B
+  __shared__ uint16_t s_f[2][XSUB];  // descent frontiers: node positions within the subtree
   __shared__ u32 s_wave[DB / WAVE + 1];
-  __shared__ u32 s_bc[DB];             // rows per bucket: A in the low, B in the high half
-  const u32 depth = p.ta.depth;
-  const u64 tile = blockIdx.x, bpt = diff_bpt(depth), b0 = tile * bpt;
+  __shared__ u32 s_list[RCAP];       // listed rows: bit 31 = store B; offset from the subtree's first row
+  __shared__ u64 s_k[RCAP], s_h[RCAP];
+  const u32 depth = p.ta.depth, sub = p.sub, Ls = depth - sub, nb = 1u << sub;
+  const u64 tile = blockIdx.x;
   const int tid = threadIdx.x;
-  const u32 rl = depth >= 8 ? depth - 8 : 0;
-  const u64 root = ((1ull << rl) - 1) + tile;
+  const u64 root = ((1ull << Ls) - 1) + tile;
   const u64 nbnd = p.ntiles + 1;
-  const bool in = (u64)tid < bpt;
-  const u64 b = b0 + tid;
-  const u64 leaf = ((1ull << depth) - 1) + b;
-  // one round of independent loads: the subtree roots, the tile's row bounds, the leaves
-  const u64 root_a = p.ta.nodes[root], root_b = p.tb.nodes[root];
-  const u64 a0 = p.bnd[tile], a1 = p.bnd[tile + 1], c0 = p.bnd[nbnd + tile], c1 = p.bnd[nbnd + tile + 1];
-  const u64 leaf_a = in ? p.ta.nodes[leaf] : 0, leaf_b = in ? p.tb.nodes[leaf] : 0;
-  if (root_a == root_b) {  // uniform: the whole tile matches
+  if (p.ta.nodes[root] == p.tb.nodes[root]) {  // uniform: the whole subtree matches
     if (tid == 0) p.cnt[tile] = 0;
     return;
   }
+  // ---- descent: frontier = the differing nodes of level Ls + l (positions in the subtree)
+  u32 nf = 1, cur = 0;
+  if (tid == 0) s_f[0][0] = 0;
+  __syncthreads();
+  for (u32 l = 1; l <= sub; l++) {
+    const u64 first = ((1ull << (Ls + l)) - 1) + (tile << l);  // the subtree's first node of the level
+    u32 nn = 0;
+    for (u32 j0 = 0; j0 < nf; j0 += DB) {  // uniform loop
+      const u32 j = j0 + tid;
+      u32 f = 0, d0 = 0, d1 = 0;
+      if (j < nf) {
+        f = s_f[cur][j];
+        const u64 c = first + 2 * (u64)f;
+        const u64 a0 = p.ta.nodes[c], a1 = p.ta.nodes[c + 1];
+        const u64 b0 = p.tb.nodes[c], b1 = p.tb.nodes[c + 1];
+        d0 = a0 != b0;
+        d1 = a1 != b1;
+      }
+      u32 tot;
+      const u32 o = nn + block_excl_scan<DB>(d0 + d1, s_wave, &tot);
+      if (d0) s_f[cur ^ 1][o] = (uint16_t)(2 * f);
+      if (d1) s_f[cur ^ 1][o + d0] = (uint16_t)(2 * f + 1);
+      nn += tot;
+      __syncthreads();  // (s_wave reuse; the frontier of level l complete)
+    }
+    nf = nn;
+    cur ^= 1;
+  }
+  // s_f[cur][0, nf): the differing buckets, ascending.  Thread tid owns buckets
+  // [16 tid, 16 tid + 16): mark its differing ones (a 16-bit mask) from the list.
+  u32 mine = 0;
+  {
+    // owner of list entry j is s_f[cur][j] / 16; entries are ascending, so a thread finds
+    // its range by two searches of the (LDS) list
+    const u32 lo_b = (u32)tid * OWN;
+    u32 lo = 0, hi = nf;
+    while (lo < hi) {
+      const u32 m = (lo + hi) >> 1;
+      if (s_f[cur][m] < lo_b) lo = m + 1; else hi = m;
+    }
+    for (u32 j = lo; j < nf && s_f[cur][j] < lo_b + OWN; j++) mine |= 1u << (s_f[cur][j] - lo_b);
+  }
+  // row counts of the owned buckets in both trees, and their row offsets in the subtree
+  const u64 a0 = p.bnd[tile], c0 = p.bnd[nbnd + tile];
+  const u64 bucket0 = tile << sub;
+  u32 ca[8], cb[8];
+  const bool owns = (u32)tid * OWN < nb;
+  if (owns) {
+    load_counts16(p.ta.counts + bucket0, nb, (u32)tid * OWN, ca);
+    load_counts16(p.tb.counts + bucket0, nb, (u32)tid * OWN, cb);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; q++) ca[q] = cb[q] = 0;
+  }
+  u32 ta_ = 0, tb_ = 0, rd = 0;
+#pragma unroll
+  for (u32 i = 0; i < OWN; i++) {
+    const u32 x = half16(ca, i), y = half16(cb, i);
+    ta_ += x;
+    tb_ += y;
+    if (mine >> i & 1u) rd += x + y;
+  }
+  u32 tot;
+  const u32 offa = block_excl_scan<DB>(ta_, s_wave, &tot);
+  __syncthreads();
+  const u32 offb = block_excl_scan<DB>(tb_, s_wave, &tot);
+  __syncthreads();
+  u32 R;
+  const u32 slot0 = block_excl_scan<DB>(rd, s_wave, &R);
+  __syncthreads();
   const u64 base = a0 + c0;
-  const u32 na = (u32)(a1 - a0), nc = (u32)(c1 - c0);
-  const bool walk = in && leaf_a != leaf_b;
-  const bool last = (u64)tid == bpt - 1;
-  const u64 lk = bucket_first_key(p.ta, b), hk = last ? 0 : bucket_first_key(p.ta, b + 1);
-  bool lds = a1 - a0 <= DCAP && c1 - c0 <= DCAP;  // uniform
-  u32 ia = 0, ie = 0, jb = 0, je = 0, r0 = 0;
+  const bool lds = R <= RCAP;  // uniform
   if (lds) {
-    {  // every staging load in flight at once (DCAP / DB = 4 per store per thread)
-      constexpr int Q = DCAP / DB;
-      u64 ka[Q], kb[Q];
+    // list the differing buckets' rows (A rows, then B rows, bucket by bucket)
+    u32 slot = slot0, ra = offa, rb = offb;
 #pragma unroll
-      for (int q = 0; q < Q; q++) {
-        const u32 x = q * DB + tid;
-        ka[q] = x < na ? p.sa.key[a0 + x] : 0;
-        kb[q] = x < nc ? p.sb.key[c0 + x] : 0;
+    for (u32 i = 0; i < OWN; i++) {
+      const u32 x = half16(ca, i), y = half16(cb, i);
+      if (mine >> i & 1u) {
+        for (u32 r = 0; r < x; r++) s_list[slot++] = ra + r;
+        for (u32 r = 0; r < y; r++) s_list[slot++] = 0x80000000u | (rb + r);
       }
+      ra += x;
+      rb += y;
+    }
+    __syncthreads();
+    // hash them all at once: up to RCAP / DB rows per thread, loads in flight together
 #pragma unroll
-      for (int q = 0; q < Q; q++) {
-        const u32 x = q * DB + tid;
-        if (x < na) s_ka[x] = ka[q];
-        if (x < nc) s_kb[x] = kb[q];
-      }
-      s_bc[tid] = 0;
-      __syncthreads();
-      // every bucket's row range from a histogram of the staged keys (LDS atomics) and one
-      // scan, instead of four binary searches per differing bucket
-      const u64 kbase = p.ta.sb ? (p.ta.shard << (64 - p.ta.sb)) : 0ull;
-      const u32 sh = 64 - p.ta.sb - depth;
-#pragma unroll
-      for (int q = 0; q < Q; q++) {
-        const u32 x = q * DB + tid;
-        const u64 la = ((ka[q] - kbase) >> sh) - b0, lb = ((kb[q] - kbase) >> sh) - b0;
-        if (x < na && la < bpt) atomicAdd(&s_bc[la], 1u);  // (bounds: the tile's buckets)
-        if (x < nc && lb < bpt) atomicAdd(&s_bc[lb], 1u << 16);
+    for (u32 u = 0; u < RCAP / DB; u++) {
+      const u32 q = u * DB + tid;
+      if (q < R) {
+        const u32 e = s_list[q];
+        if (e & 0x80000000u) {
+          const u64 i = c0 + (e & 0x7FFFFFFFu);
+          s_k[q] = p.sb.key[i];
+          s_h[q] = rh(p.sb, i, p.tb.th);
+        } else {
+          const u64 i = a0 + e;
+          s_k[q] = p.sa.key[i];
+          s_h[q] = rh(p.sa, i, p.ta.th);
+        }
       }
     }
     __syncthreads();
-    {
-      const u32 bc = in ? s_bc[tid] : 0u;
-      u32 tot_bc;
-      const u32 st = block_excl_scan<DB>(bc, s_wave, &tot_bc);  // (counts <= DCAP: no carry)
-      ia = st & 0xffffu;
-      ie = ia + (bc & 0xffffu);
-      jb = st >> 16;
-      je = jb + (bc >> 16);
-      if (!walk) {  // only the differing buckets' rows are listed and merged
-        ie = ia;
-        je = jb;
-      }
-    }
-    // list the differing buckets' rows, then hash them all at once
-    u32 tot_rows;
-    r0 = block_excl_scan<DB>((ie - ia) + (je - jb), s_wave, &tot_rows);
-    lds = tot_rows <= LCAP;  // uniform
-    if (lds) {
-      u32 o = r0;
-      for (u32 x = ia; x < ie; x++) s_list[o++] = (uint16_t)x;
-      for (u32 x = jb; x < je; x++) s_list[o++] = (uint16_t)(x | 0x8000u);
-      __syncthreads();
-      for (u32 q = tid; q < tot_rows; q += DB) {
-        const u32 e = s_list[q];
-        s_h[q] = (e & 0x8000u) ? rh(p.sb, c0 + (e & 0x7FFFu)) : rh(p.sa, a0 + e);
-      }
-      __syncthreads();
-    }
   }
-  if (!lds) {  // fallback: per-bucket merges over global memory
-    u32 c = 0;
-    if (walk) {
-      const u64* ka = p.sa.key + a0;
-      const u64* kb = p.sb.key + c0;
-      ia = (b == b0) ? 0u : lb_small(ka, na, lk);
-      ie = last ? na : lb_small(ka, na, hk);
-      jb = (b == b0) ? 0u : lb_small(kb, nc, lk);
-      je = last ? nc : lb_small(kb, nc, hk);
-      c = merge_bucket<false, false>(p.sa, a0 + ia, a0 + ie, p.sb, nullptr, nullptr, c0 + jb, c0 + je,
-                                     nullptr, 0, 0);
-    }
-    u32 tot;
-    const u32 ex = block_excl_scan<DB>(c, s_wave, &tot);
-    if (c)
-      merge_bucket<false, true>(p.sa, a0 + ia, a0 + ie, p.sb, nullptr, nullptr, c0 + jb, c0 + je,
-                                p.keys + base, ex, ~0ull);
-    if (tid == 0) {
-      p.cnt[tile] = tot;
-      if (tot) atomicAdd((unsigned long long*)&p.bsum[tile / DB], (unsigned long long)tot);
-    }
-    return;
-  }
-  // merge the differing buckets' keys from LDS: count, then write at the scanned offset.
-  // This bucket's A rows' hashes sit at s_h[r0 + (x - ia)], its B rows' after them.
-  const u32 hb0 = r0 + (ie - ia) - jb;
+  // merge each owned differing bucket's keys: count, then write at the scanned offset
   u32 c = 0;
   for (int pass = 0; pass < 2; pass++) {
     u32 o = 0;
     if (pass == 1) {
-      u32 tot;
-      o = block_excl_scan<DB>(c, s_wave, &tot);
+      u32 t2;
+      o = block_excl_scan<DB>(c, s_wave, &t2);
       if (tid == 0) {
-        p.cnt[tile] = tot;
-        if (tot) atomicAdd((unsigned long long*)&p.bsum[tile / DB], (unsigned long long)tot);
+        p.cnt[tile] = t2;
+        if (t2) atomicAdd((unsigned long long*)&p.bsum[tile / DB], (unsigned long long)t2);
       }
     }
-    if (walk) {
-      u32 i = ia, j = jb, k2 = 0;
-      while (i < ie || j < je) {
-        const u64 ka = i < ie ? s_ka[i] : ~0ull, kb = j < je ? s_kb[j] : ~0ull;
-        const u64 k = ka < kb ? ka : kb;
-        u64 ha = 0, hb = 0;
-        const bool pa = ka == k, pb = kb == k;
-        for (; i < ie && s_ka[i] == k; i++) ha += s_h[r0 + (i - ia)];
-        for (; j < je && s_kb[j] == k; j++) hb += s_h[hb0 + j];
-        if (!(pa && pb) || ha != hb) {
-          if (pass == 1) p.keys[base + o + k2] = k;
-          k2++;
+    u32 k2 = 0, slot = slot0, ra = offa, rb = offb;
+    for (u32 i = 0; i < OWN; i++) {
+      const u32 x = half16(ca, i), y = half16(cb, i);
+      if (mine >> i & 1u) {
+        if (lds) {
+          u32 ia = slot, ie = slot + x, jb = slot + x, je = slot + x + y;
+          while (ia < ie || jb < je) {
+            const u64 ka = ia < ie ? s_k[ia] : ~0ull, kb = jb < je ? s_k[jb] : ~0ull;
+            const u64 k = ka < kb ? ka : kb;
+            u64 ha = 0, hb = 0;
+            const bool pa = ia < ie && ka == k, pb = jb < je && kb == k;
+            for (; ia < ie && s_k[ia] == k; ia++) ha += s_h[ia];
+            for (; jb < je && s_k[jb] == k; jb++) hb += s_h[jb];
+            if (!(pa && pb) || ha != hb) {
+              if (pass == 1) p.keys[base + o + k2] = k;
+              k2++;
+            }
+          }
+          slot += x + y;
+        } else if (pass == 0) {
+          k2 += merge_bucket<false, false>(p.sa, p.ta.th, a0 + ra, a0 + ra + x, p.sb, p.tb.th,
+                                           nullptr, nullptr, c0 + rb, c0 + rb + y, nullptr, 0, 0);
+        } else {
+          k2 += merge_bucket<false, true>(p.sa, p.ta.th, a0 + ra, a0 + ra + x, p.sb, p.tb.th,
+                                          nullptr, nullptr, c0 + rb, c0 + rb + y, p.keys + base,
+                                          o + k2, ~0ull);
         }
       }
-      c = k2;
+      ra += x;
+      rb += y;
     }
+    c = k2;
   }
 }
 
@@ -562,6 +642,7 @@ __global__ __launch_bounds__(DSB) void tile_scan_kernel(const u64* cnt, u64* off
 // the tile's keys from scratch to the output below cap.  The last tile's wave writes
 // the total.
 __global__ __launch_bounds__(WAVE) void merkle_diff_write_kernel(DiffArgs p) {
+  // (subtree `tile`'s keys sit at bnd[tile] + bnd[ntiles + 1 + tile] in scratch)
   const int lane = threadIdx.x;
   const u64 tile = blockIdx.x, grp = tile / DB;
   const u64 n = p.cnt[tile];
@@ -640,7 +721,7 @@ __global__ __launch_bounds__(PB) void leaves_kernel(MT t, Rows s, const u64* buc
   for (u64 x = r; x < re;) {
     const u64 k = s.key[x];
     u64 h = 0;
-    for (; x < re && s.key[x] == k; x++) h += rh(s, x);
+    for (; x < re && s.key[x] == k; x++) h += rh(s, x, t.th);
     ok[o] = k;
     oh[o++] = h;
   }
@@ -662,7 +743,7 @@ __global__ __launch_bounds__(PB) void leafdiff_kernel(MT t, Rows s, const u64* b
     re = bucket_start(t, s.key, s.n, b + 1);
     j = bucket_start(t, pk, np, b);
     je = bucket_start(t, pk, np, b + 1);
-    c = merge_bucket<true, false>(s, r, re, s, pk, ph, j, je, nullptr, 0, 0);
+    c = merge_bucket<true, false>(s, t.th, r, re, s, t.th, pk, ph, j, je, nullptr, 0, 0);
   }
   u32 tot;
   const u32 ex = block_excl_scan<PB>(c, s_wave, &tot);
@@ -671,7 +752,7 @@ __global__ __launch_bounds__(PB) void leafdiff_kernel(MT t, Rows s, const u64* b
     return;
   }
   const u64 o = off[blockIdx.x] + ex;
-  if (c && o < cap) merge_bucket<true, true>(s, r, re, s, pk, ph, j, je, out, o, cap);
+  if (c && o < cap) merge_bucket<true, true>(s, t.th, r, re, s, t.th, pk, ph, j, je, out, o, cap);
 }
 
 __global__ void pairs_before_kernel(MT t, const u64* keys, u64 n, const u64* bucket, u64* out) {
@@ -684,6 +765,8 @@ MT mt_of(const MerkleT& m) {
   t.sb = m.sb;
   t.shard = m.shard;
   t.nodes = m.nodes;
+  t.counts = m.counts;
+  t.th = m.th;
   return t;
 }
 
@@ -728,10 +811,10 @@ hipError_t launch_merkle_diff(const MerkleT& a, const Rows& sa, const MerkleT& b
   p.out = out_keys;
   p.cap = cap;
   p.ntiles = diff_tiles(a.depth);
+  p.sub = diff_sub(a.depth);
   p.bnd = scratch;
   p.cnt = scratch + 2 * (p.ntiles + 1);
-  p.off = p.cnt + p.ntiles;
-  p.keys = p.off + p.ntiles;
+  p.keys = p.cnt + p.ntiles;
   p.bsum = p.keys + sa.n + sb.n + 1;
   p.d_count = d_count;
   const u64 waves = 2 * (p.ntiles + 1);

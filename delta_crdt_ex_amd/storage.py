@@ -15,9 +15,10 @@ The header holds node_id, sequence_number, the row and context counts, the conte
 kind, the byte length and xxh64 of each column, and the exact interning tables of
 the state's Universe (keys, values and nodes as tagged terms), so `read` restores the
 same terms, ids and rows.  Columns are the raw SoA arrays (key, val, ts, node, cnt,
-ctx node, ctx cnt, and the Merkle tree's nodes when one is persisted): 36 B per dot +
-12 B per context entry + 8 B per tree node, copied device -> host by one D2H copy
-each.  The header names the tree's depth and key-hash shard.  A checksum mismatch
+ctx node, ctx cnt, and the Merkle tree's nodes and per-bucket row counts when one is
+persisted): 36 B per dot + 12 B per context entry + 8 B per tree node + 2 B per bucket,
+copied device -> host by one D2H copy each.  A persisted tree hashes terms (the
+Universe's term hashes, interning.py), so it is valid for the restored ids.  The header names the tree's depth and key-hash shard.  A checksum mismatch
 raises; the file is written to a temporary name, fsynced and renamed over the old one.
 """
 from __future__ import annotations
@@ -122,11 +123,13 @@ def _universe_from(tables) -> interning.Universe:
 
 def write_arrays(path, node_id, sequence_number: int, rows, ctx, universe, merkle=None) -> None:
     """The snapshot file from host arrays: rows = (key, val, ts, node, cnt) numpy columns,
-    ctx = (kind, node, cnt), merkle = None or (depth, shard_bits, shard, nodes uint64)."""
+    ctx = (kind, node, cnt), merkle = None or (depth, shard_bits, shard, nodes uint64,
+    counts uint16)."""
     cols = [np.ascontiguousarray(c, dt) for c, (_, dt) in zip(rows, _COLS)]
     cols += [np.ascontiguousarray(ctx[1], np.uint32), np.ascontiguousarray(ctx[2], np.uint64)]
     if merkle is not None:
         cols.append(np.ascontiguousarray(merkle[3], np.uint64))
+        cols.append(np.ascontiguousarray(merkle[4], np.uint16))
     blobs = [c.tobytes() for c in cols]
     header = {
         "node_id": _pack(node_id),
@@ -154,7 +157,7 @@ def write_arrays(path, node_id, sequence_number: int, rows, ctx, universe, merkl
 
 def read_arrays(path):
     """(node_id, sequence_number, rows, ctx, universe, merkle) from a snapshot file as
-    host arrays (merkle: None or (depth, shard_bits, shard, nodes)); None if absent."""
+    host arrays (merkle: None or (depth, shard_bits, shard, nodes, counts)); None if absent."""
     if not os.path.exists(path):
         return None
     with open(path, "rb") as f:
@@ -167,14 +170,14 @@ def read_arrays(path):
         (hl,) = struct.unpack("<Q", f.read(8))
         header = msgpack.unpackb(f.read(hl), raw=False, strict_map_key=False)
         arrays = []
-        dtypes = [d for _, d in _COLS] + [np.uint32, np.uint64, np.uint64]
+        dtypes = [d for _, d in _COLS] + [np.uint32, np.uint64, np.uint64, np.uint16]
         for (nbytes, digest), dt in zip(header["columns"], dtypes):
             b = f.read(nbytes)
             if len(b) != nbytes or xxhash.xxh64_intdigest(b) != digest:
                 raise ValueError(f"{path}: column checksum mismatch")
             arrays.append(np.frombuffer(b, dtype=dt).copy())
     m = header.get("merkle")
-    merkle = None if m is None else (int(m[0]), int(m[1]), int(m[2]), arrays[7])
+    merkle = None if m is None else (int(m[0]), int(m[1]), int(m[2]), arrays[7], arrays[8])
     return (_unpack(header["node_id"]), header["sequence_number"], tuple(arrays[:5]),
             (header["ctx_kind"], arrays[5], arrays[6]), _universe_from(header["universe"]), merkle)
 
@@ -186,7 +189,7 @@ def write(path, node_id, sequence_number: int, state, merkle_map=None) -> None:
     m = None
     if merkle_map is not None:
         m = (merkle_map.depth, merkle_map.shard_bits, merkle_map.shard,
-             merkle_map.nodes.cpu().numpy().view(np.uint64))
+             merkle_map.nodes.cpu().numpy().view(np.uint64), merkle_map.bucket_counts())
     write_arrays(path, node_id, sequence_number, state.rows.to_numpy(),
                  (state.ctx.kind,) + tuple(state.ctx.to_numpy()), state.universe, m)
 
@@ -198,7 +201,7 @@ def read(path, device=None):
     import torch
 
     from . import aw_lww_map as M
-    from .store import Context, MerkleTree, Store
+    from .store import Context, MerkleTree, Store, TermHashes
     got = read_arrays(path)
     if got is None:
         return None
@@ -209,9 +212,11 @@ def read(path, device=None):
     if merkle is None:
         tree = None
     else:
-        depth, sb, shard, nodes = merkle
-        tree = MerkleTree(depth, torch.from_numpy(nodes.view(np.int64).copy()).to(dev), 0, sb, shard,
-                          st)
+        depth, sb, shard, nodes, counts = merkle
+        tree = MerkleTree.empty(depth, dev, sb, shard, TermHashes.of(U, dev))
+        tree.nodes.copy_(torch.from_numpy(nodes.view(np.int64).copy()))
+        tree.counts[: 1 << depth].copy_(torch.from_numpy(counts.view(np.int16).copy()))
+        tree.store = st
         tree.n_keys = int(len(np.unique(rows[0])))
     return node_id, seq, state, tree
 

@@ -127,10 +127,37 @@ class Context:
                                self.cap)
 
 
+class TermHashes:
+    """Device term-hash tables of a tree's rows (include/deltagpu.h dg_term_hashes):
+    node_hash[node id], and the ascending non-canonical value ids with their hashes --
+    `interning.Universe.term_tables()`.  Trees built with them compare across interning
+    tables (replicas on other BEAM nodes)."""
+
+    def __init__(self, node_hash, val_id, val_hash, device):
+        def dev(a):
+            a = np.ascontiguousarray(np.asarray(a, np.uint64))
+            return _np_to_dev(a, np.int64, device) if len(a) else torch.zeros(1, dtype=_I64,
+                                                                                 device=device)
+        self.nh, self.vid, self.vh = dev(node_hash), dev(val_id), dev(val_hash)
+        self.c = _abi.dg_term_hashes(self.nh.data_ptr(), len(node_hash), self.vid.data_ptr(),
+                                     self.vh.data_ptr(), len(val_id))
+
+    @staticmethod
+    def of(universe, device) -> "TermHashes":
+        """The universe's current tables, uploaded once per version (cached on it)."""
+        cached = getattr(universe, "_dev_terms", None)
+        if cached is not None and cached[0] == universe.terms_version and cached[1] == str(device):
+            return cached[2]
+        th = TermHashes(*universe.term_tables(), device)
+        universe._dev_terms = (universe.terms_version, str(device), th)
+        return th
+
+
 @dataclass(eq=False)
 class MerkleTree:
-    """A device Merkle tree (include/deltagpu.h dg_merkle) and the store it indexes (the
-    diff recomputes key leaves from the store's rows)."""
+    """A device Merkle tree (include/deltagpu.h dg_merkle): its node heap, the rows per
+    bucket, the term hashes its rows were hashed with (None: the ids), and the store it
+    indexes (the diff recomputes key leaves from the store's rows)."""
 
     depth: int
     nodes: torch.Tensor
@@ -138,11 +165,19 @@ class MerkleTree:
     shard_bits: int = 0
     shard: int = 0
     store: Store | None = None
+    counts: torch.Tensor | None = None
+    terms: TermHashes | None = None
 
     @staticmethod
-    def empty(depth: int, device, shard_bits: int = 0, shard: int = 0) -> "MerkleTree":
+    def empty(depth: int, device, shard_bits: int = 0, shard: int = 0,
+              terms: TermHashes | None = None) -> "MerkleTree":
         return MerkleTree(depth, torch.empty(2 * (1 << depth) - 1, dtype=_I64, device=device), 0,
-                          shard_bits, shard)
+                          shard_bits, shard, None,
+                          torch.empty(max(1 << depth, 8), dtype=torch.int16, device=device), terms)
+
+    def clone(self) -> "MerkleTree":
+        return MerkleTree(self.depth, self.nodes.clone(), self.n_keys, self.shard_bits, self.shard,
+                          self.store, self.counts.clone(), self.terms)
 
     def abi(self) -> _abi.dg_merkle:
         t = _abi.dg_merkle()
@@ -151,7 +186,12 @@ class MerkleTree:
         t.shard = self.shard
         t.nodes = self.nodes.data_ptr()
         t.n_keys = self.n_keys
+        t.counts = self.counts.data_ptr()
+        t.terms = C.pointer(self.terms.c) if self.terms is not None else None
         return t
+
+    def bucket_counts(self) -> np.ndarray:
+        return self.counts[: 1 << self.depth].cpu().numpy().view(np.uint16)
 
     def root(self) -> int:
         return int(self.nodes[0].item()) & ((1 << 64) - 1)
@@ -501,11 +541,16 @@ class Engine:
 
     # ---------------------------------------------------------------- merkle
     def merkle_build(self, s: Store, depth: int, tree: MerkleTree | None = None,
-                     shard_bits: int = 0, shard: int = 0) -> MerkleTree:
-        """MerkleMap over every key of `s` (or of its key-hash shard)."""
+                     shard_bits: int = 0, shard: int = 0,
+                     terms: TermHashes | None = None) -> MerkleTree:
+        """MerkleMap over every key of `s` (or of its key-hash shard); `terms`: hash the
+        rows' terms instead of their ids (a given `tree` keeps its own)."""
         self._order()
         if tree is None or tree.depth != depth:
-            tree = MerkleTree.empty(depth, self.device, shard_bits, shard)
+            tree = MerkleTree.empty(depth, self.device, shard_bits, shard,
+                                    terms if terms is not None else (tree.terms if tree else None))
+        elif terms is not None:
+            tree.terms = terms
         tree.shard_bits, tree.shard = shard_bits, shard
         t = tree.abi()
         ss = s.abi()
@@ -646,5 +691,5 @@ def u64(t: torch.Tensor) -> np.ndarray:
     return t.cpu().numpy().view(np.uint64)
 
 
-__all__ = ["Store", "Context", "MerkleTree", "MerkleCont", "Engine", "fold_roots", "u64",
+__all__ = ["Store", "Context", "MerkleTree", "MerkleCont", "TermHashes", "Engine", "fold_roots", "u64",
            "DG_CTX_VV", "DG_CTX_DOTS"]

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define DG_ABI_VERSION 2
+#define DG_ABI_VERSION 3
 
 enum dg_status {
   DG_OK = 0,
@@ -76,6 +76,24 @@ typedef struct dg_context {
   uint64_t cap;
 } dg_context;
 
+/* Term hashes for the Merkle rows: with them a tree covers the TERMS of each row, not the
+ * ids one host's interning tables gave them, so two replicas' trees compare on any BEAM
+ * node (the reference hashes the raw value map, causal_crdt.ex:390-394, and diffs against
+ * neighbours on other nodes, causal_crdt_test.exs:68-78).  In a row's hash
+ *   the node id n becomes node_hash[n]                         (n < n_nodes)
+ *   the value id v becomes val_hash[j] where val_id[j] == v    (v outside [2^58, 2^63))
+ * -- a canonical integer value's id (v + 2^62 for integers in [-2^62 + 2^58, 2^62)) is the
+ * same on every host and hashes as itself; key ids are term hashes already.  The Python
+ * mirror (interning.py Universe.term_tables) and the NIF (c_src/marshal.c dgm_node_hashes,
+ * dgm_value_hashes) produce these tables; ids missing from them hash as themselves. */
+typedef struct dg_term_hashes {
+  const uint64_t* node_hash; /* device: the hash of node id i, n_nodes entries */
+  uint64_t n_nodes;
+  const uint64_t* val_id;    /* device, ascending: the non-canonical value ids */
+  const uint64_t* val_hash;  /* device: their term hashes */
+  uint64_t n_vals;
+} dg_term_hashes;
+
 /* Merkle index over a store (the MerkleMap role, causal_crdt.ex:21,94,96,254,255,390-394).
  * The tree covers the keys whose top `shard_bits` bits equal `shard` (a key-hash shard,
  * SURVEY.md §8(e); shard_bits = 0: every key) in 2^depth buckets by the next `depth`
@@ -84,7 +102,9 @@ typedef struct dg_context {
  *                 over its own rows: its raw value map, causal_crdt.ex:392)
  *   parent      = node_hash(left, right)                       (dg_hash.h)
  * `nodes` is a heap in level order: level l (root l = 0) occupies [2^l - 1, 2^(l+1) - 1);
- * level `depth` holds the buckets.  The tree keeps no per-key leaves: a diff recomputes
+ * level `depth` holds the buckets.  `counts` holds each bucket's row count (at most 65535
+ * rows per bucket; DG_E_CAPACITY beyond): the diff finds a differing bucket's rows from
+ * them instead of reading every key.  The tree keeps no per-key leaves: a diff recomputes
  * them from the store the tree indexes, so the diff entry points take the stores too.
  * The 2^b shard trees (shard_bits = b, depth d - b) are exactly the level-b subtrees of
  * the unsharded depth-d tree; dg_merkle_fold_roots recombines their roots. */
@@ -94,6 +114,8 @@ typedef struct dg_merkle {
   uint64_t shard;      /* < 2^shard_bits */
   uint64_t* nodes;     /* 2^(depth+1) - 1 entries (caller-allocated, device) */
   uint64_t n_keys;     /* distinct keys indexed (set by build / update) */
+  uint16_t* counts;    /* 2^depth entries (caller-allocated, device; set by build / update) */
+  const dg_term_hashes* terms; /* host pointer (its arrays: device); NULL: hash the ids */
 } dg_merkle;
 
 /* A partial-diff continuation (the `continuation` of CausalCrdt's %Diff{},
@@ -292,8 +314,9 @@ int dg_remap_values(dg_engine* e, dg_store* s, const uint64_t* old_ids, const ui
 
 /* ---- Merkle anti-entropy (MerkleMap role) --------------------------------- */
 /* Build the tree of `s` (MerkleMap.new + put of every key, causal_crdt.ex:21,390-394):
- * t->depth, shard_bits, shard and nodes set by the caller; sets t->n_keys.  DG_E_INVAL
- * if a row's key is outside the tree's shard.  Synchronous. */
+ * t->depth, shard_bits, shard, nodes, counts and terms set by the caller; sets t->n_keys.
+ * DG_E_INVAL if a row's key is outside the tree's shard, DG_E_CAPACITY if a bucket holds
+ * more than 65535 rows (use a deeper tree).  Synchronous. */
 int dg_merkle_build(dg_engine* e, const dg_store* s, dg_merkle* t);
 /* Same, asynchronous on the engine stream: the distinct-key count goes to d_n_keys[0]
  * (device); t->n_keys is not updated and a key outside the shard is not reported. */
@@ -301,7 +324,8 @@ int dg_merkle_build_async(dg_engine* e, const dg_store* s, dg_merkle* t, uint64_
 
 /* MerkleMap.put/delete of the keys a join changed plus update_hashes
  * (update_state_with_delta, causal_crdt.ex:383-394; update_hashes :94,254): `t` indexes
- * `old_s`; afterwards it indexes `new_s`, bit-identical to dg_merkle_build(new_s), having
+ * `old_s`; afterwards it indexes `new_s`, bit-identical (nodes and counts) to
+ * dg_merkle_build(new_s), having
  * re-hashed only `keys` (device, ascending unique: every key whose rows differ between
  * the stores, e.g. dg_join2_changes's output; extra keys are harmless) and the 2^11-bucket
  * chunks they touch.  Synchronous. */
@@ -310,7 +334,9 @@ int dg_merkle_update(dg_engine* e, dg_merkle* t, const dg_store* old_s, const dg
 
 /* The keys whose raw value maps differ between two indexed stores (present in one only,
  * or with different rows), ascending -- the key list MerkleMap.continue_partial_diff ends
- * with (causal_crdt.ex:96,104-105), here with both trees at hand.  The first
+ * with (causal_crdt.ex:96,104-105), here with both trees at hand.  The trees are descended
+ * from the roots of their 4096-bucket subtrees through the differing nodes only, and only
+ * the rows of differing buckets are read (located by the trees' row counts).  The first
  * min(total, cap) keys are written to out_keys, *n_out = that number and *n_total = the
  * total: a total above cap is the reference's truncate(keys, max_sync_size)
  * (Enum.take, causal_crdt.ex:105,206-210), not an error.  Trees: same depth and shard. */

@@ -351,12 +351,29 @@ static inline uint64_t mix64(uint64_t x) {
   return x;
 }
 
-uint64_t ref_row_hash(uint64_t key, uint64_t val, int64_t ts, uint32_t node, uint64_t cnt) {
+uint64_t ref_row_hash(uint64_t key, uint64_t val, int64_t ts, uint64_t node, uint64_t cnt) {
   uint64_t h = mix64(key ^ 0x9E3779B97F4A7C15ULL);
   h = mix64(h ^ val);
   h = mix64(h ^ (uint64_t)ts);
-  h = mix64(h ^ (uint64_t)node);
+  h = mix64(h ^ node);
   return mix64(h ^ cnt);
+}
+
+/* The term in a row hash of a value id / node id (include/deltagpu.h dg_term_hashes; the
+ * arrays here are HOST arrays): th == NULL, a canonical integer value id [2^58, 2^63) and
+ * ids absent from the tables stand for themselves. */
+uint64_t ref_term_val(const dg_term_hashes* th, uint64_t v) {
+  if (!th || !th->val_id || !th->val_hash || (v >= (1ULL << 58) && v < (1ULL << 63))) return v;
+  uint64_t lo = 0, hi = th->n_vals;
+  while (lo < hi) {
+    uint64_t mid = (lo + hi) / 2;
+    if (th->val_id[mid] < v) lo = mid + 1; else hi = mid;
+  }
+  return (lo < th->n_vals && th->val_id[lo] == v) ? th->val_hash[lo] : v;
+}
+
+uint64_t ref_term_node(const dg_term_hashes* th, uint32_t n) {
+  return (th && th->node_hash && n < th->n_nodes) ? th->node_hash[n] : (uint64_t)n;
 }
 
 uint64_t ref_node_hash(uint64_t left, uint64_t right) {
@@ -367,21 +384,38 @@ uint64_t ref_node_hash(uint64_t left, uint64_t right) {
  * keys whose top `sb` bits equal `shard`, 2^depth buckets by the next depth bits;
  * bucket = Σ row hashes of its rows (a key's leaf = Σ over its rows, the raw per-key
  * value map, causal_crdt.ex:392), parents = ref_node_hash(children).  `nodes` holds
- * 2^(depth+1) - 1 entries in level order.  DG_E_INVAL for a key outside the shard. */
+ * 2^(depth+1) - 1 entries in level order, `counts` (may be NULL) each bucket's rows.
+ * th: term hashes (host arrays) or NULL.  DG_E_INVAL for a key outside the shard,
+ * DG_E_CAPACITY for a bucket over 65535 rows. */
 int ref_merkle_build(const dg_store* s, uint32_t depth, uint32_t sb, uint64_t shard,
-                     uint64_t* nodes, uint64_t* n_keys) {
+                     const dg_term_hashes* th, uint64_t* nodes, uint16_t* counts, uint64_t* n_keys) {
   if (depth < 1 || depth > 28 || sb > 16 || depth + sb > 44) REF_E(DG_E_INVAL);
   uint64_t nb = 1ULL << depth;
   uint64_t base = nb - 1;
   memset(nodes, 0, (2 * nb - 1) * 8);
+  uint32_t* c32 = (uint32_t*)calloc(nb, sizeof *c32);
+  if (!c32) REF_E(DG_E_NOMEM);
   uint64_t keys = 0;
   for (uint64_t i = 0; i < s->n; i++) {
     uint64_t key = s->key[i];
-    if (sb && (key >> (64 - sb)) != shard) REF_E(DG_E_INVAL);
+    if (sb && (key >> (64 - sb)) != shard) {
+      free(c32);
+      REF_E(DG_E_INVAL);
+    }
     if (i == 0 || s->key[i - 1] != key) keys++;
-    nodes[base + ((key << sb) >> (64 - depth))] +=
-        ref_row_hash(key, s->val[i], s->ts[i], s->node[i], s->cnt[i]);
+    const uint64_t b = (key << sb) >> (64 - depth);
+    nodes[base + b] += ref_row_hash(key, ref_term_val(th, s->val[i]), s->ts[i],
+                                    ref_term_node(th, s->node[i]), s->cnt[i]);
+    c32[b]++;
   }
+  for (uint64_t b = 0; b < nb; b++) {
+    if (c32[b] > 0xFFFF) {
+      free(c32);
+      REF_E(DG_E_CAPACITY);
+    }
+    if (counts) counts[b] = (uint16_t)c32[b];
+  }
+  free(c32);
   for (int l = (int)depth - 1; l >= 0; l--) {
     uint64_t first = (1ULL << l) - 1;
     for (uint64_t x = 0; x < (1ULL << l); x++) {

@@ -42,10 +42,16 @@ def lib():
         L.ref_compress_dots.argtypes = [X, X]
         L.ref_read_lww.argtypes = [S, _abi.P64, C.c_uint64, _abi.P64, _abi.P64, C.c_uint64,
                                    _abi.P64]
-        L.ref_merkle_build.argtypes = [S, C.c_uint32, C.c_uint32, C.c_uint64, _abi.P64, _abi.P64]
+        TH = C.POINTER(_abi.dg_term_hashes)
+        L.ref_merkle_build.argtypes = [S, C.c_uint32, C.c_uint32, C.c_uint64, TH, _abi.P64,
+                                       C.c_void_p, _abi.P64]
+        L.ref_term_val.argtypes = [TH, C.c_uint64]
+        L.ref_term_val.restype = C.c_uint64
+        L.ref_term_node.argtypes = [TH, C.c_uint32]
+        L.ref_term_node.restype = C.c_uint64
         L.ref_store_diff.argtypes = [S, S, _abi.P64, C.c_uint64, _abi.P64]
         L.ref_store_check.argtypes = [S]
-        L.ref_row_hash.argtypes = [C.c_uint64, C.c_uint64, C.c_int64, C.c_uint32, C.c_uint64]
+        L.ref_row_hash.argtypes = [C.c_uint64, C.c_uint64, C.c_int64, C.c_uint64, C.c_uint64]
         L.ref_row_hash.restype = C.c_uint64
         L.ref_node_hash.argtypes = [C.c_uint64, C.c_uint64]
         L.ref_node_hash.restype = C.c_uint64
@@ -223,13 +229,31 @@ def read_lww(rows, keys=None):
     return ok[:m], ov[:m]
 
 
-class Tree:
-    """The oracle's Merkle tree (deltaref.c ref_merkle_build): `nodes` in level order."""
+class Terms:
+    """Term-hash tables (dg_term_hashes) as host arrays: node_hash[node id], and the
+    ascending non-canonical value ids with their hashes (interning.Universe.term_tables)."""
 
-    def __init__(self, depth, shard_bits=0, shard=0):
+    def __init__(self, node_hash, val_id, val_hash):
+        self.arrays = (np.ascontiguousarray(node_hash, np.uint64),
+                       np.ascontiguousarray(val_id, np.uint64),
+                       np.ascontiguousarray(val_hash, np.uint64))
+        nh, vi, vh = self.arrays
+        self.c = _abi.dg_term_hashes(nh.ctypes.data, len(nh), vi.ctypes.data, vh.ctypes.data, len(vi))
+
+    def ptr(self):
+        return C.pointer(self.c)
+
+
+class Tree:
+    """The oracle's Merkle tree (deltaref.c ref_merkle_build): `nodes` in level order,
+    `counts` rows per bucket, `terms` the term hashes it was built with (or None)."""
+
+    def __init__(self, depth, shard_bits=0, shard=0, terms=None):
         self.depth, self.shard_bits, self.shard = depth, shard_bits, shard
         self.nodes = np.zeros(2 * (1 << depth) - 1, np.uint64)
+        self.counts = np.zeros(1 << depth, np.uint16)
         self.n_keys = 0
+        self.terms = terms
 
     def level(self, lv):
         return self.nodes[(1 << lv) - 1: (1 << (lv + 1)) - 1]
@@ -240,14 +264,26 @@ class Tree:
             return ((k << np.uint64(self.shard_bits)) >> np.uint64(64 - self.depth)).astype(np.int64)
 
 
-def merkle_build(rows, depth, shard_bits=0, shard=0):
+def merkle_build(rows, depth, shard_bits=0, shard=0, terms: Terms | None = None):
     s, rows = _store(rows)
-    t = Tree(depth, shard_bits, shard)
+    t = Tree(depth, shard_bits, shard, terms)
     nk = np.zeros(1, np.uint64)
-    _check(lib().ref_merkle_build(C.byref(s), depth, shard_bits, shard, _p(t.nodes, _abi.P64),
-                                  _p(nk, _abi.P64)), "ref_merkle_build")
+    _check(lib().ref_merkle_build(C.byref(s), depth, shard_bits, shard,
+                                  terms.ptr() if terms is not None else None,
+                                  _p(t.nodes, _abi.P64), t.counts.ctypes.data, _p(nk, _abi.P64)),
+           "ref_merkle_build")
     t.n_keys = int(nk[0])
     return t
+
+
+def row_hashes(rows, terms: Terms | None = None) -> np.ndarray:
+    """The Merkle row hash of every row (with the tree's term hashes, if any)."""
+    L = lib()
+    th = terms.ptr() if terms is not None else None
+    k, v, t, nd, c = as_rows(rows)
+    return np.array([L.ref_row_hash(int(k[i]), L.ref_term_val(th, int(v[i])), int(t[i]),
+                                    L.ref_term_node(th, int(nd[i])), int(c[i]))
+                     for i in range(len(k))], np.uint64)
 
 
 def merkle_diff(ta: Tree, ra, tb: Tree, rb, cap=None):
@@ -269,13 +305,15 @@ def fold_roots(roots):
 
 def leaf_pairs(rows, tree: Tree, buckets):
     """(key, Σ row hash) of every key of `rows` in the given buckets, ascending."""
+    L = lib()
+    th = tree.terms.ptr() if tree.terms is not None else None
     k = rows[0]
     b = tree.bucket_of(k)
     m = np.isin(b, np.asarray(buckets, np.int64))
     keys, hs = [], []
     for i in np.flatnonzero(m):
-        h = int(lib().ref_row_hash(int(k[i]), int(rows[1][i]), int(rows[2][i]), int(rows[3][i]),
-                                   int(rows[4][i])))
+        h = int(L.ref_row_hash(int(k[i]), L.ref_term_val(th, int(rows[1][i])), int(rows[2][i]),
+                               L.ref_term_node(th, int(rows[3][i])), int(rows[4][i])))
         if keys and keys[-1] == int(k[i]):
             hs[-1] = (hs[-1] + h) & ((1 << 64) - 1)
         else:

@@ -14,6 +14,9 @@ Fixtures (one .npz each):
   history_*     random multi-replica histories (ops + directional syncs) with ts ties,
                 joined pairwise: join rows/context, read/1, and the Merkle diff
   config1_small config-1-shaped replicas (bench/basic_operations.exs style), 500 keys
+  term_hash_vectors.json  the canonical encoding, key id and node / value term hashes of
+                terms of every class (delta_crdt_ex_amd/interning.py; c_src/marshal.c
+                builds the same bytes and hashes, tests/test_term_hash.py checks both)
 """
 from __future__ import annotations
 
@@ -39,13 +42,13 @@ def snapshot_case():
     """tests/golden/snapshot_terms.dgsnap: what Storage.write persists after a delta,
     {node_id, sequence_number, crdt_state, merkle_map} (causal_crdt.ex:242-250), for a
     term-valued replica of history("terms", seed 7): its SoA rows and context through a
-    fresh Universe, and the depth-6 Merkle tree of the C oracle."""
+    fresh Universe, and the depth-6 Merkle tree of the C oracle over the rows' terms."""
     U = Universe()
     A = history(7, U, values=TERM_VALUES)[0]
     rows, ctx = CV.state_to_soa(A, U)
-    tree = R.merkle_build(rows, 6)
+    tree = R.merkle_build(rows, 6, terms=R.Terms(*U.term_tables()))  # a tree over terms
     storage.write_arrays(os.path.join(HERE, "snapshot_terms.dgsnap"), Atom("replica_a"), 3, rows,
-                         ctx, U, (6, 0, 0, tree.nodes))
+                         ctx, U, (6, 0, 0, tree.nodes, tree.counts))
     return A
 
 
@@ -148,7 +151,45 @@ def history(seed, U, n_keys=40, n_rep=3, steps=200, ts_ties=True, values=None):
     return reps
 
 
+# terms of every class the mirror has a stand-in for, with the boundaries of the closed-form
+# integer ids, bignums, the two zeros and nested containers
+VECTOR_TERMS = [
+    0, 1, -1, 255, 256, -(1 << 62) + (1 << 58), -(1 << 62) + (1 << 58) - 1, (1 << 62) - 1, 1 << 62,
+    (1 << 64) - 1, 1 << 64, -(1 << 64), 1 << 100, -(3 ** 50),
+    0.0, -0.0, 1.0, -2.5, 1e300, 5e-324,
+    Atom("a"), Atom("hello_world"), Atom("ünïcode"), None, True, False,
+    "", "k1", "ünïcode", b"\x00\xff",
+    (), (1,), (1, 2.0, "x"), ((), (Atom("n"), -1)),
+    EList(), EList([1, 2, 3]), EList([EList(), (1,)]),
+]
+
+
+def term_vectors():
+    """tests/golden/term_hash_vectors.json (see the module docstring)."""
+    import json
+    from delta_crdt_ex_amd import interning as I
+    from delta_crdt_ex_amd.storage import _pack
+    from oracle.erlterm import emap
+    terms = VECTOR_TERMS + [emap({1: 2, Atom("a"): "b"}), emap({2.0: 1, 2: (3,)}),
+                            (emap({}), EList([emap({0: 0})]))]
+    def jpack(x):  # storage._pack with binaries as hex (JSON-safe)
+        if isinstance(x, list):
+            if x and x[0] == "y":
+                return ["yh", x[1].hex()]
+            return [jpack(y) for y in x]
+        return x
+
+    out = []
+    for t in terms:
+        out.append({"term": jpack(_pack(t)), "canon": bytes(I.canon(t)).hex(), "key_id": str(I.key_id(t)),
+                    "node_hash": str(I.node_hash(t)), "value_hash": str(I.value_hash(t)),
+                    "canonical_value": I.is_canonical_int(t)})
+    with open(os.path.join(HERE, "term_hash_vectors.json"), "w") as f:
+        json.dump(out, f, indent=1, ensure_ascii=True)
+
+
 def main():
+    term_vectors()
     U = Universe()
     kats(U)
     for seed in range(4):
@@ -186,7 +227,7 @@ def main():
             B = T.join(B, T.add(k, k + 1, 2, B, n * 1000 + k), [k])
     write_case("config1_small", A, B, sorted(set(A.value) | set(B.value)), U,
                "config 1 shape (bench/basic_operations.exs), 500 keys")
-    print("wrote", sorted(f for f in os.listdir(HERE) if f.endswith((".npz", ".dgsnap"))))
+    print("wrote", sorted(f for f in os.listdir(HERE) if f.endswith((".npz", ".dgsnap", ".json"))))
 
 
 if __name__ == "__main__":

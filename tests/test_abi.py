@@ -30,7 +30,7 @@ def test_every_header_function_is_exported(lib):
 
 
 def test_abi_version(lib):
-    assert lib.dg_abi_version() == 2
+    assert lib.dg_abi_version() == 3
 
 
 LAYOUT_C = r"""
@@ -46,7 +46,10 @@ int main(void) {
   F(dg_context, kind) F(dg_context, node) F(dg_context, cnt) F(dg_context, n) F(dg_context, cap)
   printf("dg_merkle %zu\n", sizeof(dg_merkle));
   F(dg_merkle, depth) F(dg_merkle, shard_bits) F(dg_merkle, shard) F(dg_merkle, nodes)
-  F(dg_merkle, n_keys)
+  F(dg_merkle, n_keys) F(dg_merkle, counts) F(dg_merkle, terms)
+  printf("dg_term_hashes %zu\n", sizeof(dg_term_hashes));
+  F(dg_term_hashes, node_hash) F(dg_term_hashes, n_nodes) F(dg_term_hashes, val_id)
+  F(dg_term_hashes, val_hash) F(dg_term_hashes, n_vals)
   printf("dg_merkle_cont %zu\n", sizeof(dg_merkle_cont));
   F(dg_merkle_cont, level) F(dg_merkle_cont, pos) F(dg_merkle_cont, hash) F(dg_merkle_cont, n)
   F(dg_merkle_cont, cap) F(dg_merkle_cont, bucket) F(dg_merkle_cont, n_buckets)
@@ -67,12 +70,26 @@ def test_struct_layout_matches_header():
     for line in out.strip().splitlines():
         name, v = line.split()
         want[name] = int(v)
-    for cls in (_abi.dg_store, _abi.dg_context, _abi.dg_merkle, _abi.dg_merkle_cont):
+    for cls in (_abi.dg_store, _abi.dg_context, _abi.dg_merkle, _abi.dg_merkle_cont,
+                _abi.dg_term_hashes):
         assert C.sizeof(cls) == want[cls.__name__]
         for fname, _ in cls._fields_:
             key = f"{cls.__name__}.{fname}"
             if key in want:
                 assert getattr(cls, fname).offset == want[key], key
+
+
+def test_stale_library_is_refused(tmp_path, monkeypatch):
+    """The library embeds its sources' digest (dg_build_digest); a library built from other
+    sources is refused at load (a stale build must never be what runs)."""
+    lib = _abi.load()
+    assert lib.dg_build_digest().decode() == _abi.source_digest()
+    hdr = tmp_path / "deltagpu.h"
+    hdr.write_text(open(_abi.HEADER).read() + "\n/* changed */\n")
+    monkeypatch.setattr(_abi, "HEADER", str(hdr))
+    monkeypatch.setattr(_abi, "_lib", None)
+    with pytest.raises(RuntimeError, match="stale"):
+        _abi.load()
 
 
 def test_no_device_fails_loudly(lib):

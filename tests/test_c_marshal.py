@@ -38,3 +38,14 @@ def test_marshal_c_gpu():
     rc, out = early_result("c_marshal")
     assert rc == 0, out
     assert "gpu marshal/sort/join/read ok" in out and "gpu relabel remap ok" in out
+
+
+def test_nif_source_type_checks():
+    """c_src/deltagpu_nif.c compiles (-fsyntax-only, warnings as errors) against the erl_nif
+    API declarations restated in c_src/syntax_check/erl_nif.h -- this image has no
+    Erlang/OTP, so the NIF itself is built by the Elixir project."""
+    r = subprocess.run(["gcc", "-std=c11", "-Wall", "-Wextra", "-Werror", "-fsyntax-only",
+                        "-I", os.path.join(ROOT, "c_src", "syntax_check"),
+                        os.path.join(ROOT, "c_src", "deltagpu_nif.c")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr

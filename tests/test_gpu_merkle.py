@@ -45,6 +45,7 @@ def test_build_and_diff(engine, depth):
     for t, r in ((ta, ra), (tb, rb)):
         assert t.n_keys == r.n_keys
         assert np.array_equal(nodes(t), r.nodes)
+        assert np.array_equal(t.bucket_counts(), r.counts)
     d = engine.merkle_diff(ta, tb)
     assert np.array_equal(u64(d), R.store_diff(a["rows"], b["rows"]))
     assert engine.merkle_diff(ta, ta).numel() == 0
@@ -92,6 +93,7 @@ def test_update_after_join_equals_fresh_build(engine, seed):
         engine.merkle_update(t, out, changed)
         fresh = engine.merkle_build(out, depth)
         assert np.array_equal(nodes(t), nodes(fresh))
+        assert np.array_equal(t.bucket_counts(), fresh.bucket_counts())
         assert t.n_keys == fresh.n_keys
         assert t.store is out
 
@@ -103,7 +105,9 @@ def test_update_config2_scale(engine):
     t = engine.merkle_build(sa, 17)
     out, octx, changed = engine.join2_changes(sa, ca, sb, cb)
     engine.merkle_update(t, out, changed)
-    assert np.array_equal(nodes(t), nodes(engine.merkle_build(out, 17)))
+    fresh = engine.merkle_build(out, 17)
+    assert np.array_equal(nodes(t), nodes(fresh))
+    assert np.array_equal(t.bucket_counts(), fresh.bucket_counts())
     # no change: an update with no keys leaves the tree as it is
     before = nodes(t).copy()
     engine.merkle_update(t, out, keys_dev(np.zeros(0, np.uint64)))
@@ -200,3 +204,57 @@ def test_shard_trees_fold_to_the_unsharded_root(engine, bits):
     assert fold_roots(roots) == whole.root()
     with pytest.raises(DeltaGpuError):  # rows outside the tree's shard
         engine.merkle_build(up(a)[0], depth - bits, shard_bits=bits, shard=0)
+
+
+@pytest.mark.parametrize("depth,n_keys", [(12, 60000), (14, 60000), (3, 2000)])
+def test_dense_diff(engine, depth, n_keys):
+    """Every key differs: a subtree's differing rows overflow the LDS stage and its
+    buckets merge over global memory (and depth 3: subtrees of fewer than 16 buckets)."""
+    a, b = W.merkle_pair(n_keys=n_keys, diff_frac=1.0, seed=depth)
+    sa, _ = up(a)
+    sb, _ = up(b)
+    ta, tb = engine.merkle_build(sa, depth), engine.merkle_build(sb, depth)
+    full = R.store_diff(a["rows"], b["rows"])
+    assert len(full) == n_keys
+    got, total = engine.merkle_diff(ta, tb, cap=len(full) // 3, with_total=True)
+    assert total == len(full) and np.array_equal(u64(got), full[: len(full) // 3])
+    # one replica empty: every key of the other
+    e = Store.empty(1, DEV)
+    te = engine.merkle_build(e, depth)
+    assert np.array_equal(u64(engine.merkle_diff(ta, te)), np.unique(a["rows"][0]))
+
+
+def test_bucket_over_65535_rows_is_refused(engine):
+    k = np.zeros(70000, np.uint64)  # one key, 70,000 entries: one bucket
+    rows = (k, np.arange(70000, dtype=np.uint64), np.zeros(70000, np.int64),
+            np.zeros(70000, np.uint32), np.arange(1, 70001, dtype=np.uint64))
+    from delta_crdt_ex_amd._abi import CapacityError
+    with pytest.raises(CapacityError):
+        engine.merkle_build(Store.from_numpy(*rows, device=DEV), 4)
+
+
+def test_config4_shard_full_size(engine):
+    """BASELINE config 4 at the bench's per-GPU shard: 12.5M keys (a key-hash eighth of
+    100M), depth 22, the replicas differing on 1 % of the keys.  Diff == the exact
+    row-set diff; the sync delta Map.take(B.value, keys) joined into A over those keys
+    == the C oracle's join; the Merkle update of the changed keys == a fresh build."""
+    a, b = W.config4_shard(0, 8, keys_per_rank=12_500_000, diff_frac=0.01)
+    sa, ca = up(a)
+    sb, cb = up(b)
+    depth = 22
+    ta = engine.merkle_build(sa, depth, shard_bits=3, shard=0)
+    tb = engine.merkle_build(sb, depth, shard_bits=3, shard=0)
+    ra = R.merkle_build(a["rows"], depth, 3, 0)
+    assert np.array_equal(nodes(ta), ra.nodes) and np.array_equal(ta.bucket_counts(), ra.counts)
+    want = R.store_diff(a["rows"], b["rows"])
+    keys, total = engine.merkle_diff(ta, tb, with_total=True)
+    assert total == len(want) and np.array_equal(u64(keys), want)
+    delta = engine.take_keys(sb, keys)
+    out, octx, changed = engine.join2_changes(sa, ca, delta, cb, keys=keys)
+    wrows, wctx = R.join2(a["rows"], a["ctx"], tuple(c for c in delta.to_numpy()), b["ctx"], keys=want)
+    for x, y in zip(out.to_numpy(), wrows):
+        assert np.array_equal(x, y)
+    engine.merkle_update(ta, out, changed)
+    fresh = engine.merkle_build(out, depth, shard_bits=3, shard=0)
+    assert np.array_equal(nodes(ta), nodes(fresh))
+    assert np.array_equal(ta.bucket_counts(), fresh.bucket_counts())

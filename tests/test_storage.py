@@ -61,9 +61,17 @@ def test_golden_snapshot_matches_the_oracle():
     ok, ov = R.read_lww(rows)
     got = {U.key_term(int(k)): U.value_term(int(v)) for k, v in zip(ok, ov)}
     assert {k: repr(v) for k, v in got.items()} == {k: repr(v) for k, v in T.read(A).items()}
-    depth, sb, shard, nodes = merkle
+    depth, sb, shard, nodes, counts = merkle
     assert (depth, sb, shard) == (6, 0, 0)
-    assert np.array_equal(nodes, R.merkle_build(rows, 6).nodes)
+    want = R.merkle_build(rows, 6, terms=R.Terms(*U.term_tables()))  # a tree over terms
+    assert np.array_equal(nodes, want.nodes) and np.array_equal(counts, want.counts)
+
+
+def test_old_snapshot_layout_is_refused(tmp_path):
+    p = tmp_path / "old.dgsnap"
+    p.write_bytes(b"DGSNAP01" + bytes(16))
+    with pytest.raises(ValueError, match="DGSNAP01"):
+        storage.read_arrays(p)
 
 
 def test_snapshot_write_is_atomic(tmp_path):
@@ -95,8 +103,9 @@ def test_golden_snapshot_on_the_device():
     ctx = (st.ctx.kind,) + tuple(st.ctx.to_numpy())
     assert CV.soa_canon(rows, ctx, st.universe) == CV.term_canon(A)
     assert {k: repr(v) for k, v in M.read(st).items()} == {k: repr(v) for k, v in T.read(A).items()}
-    fresh = M.engine().merkle_build(st.rows, tree.depth)
+    fresh = M.merkle_map(st, tree.depth)
     assert np.array_equal(tree.nodes.cpu().numpy(), fresh.nodes.cpu().numpy())
+    assert np.array_equal(tree.bucket_counts(), fresh.bucket_counts())
     assert M.engine().merkle_diff(tree, fresh).numel() == 0
 
 
@@ -108,13 +117,12 @@ def test_snapshot_round_trip(tmp_path):
         st = M.join(st, M.add(k, v, Atom("node1"), st, ts=100 + i), [k])
     st = M.join(st, M.remove(Atom("b"), Atom("node1"), st), [Atom("b")])
     p = tmp_path / "replica.dgsnap"
-    tree = M.engine().merkle_build(st.rows, 5)
+    tree = M.merkle_map(st, 5)
     storage.write(p, Atom("node1"), 7, st, tree)
     node, seq, back, back_tree = storage.read(p)
     assert node == Atom("node1") and seq == 7
     assert back_tree.depth == 5 and back_tree.root() == tree.root()
-    assert np.array_equal(back_tree.nodes.cpu().numpy(),
-                          M.engine().merkle_build(back.rows, 5).nodes.cpu().numpy())
+    assert np.array_equal(back_tree.nodes.cpu().numpy(), M.merkle_map(back, 5).nodes.cpu().numpy())
     for x, y in zip(st.rows.to_numpy(), back.rows.to_numpy()):
         assert np.array_equal(x, y)
     for x, y in zip(st.ctx.to_numpy(), back.ctx.to_numpy()):
