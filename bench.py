@@ -100,34 +100,62 @@ def cpu_baseline(a, b, budget_s=6.0):
     }
 
 
+def _diff_accounting(ta, tb):
+    """Algorithmic bytes of a dg_merkle_diff (16 B per node pair visited +
+    8 B per differing key, plus what the descent reads to reach the rows: the u16 row
+    counts of both trees over every dirty subtree, and 36 B per row of a differing
+    bucket).  Node pairs visited: every subtree root, then both children of each
+    differing node, level by level (csrc/merkle.hip merkle_diff_count_kernel)."""
+    depth = ta.depth
+    sub = min(depth, 12)
+    Ls = depth - sub
+    na = ta.nodes.cpu().numpy().view(np.uint64)
+    nb = tb.nodes.cpu().numpy().view(np.uint64)
+    lvl = lambda a, l: a[(1 << l) - 1: (1 << (l + 1)) - 1]  # noqa: E731
+    differ = lvl(na, Ls) != lvl(nb, Ls)
+    dirty = int(differ.sum())
+    visited = 1 << Ls
+    for l in range(Ls + 1, depth + 1):
+        parent = np.repeat(differ, 2)
+        visited += 2 * int(differ.sum())
+        differ = parent & (lvl(na, l) != lvl(nb, l))
+    ca, cb = ta.bucket_counts(), tb.bucket_counts()
+    rows = int(ca[differ].astype(np.int64).sum() + cb[differ].astype(np.int64).sum())
+    return {"node_pairs_visited": visited, "dirty_subtrees": dirty, "subtrees": 1 << Ls,
+            "differing_buckets": int(differ.sum()), "rows_read": rows,
+            "bytes_no_keys": 16 * visited + 4 * dirty * (1 << sub) + 36 * rows}
+
+
 def config4_round(eng, torch, dev, rank=0, world=1, keys_per_rank=12_500_000, steps=10,
-                  max_sync_size=None):
+                  max_sync_size=None, cdev=None):
     """BASELINE config 4 on this rank's key-hash shard (12.5M keys per GPU: 100M over 8):
     two replicas differing on 1 % of the keys.  Measures
       * build: dg_merkle_build_async of both replicas' shard trees (MerkleMap over every
-        key), HIP events on the engine stream around `steps` builds -> the roofline of
-        the build kernels (36 B/row read + the bucket level written, read by the upsweep
-        and the upper levels written: 24 B/bucket);
+        key, rows hashed through their node TERMS: dg_term_hashes), HIP events on the
+        engine stream around `steps` builds -> the roofline of the one-launch build
+        (36 B/row read, the node heap written once: 16 B per bucket, the u16 row counts);
       * the anti-entropy round as CausalCrdt runs it (causal_crdt.ex:91-123,324-335,
         383-394), each a synchronous call: Merkle diff (keys, truncated to
         max_sync_size), the sync delta Map.take(B.value, keys) (dg_take_keys), the
         keyed join with its changed keys (dg_join2_changes), and the MerkleMap
         put/delete + update_hashes of those keys (dg_merkle_update, incremental);
+        the diff's roofline from its algorithmic bytes (_diff_accounting);
       * at world > 1: the shard roots all-gathered and folded (== the unsharded root)
-        and the VV all-reduce(max), over RCCL."""
-    import torch.distributed as dist
-
+        and the VV all-reduce(max) on the device context, over RCCL.
+    Returns the rank's dict and the (keys, seconds) its aggregate needs."""
     from delta_crdt_ex_amd import sharding as S
     from delta_crdt_ex_amd import workloads as W
-    from delta_crdt_ex_amd.store import Context, MerkleTree, Store
+    from delta_crdt_ex_amd.store import Context, MerkleTree, Store, TermHashes
     a, b = W.config4_shard(rank, max(world, 1), keys_per_rank=keys_per_rank, diff_frac=0.01)
+    N = a["nodes"]
+    terms = TermHashes(*N.universe.term_tables(), dev)  # node term hashes of the replicas
     sa, sb = Store.from_numpy(*a["rows"], device=dev), Store.from_numpy(*b["rows"], device=dev)
     ca, cb = Context.from_numpy(*a["ctx"], dev), Context.from_numpy(*b["ctx"], dev)
     sbits = S.shard_bits(world) if world > 1 else 0
     n_keys = len(a["rows"][0])
     depth = max(8, min(28, int(np.ceil(np.log2(max(n_keys, 2) / 3)))))  # ~3 keys per bucket
-    ta = MerkleTree.empty(depth, dev, sbits, rank if sbits else 0)
-    tb = MerkleTree.empty(depth, dev, sbits, rank if sbits else 0)
+    ta = MerkleTree.empty(depth, dev, sbits, rank if sbits else 0, terms)
+    tb = MerkleTree.empty(depth, dev, sbits, rank if sbits else 0, terms)
     dk = torch.zeros(8, dtype=torch.int64, device=dev)
     la, lb = eng.prepare_merkle_build(sa, ta, dk[0:1]), eng.prepare_merkle_build(sb, tb, dk[1:2])
     la(), lb()
@@ -142,15 +170,18 @@ def config4_round(eng, torch, dev, rank=0, world=1, keys_per_rank=12_500_000, st
     build_us = ev0.elapsed_time(ev1) * 1e3 / (2 * steps)
     rows = (sa.n + sb.n) / 2
     nb = 1 << depth
-    build_alg = 36 * rows + 24 * nb
+    build_alg = 36 * rows + 16 * nb + 2 * nb
     eng.merkle_build(sa, depth, ta, sbits, rank if sbits else 0)  # n_keys, shard check
     eng.merkle_build(sb, depth, tb, sbits, rank if sbits else 0)
     cap = max_sync_size or (ta.n_keys + tb.n_keys)
 
     def one_round():
         t = {}
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
+        e0.record(eng.stream)
         keys, total = eng.merkle_diff(ta, tb, cap=cap, with_total=True)
+        e1.record(eng.stream)
         t1 = time.perf_counter()
         delta = eng.take_keys(sb, keys)
         t2 = time.perf_counter()
@@ -162,27 +193,41 @@ def config4_round(eng, torch, dev, rank=0, world=1, keys_per_rank=12_500_000, st
         torch.cuda.synchronize()
         t5 = time.perf_counter()
         t.update(diff=t1 - t0, take=t2 - t1, join=t3 - t2, update=t5 - t4, total=(t5 - t4) + (t3 - t0),
+                 diff_ev=e0.elapsed_time(e1) * 1e-3,
                  keys=int(keys.numel()), total_keys=total, rows=delta.n, changed=int(changed.numel()))
-        t["ok"] = tt.root() == eng.merkle_build(out, depth, None, sbits, rank if sbits else 0).root()
+        t["ok"] = tt.root() == eng.merkle_build(out, depth, None, sbits, rank if sbits else 0,
+                                                terms=terms).root()
         return t
 
     one_round()
     rounds = [one_round() for _ in range(5)]
-    med = {k: float(np.median([r[k] for r in rounds])) for k in ("diff", "take", "join", "update", "total")}
+    med = {k: float(np.median([r[k] for r in rounds]))
+           for k in ("diff", "take", "join", "update", "total", "diff_ev")}
     last = rounds[-1]
+    acc = _diff_accounting(ta, tb)
+    diff_alg = acc["bytes_no_keys"] + 8 * last["total_keys"]
     res = {
         "metric": "Merkle diff keys/s, config 4 (key-hash shard of 100M keys, 1 % differing)",
         "keys_per_gpu": n_keys, "depth": depth, "shard_bits": sbits,
         "value": 2 * n_keys / (2 * build_us * 1e-6 + med["diff"]), "unit": "keys/s",
         "note": "value = keys of both replicas / (hash both: two full builds + the diff)",
         "build_us": build_us,
-        "roofline": {"bound": "hbm", "kernel": "merkle_build_kernel + merkle_upsweep_kernel",
+        "roofline": {"bound": "hbm", "kernel": "merkle_chunk_kernel<BUILD> (one launch)",
                      "alg_bytes_per_launch": build_alg, "avg_launch_us": build_us,
                      "achieved": build_alg / (build_us * 1e-6) / 1e9, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s",
                      "frac": build_alg / (build_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
                      "launch_timing": "HIP events on the engine stream around the async builds"},
-        "round_us": {k: v * 1e6 for k, v in med.items()},
+        "diff_roofline": {"bound": "hbm",
+                          "kernel": "merkle_diff_bounds + merkle_diff_count (descent) + merkle_diff_write",
+                          "alg_bytes_per_call": diff_alg, "avg_call_us": med["diff_ev"] * 1e6,
+                          "achieved": diff_alg / med["diff_ev"] / 1e9, "peak": HBM_PEAK_GBS,
+                          "unit": "GB/s", "frac": diff_alg / med["diff_ev"] / 1e9 / HBM_PEAK_GBS,
+                          **acc,
+                          "launch_timing": "HIP events on the engine stream around one "
+                                           "synchronous dg_merkle_diff (its kernels + the count "
+                                           "publish), median of 5 rounds"},
+        "round_us": {k: v * 1e6 for k, v in med.items() if k != "diff_ev"},
         "round_keys": last["keys"], "round_total_keys": last["total_keys"],
         "round_delta_rows": last["rows"], "round_changed_keys": last["changed"],
         "update_equals_rebuild": all(r["ok"] for r in rounds),
@@ -192,11 +237,10 @@ def config4_round(eng, torch, dev, rank=0, world=1, keys_per_rank=12_500_000, st
     if world > 1:
         t0 = time.perf_counter()
         roots_a, root_a = S.merkle_roots(ta.root())
-        node, cnt = ca.to_numpy()
-        S.vv_allreduce_max(node, cnt)
+        S.vv_allreduce_max_context(ca, len(N.dense))
         res["collectives_us"] = (time.perf_counter() - t0) * 1e6
         res["replica_root"] = hex(root_a)
-    return res
+    return res, (2 * n_keys, 2 * build_us * 1e-6 + med["diff"])
 
 
 def _timed(torch, fn, reps):
@@ -212,15 +256,17 @@ def _timed(torch, fn, reps):
     return float(np.median(ts))
 
 
-def config3_rate(eng, torch, dev, n_keys=10_000_000, reps=3):
+def config3_rate(eng, torch, dev, rank=0, world=1, n_keys=10_000_000, reps=3):
     """Config 3: 64 sync-shaped deltas (1 % of the keys each, 80 % adds / 20 % removes)
     applied to a 10M-key state with dg_apply_deltas (the fold of join/3 with each
-    delta's keys; one pass over the state, csrc/kfold.hip).  Rate = (state rows + delta
-    rows) / wall time, SURVEY §8(d)'s N_in ≈ 15M; the delta-by-delta fold is timed beside
-    it (DG_APPLY_MODE=fold)."""
+    delta's keys; one pass over the state, csrc/kfold.hip).  At N ranks the state and
+    every delta are split by key hash (strong scaling: each rank folds its shard).  Rate
+    = (state rows + delta rows) / wall time, SURVEY §8(d)'s N_in ≈ 15M; at N = 1 the
+    delta-by-delta fold is timed beside it (DG_APPLY_MODE=fold).  The call's device time
+    comes from HIP events around back-to-back prepared calls."""
     from delta_crdt_ex_amd import workloads as W
     from delta_crdt_ex_amd.store import Context, Engine, Store
-    base, deltas = W.config3(n_keys=n_keys, n_replicas=64, touch=0.01, seed=3)
+    base, deltas = W.config3_shard(rank, world, n_keys=n_keys)
     sb = Store.from_numpy(*base["rows"], device=dev)
     cb = Context.from_numpy(*base["ctx"], dev)
     ds = [Store.from_numpy(*d["rows"], device=dev) for d in deltas]
@@ -237,27 +283,47 @@ def config3_rate(eng, torch, dev, n_keys=10_000_000, reps=3):
     call = eng.prepare_apply_deltas(sb, cb, ds, dc, ks, out, octx)  # marshalled once
     el = _timed(torch, call, reps)
     res["n"] = out.n
-    os.environ["DG_APPLY_MODE"] = "fold"
-    try:
-        fe = Engine(0)
-    finally:
-        del os.environ["DG_APPLY_MODE"]
-    n_one = res["n"]
-    el_fold = _timed(torch, lambda: run(fe), reps)
-    fe.close()
-    assert res["n"] == n_one
+    # the call's device time: events around back-to-back calls (each ends in a host sync,
+    # so this includes the synchronous call's gaps; rocprofv3 gives the kernels alone)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(eng.stream)
+    for _ in range(reps):
+        call()
+    ev1.record(eng.stream)
+    torch.cuda.synchronize()
+    el_ev = ev0.elapsed_time(ev1) * 1e-3 / reps
+    el_fold = None
+    if world == 1:
+        os.environ["DG_APPLY_MODE"] = "fold"
+        try:
+            fe = Engine(0)
+        finally:
+            del os.environ["DG_APPLY_MODE"]
+        n_one = res["n"]
+        el_fold = _timed(torch, lambda: run(fe), reps)
+        fe.close()
+        assert res["n"] == n_one
     d_rows = sum(d.n for d in ds)
     n_keys_total = sum(int(k.numel()) for k in ks)
     rows_in = sb.n + d_rows
     alg = 36 * (rows_in + res["n"]) + 8 * n_keys_total
-    return {"metric": "merged dots/s, config 3 (64 keyed sync deltas into a 10M-key state)",
-            "value": rows_in / el, "unit": "merged dots/s", "ms_per_batch": el * 1e3,
-            "alg_bytes": alg, "alg_GBps": alg / el / 1e9,
-            "alg_frac": alg / el / 1e9 / HBM_PEAK_GBS,  # of the HBM peak, over the whole call
-            "state_rows": sb.n, "delta_rows": d_rows, "keyset_entries": n_keys_total,
-            "rows_out": res["n"], "stepwise_ms_per_batch": el_fold * 1e3,
-            "note": "dg_apply_deltas, synchronous (one host sync), arguments marshalled once "
-                    "(prepare_apply_deltas); stepwise = 64 joins of join/3 back to back"}
+    r = {"metric": "merged dots/s, config 3 (64 keyed sync deltas into a 10M-key state)",
+         "value": rows_in / el, "unit": "merged dots/s", "ms_per_batch": el * 1e3,
+         "alg_bytes": alg, "alg_GBps": alg / el / 1e9,
+         "alg_frac": alg / el / 1e9 / HBM_PEAK_GBS,  # of the HBM peak, over the whole call
+         "roofline": {"bound": "hbm", "kernel": "kfold_fill_kernel + kfold_kernel",
+                      "alg_bytes_per_launch": alg, "avg_launch_us": el_ev * 1e6,
+                      "achieved": alg / el_ev / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                      "frac": alg / el_ev / 1e9 / HBM_PEAK_GBS,
+                      "launch_timing": f"HIP events on the engine stream around {reps} "
+                                       "back-to-back prepared dg_apply_deltas calls"},
+         "state_rows": sb.n, "delta_rows": d_rows, "keyset_entries": n_keys_total,
+         "rows_out": res["n"],
+         "note": "dg_apply_deltas, synchronous (one host sync), arguments marshalled once "
+                 "(prepare_apply_deltas); stepwise = 64 joins of join/3 back to back"}
+    if el_fold is not None:
+        r["stepwise_ms_per_batch"] = el_fold * 1e3
+    return r, (rows_in, el)
 
 
 def changes_rate(eng, torch, pr, reps=20):
@@ -325,15 +391,17 @@ def e2e_rate(eng, torch, pr, reps=20):
                     "median of reps"}
 
 
-def config5_rate(eng, torch, dev, n_keys=12_500_000, reps=5, steps=20):
+def config5_rate(eng, torch, dev, rank=0, world=1, n_keys=12_500_000, reps=5, steps=20):
     """Config 5 at one GPU's share of 100M keys over 8 GPUs: full-state join of two
     remove-heavy replicas (50 % removes, 64 nodes, ts in [0,16): LWW ties everywhere),
-    then read/1 of the result."""
+    then read/1 of the result.  At N ranks each rank joins its key-hash shard of
+    N x 12.5M keys (weak scaling: 100M keys at N = 8)."""
     from delta_crdt_ex_amd import workloads as W
     from delta_crdt_ex_amd.store import Context, Store
-    a, b = W.config5(n_keys=n_keys, n_nodes=64, seed=5)
+    a, b = W.config5_shard(rank, world, keys_per_rank=n_keys)
     sa, sb = Store.from_numpy(*a["rows"], device=dev), Store.from_numpy(*b["rows"], device=dev)
     ca, cb = Context.from_numpy(*a["ctx"], dev), Context.from_numpy(*b["ctx"], dev)
+    del a, b
     out = Store.empty(sa.n + sb.n, dev)
     octx = Context.empty(0, ca.n + cb.n, dev)
     res = {}
@@ -364,21 +432,22 @@ def config5_rate(eng, torch, dev, n_keys=12_500_000, reps=5, steps=20):
     tr = _timed(torch, read, reps)
     n_in = sa.n + sb.n
     alg = 36 * (n_in + out.n)
-    return {"metric": "merged dots/s, config 5 (remove-heavy, LWW ties), 12.5M keys per GPU",
-            "value": n_in / tj, "unit": "merged dots/s", "ms_per_join": tj * 1e3,
-            "join_alg_GBps": alg / tj / 1e9,
-            "roofline": {"bound": "hbm", "kernel": "join2_partition_kernel + join2_stream_kernel",
-                         "alg_bytes_per_launch": alg, "avg_launch_us": tk * 1e6,
-                         "achieved": alg / tk / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": alg / tk / 1e9 / HBM_PEAK_GBS,
-                         "launch_timing": f"HIP events on the engine stream around {steps} "
-                                          "back-to-back dg_join2_async launches"},
-            "rows_in": n_in, "rows_out": out.n, "ms_per_read": tr * 1e3,
-            "read_rows_per_s": out.n / tr, "read_keys_per_s": res["keys"] / tr,
-            "read_keys": res["keys"], "read_alg_GBps": (36 * out.n + 16 * res["keys"]) / tr / 1e9,
-            "note": "value / ms_per_join: one dg_join2_async + host sync per join (arguments "
-                    "marshalled once); roofline: the launches back to back; dg_read_lww "
-                    "synchronous"}
+    r = {"metric": "merged dots/s, config 5 (remove-heavy, LWW ties), 12.5M keys per GPU",
+         "value": n_in / tj, "unit": "merged dots/s", "ms_per_join": tj * 1e3,
+         "join_alg_GBps": alg / tj / 1e9,
+         "roofline": {"bound": "hbm", "kernel": "join2_partition_kernel + join2_stream_kernel",
+                      "alg_bytes_per_launch": alg, "avg_launch_us": tk * 1e6,
+                      "achieved": alg / tk / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                      "frac": alg / tk / 1e9 / HBM_PEAK_GBS,
+                      "launch_timing": f"HIP events on the engine stream around {steps} "
+                                       "back-to-back dg_join2_async launches"},
+         "rows_in": n_in, "rows_out": out.n, "ms_per_read": tr * 1e3,
+         "read_rows_per_s": out.n / tr, "read_keys_per_s": res["keys"] / tr,
+         "read_keys": res["keys"], "read_alg_GBps": (36 * out.n + 16 * res["keys"]) / tr / 1e9,
+         "note": "value / ms_per_join: one dg_join2_async + host sync per join (arguments "
+                 "marshalled once); roofline: the launches back to back; dg_read_lww "
+                 "synchronous"}
+    return r, (n_in, tj)
 
 
 def read_runs_rate(eng, torch, dev, n_keys=1_000_000, max_entries=32, reps=5):
@@ -579,19 +648,38 @@ def main():
                 "per_step_event_median_us": step_event_median_us,
             },
         }
-    if not args.no_merkle:  # every rank runs its shard's round; rank 0 reports its own
-        c4 = config4_round(eng, torch, dev, rank, world)
-        if rank == 0:
-            res["merkle"] = c4
+    def aggregate(r, units_secs):
+        """Σ over ranks of the units, max over ranks of the time: the whole-job figure."""
+        units, secs = units_secs
+        if world > 1:
+            u = torch.tensor([float(units)], dtype=torch.float64, device=cdev)
+            t = torch.tensor([float(secs)], dtype=torch.float64, device=cdev)
+            dist.all_reduce(u, op=dist.ReduceOp.SUM)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            units, secs = float(u.item()), float(t.item())
+        r["aggregate"] = {"ranks": world, "value": units / secs, "units": units,
+                          "max_rank_seconds": secs,
+                          "note": "Σ units over ranks / max time over ranks (rank 0's own "
+                                  "figures above)"}
+        return r
+
+    secondaries = {}
+    if not args.no_merkle:  # every rank runs its shard's round
+        secondaries["merkle"] = aggregate(*config4_round(eng, torch, dev, rank, world, cdev=cdev))
+    if not args.no_configs:
+        if world == 1:  # per-GPU secondaries of the config-2 pair: measured at N = 1
+            secondaries["changes"] = changes_rate(eng, torch, pairs[0])
+            secondaries["end_to_end"] = e2e_rate(eng, torch, pairs[0])
+        for r in pairs:  # free the config-2 replicas before the larger configs
+            r.clear()
+        torch.cuda.empty_cache()
+        secondaries["config3"] = aggregate(*config3_rate(eng, torch, dev, rank, world))
+        torch.cuda.empty_cache()
+        secondaries["config5"] = aggregate(*config5_rate(eng, torch, dev, rank, world))
+        if world == 1:
+            secondaries["read_runs32"] = read_runs_rate(eng, torch, dev)
     if rank == 0:
-        if not args.no_configs and world == 1:  # per-GPU secondaries: measured at N=1
-            res["changes"] = changes_rate(eng, torch, pairs[0])
-            res["end_to_end"] = e2e_rate(eng, torch, pairs[0])
-            for r in pairs:  # free the config-2 replicas before the larger configs
-                r.clear()
-            res["config3"] = config3_rate(eng, torch, dev)
-            res["config5"] = config5_rate(eng, torch, dev)
-            res["read_runs32"] = read_runs_rate(eng, torch, dev)
+        res.update(secondaries)
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(a, b)
         elif not args.no_cpu_baseline:

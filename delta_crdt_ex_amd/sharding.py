@@ -6,8 +6,9 @@ floor(key * N / 2^64) == s.  Join and read are per key, so every rank joins its 
 shard with no data exchange.  The only cross-rank steps are tiny:
 
 * the causal context: every shard carries the replica's full VV, so the union is
-  computed redundantly on every rank; `vv_allreduce_max` is the RCCL (or gloo)
-  all-reduce that keeps them identical when shards were updated independently;
+  computed redundantly on every rank; `vv_allreduce_max_context` is the RCCL (or gloo)
+  all-reduce that keeps them identical when shards were updated independently -- on the
+  context's own device tensors (`vv_allreduce_max` is the host-array form);
 * the Merkle tree: each rank builds the tree of its shard's key range (a level-log2(N)
   subtree of the unsharded tree); `merkle_roots` all-gathers the N shard roots (8 bytes
   each) and folds them into the replica's root -- the unsharded tree's root, so roots
@@ -102,6 +103,39 @@ def vv_allreduce_max(node: np.ndarray, cnt: np.ndarray, group=None):
     out = t.cpu().numpy()[:m]
     have = np.flatnonzero(out)
     return have.astype(np.uint32), (out[have] - 1).astype(np.uint64)
+
+
+def vv_allreduce_max_context(ctx, n_nodes: int, group=None):
+    """All-reduce(max) of a device version vector (store.Context, kind VV) across the
+    ranks of `group`, without leaving the device: the VV is scattered into a dense counter
+    vector indexed by node id (counter + 1; 0 = absent), all-reduced with MAX (RCCL over
+    xGMI on MI355X: one latency-bound all-reduce of n_nodes x 8 bytes), and compacted back
+    to (node, counter) pairs.  The ranks' node ids must be one interning (a replica set's
+    shards share its dense ids) and n_nodes their common count; counters < 2^63 - 1.
+    Dots.union/2 of VVs (aw_lww_map.ex:39-52) across key-hash shards."""
+    import torch
+    import torch.distributed as dist
+
+    from .store import DG_CTX_VV, Context
+    if ctx.kind != DG_CTX_VV:
+        raise ValueError("vv_allreduce_max_context: the context is not a version vector")
+    dev = ctx.node.device
+    cdev = _coll_device(group)
+    n = ctx.n
+    dense = torch.zeros(max(int(n_nodes), 1), dtype=torch.int64, device=dev)
+    if n:
+        dense.scatter_(0, ctx.node[:n].long(), ctx.cnt[:n] + 1)
+    t = dense if cdev.type == dev.type else dense.to(cdev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    if t is not dense:
+        dense = t.to(dev)
+    node = torch.nonzero(dense).squeeze(1)
+    m = int(node.numel())
+    out = Context.empty(DG_CTX_VV, max(m, 1), dev)
+    out.node[:m] = node.to(torch.int32)
+    out.cnt[:m] = dense[node] - 1
+    out.n = m
+    return out
 
 
 def _mix64(x: int) -> int:

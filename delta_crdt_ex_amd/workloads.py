@@ -258,7 +258,7 @@ def _take_rows(rows, key_ids):
 
 
 def config3(n_keys: int = 10_000_000, n_replicas: int = 64, touch: float = 0.01,
-            remove_frac: float = 0.2, seed: int = 3, nodes: NodeTable | None = None):
+            remove_frac: float = 0.2, seed: int = 3, nodes: NodeTable | None = None, keys=None):
     """Config 3: a base state (node 0 wrote k = 1..n, counter k, ts = k * 1000) and
     `n_replicas` replicas (nodes 1..R) that each touched ~touch * n keys of it: 80 %
     re-added (AWLWWMap.add/4: the key's old entries go, one new entry with dot
@@ -268,9 +268,11 @@ def config3(n_keys: int = 10_000_000, n_replicas: int = 64, touch: float = 0.01,
 
     Returns (base, deltas) where base = {"rows", "ctx"} and each delta =
     {"rows", "ctx", "keys"} (keys: ascending unique key ids).  Applying them is the
-    fold join(state, delta_r, keys_r) over r = 1..R (causal_crdt.ex:383-384)."""
+    fold join(state, delta_r, keys_r) over r = 1..R (causal_crdt.ex:383-384).
+    `keys` (uint64 array of k) overrides the key range (a key-hash shard)."""
     N = nodes or NodeTable(n_replicas + 1, seed)
-    k = np.arange(1, n_keys + 1, dtype=np.uint64)
+    k = np.arange(1, n_keys + 1, dtype=np.uint64) if keys is None else np.asarray(keys, np.uint64)
+    n_keys = len(k)
     key = splitmix64_np(k)
     base = {"rows": sort_rows(key, encode_int_value(k.astype(np.int64)),
                               k.astype(np.int64) * 1000, np.full(n_keys, N[0], np.uint32), k.copy()),
@@ -305,6 +307,28 @@ def config4_shard(rank: int, world: int, keys_per_rank: int = 12_500_000,
                        n_total=world * keys_per_rank)
 
 
+def shard_keys(rank: int, world: int, n_total: int) -> np.ndarray:
+    """The integer keys k in 1..n_total whose key id falls in key-hash shard `rank`."""
+    k = np.arange(1, n_total + 1, dtype=np.uint64)
+    if world == 1:
+        return k
+    return k[shard_of(splitmix64_np(k), world) == rank]
+
+
+def config5_shard(rank: int, world: int, keys_per_rank: int = 12_500_000, seed: int = 5):
+    """Config 5 at weak scaling: key-hash shard `rank` of world * keys_per_rank keys (100M
+    over 8 GPUs), each rank's pair drawn with the config-5 distribution (seed per rank)."""
+    return config5(keys=shard_keys(rank, world, world * keys_per_rank), n_nodes=64,
+                   seed=seed + 1000 * rank if world > 1 else seed)
+
+
+def config3_shard(rank: int, world: int, n_keys: int = 10_000_000, seed: int = 3):
+    """Config 3 split over ranks (strong scaling): key-hash shard `rank` of the 10M-key
+    state and of every replica's delta (each touches 1 % of the shard's keys)."""
+    return config3(keys=shard_keys(rank, world, n_keys), n_replicas=64, touch=0.01,
+                   seed=seed + 1000 * rank if world > 1 else seed)
+
+
 def sync_delta(rep, keys):
     """The sync message a replica sends for `keys` (causal_crdt.ex:324-335): its
     context and Map.take of its rows; `keys` ascending unique key ids."""
@@ -314,17 +338,19 @@ def sync_delta(rep, keys):
 
 def config5(n_keys: int = 100_000_000, n_nodes: int = 64, remove_frac: float = 0.5,
             readd_frac: float = 0.2, ts_range: int = 16, max_entries: int = 3, seed: int = 5,
-            nodes: NodeTable | None = None):
+            nodes: NodeTable | None = None, keys=None):
     """Config 5, remove-heavy adversarial pair.  Base: every key holds 1..max_entries
     concurrent entries written by random nodes 0..n_nodes-3 (dots {node, c}, c
     counting per node in key order), small values and ts in [0, ts_range) so LWW ties
     are everywhere.  Replicas A (node n_nodes-2) and B (node n_nodes-1) each saw the
     whole base (dense VVs: they cover every dot they hold) and then independently
     removed `remove_frac` of the keys and re-added (add/4: the key's entries replaced
-    by one new entry) `readd_frac` of the rest.  Returns (A, B)."""
+    by one new entry) `readd_frac` of the rest.  `keys` (uint64 array of k) overrides
+    the key range (a key-hash shard).  Returns (A, B)."""
     N = nodes or NodeTable(n_nodes, seed)
     rng = np.random.default_rng(seed)
-    k = np.arange(1, n_keys + 1, dtype=np.uint64)
+    k = np.arange(1, n_keys + 1, dtype=np.uint64) if keys is None else np.asarray(keys, np.uint64)
+    n_keys = len(k)
     key = splitmix64_np(k)
     ne = rng.integers(1, min(max_entries, n_nodes - 2) + 1, n_keys)
     ekey = np.repeat(key, ne)

@@ -15,7 +15,8 @@ RCCL.  Each rank, on its shard of two replicas A and B that differ on 2 % of the
     differing keys -- takes B's sync delta for them (dg_take_keys) and joins it into A
     with its changed keys (dg_join2_changes): the shard's slice of the oracle's
     full-state join;
-  * all-reduces the joined version vector (sharding.vv_allreduce_max): the oracle's;
+  * all-reduces the joined version vector (sharding.vv_allreduce_max and, on the
+    device tensors, vv_allreduce_max_context): the oracle's;
   * updates A's tree from the changed keys (dg_merkle_update): equal to a fresh build,
     and the joined replica's folded root is the oracle's root of the joined rows.
 
@@ -88,6 +89,10 @@ def _rank(rank, world, port, kpr, q):
             assert np.array_equal(x, y), "shard join rows"
         node, cnt = S.vv_allreduce_max(*octx.to_numpy())
         assert np.array_equal(node, want_ctx[1]) and np.array_equal(cnt, want_ctx[2]), "VV"
+        # on the device tensors themselves (gloo takes a host hop; RCCL stays on the GPU)
+        vv = S.vv_allreduce_max_context(octx, len(a["nodes"].dense))
+        gn, gc = vv.to_numpy()
+        assert np.array_equal(gn, want_ctx[1]) and np.array_equal(gc, want_ctx[2]), "device VV"
 
         eng.merkle_update(ta, out, changed)
         fresh = eng.merkle_build(out, d, shard_bits=sb_bits, shard=rank)

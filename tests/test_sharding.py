@@ -67,6 +67,18 @@ def _worker(rank, world, port, q):
             node, cnt = S.vv_allreduce_max(ctx[1], ctx[2])
             want_rows, want_ctx = R.join2(A["rows"], A["ctx"], B["rows"], B["ctx"])
             assert np.array_equal(node, want_ctx[1]) and np.array_equal(cnt, want_ctx[2])
+            # the same on the context's own tensors (no host arrays): this rank's VV is
+            # its own half of the union, the all-reduce restores the whole
+            import torch
+            from delta_crdt_ex_amd.store import Context
+            half = (slice(None, None, 2) if rank == 0 else slice(1, None, 2))
+            hn, hc = ctx[1][half], ctx[2][half]
+            c = Context(ctx[0], torch.from_numpy(hn.astype(np.int32)),
+                        torch.from_numpy(np.ascontiguousarray(hc).view(np.int64)), len(hn))
+            n_nodes = int(max(A["ctx"][1].max(initial=0), B["ctx"][1].max(initial=0))) + 1
+            got = S.vv_allreduce_max_context(c, n_nodes)
+            gn, gc = got.to_numpy()
+            assert np.array_equal(gn, want_ctx[1]) and np.array_equal(gc, want_ctx[2])
             # the shard's output is exactly the unsharded output's slice
             want_mine = S.split_rows(want_rows, world)[rank]
             for x, y in zip(rows, want_mine):
