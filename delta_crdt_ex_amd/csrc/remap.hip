@@ -3,8 +3,11 @@
 //
 // Value ids are order-preserving ranks in Erlang term order (the read
 // tie-break of aw_lww_map.ex:211-216) allocated with gaps; when a gap is used up the
-// host re-spaces every id.  The map old id -> new id is strictly increasing, so a
-// store stays sorted by (key, val, ts, node, cnt) and the rewrite is one streaming
+// host re-spaces the ids of one region (interning.py / marshal.c: the table values below
+// and above the canonical integers).  The map old id -> new id is strictly increasing and
+// keeps each id inside its region, so ids outside [old_ids[0], old_ids[n-1]] (canonical
+// integers, the other region) pass unchanged, a store stays sorted by
+// (key, val, ts, node, cnt) and the rewrite is one streaming
 // pass over the val column: 8 B read + 8 B written per row, plus a binary search in
 // the (L2-resident) id table.  The table is staged in LDS in 2048-entry slices when
 // it is small enough to fit; larger tables are searched in global memory.
@@ -40,11 +43,12 @@ __global__ __launch_bounds__(RB) void remap_values_kernel(u64* val, u64 n, const
   for (u64 i = (u64)blockIdx.x * RB + threadIdx.x; i < n; i += (u64)gridDim.x * RB) {
     const u64 v = val[i];
     const u64 j = staged ? lower_bound_u64(s_old, n_ids, v) : lower_bound_u64(old_ids, n_ids, v);
-    const bool hit = j < n_ids && (staged ? s_old[j] : old_ids[j]) == v;
-    if (hit)
+    const bool inside = j < n_ids && (j > 0 || v == (staged ? s_old[0] : old_ids[0]));
+    if (!inside) continue;  // outside the relabelled region: unchanged
+    if ((staged ? s_old[j] : old_ids[j]) == v)
       val[i] = new_ids[j];
     else
-      atomicOr(err, 1u);
+      atomicOr(err, 1u);  // inside the region but not in its table: a stale id
   }
 }
 

@@ -305,10 +305,12 @@ int dg_sort_context(dg_engine* e, const dg_context* in, dg_context* out);
 /* ---- interning maintenance -------------------------------------------------- */
 /* Value ids are order-preserving ranks in Erlang term order with gaps (the read
  * tie-break, aw_lww_map.ex:211-216).  When the host's value table runs out of room
- * between two neighbours it re-spaces every id (a strictly increasing map); this
- * rewrites s->val in place: val = new_ids[j] where old_ids[j] == val.  old_ids /
- * new_ids: device arrays of n_ids entries, both ascending.  The store stays sorted.
- * DG_E_INVAL if a row's value is not in old_ids.  Synchronous. */
+ * between two neighbours it re-spaces the ids of that region (a strictly increasing
+ * map inside the region); this rewrites s->val in place: val = new_ids[j] where
+ * old_ids[j] == val; values outside [old_ids[0], old_ids[n_ids-1]] (canonical integers,
+ * the other region) are left as they are.  old_ids / new_ids: device arrays of n_ids
+ * entries, both ascending.  The store stays sorted.  DG_E_INVAL if a row's value lies
+ * inside that range but is not in old_ids (a stale id).  Synchronous. */
 int dg_remap_values(dg_engine* e, dg_store* s, const uint64_t* old_ids, const uint64_t* new_ids,
                     uint64_t n_ids);
 

@@ -186,3 +186,38 @@ def test_config4_round_device_resident(engine, rank):
     wr, wc = R.join2(a["rows"], a["ctx"], b["rows"], b["ctx"])
     rows_eq(out, wr)
     ctx_eq(octx, wc)
+
+
+@pytest.mark.timeout(600)
+def test_config4_full_shard_round(engine):
+    """The bench's config-4 round at its own size: one 12.5M-key shard of 100M keys
+    (rank 3 of 8, depth 22, trees hashed through node terms), two replicas differing on
+    1 % of the keys.  Merkle diff == the oracle's differing keys; the keyed join of the
+    sync delta Map.take(B, diff) with its changed keys == the full-state join; the
+    incremental tree update == a fresh build of the joined store."""
+    from delta_crdt_ex_amd.store import MerkleTree, TermHashes
+    rank, world = 3, 8
+    a, b = W.config4_shard(rank, world, keys_per_rank=12_500_000, diff_frac=0.01)
+    terms = TermHashes(*a["nodes"].universe.term_tables(), DEV)
+    sa, ca = up(a)
+    sb, cb = up(b)
+    depth = 22
+    ta = engine.merkle_build(sa, depth, MerkleTree.empty(depth, DEV, 3, rank, terms), 3, rank)
+    tb = engine.merkle_build(sb, depth, MerkleTree.empty(depth, DEV, 3, rank, terms), 3, rank)
+    diff, total = engine.merkle_diff(ta, tb, with_total=True)
+    want = R.store_diff(a["rows"], b["rows"])
+    assert total == len(want) and np.array_equal(u64(diff), want)
+    cap = 1000  # max_sync_size: the first keys in key order, and the total
+    first, total_c = engine.merkle_diff(ta, tb, cap=cap, with_total=True)
+    assert total_c == len(want) and np.array_equal(u64(first), want[:cap])
+    delta = engine.take_keys(sb, diff)
+    rows_eq(delta, W.sync_delta(b, want)["rows"])
+    out, octx, changed = engine.join2_changes(sa, ca, delta, cb, keys=diff)
+    wr, wc = R.join2(a["rows"], a["ctx"], b["rows"], b["ctx"])
+    rows_eq(out, wr)
+    ctx_eq(octx, wc)
+    tt = ta.clone()
+    engine.merkle_update(tt, out, changed)
+    fresh = engine.merkle_build(out, depth, None, 3, rank, terms=terms)
+    assert np.array_equal(tt.nodes.cpu().numpy(), fresh.nodes.cpu().numpy())
+    assert tt.root() == tb.root()  # the joined shard holds exactly B's rows of the shard

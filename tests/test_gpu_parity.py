@@ -349,3 +349,26 @@ def test_sort_context_dots(engine):
     c = Context.from_numpy(W.DOTS, pairs[perm, 0].astype(np.uint32), pairs[perm, 1].astype(np.uint64), DEV)
     got = engine.sort_context(c)
     ctx_eq(got, (W.DOTS, pairs[:, 0].astype(np.uint32), pairs[:, 1].astype(np.uint64)))
+
+
+def test_remap_values_region_local(engine):
+    """dg_remap_values rewrites only the relabelled region's ids (ids outside
+    [old_ids[0], old_ids[-1]] -- canonical integers, the other region -- stay), keeps the
+    store sorted, and refuses an id inside the region that its table lacks."""
+    from delta_crdt_ex_amd._abi import DeltaGpuError
+    key = np.repeat(np.arange(1, 5, dtype=np.uint64), 4)
+    val = np.tile(np.array([5, 1 << 60, (1 << 60) + 8, 1 << 63], np.uint64), 4)
+    rows = (key, val, np.zeros(16, np.int64), np.zeros(16, np.uint32),
+            np.arange(1, 17, dtype=np.uint64))
+    s = Store.from_numpy(*rows, device=DEV)
+    old = np.array([1 << 60, (1 << 60) + 8], np.uint64)
+    new = np.array([(1 << 60) - 100, (1 << 60) + 100], np.uint64)
+    engine.remap_values(s, old, new)
+    got = s.to_numpy()[1]
+    want = val.copy()
+    want[val == old[0]], want[val == old[1]] = new[0], new[1]
+    assert np.array_equal(got, want)
+    engine.store_check(s)
+    with pytest.raises(DeltaGpuError):  # (1 << 60) + 4 lies inside the region, not in its table
+        engine.remap_values(s, np.array([(1 << 60) - 100, (1 << 60) + 4, (1 << 60) + 100],
+                                        np.uint64), np.array([1, 2, 3], np.uint64) + (1 << 60))
