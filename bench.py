@@ -201,6 +201,7 @@ def config4_round(eng, torch, dev, rank=0, world=1, keys_per_rank=12_500_000, st
 
     one_round()
     rounds = [one_round() for _ in range(5)]
+    resident = resident_delta(eng, torch, sa, ca, cb, ta, tb, b)
     med = {k: float(np.median([r[k] for r in rounds]))
            for k in ("diff", "take", "join", "update", "total", "diff_ev")}
     last = rounds[-1]
@@ -231,6 +232,7 @@ def config4_round(eng, torch, dev, rank=0, world=1, keys_per_rank=12_500_000, st
         "round_keys": last["keys"], "round_total_keys": last["total_keys"],
         "round_delta_rows": last["rows"], "round_changed_keys": last["changed"],
         "update_equals_rebuild": all(r["ok"] for r in rounds),
+        "resident_delta": resident,
         "round_note": "synchronous calls: merkle_diff -> take_keys -> join2_changes (keyed) -> "
                       "merkle_update (incremental put/delete + update_hashes of the changed keys)",
     }
@@ -241,6 +243,66 @@ def config4_round(eng, torch, dev, rank=0, world=1, keys_per_rank=12_500_000, st
         res["collectives_us"] = (time.perf_counter() - t0) * 1e6
         res["replica_root"] = hex(root_a)
     return res, (2 * n_keys, 2 * build_us * 1e-6 + med["diff"])
+
+
+def resident_delta(eng, torch, sa, ca, cb, ta, tb, b, reps=7):
+    """What a NIF caller pays per sync delta against a device-resident state
+    (join_delta; the reference's update_state_with_delta,
+    causal_crdt.ex:383-404), at wall time on the config-4 shard: H2D of the delta's rows
+    and keyset from pinned host memory, dg_join2_changes (the keyed join as a splice plus
+    the changed keys), dg_merkle_update of those keys, and D2H of the changed keys and
+    their rows (dg_take_keys) for the on_diffs callback."""
+    from delta_crdt_ex_amd import workloads as W
+    from delta_crdt_ex_amd.store import Context, Store
+    dev = sa.key.device
+    keys_np = eng.merkle_diff(ta, tb).cpu().numpy().view(np.uint64)  # the differing keys
+    d = W.sync_delta(b, keys_np)
+    n = len(d["rows"][0])
+    cols = [np.ascontiguousarray(c) for c in d["rows"]] + [np.ascontiguousarray(keys_np)]
+    pinned = [torch.from_numpy(c.view(np.int64 if c.dtype.itemsize == 8 else np.int32)).pin_memory()
+              for c in cols]
+    dst = Store.empty(max(n, 1), dev)
+    kdst = torch.empty(max(len(keys_np), 1), dtype=torch.int64, device=dev)
+    out = Store.empty(sa.n + n, dev)
+    octx = Context.empty(0, ca.n + cb.n, dev)
+    back = None
+    ph = {}
+    for it in range(reps + 1):
+        tt = ta.clone()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for h, t in zip(pinned, (dst.key, dst.val, dst.ts, dst.node, dst.cnt, kdst)):
+            t[: h.numel()].copy_(h, non_blocking=True)
+        dst.n = n
+        kd = kdst[: len(keys_np)]
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        out, octx, changed = eng.join2_changes(sa, ca, dst, cb, keys=kd, out=out, out_ctx=octx)
+        t2 = time.perf_counter()
+        eng.merkle_update(tt, out, changed)
+        t3 = time.perf_counter()
+        rows = eng.take_keys(out, changed)
+        if back is None:
+            back = [torch.empty(out.n, dtype=c.dtype).pin_memory()
+                    for c in (rows.key, rows.val, rows.ts, rows.node, rows.cnt)]
+        nr = rows.n
+        for h, c in zip(back, (rows.key, rows.val, rows.ts, rows.node, rows.cnt)):
+            h[:nr].copy_(c[:nr], non_blocking=True)
+        ck = changed.cpu()
+        torch.cuda.synchronize()
+        t4 = time.perf_counter()
+        if it:
+            for k, v in (("h2d", t1 - t0), ("join_changes", t2 - t1), ("merkle_update", t3 - t2),
+                         ("d2h_changed_rows", t4 - t3), ("total", t4 - t0)):
+                ph.setdefault(k, []).append(v)
+    med = {k: float(np.median(v)) * 1e6 for k, v in ph.items()}
+    return {"metric": "sync delta applied to a device-resident state (config-4 shard), wall time",
+            "us": med, "delta_rows": n, "keyset": int(len(keys_np)), "changed_keys": int(ck.numel()),
+            "rows_back": int(nr), "state_rows": sa.n,
+            "bytes_h2d": 36 * n + 8 * len(keys_np), "bytes_d2h": 36 * int(nr) + 8 * int(ck.numel()),
+            "deltas_per_s": 1e6 / med["total"],
+            "note": "synchronous calls, pinned host buffers reused, median of reps; the keyed "
+                    "join is the splice (csrc/splice.hip): untouched rows streamed once"}
 
 
 def _timed(torch, fn, reps):

@@ -35,6 +35,11 @@ struct dg_engine {
   // ping-pong intermediate states of dg_joink / dg_apply_deltas
   void* fold = nullptr;
   size_t fold_cap = 0;
+  bool splice = true;  // sparse keyed joins as a splice (DG_SPLICE=0: the full join)
+  // the splice's taken rows, edit and per-key index (its own: a stepwise fold's joins
+  // splice while their inputs live in `fold`)
+  void* spl = nullptr;
+  size_t spl_cap = 0;
   u32 epoch = 0;
   // small device counters + pinned host mirror.  d_counts[0..8) and ticket[0..16) are one
   // device allocation (ticket == (u32*)(d_counts + 8)), so a synchronous call brings its
@@ -372,6 +377,118 @@ int join2_enqueue(dg_engine* e, const dg_store* a, const dg_context* ca, const d
   return DG_OK;
 }
 
+// Engine scratch that persists across calls (the fold's ping-pong states; the splice's
+// taken rows, edit and index), grown on demand.
+int ensure_buf(dg_engine* e, void** buf, size_t* cap, size_t bytes) {
+  if (bytes <= *cap) return DG_OK;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (*buf) HIP_TRY(hipFree(*buf));
+  *buf = nullptr;
+  *cap = 0;
+  if (hipMalloc(buf, bytes) != hipSuccess)
+    return fail(DG_E_NOMEM, "hipMalloc of %zu scratch bytes failed", bytes);
+  *cap = bytes;
+  return DG_OK;
+}
+
+// A store of `rows` rows carved from p (columns 256-B aligned); advances p.
+dg_store carve_store(char*& p, u64 rows) {
+  auto take = [&](size_t bytes) {
+    char* q = p;
+    p += (bytes + 255) / 256 * 256;
+    return q;
+  };
+  dg_store s{};
+  s.key = (uint64_t*)take(rows * 8);
+  s.val = (uint64_t*)take(rows * 8);
+  s.ts = (int64_t*)take(rows * 8);
+  s.cnt = (uint64_t*)take(rows * 8);
+  s.node = (uint32_t*)take(rows * 4);
+  s.cap = rows;
+  s.n = 0;
+  return s;
+}
+
+// A keyed join whose delta and keyset are small against the state (CausalCrdt's sync
+// deltas, causal_crdt.ex:383-384) as a splice (csrc/splice.hip): the state's rows of the
+// keyset are taken out, joined with the delta on the join kernels, and the output is
+// written in one streaming pass (the untouched rows moved, the joined keys' rows in the
+// holes).  *done = false (and nothing of the caller's changed) when the splice does not
+// apply: the delta holds a key outside the keyset (its right-biased carry would replace
+// state rows the splice keeps), the taken rows exceed their bound, or the join grid
+// aborted; the caller then runs the full join.  Synchronous (two host syncs).
+bool splice_wanted(const dg_engine* e, const dg_store* a, const dg_store* b, const uint64_t* keys,
+                   uint64_t n_keys) {
+  return e->splice && keys && n_keys > 0 && (n_keys + b->n) * 8 <= a->n;
+}
+
+int splice_join(dg_engine* e, const dg_store* a, const dg_context* ca, const dg_store* b,
+                const dg_context* cb, const uint64_t* keys, uint64_t n_keys, dg_store* out,
+                dg_context* out_ctx, bool with_changes, uint64_t* changed, uint64_t cap,
+                uint64_t* n_changed, bool* done) {
+  *done = false;
+  TRY(check_store(a, "dg_join2 a"));
+  TRY(check_store(b, "dg_join2 b"));
+  TRY(check_ctx(ca, "dg_join2 ca"));
+  TRY(check_ctx(cb, "dg_join2 cb"));
+  if (!out || !out_ctx) return fail(DG_E_INVAL, "dg_join2: null output");
+  if (out->cap < a->n + b->n)
+    return fail(DG_E_CAPACITY, "dg_join2: out cap %llu < %llu rows in", (unsigned long long)out->cap,
+                (unsigned long long)(a->n + b->n));
+  if (!out->key || !out->val || !out->ts || !out->node || !out->cnt)
+    return fail(DG_E_INVAL, "dg_join2: null output column");
+  TRY(set_device(e));
+  const u64 cap_k = std::min<u64>(a->n, 16 * n_keys + 4096);  // taken rows: a few per key
+  const u64 cap_e = cap_k + b->n;
+  const size_t idx_bytes = ((n_keys + 1) * 8 + 255) / 256 * 256;
+  const size_t bytes = ((cap_k * 36 + 5 * 256) + (cap_e * 36 + 5 * 256) + 5 * idx_bytes + 255) / 256 * 256;
+  TRY(ensure_buf(e, &e->spl, &e->spl_cap, bytes));
+  char* p = (char*)e->spl;
+  dg_store ak = carve_store(p, cap_k);
+  dg_store ed = carve_store(p, cap_e);
+  u64* a_lo = (u64*)p;
+  u64* a_off = (u64*)(p + idx_bytes);
+  u64* end = (u64*)(p + 2 * idx_bytes);
+  i64* shift = (i64*)(p + 3 * idx_bytes);
+  i64* gap = (i64*)(p + 4 * idx_bytes);
+  TRY(ensure_state(e, take_tiles(n_keys) + 2));
+  Scan sc;
+  TRY(next_scan(e, &sc));
+  HIP_TRY(hipMemsetAsync(e->d_counts + 3, 0, 2 * sizeof(u64), e->stream));
+  HIP_TRY(launch_take_keys(rows_of(a), keys, n_keys, rows_out_of(&ak), cap_k, sc, e->d_counts + 3,
+                           e->stream, a_lo, a_off));
+  HIP_TRY(launch_splice_check(b->key, b->n, keys, n_keys, e->d_counts + 4, e->stream));
+  TRY(read_counts(e, 5));
+  const u64 n_ak = e->h_counts[3];
+  if (e->h_counts[4] != 0 || n_ak > cap_k) return DG_OK;  // the full join applies
+  ak.n = n_ak;
+  void* chg = nullptr;
+  TRY(join2_enqueue(e, &ak, ca, b, cb, keys, n_keys, &ed, out_ctx, e->d_counts,
+                    with_changes ? &chg : nullptr));
+  if (with_changes)
+    HIP_TRY(launch_join2_changes(ak.n, b->n, chg, changed, cap, e->d_counts + 2, e->stream));
+  SpliceArgs sp{};
+  sp.a = rows_of(a);
+  sp.keys = keys;
+  sp.nk = n_keys;
+  sp.a_lo = a_lo;
+  sp.a_off = a_off;
+  sp.end = end;
+  sp.shift = shift;
+  sp.gap = gap;
+  sp.e = rows_of(&ed);
+  sp.e.n = ak.n + b->n;  // a bound: the kernels read the count
+  sp.d_ne = e->d_counts;
+  sp.out = rows_out_of(out);
+  HIP_TRY(launch_splice(sp, e->stream));
+  if (read_counts(e, 3) != DG_OK) return DG_OK;  // a grid aborted: the full join re-runs
+  out->n = a->n - n_ak + e->h_counts[0];
+  out_ctx->n = e->h_counts[1];
+  if (n_changed) *n_changed = e->h_counts[2];
+  *done = true;
+  return DG_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -394,6 +511,8 @@ int dg_engine_create(int device, void* hip_stream, dg_engine** out) {
     if (v && atoi(v) > 0) e->join_workers = atoi(v);
     const char* m = getenv("DG_JOIN_MODE");
     if (m && m[0] == '2') e->join_mode = JOIN_TWO_PASS;
+    const char* sp = getenv("DG_SPLICE");
+    if (sp && sp[0] == '0') e->splice = false;
     const char* am = getenv("DG_APPLY_MODE");
     if (am && strcmp(am, "fold") == 0) e->apply_mode = 1;
     if (am && strcmp(am, "onepass") == 0) e->apply_mode = 2;
@@ -461,6 +580,7 @@ int dg_engine_destroy(dg_engine* e) {
   if (e->counts) hipFree(e->counts);
   if (e->started) hipFree(e->started);
   if (e->fold) hipFree(e->fold);
+  if (e->spl) hipFree(e->spl);
   if (e->h_stage) hipHostFree(e->h_stage);
   if (e->own_stream && e->stream) hipStreamDestroy(e->stream);
   if (e->ev_in || e->ev_out) {  // a registered engine (creation got past the registry)
@@ -557,6 +677,11 @@ int dg_join2(dg_engine* e, const dg_store* a, const dg_context* ca, const dg_sto
              dg_context* out_ctx) {
   if (!e) return fail(DG_E_INVAL, "null engine");
   TRY(settle(e));  // earlier asynchronous calls
+  if (splice_wanted(e, a, b, keys, n_keys)) {
+    bool done = false;
+    TRY(splice_join(e, a, ca, b, cb, keys, n_keys, out, out_ctx, false, nullptr, 0, nullptr, &done));
+    if (done) return DG_OK;
+  }
   TRY(join2_enqueue(e, a, ca, b, cb, keys, n_keys, out, out_ctx, e->d_counts));
   if (read_counts(e, 2) != DG_OK) {
     // a single-pass grid that could not become resident (another process's persistent
@@ -575,6 +700,16 @@ int dg_join2_changes(dg_engine* e, const dg_store* a, const dg_context* ca, cons
   if (!e) return fail(DG_E_INVAL, "null engine");
   if (!n_changed || (cap && !changed)) return fail(DG_E_INVAL, "dg_join2_changes: null output");
   TRY(settle(e));
+  if (splice_wanted(e, a, b, keys, n_keys)) {
+    bool done = false;
+    TRY(splice_join(e, a, ca, b, cb, keys, n_keys, out, out_ctx, true, changed, cap, n_changed, &done));
+    if (done) {
+      if (*n_changed > cap)
+        return fail(DG_E_CAPACITY, "dg_join2_changes: %llu changed keys > cap %llu",
+                    (unsigned long long)*n_changed, (unsigned long long)cap);
+      return DG_OK;
+    }
+  }
   void* chg = nullptr;
   TRY(join2_enqueue(e, a, ca, b, cb, keys, n_keys, out, out_ctx, e->d_counts, &chg));
   HIP_TRY(launch_join2_changes(a->n, b->n, chg, changed, cap, e->d_counts + 2, e->stream));
@@ -606,15 +741,7 @@ namespace {
 // `ctx` context entries, carved from engine scratch that persists across calls.
 int fold_buffers(dg_engine* e, u64 rows, u64 ctx, dg_store* st, dg_context* cx) {
   const size_t half = ((rows * 36 + ctx * 12 + 1024) + 255) / 256 * 256;
-  if (2 * half > e->fold_cap) {
-    HIP_TRY(hipStreamSynchronize(e->stream));
-    if (e->fold) HIP_TRY(hipFree(e->fold));
-    e->fold = nullptr;
-    e->fold_cap = 0;
-    if (hipMalloc(&e->fold, 2 * half) != hipSuccess)
-      return fail(DG_E_NOMEM, "hipMalloc of %zu fold scratch bytes failed", 2 * half);
-    e->fold_cap = 2 * half;
-  }
+  TRY(ensure_buf(e, &e->fold, &e->fold_cap, 2 * half));
   for (int w = 0; w < 2; w++) {
     char* p = (char*)e->fold + w * half;
     st[w].key = (uint64_t*)p;

@@ -129,9 +129,36 @@ hipError_t launch_kfold(const KFoldArgs& p, hipStream_t st);
 // ---- take.hip (sync-delta values: Map.take(value, keys))
 inline u64 take_tiles(u64 n_keys) { return (n_keys + 1023) / 1024; }
 // rows of s whose key is in keys (ascending) into out[0, cap); *d_count = their number.
-// Uses look-back granules [0, take_tiles(n_keys)).
+// Uses look-back granules [0, take_tiles(n_keys)).  key_lo / key_off (optional, n_keys and
+// n_keys + 1 entries): per key its first row in s (the first row >= the key) and the
+// output offset of its rows (key_off[n_keys] = *d_count).
 hipError_t launch_take_keys(const Rows& s, const u64* keys, u64 n_keys, const RowsOut& out,
-                            u64 cap, const Scan& scan, u64* d_count, hipStream_t st);
+                            u64 cap, const Scan& scan, u64* d_count, hipStream_t st,
+                            u64* key_lo = nullptr, u64* key_off = nullptr);
+
+// ---- splice.hip (a sparse keyed join applied to a large state without merging it)
+// The keyed join of a small delta into a large state, as a splice: the state's rows of the
+// keyset K are taken out (launch_take_keys with the per-key index), joined with the delta
+// (the join kernels on the small inputs: the edit E), and the output is the state with
+// each key's rows replaced by E's, its untouched rows moved by a streaming copy.
+struct SpliceArgs {
+  Rows a;              // the state
+  const u64* keys;     // K, ascending unique
+  u64 nk;
+  const u64* a_lo;     // nk: first row of A >= K[u]                        (take)
+  const u64* a_off;    // nk + 1: rows of A with keys K[0..u)                (take)
+  u64* end;            // nk: a_lo[u] + rows of K[u] in A                     (index)
+  i64* shift;          // nk + 1: out - in of the A rows after K[u-1], before K[u] (index)
+  i64* gap;            // nk: A rows outside K before K[u]                    (index)
+  Rows e;              // the edit (e.n: an upper bound; the count is *d_ne)
+  const u64* d_ne;
+  RowsOut out;
+  u64 a_tiles, e_tiles;
+};
+// every row of b whose key starts a run and is not in keys: *d_bad += 1
+hipError_t launch_splice_check(const u64* bkey, u64 nb, const u64* keys, u64 nk, u64* d_bad,
+                               hipStream_t st);
+hipError_t launch_splice(SpliceArgs p, hipStream_t st);
 
 // ---- mutate.hip (a batch of add/remove ops as one delta; see the file header)
 inline u64 mutate_tiles(u64 m) { return (m + 1023) / 1024; }

@@ -1,0 +1,222 @@
+// splice.hip — a sparse keyed join applied to a large device-resident state.
+//
+// CausalCrdt applies every sync delta as join(state, delta, keys)
+// (reference causal_crdt.ex:383-384; aw_lww_map.ex:153-209).  A delta carries the rows of
+// a few keys (Map.take(value, keys), causal_crdt.ex:324-335), so the join changes only
+// those keys; every other key keeps its rows (the right-biased carry of :185-188 hands A's
+// rows through when B lacks the key).  Merging the whole state (dg_join2's stream kernel)
+// reads and writes every row through the merge; the splice instead
+//   1. takes the state's rows of the keyset out (take_keys_kernel with the per-key index:
+//      a_lo[u], the first row >= K[u], and a_off[u], the rows of K[0..u)),
+//   2. joins them with the delta on the join kernels (small: the edit E, = the output's
+//      rows of every key of K, sorted),
+//   3. (this file) computes per key where the untouched rows between two keyset keys move
+//      (splice_index_kernel) and writes the output in one streaming pass: the untouched
+//      rows at their new positions and E's rows in the holes (splice_kernel).
+// The output is bit-identical to the full keyed join's whenever the delta's keys are a
+// subset of the keyset; the caller checks that first (splice_check_kernel) and otherwise
+// takes the full join.
+//
+// Positions.  With PA[u] = a_off[u] (state rows of K[0..u)) and PE[u] = E's rows with key
+// < K[u], a state row i outside K whose first keyset key above it is K[u] goes to
+// i - PA[u] + PE[u]: the shift of its gap.  E's row j of key K[u] goes to
+// j + a_lo[u] - PA[u]: the state rows outside K before K[u] come first.
+//
+// Roofline: the copy is 36 B read + 36 B written per untouched row, plus E's rows; the
+// index is O(|K| log |E|).  Nothing else touches the state.
+#include "dg_launch.h"
+
+namespace dg {
+
+namespace {
+
+constexpr int SB = 256;            // threads per workgroup
+constexpr int SR = 16;             // rows per thread
+constexpr int ST = SB * SR;        // rows per tile
+constexpr int SLC = 1024;          // keyset entries of a tile staged in LDS
+
+// first index in [0, n) whose value is > x (a nondecreasing), by all lanes of one wave:
+// 64-ary rounds (3 at 2^18 entries) instead of a binary search's 18 dependent loads
+__device__ __forceinline__ u64 wave_upper(const u64* a, u64 n, u64 x) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  u64 lo = 0, hi = n;
+  while (hi - lo > WAVE) {
+    const u64 span = hi - lo;
+    const u64 q = lo + span * (u64)(lane + 1) / (WAVE + 1);
+    const int c = __popcll(__ballot(a[q] <= x));  // true on a prefix of the lanes
+    const u64 nlo = c ? lo + span * (u64)c / (WAVE + 1) + 1 : lo;
+    const u64 nhi = c < WAVE ? lo + span * (u64)(c + 1) / (WAVE + 1) : hi;
+    lo = nlo;
+    hi = nhi;
+  }
+  const bool le = lo + lane < hi && a[lo + lane] <= x;
+  return lo + (u64)__popcll(__ballot(le));
+}
+
+__device__ __forceinline__ u64 lower_bound(const u64* a, u64 lo, u64 hi, u64 x) {
+  while (lo < hi) {
+    const u64 m = (lo + hi) >> 1;
+    if (a[m] < x)
+      lo = m + 1;
+    else
+      hi = m;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(SB) void splice_check_kernel(const u64* bkey, u64 nb, const u64* keys,
+                                                          u64 nk, u64* d_bad) {
+  const u64 j = (u64)blockIdx.x * SB + threadIdx.x;
+  if (j >= nb) return;
+  const u64 k = bkey[j];
+  if (j > 0 && bkey[j - 1] == k) return;  // one probe per key
+  const u64 u = lower_bound(keys, 0, nk, k);
+  if (u == nk || keys[u] != k) atomicAdd((unsigned long long*)d_bad, 1ull);
+}
+
+// per keyset entry u: end[u], gap[u] and shift[u] (shift[nk]: after the last key)
+__global__ __launch_bounds__(SB) void splice_index_kernel(SpliceArgs p) {
+  const u64 u = (u64)blockIdx.x * SB + threadIdx.x;
+  if (u > p.nk) return;
+  const u64 ne = *p.d_ne;
+  const u64 pa = p.a_off[u];
+  const u64 pe = u < p.nk ? lower_bound(p.e.key, 0, ne, p.keys[u]) : ne;
+  p.shift[u] = (i64)pe - (i64)pa;
+  if (u < p.nk) {
+    p.end[u] = p.a_lo[u] + (p.a_off[u + 1] - pa);
+    p.gap[u] = (i64)p.a_lo[u] - (i64)pa;
+  }
+}
+
+template <class T>
+__device__ __forceinline__ void move_col(const T* src, T* dst, const u64 (&from)[SR], const i64 (&to)[SR]) {
+  T v[SR];
+#pragma unroll
+  for (int q = 0; q < SR; q++) v[q] = to[q] >= 0 ? src[from[q]] : T(0);
+#pragma unroll
+  for (int q = 0; q < SR; q++)
+    if (to[q] >= 0) dst[to[q]] = v[q];
+}
+
+// Workgroups [0, e_tiles): E's rows (issued first, so their key searches overlap the
+// state's copy); then one workgroup per ST state rows.
+__global__ __launch_bounds__(SB) void splice_kernel(SpliceArgs p) {
+  __shared__ u64 s_end[SLC], s_lo[SLC];
+  __shared__ i64 s_shift[SLC];
+  __shared__ u64 s_b[2];
+  u64 from[SR];
+  i64 to[SR];
+  if (blockIdx.x < p.e_tiles) {
+    const u64 ne = *p.d_ne;
+    const u64 j0 = (u64)blockIdx.x * ST;
+    if (j0 >= ne) return;  // block-uniform
+    const u64 j1 = min<u64>(j0 + ST, ne);
+    // the keyset entries of the tile's keys lie in [u0, u1]: E's keys are keyset keys
+    // (clamped into [0, nk): the caller checked that they are, an index stays in bounds
+    // whatever the input)
+    if (threadIdx.x < WAVE) {
+      const u64 u = wave_upper(p.keys, p.nk, p.e.key[j0]);
+      if (threadIdx.x == 0) s_b[0] = u ? u - 1 : 0;
+    } else if (threadIdx.x < 2 * WAVE) {
+      const u64 u = wave_upper(p.keys, p.nk, p.e.key[j1 - 1]);
+      if ((threadIdx.x & (WAVE - 1)) == 0) s_b[1] = u ? u - 1 : 0;
+    }
+    __syncthreads();
+    const u64 u0 = s_b[0], u1 = max(s_b[0], s_b[1]);
+#pragma unroll
+    for (int q = 0; q < SR; q++) {
+      const u64 j = j0 + (u64)q * SB + threadIdx.x;
+      from[q] = j;
+      to[q] = -1;
+      if (j < j1) {
+        const u64 u = min(lower_bound(p.keys, u0, u1 + 1, p.e.key[j]), u1);
+        to[q] = (i64)j + p.gap[u];
+      }
+    }
+    move_col(p.e.key, p.out.key, from, to);
+    move_col(p.e.val, p.out.val, from, to);
+    move_col(p.e.ts, p.out.ts, from, to);
+    move_col(p.e.node, p.out.node, from, to);
+    move_col(p.e.cnt, p.out.cnt, from, to);
+    return;
+  }
+  const u64 i0 = (u64)(blockIdx.x - p.e_tiles) * ST;
+  const u64 i1 = min<u64>(i0 + ST, p.a.n);
+  // row i's first keyset entry whose state rows end after it: u*(i) = first u with
+  // end[u] > i (nk if none); the tile's rows have u* in [u0, u1]
+  if (threadIdx.x < WAVE) {
+    const u64 u = wave_upper(p.end, p.nk, i0);
+    if (threadIdx.x == 0) s_b[0] = u;
+  } else if (threadIdx.x < 2 * WAVE) {
+    const u64 u = wave_upper(p.end, p.nk, i1 - 1);
+    if ((threadIdx.x & (WAVE - 1)) == 0) s_b[1] = u;
+  }
+  __syncthreads();
+  const u64 u0 = s_b[0], u1 = s_b[1];
+  const u64 m = u1 - u0 + 1;
+  const bool staged = m <= (u64)SLC;  // block-uniform
+  if (staged) {
+    for (u64 e = threadIdx.x; e < m; e += SB) {
+      const u64 u = u0 + e;
+      s_end[e] = u < p.nk ? p.end[u] : ~0ull;
+      s_lo[e] = u < p.nk ? p.a_lo[u] : ~0ull;
+      s_shift[e] = p.shift[u];
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int q = 0; q < SR; q++) {
+    const u64 i = i0 + (u64)q * SB + threadIdx.x;
+    from[q] = i;
+    to[q] = -1;
+    if (i >= i1) continue;
+    u64 lo = 0, hi = m - 1;  // entry u0 + lo: the first whose end is > i (u1's is)
+    if (staged) {
+      while (lo < hi) {
+        const u64 mid = (lo + hi) >> 1;
+        if (s_end[mid] > i)
+          hi = mid;
+        else
+          lo = mid + 1;
+      }
+      if (s_lo[lo] > i) to[q] = (i64)i + s_shift[lo];  // else: a keyset key's row (E's)
+    } else {
+      while (lo < hi) {
+        const u64 mid = (lo + hi) >> 1;
+        if (p.end[u0 + mid] > i)
+          hi = mid;
+        else
+          lo = mid + 1;
+      }
+      const u64 u = u0 + lo;
+      if (u == p.nk || p.a_lo[u] > i) to[q] = (i64)i + p.shift[u];
+    }
+  }
+  move_col(p.a.key, p.out.key, from, to);
+  move_col(p.a.val, p.out.val, from, to);
+  move_col(p.a.ts, p.out.ts, from, to);
+  move_col(p.a.node, p.out.node, from, to);
+  move_col(p.a.cnt, p.out.cnt, from, to);
+}
+
+}  // namespace
+
+hipError_t launch_splice_check(const u64* bkey, u64 nb, const u64* keys, u64 nk, u64* d_bad,
+                               hipStream_t st) {
+  if (nb == 0) return hipSuccess;
+  hipLaunchKernelGGL(splice_check_kernel, dim3((unsigned)((nb + SB - 1) / SB)), dim3(SB), 0, st,
+                     bkey, nb, keys, nk, d_bad);
+  return hipGetLastError();
+}
+
+hipError_t launch_splice(SpliceArgs p, hipStream_t st) {
+  hipLaunchKernelGGL(splice_index_kernel, dim3((unsigned)((p.nk + 1 + SB - 1) / SB)), dim3(SB), 0,
+                     st, p);
+  p.a_tiles = (p.a.n + ST - 1) / ST;
+  p.e_tiles = (p.e.n + ST - 1) / ST;
+  if (p.a_tiles + p.e_tiles == 0) return hipGetLastError();
+  hipLaunchKernelGGL(splice_kernel, dim3((unsigned)(p.a_tiles + p.e_tiles)), dim3(SB), 0, st, p);
+  return hipGetLastError();
+}
+
+}  // namespace dg

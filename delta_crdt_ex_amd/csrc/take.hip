@@ -20,7 +20,7 @@ constexpr int TB = 256, TI = 4, TK = TB * TI;
 
 __global__ __launch_bounds__(TB) void take_keys_kernel(Rows s, const u64* keys, u64 n_keys,
                                                       u64 ntiles, RowsOut out, u64 cap, Scan scan,
-                                                      u64* d_count) {
+                                                      u64* d_count, u64* key_lo, u64* key_off) {
   __shared__ u64 s_lo[TK];
   __shared__ u32 s_off[TK + 1];
   __shared__ u32 s_wave[TB / WAVE + 1];
@@ -81,11 +81,20 @@ __global__ __launch_bounds__(TB) void take_keys_kernel(Rows s, const u64* keys, 
     }
     if (threadIdx.x == 0) {
       s_b[1] = prefix;
-      if (tile == ntiles - 1) d_count[0] = prefix + total;
+      if (tile == ntiles - 1) {
+        d_count[0] = prefix + total;
+        if (key_off) key_off[n_keys] = prefix + total;
+      }
     }
   }
   __syncthreads();
   const u64 base = s_b[1];
+  if (key_lo) {  // the splice's per-key index (splice.hip): first row and output offset
+    for (u32 i = threadIdx.x; i < nk; i += TB) {
+      key_lo[k0 + i] = s_lo[i];
+      key_off[k0 + i] = base + s_off[i];
+    }
+  }
   for (u32 o = threadIdx.x; o < total; o += TB) {
     u32 a = 0, b = TK;  // the key whose range holds o: last i with s_off[i] <= o
     while (b - a > 1) {
@@ -109,11 +118,12 @@ __global__ __launch_bounds__(TB) void take_keys_kernel(Rows s, const u64* keys, 
 }  // namespace
 
 hipError_t launch_take_keys(const Rows& s, const u64* keys, u64 n_keys, const RowsOut& out,
-                            u64 cap, const Scan& scan, u64* d_count, hipStream_t st) {
+                            u64 cap, const Scan& scan, u64* d_count, hipStream_t st, u64* key_lo,
+                            u64* key_off) {
   const u64 ntiles = take_tiles(n_keys);
-  if (ntiles == 0 || s.n == 0) return hipMemsetAsync(d_count, 0, sizeof(u64), st);
+  if (ntiles == 0) return hipMemsetAsync(d_count, 0, sizeof(u64), st);
   hipLaunchKernelGGL(take_keys_kernel, dim3((unsigned)ntiles), dim3(TB), 0, st, s, keys, n_keys,
-                     ntiles, out, cap, scan, d_count);
+                     ntiles, out, cap, scan, d_count, key_lo, key_off);
   return hipGetLastError();
 }
 
