@@ -45,8 +45,9 @@ constexpr int CS = KFOLD_CAP_S;  // state rows per bucket
 constexpr int CD = KFOLD_CAP_D;  // delta rows per bucket
 constexpr int CM = KFOLD_CAP_M;  // keyset markers per bucket
 constexpr int CU = CD + CM;
-constexpr u32 MARK = 1u << 15;   // utag: (src << 16) | MARK? | pre-sort slot
-constexpr u32 SLOT = MARK - 1;
+constexpr u32 MARK = 1u << 15;   // utag: (src << 16) | MARK? | KIN? | pre-sort slot
+constexpr u32 KIN = 1u << 14;    // a delta row whose key is in its own delta's keyset
+constexpr u32 SLOT = KIN - 1;
 static_assert(2 * KFOLD_MAX_K <= KB, "one thread per run");
 static_assert(CU <= SLOT + 1, "slot bits");
 
@@ -465,6 +466,42 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
   }
   KSTAMP(t, 1);
   __syncthreads();  // (the run pointers in s.x are dead: the histogram takes it)
+
+  // ---- a keyset entry of a delta that also has rows of the key is folded into those
+  //      rows (KIN on their tags) and dropped from the items: a sync delta's keyset is
+  //      mostly its row keys (Map.take(value, keys)), so the sort and every walk below
+  //      see about half the items.  Rows search their delta's keyset slice, entries their
+  //      delta's row slice (both sorted, both staged: slot q holds item q).
+  bool keep = false;
+  if (q < nU) {
+    const u32 src = itag >> 16;
+    const bool mark = itag & MARK;
+    const u32 lo = mark ? s.roff[src] : s.roff[k + src];
+    const u32 hi = mark ? s.roff[src + 1] : s.roff[k + src + 1];
+    const u64* col = mark ? s.dkey : s.ukey;
+    u32 a = lo, b = hi;
+    while (a < b) {
+      const u32 m = (a + b) >> 1;
+      if (col[m] < ir.key)
+        a = m + 1;
+      else
+        b = m;
+    }
+    const bool found = a < hi && col[a] == ir.key;
+    if (!mark && found) itag |= KIN;
+    keep = mark && !found;
+  }
+  u32 n_keep;
+  // (the scan's barriers come after every search: the entries may move after it)
+  const u32 kpos = block_excl_scan<KB>(keep ? 1u : 0u, s.wave, &n_keep);
+  if (q < nD) {
+    s.utag[q] = itag;
+  } else if (keep) {
+    const u32 nq = nD + kpos;
+    s.ukey[nq] = ir.key;
+    s.utag[nq] = (itag & ~SLOT) | nq;
+  }
+  nU = nD + n_keep;
   for (u32 b = tid; b < NSUB; b += KB) s.x.ucnt[b] = 0;
   __syncthreads();
 
@@ -542,9 +579,8 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
     s.slbu[i] = (unsigned short)e;
     for (; e < qe && s.ukey[e] == r.key; e++) {
       const u32 tg = s.utag[e], src = tg >> 16;
-      if (tg & MARK) {
-        cs.K |= 1ull << src;
-      } else {
+      if (tg & (MARK | KIN)) cs.K |= 1ull << src;
+      if (!(tg & MARK)) {
         cs.R |= 1ull << src;
         if (row_eq(drow(s, tg & SLOT), r)) cs.M |= 1ull << src;
       }
@@ -563,9 +599,8 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
     while (e > 0 && s.ukey[e - 1] == r.key) e--;
     for (; e < nU && s.ukey[e] == r.key; e++) {
       const u32 te = s.utag[e], se = te >> 16;
-      if (te & MARK) {
-        cu.K |= 1ull << se;
-      } else {
+      if (te & (MARK | KIN)) cu.K |= 1ull << se;
+      if (!(te & MARK)) {
         cu.R |= 1ull << se;
         if (row_eq(drow(s, te & SLOT), r)) {
           cu.M |= 1ull << se;

@@ -369,6 +369,6 @@ def test_remap_values_region_local(engine):
     want[val == old[0]], want[val == old[1]] = new[0], new[1]
     assert np.array_equal(got, want)
     engine.store_check(s)
-    with pytest.raises(DeltaGpuError):  # (1 << 60) + 4 lies inside the region, not in its table
-        engine.remap_values(s, np.array([(1 << 60) - 100, (1 << 60) + 4, (1 << 60) + 100],
-                                        np.uint64), np.array([1, 2, 3], np.uint64) + (1 << 60))
+    with pytest.raises(DeltaGpuError):  # rows hold (1 << 60) -+ 100: inside, not in the table
+        engine.remap_values(s, np.array([(1 << 60) - 200, (1 << 60) + 200], np.uint64),
+                            np.array([(1 << 60) - 300, (1 << 60) + 300], np.uint64))

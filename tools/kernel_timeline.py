@@ -1,0 +1,25 @@
+"""Per-kernel stats and the last N dispatches (start offset, duration, gap before) of a
+rocprofv3 --kernel-trace --output-format csv directory.  Usage: kernel_timeline.py DIR [N]"""
+import csv
+import glob
+import os
+import sys
+
+d = sys.argv[1]
+n = int(sys.argv[2]) if len(sys.argv) > 2 else 40
+stats = glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True)
+trace = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+if stats:
+    for r in csv.DictReader(open(stats[0])):
+        print(f'{r["Name"][:72]:72s} calls={r["Calls"]:>5} avg_us={float(r["AverageNs"]) / 1e3:9.2f}')
+if trace:
+    rows = sorted(csv.DictReader(open(trace[0])), key=lambda r: int(r["Start_Timestamp"]))
+    rows = rows[-n:]
+    t0 = int(rows[0]["Start_Timestamp"])
+    prev = None
+    print(f"--- last {len(rows)} dispatches (us: start, duration, gap after the previous end)")
+    for r in rows:
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        gap = (s - prev) / 1e3 if prev is not None else 0.0
+        print(f'{(s - t0) / 1e3:9.1f} {(e - s) / 1e3:8.1f} {gap:8.1f}  {r["Kernel_Name"][:80]}')
+        prev = e
