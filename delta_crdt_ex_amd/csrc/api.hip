@@ -417,9 +417,17 @@ dg_store carve_store(char*& p, u64 rows) {
 // apply: the delta holds a key outside the keyset (its right-biased carry would replace
 // state rows the splice keeps), the taken rows exceed their bound, or the join grid
 // aborted; the caller then runs the full join.  Synchronous (two host syncs).
+// (the splice moves rows in 16-byte pairs: the state's and the output's 8-byte columns
+// must be 16-byte aligned, their node columns 8-byte aligned)
+bool pair_aligned(const void* k, const void* v, const void* t, const void* n, const void* c) {
+  return !(((uintptr_t)k | (uintptr_t)v | (uintptr_t)t | (uintptr_t)c) & 15) && !((uintptr_t)n & 7);
+}
+
 bool splice_wanted(const dg_engine* e, const dg_store* a, const dg_store* b, const uint64_t* keys,
-                   uint64_t n_keys) {
-  return e->splice && keys && n_keys > 0 && (n_keys + b->n) * 8 <= a->n;
+                   uint64_t n_keys, const dg_store* out) {
+  return e->splice && keys && n_keys > 0 && (n_keys + b->n) * 8 <= a->n && out &&
+         pair_aligned(a->key, a->val, a->ts, a->node, a->cnt) &&
+         pair_aligned(out->key, out->val, out->ts, out->node, out->cnt);
 }
 
 int splice_join(dg_engine* e, const dg_store* a, const dg_context* ca, const dg_store* b,
@@ -441,7 +449,9 @@ int splice_join(dg_engine* e, const dg_store* a, const dg_context* ca, const dg_
   const u64 cap_k = std::min<u64>(a->n, 16 * n_keys + 4096);  // taken rows: a few per key
   const u64 cap_e = cap_k + b->n;
   const size_t idx_bytes = ((n_keys + 1) * 8 + 255) / 256 * 256;
-  const size_t bytes = ((cap_k * 36 + 5 * 256) + (cap_e * 36 + 5 * 256) + 5 * idx_bytes + 255) / 256 * 256;
+  const size_t tile_bytes = ((splice_tiles(a->n) + 1) * 8 + 255) / 256 * 256;
+  const size_t bytes = ((cap_k * 36 + 5 * 256) + (cap_e * 36 + 5 * 256) + 5 * idx_bytes +
+                        tile_bytes + 255) / 256 * 256;
   TRY(ensure_buf(e, &e->spl, &e->spl_cap, bytes));
   char* p = (char*)e->spl;
   dg_store ak = carve_store(p, cap_k);
@@ -451,6 +461,7 @@ int splice_join(dg_engine* e, const dg_store* a, const dg_context* ca, const dg_
   u64* end = (u64*)(p + 2 * idx_bytes);
   i64* shift = (i64*)(p + 3 * idx_bytes);
   i64* gap = (i64*)(p + 4 * idx_bytes);
+  u64* tile_u0 = (u64*)(p + 5 * idx_bytes);
   TRY(ensure_state(e, take_tiles(n_keys) + 2));
   Scan sc;
   TRY(next_scan(e, &sc));
@@ -476,6 +487,7 @@ int splice_join(dg_engine* e, const dg_store* a, const dg_context* ca, const dg_
   sp.end = end;
   sp.shift = shift;
   sp.gap = gap;
+  sp.tile_u0 = tile_u0;
   sp.e = rows_of(&ed);
   sp.e.n = ak.n + b->n;  // a bound: the kernels read the count
   sp.d_ne = e->d_counts;
@@ -677,7 +689,7 @@ int dg_join2(dg_engine* e, const dg_store* a, const dg_context* ca, const dg_sto
              dg_context* out_ctx) {
   if (!e) return fail(DG_E_INVAL, "null engine");
   TRY(settle(e));  // earlier asynchronous calls
-  if (splice_wanted(e, a, b, keys, n_keys)) {
+  if (splice_wanted(e, a, b, keys, n_keys, out)) {
     bool done = false;
     TRY(splice_join(e, a, ca, b, cb, keys, n_keys, out, out_ctx, false, nullptr, 0, nullptr, &done));
     if (done) return DG_OK;
@@ -700,7 +712,7 @@ int dg_join2_changes(dg_engine* e, const dg_store* a, const dg_context* ca, cons
   if (!e) return fail(DG_E_INVAL, "null engine");
   if (!n_changed || (cap && !changed)) return fail(DG_E_INVAL, "dg_join2_changes: null output");
   TRY(settle(e));
-  if (splice_wanted(e, a, b, keys, n_keys)) {
+  if (splice_wanted(e, a, b, keys, n_keys, out)) {
     bool done = false;
     TRY(splice_join(e, a, ca, b, cb, keys, n_keys, out, out_ctx, true, changed, cap, n_changed, &done));
     if (done) {

@@ -217,6 +217,62 @@ __device__ __forceinline__ u64 wave_lower_bound(const u64* k, u64 n, u64 x) {
   return lo + (u64)__popcll(__ballot(lt));
 }
 
+// First index in [lo, hi) whose key is >= x (hi if none), keys ascending.  Key ids are
+// 64-bit hashes, uniform over the store's range, so the answer lies within about
+// sqrt(m f (1 - f)) rows of the interpolated position in a bracket of m rows: each round
+// probes the two rows 2 such deviations either side of it (two independent loads, one
+// round trip) and keeps the sub-bracket that holds x -- about 7000, 170, 30, then <= 16
+// rows at 12.5M uniform keys -- and the last <= 16 keys (one or two cache lines) are
+// read at once.  About 6 dependent memory rounds instead of a binary search's 24 (a
+// one-sided interpolation search stalls on one side: 29-30 probes for 1 key in 10).
+// Exact for any key distribution: a round that does not bracket still narrows, and the
+// finish is a plain binary search once the round budget is spent.
+__device__ __forceinline__ u64 interp_lower_bound(const u64* k, u64 lo, u64 hi, u64 x) {
+  if (lo >= hi) return lo;
+  u64 kl = k[lo], kh = k[hi - 1];
+  if (x <= kl) return lo;
+  if (x > kh) return hi;
+  u64 a = lo, b = hi - 1;  // k[a] < x <= k[b]: the answer is in (a, b]
+#pragma unroll 1
+  for (int it = 0; it < 6 && b - a > 16; it++) {
+    const double m = (double)(b - a);
+    const double f = (double)(x - kl) / (double)(kh - kl);
+    const double g = (double)a + f * m;
+    const double e = 2.0 * __builtin_sqrt(m * f * (1.0 - f)) + 4.0;
+    const double lo_g = g - e, hi_g = g + e;
+    const u64 g0 = lo_g <= (double)(a + 1) ? a + 1 : (lo_g >= (double)(b - 1) ? b - 1 : (u64)lo_g);
+    const u64 g1 = hi_g <= (double)(a + 1) ? a + 1 : (hi_g >= (double)(b - 1) ? b - 1 : (u64)hi_g);
+    const u64 k0 = k[g0], k1 = k[g1];
+    if (k0 >= x) {
+      b = g0;
+      kh = k0;
+    } else if (k1 < x) {
+      a = g1;
+      kl = k1;
+    } else {
+      a = g0;
+      kl = k0;
+      b = g1;
+      kh = k1;
+    }
+  }
+  if (b - a <= 16) {  // the keys of (a, b): loaded together, counted
+    u64 c = 0;
+#pragma unroll
+    for (u64 j = 1; j < 16; j++) c += (a + j < b && k[a + j] < x) ? 1 : 0;
+    return a + 1 + c;
+  }
+  u64 l2 = a + 1, h2 = b;
+  while (l2 < h2) {
+    const u64 mid = (l2 + h2) >> 1;
+    if (k[mid] < x)
+      l2 = mid + 1;
+    else
+      h2 = mid;
+  }
+  return l2;
+}
+
 __device__ __forceinline__ bool keyset_has(const u64* keys, u64 n, u64 k) {
   u64 lo = 0, hi = n;
   while (lo < hi) {

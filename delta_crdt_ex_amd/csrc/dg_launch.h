@@ -150,6 +150,7 @@ struct SpliceArgs {
   u64* end;            // nk: a_lo[u] + rows of K[u] in A                     (index)
   i64* shift;          // nk + 1: out - in of the A rows after K[u-1], before K[u] (index)
   i64* gap;            // nk: A rows outside K before K[u]                    (index)
+  u64* tile_u0;        // a_tiles + 1: first u with end[u] > the tile's first row (index)
   Rows e;              // the edit (e.n: an upper bound; the count is *d_ne)
   const u64* d_ne;
   RowsOut out;
@@ -159,6 +160,7 @@ struct SpliceArgs {
 hipError_t launch_splice_check(const u64* bkey, u64 nb, const u64* keys, u64 nk, u64* d_bad,
                                hipStream_t st);
 hipError_t launch_splice(SpliceArgs p, hipStream_t st);
+u64 splice_tiles(u64 n);  // state tiles of the copy (tile_u0 holds one more entry)
 
 // ---- mutate.hip (a batch of add/remove ops as one delta; see the file header)
 inline u64 mutate_tiles(u64 m) { return (m + 1023) / 1024; }

@@ -31,10 +31,12 @@
 //    new store and adds the difference to its bucket (put/delete); the upsweep then
 //    re-reduces only the 2^11-bucket chunks an update touched (update_hashes).
 //  * diff: a workgroup per subtree of 4096 buckets; a subtree whose root matches is
-//    skipped, otherwise the workgroup descends it level by level through the differing
-//    nodes only (a frontier in LDS), locates each differing bucket's rows from the trees'
-//    per-bucket row counts, hashes just those rows and merges them key by key.  count /
-//    write passes; keys past `cap` are counted, not written (max_sync_size truncation).
+//    skipped, otherwise the workgroup descends it in strides of 4 levels (each thread
+//    owns 16 buckets and compares their ancestors 4 and 8 levels up, then the buckets
+//    only below differing ancestors: two round trips instead of twelve), locates each
+//    differing bucket's rows from the trees' per-bucket row counts, hashes just those
+//    rows and merges them key by key.  count / write passes; keys past `cap` are
+//    counted, not written (max_sync_size truncation).
 //  * partial diff: node-form continuations (positions + the sender's hashes at one
 //    level) are compared and expanded `levels` levels down; at the bucket level the
 //    reply is a leaf-form continuation (the sender's (key, leaf) pairs of the
@@ -309,7 +311,7 @@ constexpr int UB = 256;
 
 // Σ row_hash of key x's rows in s (0 if absent); *rows = their number.
 __device__ __forceinline__ u64 key_leaf(const Rows& s, u64 x, const TermH& th, u32* rows) {
-  u64 i = lower_bound_key(s.key, s.n, x);
+  u64 i = interp_lower_bound(s.key, 0, s.n, x);
   u64 h = 0;
   u32 r = 0;
   for (; i < s.n && s.key[i] == x; i++, r++) h += rh(s, i, th);
@@ -401,11 +403,13 @@ __device__ u32 merge_bucket(const Rows& A, const TermH& tha, u64 ia, u64 ie, con
 //  1. bounds: one wave per subtree boundary finds the boundary's first row in both stores
 //     (a 64-ary wave lower bound: 4 dependent load rounds at 12.5M rows).
 //  2. count: a subtree whose roots match is skipped.  Otherwise the workgroup descends it
-//     level by level: the frontier (differing nodes of one level, ascending) lives in
-//     LDS, and only the children of differing nodes are loaded and compared -- about
-//     2 x (differing nodes) per level, one round trip each.  The last level's frontier
-//     is the differing buckets.  Each thread owns 16 consecutive buckets: it loads their
-//     row counts in both trees (u16), and a block scan turns them into row ranges.  The
+//     in strides of 4 levels.  Each thread owns 16 consecutive buckets: their ancestors
+//     4 and 8 levels up (one node each), the subtree's root and the buckets' row counts
+//     in both trees (u16) are loaded in one round trip, the 16 bucket nodes (the second
+//     round trip) only where both ancestors differ.  (A level-by-level descent through a
+//     frontier in LDS read 40 % fewer node bytes at 1 % differing keys but took 12 round
+//     trips and 24 barriers: 281 us per config-4 diff.)  A block scan turns the row
+//     counts into row ranges.  The
 //     differing buckets' rows are listed and hashed by all threads at once (one round of
 //     independent loads), and each thread merges its differing buckets' keys from LDS.
 //     The subtree's differing keys go to scratch at (A start + B start) of the subtree,
@@ -416,7 +420,9 @@ __device__ u32 merge_bucket(const Rows& A, const TermH& tha, u64 ia, u64 ie, con
 constexpr int DB = DIFF_BLOCK;
 constexpr u32 XSUB = 1u << DIFF_SUB;  // buckets per subtree (at most)
 constexpr u32 OWN = XSUB / DB;        // buckets per thread
-constexpr u32 RCAP = 2048;            // rows of the differing buckets staged in LDS
+constexpr u32 RCAP = 1792;            // rows of the differing buckets staged in LDS
+constexpr u32 DCAP = 512;             // differing buckets listed in LDS (36.9 KB in all:
+                                      // 4 workgroups per CU)
 static_assert(OWN == 16, "a thread owns 16 buckets: two 16-byte count loads per tree");
 
 struct DiffArgs {
@@ -461,67 +467,37 @@ __device__ __forceinline__ void load_counts16(const uint16_t* c, u32 nb, u32 fir
 
 __device__ __forceinline__ u32 half16(const u32 w[8], u32 i) { return (w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu; }
 
-__global__ __launch_bounds__(DB) void merkle_diff_count_kernel(DiffArgs p) {
-  __shared__ uint16_t s_f[2][XSUB];  // descent frontiers: node positions within the subtree
+__global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) {  // 4 per CU: all resident
   __shared__ u32 s_wave[DB / WAVE + 1];
-  __shared__ u32 s_list[RCAP];       // listed rows: bit 31 = store B; offset from the subtree's first row
-  __shared__ u64 s_k[RCAP], s_h[RCAP];
+  __shared__ u32 s_da[DCAP], s_db[DCAP];  // a differing bucket's first row in A / B (from the subtree's)
+  __shared__ u32 s_dp[DCAP + 1];          // its first staged row
+  __shared__ u32 s_dn[DCAP];              // its rows in A (high half) and B (low half)
+  __shared__ u64 s_k[RCAP], s_h[RCAP];    // the staged rows' keys and row hashes
   const u32 depth = p.ta.depth, sub = p.sub, Ls = depth - sub, nb = 1u << sub;
   const u64 tile = blockIdx.x;
   const int tid = threadIdx.x;
   const u64 root = ((1ull << Ls) - 1) + tile;
   const u64 nbnd = p.ntiles + 1;
-  if (p.ta.nodes[root] == p.tb.nodes[root]) {  // uniform: the whole subtree matches
-    if (tid == 0) p.cnt[tile] = 0;
-    return;
+  // ---- descent in strides of 4 levels: thread tid owns buckets [16 tid, 16 tid + 16) of
+  //      the subtree, and their common ancestors 4 and 8 levels up (one node each) are
+  //      loaded with the subtree's root and the owned buckets' row counts in ONE round
+  //      trip; the 16 bucket nodes only below differing ancestors, in a second one
+  const bool owns = (u32)tid * OWN < nb;
+  const u64 b0 = (tile << sub) + (u64)tid * OWN;  // the first owned bucket (tree-wide)
+  const u64 ra = p.ta.nodes[root], rb = p.tb.nodes[root];
+  u64 ga = 0, gb = 0, qa = 0, qb = 0;
+  if (owns && sub >= 8) {
+    const u64 g = ((1ull << (depth - 8)) - 1) + (b0 >> 8);
+    ga = p.ta.nodes[g];
+    gb = p.tb.nodes[g];
   }
-  // ---- descent: frontier = the differing nodes of level Ls + l (positions in the subtree)
-  u32 nf = 1, cur = 0;
-  if (tid == 0) s_f[0][0] = 0;
-  __syncthreads();
-  for (u32 l = 1; l <= sub; l++) {
-    const u64 first = ((1ull << (Ls + l)) - 1) + (tile << l);  // the subtree's first node of the level
-    u32 nn = 0;
-    for (u32 j0 = 0; j0 < nf; j0 += DB) {  // uniform loop
-      const u32 j = j0 + tid;
-      u32 f = 0, d0 = 0, d1 = 0;
-      if (j < nf) {
-        f = s_f[cur][j];
-        const u64 c = first + 2 * (u64)f;
-        const u64 a0 = p.ta.nodes[c], a1 = p.ta.nodes[c + 1];
-        const u64 b0 = p.tb.nodes[c], b1 = p.tb.nodes[c + 1];
-        d0 = a0 != b0;
-        d1 = a1 != b1;
-      }
-      u32 tot;
-      const u32 o = nn + block_excl_scan<DB>(d0 + d1, s_wave, &tot);
-      if (d0) s_f[cur ^ 1][o] = (uint16_t)(2 * f);
-      if (d1) s_f[cur ^ 1][o + d0] = (uint16_t)(2 * f + 1);
-      nn += tot;
-      __syncthreads();  // (s_wave reuse; the frontier of level l complete)
-    }
-    nf = nn;
-    cur ^= 1;
+  if (owns && sub >= 4) {
+    const u64 q = ((1ull << (depth - 4)) - 1) + (b0 >> 4);
+    qa = p.ta.nodes[q];
+    qb = p.tb.nodes[q];
   }
-  // s_f[cur][0, nf): the differing buckets, ascending.  Thread tid owns buckets
-  // [16 tid, 16 tid + 16): mark its differing ones (a 16-bit mask) from the list.
-  u32 mine = 0;
-  {
-    // owner of list entry j is s_f[cur][j] / 16; entries are ascending, so a thread finds
-    // its range by two searches of the (LDS) list
-    const u32 lo_b = (u32)tid * OWN;
-    u32 lo = 0, hi = nf;
-    while (lo < hi) {
-      const u32 m = (lo + hi) >> 1;
-      if (s_f[cur][m] < lo_b) lo = m + 1; else hi = m;
-    }
-    for (u32 j = lo; j < nf && s_f[cur][j] < lo_b + OWN; j++) mine |= 1u << (s_f[cur][j] - lo_b);
-  }
-  // row counts of the owned buckets in both trees, and their row offsets in the subtree
-  const u64 a0 = p.bnd[tile], c0 = p.bnd[nbnd + tile];
   const u64 bucket0 = tile << sub;
   u32 ca[8], cb[8];
-  const bool owns = (u32)tid * OWN < nb;
   if (owns) {
     load_counts16(p.ta.counts + bucket0, nb, (u32)tid * OWN, ca);
     load_counts16(p.tb.counts + bucket0, nb, (u32)tid * OWN, cb);
@@ -529,6 +505,31 @@ __global__ __launch_bounds__(DB) void merkle_diff_count_kernel(DiffArgs p) {
 #pragma unroll
     for (int q = 0; q < 8; q++) ca[q] = cb[q] = 0;
   }
+  if (ra == rb) {  // uniform: the whole subtree matches
+    if (tid == 0) p.cnt[tile] = 0;
+    return;
+  }
+  u32 mine = 0;  // the owned buckets that differ (bit i: bucket 16 tid + i)
+  if (owns && (sub < 8 || ga != gb) && (sub < 4 || qa != qb)) {
+    const u64 lv = ((1ull << depth) - 1) + b0;
+    const u32 m = nb < OWN ? nb : OWN;
+#pragma unroll
+    for (u32 i0 = 0; i0 < OWN; i0 += 4) {
+      u64 x[4], y[4];
+#pragma unroll
+      for (u32 i = 0; i < 4; i++) {
+        x[i] = i0 + i < m ? p.ta.nodes[lv + i0 + i] : 0ull;
+        y[i] = i0 + i < m ? p.tb.nodes[lv + i0 + i] : 0ull;
+      }
+#pragma unroll
+      for (u32 i = 0; i < 4; i++) mine |= (x[i] != y[i] ? 1u : 0u) << (i0 + i);
+    }
+  }
+  // ---- the differing buckets as a list (one entry per bucket, in bucket order): its rows'
+  //      offsets in both stores (from the subtree's first row) and their place among the
+  //      staged rows; then every per-bucket step runs one lane per differing bucket, not
+  //      every thread over its 16 owned buckets (which ran each step masked 16 times)
+  const u64 a0 = p.bnd[tile], c0 = p.bnd[nbnd + tile];
   u32 ta_ = 0, tb_ = 0, rd = 0;
 #pragma unroll
   for (u32 i = 0; i < OWN; i++) {
@@ -537,50 +538,96 @@ __global__ __launch_bounds__(DB) void merkle_diff_count_kernel(DiffArgs p) {
     tb_ += y;
     if (mine >> i & 1u) rd += x + y;
   }
-  u32 tot;
+  u32 tot, ND, R;
   const u32 offa = block_excl_scan<DB>(ta_, s_wave, &tot);
   __syncthreads();
   const u32 offb = block_excl_scan<DB>(tb_, s_wave, &tot);
   __syncthreads();
-  u32 R;
   const u32 slot0 = block_excl_scan<DB>(rd, s_wave, &R);
   __syncthreads();
+  const u32 d0 = block_excl_scan<DB>((u32)__popc(mine), s_wave, &ND);
   const u64 base = a0 + c0;
-  const bool lds = R <= RCAP;  // uniform
+  const bool lds = R <= RCAP && ND <= DCAP;  // uniform
   if (lds) {
-    // list the differing buckets' rows (A rows, then B rows, bucket by bucket)
-    u32 slot = slot0, ra = offa, rb = offb;
+    u32 d = d0, slot = slot0, ra = offa, rb = offb;
 #pragma unroll
     for (u32 i = 0; i < OWN; i++) {
       const u32 x = half16(ca, i), y = half16(cb, i);
       if (mine >> i & 1u) {
-        for (u32 r = 0; r < x; r++) s_list[slot++] = ra + r;
-        for (u32 r = 0; r < y; r++) s_list[slot++] = 0x80000000u | (rb + r);
+        s_da[d] = ra;
+        s_db[d] = rb;
+        s_dp[d] = slot;
+        s_dn[d] = (x << 16) | y;
+        d++;
+        slot += x + y;
       }
       ra += x;
       rb += y;
     }
+    if (tid == 0) s_dp[ND] = R;
     __syncthreads();
-    // hash them all at once: up to RCAP / DB rows per thread, loads in flight together
+    // hash the staged rows, all at once: row q belongs to the last differing bucket whose
+    // first staged row is <= q (a search of the LDS list), A's rows first
 #pragma unroll
-    for (u32 u = 0; u < RCAP / DB; u++) {
+    for (u32 u = 0; u < (RCAP + DB - 1) / DB; u++) {
       const u32 q = u * DB + tid;
       if (q < R) {
-        const u32 e = s_list[q];
-        if (e & 0x80000000u) {
-          const u64 i = c0 + (e & 0x7FFFFFFFu);
-          s_k[q] = p.sb.key[i];
-          s_h[q] = rh(p.sb, i, p.tb.th);
-        } else {
-          const u64 i = a0 + e;
+        u32 lo = 0, hi = ND;  // s_dp[lo] <= q < s_dp[hi]
+        while (hi - lo > 1) {
+          const u32 m = (lo + hi) >> 1;
+          if (s_dp[m] <= q)
+            lo = m;
+          else
+            hi = m;
+        }
+        const u32 r = q - s_dp[lo], na = s_dn[lo] >> 16;
+        if (r < na) {
+          const u64 i = a0 + s_da[lo] + r;
           s_k[q] = p.sa.key[i];
           s_h[q] = rh(p.sa, i, p.ta.th);
+        } else {
+          const u64 i = c0 + s_db[lo] + (r - na);
+          s_k[q] = p.sb.key[i];
+          s_h[q] = rh(p.sb, i, p.tb.th);
         }
       }
     }
     __syncthreads();
+    // merge each differing bucket's keys (one lane per bucket): count, scan, write
+    u32 c = 0;
+    for (int pass = 0; pass < 2; pass++) {
+      u32 o = 0;
+      if (pass == 1) {
+        u32 t2;
+        o = block_excl_scan<DB>(c, s_wave, &t2);
+        if (tid == 0) {
+          p.cnt[tile] = t2;
+          if (t2) atomicAdd((unsigned long long*)&p.bsum[tile / DB], (unsigned long long)t2);
+        }
+      }
+      u32 k2 = 0;
+      for (u32 d = tid; d < ND; d += DB) {
+        const u32 na = s_dn[d] >> 16;
+        u32 ia = s_dp[d], ie = ia + na, jb = ie, je = s_dp[d + 1];
+        while (ia < ie || jb < je) {
+          const u64 ka = ia < ie ? s_k[ia] : ~0ull, kb = jb < je ? s_k[jb] : ~0ull;
+          const u64 k = ka < kb ? ka : kb;
+          u64 ha = 0, hb = 0;
+          const bool pa = ia < ie && ka == k, pb = jb < je && kb == k;
+          for (; ia < ie && s_k[ia] == k; ia++) ha += s_h[ia];
+          for (; jb < je && s_k[jb] == k; jb++) hb += s_h[jb];
+          if (!(pa && pb) || ha != hb) {
+            if (pass == 1) p.keys[base + o + k2] = k;
+            k2++;
+          }
+        }
+      }
+      c = k2;
+    }
+    return;
   }
-  // merge each owned differing bucket's keys: count, then write at the scanned offset
+  // more differing rows or buckets than the LDS lists hold: each thread merges its owned
+  // differing buckets over global memory
   u32 c = 0;
   for (int pass = 0; pass < 2; pass++) {
     u32 o = 0;
@@ -592,33 +639,17 @@ __global__ __launch_bounds__(DB) void merkle_diff_count_kernel(DiffArgs p) {
         if (t2) atomicAdd((unsigned long long*)&p.bsum[tile / DB], (unsigned long long)t2);
       }
     }
-    u32 k2 = 0, slot = slot0, ra = offa, rb = offb;
+    u32 k2 = 0, ra = offa, rb = offb;
     for (u32 i = 0; i < OWN; i++) {
       const u32 x = half16(ca, i), y = half16(cb, i);
       if (mine >> i & 1u) {
-        if (lds) {
-          u32 ia = slot, ie = slot + x, jb = slot + x, je = slot + x + y;
-          while (ia < ie || jb < je) {
-            const u64 ka = ia < ie ? s_k[ia] : ~0ull, kb = jb < je ? s_k[jb] : ~0ull;
-            const u64 k = ka < kb ? ka : kb;
-            u64 ha = 0, hb = 0;
-            const bool pa = ia < ie && ka == k, pb = jb < je && kb == k;
-            for (; ia < ie && s_k[ia] == k; ia++) ha += s_h[ia];
-            for (; jb < je && s_k[jb] == k; jb++) hb += s_h[jb];
-            if (!(pa && pb) || ha != hb) {
-              if (pass == 1) p.keys[base + o + k2] = k;
-              k2++;
-            }
-          }
-          slot += x + y;
-        } else if (pass == 0) {
+        if (pass == 0)
           k2 += merge_bucket<false, false>(p.sa, p.ta.th, a0 + ra, a0 + ra + x, p.sb, p.tb.th,
                                            nullptr, nullptr, c0 + rb, c0 + rb + y, nullptr, 0, 0);
-        } else {
+        else
           k2 += merge_bucket<false, true>(p.sa, p.ta.th, a0 + ra, a0 + ra + x, p.sb, p.tb.th,
                                           nullptr, nullptr, c0 + rb, c0 + rb + y, p.keys + base,
                                           o + k2, ~0ull);
-        }
       }
       ra += x;
       rb += y;

@@ -31,7 +31,7 @@ namespace dg {
 namespace {
 
 constexpr int SB = 256;            // threads per workgroup
-constexpr int SR = 16;             // rows per thread
+constexpr int SR = 8;              // rows per thread (held in registers: 72 VGPRs)
 constexpr int ST = SB * SR;        // rows per tile
 constexpr int SLC = 1024;          // keyset entries of a tile staged in LDS
 
@@ -70,47 +70,112 @@ __global__ __launch_bounds__(SB) void splice_check_kernel(const u64* bkey, u64 n
   if (j >= nb) return;
   const u64 k = bkey[j];
   if (j > 0 && bkey[j - 1] == k) return;  // one probe per key
-  const u64 u = lower_bound(keys, 0, nk, k);
+  const u64 u = interp_lower_bound(keys, 0, nk, k);
   if (u == nk || keys[u] != k) atomicAdd((unsigned long long*)d_bad, 1ull);
 }
 
-// per keyset entry u: end[u], gap[u] and shift[u] (shift[nk]: after the last key)
+// per keyset entry u: end[u], gap[u] and shift[u] (shift[nk]: after the last key), and
+// the first entry of every state tile whose first row falls in [end[u-1], end[u]) (so
+// the copy's tiles look their entry range up instead of searching for it)
 __global__ __launch_bounds__(SB) void splice_index_kernel(SpliceArgs p) {
   const u64 u = (u64)blockIdx.x * SB + threadIdx.x;
   if (u > p.nk) return;
   const u64 ne = *p.d_ne;
   const u64 pa = p.a_off[u];
-  const u64 pe = u < p.nk ? lower_bound(p.e.key, 0, ne, p.keys[u]) : ne;
+  const u64 pe = u < p.nk ? interp_lower_bound(p.e.key, 0, ne, p.keys[u]) : ne;
   p.shift[u] = (i64)pe - (i64)pa;
+  const u64 end_hi = u < p.nk ? p.a_lo[u] + (p.a_off[u + 1] - pa) : ~0ull;
+  const u64 end_lo = u > 0 ? p.a_lo[u - 1] + (pa - p.a_off[u - 1]) : 0ull;
   if (u < p.nk) {
-    p.end[u] = p.a_lo[u] + (p.a_off[u + 1] - pa);
+    p.end[u] = end_hi;
     p.gap[u] = (i64)p.a_lo[u] - (i64)pa;
+  }
+  for (u64 t = (end_lo + ST - 1) / ST; t <= p.a_tiles && t * ST < end_hi; t++) p.tile_u0[t] = u;
+}
+
+// A tile's rows, loaded before anything says where they go.  Thread t holds the row
+// pairs (2 (q SB + t), +1), q < SR / 2: every column is read with 16-byte loads (8 bytes
+// for the node column), a wave covering 1 KB of a column per instruction.
+constexpr int SP = SR / 2;  // row pairs per thread
+struct TileRows {
+  u64 key[SR], val[SR], cnt[SR];
+  i64 ts[SR];
+  u32 node[SR];
+};
+
+__device__ __forceinline__ u64 pair_row(u64 j0, int q, int h) {
+  return j0 + 2 * ((u64)q * SB + threadIdx.x) + (u64)h;
+}
+
+template <class T>
+__device__ __forceinline__ void load2(const T* c, u64 j, u64 j1, T& x0, T& x1) {
+  if (j + 1 < j1) {  // j even: an aligned pair
+    if constexpr (sizeof(T) == 8) {
+      const ulonglong2 v = *(const ulonglong2*)(c + j);
+      x0 = (T)v.x;
+      x1 = (T)v.y;
+    } else {
+      const uint2 v = *(const uint2*)(c + j);
+      x0 = (T)v.x;
+      x1 = (T)v.y;
+    }
+  } else if (j < j1) {
+    x0 = c[j];
   }
 }
 
 template <class T>
-__device__ __forceinline__ void move_col(const T* src, T* dst, const u64 (&from)[SR], const i64 (&to)[SR]) {
-  T v[SR];
+__device__ __forceinline__ void store2(T* c, i64 t0, i64 t1, T x0, T x1) {
+  if (t0 >= 0 && t1 == t0 + 1 && !(t0 & 1)) {  // contiguous and aligned: one wide store
+    if constexpr (sizeof(T) == 8)
+      *(ulonglong2*)(c + t0) = ulonglong2{(unsigned long long)x0, (unsigned long long)x1};
+    else
+      *(uint2*)(c + t0) = uint2{(u32)x0, (u32)x1};
+  } else {
+    if (t0 >= 0) c[t0] = x0;
+    if (t1 >= 0) c[t1] = x1;
+  }
+}
+
+__device__ __forceinline__ void load_tile(const Rows& r, u64 j0, u64 j1, TileRows& x) {
 #pragma unroll
-  for (int q = 0; q < SR; q++) v[q] = to[q] >= 0 ? src[from[q]] : T(0);
+  for (int q = 0; q < SP; q++) {
+    const u64 j = pair_row(j0, q, 0);
+    load2(r.key, j, j1, x.key[2 * q], x.key[2 * q + 1]);
+    load2(r.val, j, j1, x.val[2 * q], x.val[2 * q + 1]);
+    load2(r.ts, j, j1, x.ts[2 * q], x.ts[2 * q + 1]);
+    load2(r.node, j, j1, x.node[2 * q], x.node[2 * q + 1]);
+    load2(r.cnt, j, j1, x.cnt[2 * q], x.cnt[2 * q + 1]);
+  }
+}
+
+__device__ __forceinline__ void store_tile(const RowsOut& o, const TileRows& x, const i64 (&to)[SR]) {
 #pragma unroll
-  for (int q = 0; q < SR; q++)
-    if (to[q] >= 0) dst[to[q]] = v[q];
+  for (int q = 0; q < SP; q++) {
+    const i64 t0 = to[2 * q], t1 = to[2 * q + 1];
+    store2(o.key, t0, t1, x.key[2 * q], x.key[2 * q + 1]);
+    store2(o.val, t0, t1, x.val[2 * q], x.val[2 * q + 1]);
+    store2(o.ts, t0, t1, x.ts[2 * q], x.ts[2 * q + 1]);
+    store2(o.node, t0, t1, x.node[2 * q], x.node[2 * q + 1]);
+    store2(o.cnt, t0, t1, x.cnt[2 * q], x.cnt[2 * q + 1]);
+  }
 }
 
 // Workgroups [0, e_tiles): E's rows (issued first, so their key searches overlap the
-// state's copy); then one workgroup per ST state rows.
+// state's copy); then one workgroup per ST state rows.  Every workgroup issues its rows'
+// loads first: the searches that place them run while the loads are in flight.
 __global__ __launch_bounds__(SB) void splice_kernel(SpliceArgs p) {
   __shared__ u64 s_end[SLC], s_lo[SLC];
   __shared__ i64 s_shift[SLC];
   __shared__ u64 s_b[2];
-  u64 from[SR];
+  TileRows x;
   i64 to[SR];
   if (blockIdx.x < p.e_tiles) {
     const u64 ne = *p.d_ne;
     const u64 j0 = (u64)blockIdx.x * ST;
     if (j0 >= ne) return;  // block-uniform
     const u64 j1 = min<u64>(j0 + ST, ne);
+    load_tile(p.e, j0, j1, x);
     // the keyset entries of the tile's keys lie in [u0, u1]: E's keys are keyset keys
     // (clamped into [0, nk): the caller checked that they are, an index stays in bounds
     // whatever the input)
@@ -125,34 +190,24 @@ __global__ __launch_bounds__(SB) void splice_kernel(SpliceArgs p) {
     const u64 u0 = s_b[0], u1 = max(s_b[0], s_b[1]);
 #pragma unroll
     for (int q = 0; q < SR; q++) {
-      const u64 j = j0 + (u64)q * SB + threadIdx.x;
-      from[q] = j;
+      const u64 j = pair_row(j0, q >> 1, q & 1);
       to[q] = -1;
       if (j < j1) {
-        const u64 u = min(lower_bound(p.keys, u0, u1 + 1, p.e.key[j]), u1);
+        const u64 u = min(lower_bound(p.keys, u0, u1 + 1, x.key[q]), u1);
         to[q] = (i64)j + p.gap[u];
       }
     }
-    move_col(p.e.key, p.out.key, from, to);
-    move_col(p.e.val, p.out.val, from, to);
-    move_col(p.e.ts, p.out.ts, from, to);
-    move_col(p.e.node, p.out.node, from, to);
-    move_col(p.e.cnt, p.out.cnt, from, to);
+    store_tile(p.out, x, to);
     return;
   }
-  const u64 i0 = (u64)(blockIdx.x - p.e_tiles) * ST;
+  const u64 t = blockIdx.x - p.e_tiles;
+  const u64 i0 = t * ST;
   const u64 i1 = min<u64>(i0 + ST, p.a.n);
   // row i's first keyset entry whose state rows end after it: u*(i) = first u with
-  // end[u] > i (nk if none); the tile's rows have u* in [u0, u1]
-  if (threadIdx.x < WAVE) {
-    const u64 u = wave_upper(p.end, p.nk, i0);
-    if (threadIdx.x == 0) s_b[0] = u;
-  } else if (threadIdx.x < 2 * WAVE) {
-    const u64 u = wave_upper(p.end, p.nk, i1 - 1);
-    if ((threadIdx.x & (WAVE - 1)) == 0) s_b[1] = u;
-  }
-  __syncthreads();
-  const u64 u0 = s_b[0], u1 = s_b[1];
+  // end[u] > i (nk if none); the tile's rows have u* in [u0, u1] (the index kernel's
+  // first entries of this tile and the next)
+  const u64 u0 = p.tile_u0[t], u1 = p.tile_u0[t + 1];
+  load_tile(p.a, i0, i1, x);
   const u64 m = u1 - u0 + 1;
   const bool staged = m <= (u64)SLC;  // block-uniform
   if (staged) {
@@ -166,8 +221,7 @@ __global__ __launch_bounds__(SB) void splice_kernel(SpliceArgs p) {
   }
 #pragma unroll
   for (int q = 0; q < SR; q++) {
-    const u64 i = i0 + (u64)q * SB + threadIdx.x;
-    from[q] = i;
+    const u64 i = pair_row(i0, q >> 1, q & 1);
     to[q] = -1;
     if (i >= i1) continue;
     u64 lo = 0, hi = m - 1;  // entry u0 + lo: the first whose end is > i (u1's is)
@@ -192,11 +246,7 @@ __global__ __launch_bounds__(SB) void splice_kernel(SpliceArgs p) {
       if (u == p.nk || p.a_lo[u] > i) to[q] = (i64)i + p.shift[u];
     }
   }
-  move_col(p.a.key, p.out.key, from, to);
-  move_col(p.a.val, p.out.val, from, to);
-  move_col(p.a.ts, p.out.ts, from, to);
-  move_col(p.a.node, p.out.node, from, to);
-  move_col(p.a.cnt, p.out.cnt, from, to);
+  store_tile(p.out, x, to);
 }
 
 }  // namespace
@@ -209,11 +259,13 @@ hipError_t launch_splice_check(const u64* bkey, u64 nb, const u64* keys, u64 nk,
   return hipGetLastError();
 }
 
+u64 splice_tiles(u64 n) { return (n + ST - 1) / ST; }
+
 hipError_t launch_splice(SpliceArgs p, hipStream_t st) {
-  hipLaunchKernelGGL(splice_index_kernel, dim3((unsigned)((p.nk + 1 + SB - 1) / SB)), dim3(SB), 0,
-                     st, p);
   p.a_tiles = (p.a.n + ST - 1) / ST;
   p.e_tiles = (p.e.n + ST - 1) / ST;
+  hipLaunchKernelGGL(splice_index_kernel, dim3((unsigned)((p.nk + 1 + SB - 1) / SB)), dim3(SB), 0,
+                     st, p);
   if (p.a_tiles + p.e_tiles == 0) return hipGetLastError();
   hipLaunchKernelGGL(splice_kernel, dim3((unsigned)(p.a_tiles + p.e_tiles)), dim3(SB), 0, st, p);
   return hipGetLastError();

@@ -4,7 +4,7 @@
 // rows: every row of `s` whose key is in the ascending key list, in store order.
 //
 // One workgroup per tile of TK keys (ticket order): each thread finds the row range of
-// its keys by binary search (the store is sorted by key), a block scan turns the
+// its keys by interpolation search (the store is sorted by key ids, which are hashes), a block scan turns the
 // range lengths into tile-local offsets, the tile's output offset comes from the
 // decoupled look-back, and the workgroup copies the tile's rows with coalesced
 // writes (output slot -> its key by a search over the tile-local offsets in LDS).
@@ -16,7 +16,7 @@ namespace dg {
 
 namespace {
 
-constexpr int TB = 256, TI = 4, TK = TB * TI;
+constexpr int TB = 1024, TI = 1, TK = TB * TI;  // one key per thread: the searches run side by side
 
 __global__ __launch_bounds__(TB) void take_keys_kernel(Rows s, const u64* keys, u64 n_keys,
                                                       u64 ntiles, RowsOut out, u64 cap, Scan scan,
@@ -43,14 +43,7 @@ __global__ __launch_bounds__(TB) void take_keys_kernel(Rows s, const u64* keys, 
     len[q] = 0;
     if (i < nk) {
       const u64 key = keys[k0 + i];
-      u64 a = 0, b = s.n;  // first row with key >= `key`
-      while (a < b) {
-        const u64 m = (a + b) >> 1;
-        if (s.key[m] < key)
-          a = m + 1;
-        else
-          b = m;
-      }
+      const u64 a = interp_lower_bound(s.key, 0, s.n, key);  // first row with key >= `key`
       u64 e = a;  // a key's rows are few: walk them
       while (e < s.n && s.key[e] == key) e++;
       lo[q] = a;

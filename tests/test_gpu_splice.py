@@ -124,3 +124,24 @@ def test_config4_round_splice_vs_full(engine, full_engine, rank):
     out = check(engine, full_engine, a, W.sync_delta(b, want), want)
     wr, _ = R.join2(a["rows"], a["ctx"], b["rows"], b["ctx"])
     rows_eq(out, wr)
+
+
+def test_splice_unaligned_columns_take_the_full_join(engine, full_engine, pair):
+    """A state whose columns are 8-byte offset views (not 16-byte aligned) is joined by
+    the full merge; the result is the same."""
+    a, b = pair
+    keys = np.unique(a["rows"][0][::150])
+    sa, ca = up(a)
+    n = sa.n
+    cols = []
+    for c in (sa.key, sa.val, sa.ts, sa.node, sa.cnt):
+        buf = torch.empty(n + 1, dtype=c.dtype, device=DEV)
+        buf[1:].copy_(c[:n])
+        cols.append(buf[1:])
+    su = Store(*cols, n)
+    d = W.sync_delta(b, keys)
+    sd, cd = up(d)
+    out, octx = engine.join2(su, ca, sd, cd, keys=kdev(keys))
+    wr, wc = R.join2(a["rows"], a["ctx"], d["rows"], d["ctx"], keys=keys)
+    rows_eq(out, wr)
+    ctx_eq(octx, wc)
