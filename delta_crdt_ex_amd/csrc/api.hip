@@ -855,6 +855,7 @@ int kfold_pass(dg_engine* e, const dg_store* state, const dg_context* ctx, int k
   }
   auto ceil_div = [](u64 a, u64 b) { return (a + b - 1) / b; };
   const u64 T0 = std::max<u64>({ceil_div(state->n, KFOLD_MEAN_S), ceil_div(m_rows, KFOLD_MEAN_D),
+                                ceil_div(m_keys, KFOLD_MEAN_M),
                                 ceil_div(m_rows + m_keys, KFOLD_MEAN_U), 1});
   // a bucket over capacity (key groups far larger than the mean, or keys that are not
   // uniform hashes) is retried once with 8x the buckets

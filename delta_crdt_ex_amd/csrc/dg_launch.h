@@ -90,13 +90,14 @@ constexpr int KNT = 1024;          // VV tables cover node ids < KNT
 constexpr u32 KF_PREP_FAIL = 1, KF_OVERFLOW = 2;
 constexpr u64 KFOLD_FILL_CHUNK = 1024 * 8;  // elements per workgroup of the bucket fill
 // mean fill per bucket the host sizes T for, each >= 5.5 sigma below its LDS capacity:
-// state rows (cap 1024), delta rows (their payload slots: cap 512) and all items, delta
-// rows + keyset entries (one per thread: cap 1024; a touched key brings a keyset entry and
-// usually a row, so items vary about twice as much as a Poisson count: mean 780).
-// Config 3: 14.7k buckets instead of 19.9k (separate caps 1024 / 512 / 512 and means
-// 640 / 320 / 320 before).
+// state rows (cap 1024), delta rows (their payload slots: cap 512), keyset entries as
+// staged (cap 1024: a thread stages two items) and all staged items (delta rows + keyset
+// entries, cap 1536).  After the keyset fold (entries with rows of the key fold into
+// them) at most 1024 items remain; a bucket over that re-runs the pass with 8x the
+// buckets.  Config 3: 12.7k buckets (the delta rows bind), 14.7k when every keyset entry
+// took an item slot of its own.
 constexpr u64 KFOLD_MEAN_S = 800 >> DG_KFOLD_SCALE, KFOLD_MEAN_D = 400 >> DG_KFOLD_SCALE,
-              KFOLD_MEAN_U = 780 >> DG_KFOLD_SCALE;
+              KFOLD_MEAN_M = 800 >> DG_KFOLD_SCALE, KFOLD_MEAN_U = 1200 >> DG_KFOLD_SCALE;
 struct KRun {  // delta i: its rows, keyset (keys == nullptr: every key) and context
   Rows rows;
   const u64* keys;

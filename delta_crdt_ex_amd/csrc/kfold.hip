@@ -44,12 +44,14 @@ constexpr int KB = KFOLD_BLOCK;
 constexpr int CS = KFOLD_CAP_S;  // state rows per bucket
 constexpr int CD = KFOLD_CAP_D;  // delta rows per bucket
 constexpr int CM = KFOLD_CAP_M;  // keyset markers per bucket
-constexpr int CU = CD + CM;
+constexpr int CU = CD + CM;      // items after the keyset fold (delta rows + unfolded entries)
+constexpr int CUL = CD + 2 * CM; // items staged: delta rows + keyset entries, before the fold
 constexpr u32 MARK = 1u << 15;   // utag: (src << 16) | MARK? | KIN? | pre-sort slot
 constexpr u32 KIN = 1u << 14;    // a delta row whose key is in its own delta's keyset
 constexpr u32 SLOT = KIN - 1;
 static_assert(2 * KFOLD_MAX_K <= KB, "one thread per run");
-static_assert(CU <= SLOT + 1, "slot bits");
+static_assert(CUL <= SLOT + 1, "slot bits");
+static_assert(CD <= KFOLD_BLOCK && CUL <= 2 * KFOLD_BLOCK, "items q and q + KB of a thread: the second is a keyset entry");
 
 __device__ __forceinline__ u64 bucket_of(u64 key, u64 T) { return __umul64hi(key, T); }
 
@@ -303,8 +305,16 @@ struct KLds {
   u32 dnode[CD];
   u64 ukey[CU];                       // items: delta rows [0, nD), keyset markers [nD, nU)
   u32 utag[CU];                       // (src << 16) | MARK? | slot; (key, tag) order once sorted
-  unsigned short ustart[NSUB + 1];    // sub-bucket b: items [ustart[b], ustart[b+1])
-  unsigned short sfirst[NSUB + 1];    //               state rows [sfirst[b], sfirst[b+1])
+  union {
+    struct {
+      unsigned short ustart[NSUB + 1];  // sub-bucket b: items [ustart[b], ustart[b+1])
+      unsigned short sfirst[NSUB + 1];  //               state rows [sfirst[b], sfirst[b+1])
+      unsigned short slbu[CS];          // state row -> first sorted item with key >= its key
+      unsigned char ssurv[CS], usurv[CU];  // usurv by sorted position
+    } e;
+    u64 mkey[CUL - CD];               // while staging: the keyset entries' keys, before the
+                                      // ones with rows of the key fold into those rows
+  } y;
   union {
     u32 ucnt[NSUB];                   // counting-sort histogram / fill counters
     struct {
@@ -315,8 +325,6 @@ struct KLds {
       const u64* keys[KFOLD_MAX_K];   //   keysets
     } run;
   } x;
-  unsigned short slbu[CS];            // state row -> first sorted item with key >= its key
-  unsigned char ssurv[CS], usurv[CU]; // usurv by sorted position
   u32 roff[2 * KFOLD_MAX_K + 1];
   u32 rbeg[2 * KFOLD_MAX_K];
   u32 wave[KB / WAVE + 1];
@@ -398,7 +406,7 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
   bool bad = p.sstart[t + 1] < s0;
   if (tid < nr) {
     const u32 a = p.dstart[t * nr + tid], b = p.dstart[(t + 1) * nr + tid];
-    len = b >= a ? min(b - a, (u32)CU + 1) : 0u;  // bounded: the sum cannot wrap
+    len = b >= a ? min(b - a, (u32)CUL + 1) : 0u;  // bounded: the sum cannot wrap
     bad |= b < a;
     s.rbeg[tid] = a;
   }
@@ -416,26 +424,34 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
   KSTAMP(t, 12);
   __syncthreads();
   u32 nD = s.roff[k];
-  if (bad || nS > (u32)CS || nD > (u32)CD || nU > (u32)CU) {  // (keyset entries take
-                                                              // any share of the items)
+  if (bad || nS > (u32)CS || nD > (u32)CD || nU > (u32)CUL || nU - nD > (u32)(CUL - CD)) {
     if (tid == 0) atomicOr(p.flag, KF_OVERFLOW);
     nS = nU = nD = 0;  // publish an empty bucket so the look-back chain stays live
   }
 
-  // ---- stage: state slice, delta rows (slot = pre-sort index), keyset markers; the
-  //      item's loads are issued before either row is written to LDS
-  const u32 q = tid;  // this thread's item
+  // ---- stage: state slice, delta rows (slot = pre-sort index) and the keyset entries'
+  //      keys (y.mkey, by index - nD); a thread stages items q and q + KB (the second,
+  //      past every delta row, is a keyset entry); the loads are issued before any row is
+  //      written to LDS
+  const u32 q = tid;  // this thread's items: q, and q2 = q + KB
+  const u32 q2 = tid + KB;
   Row ir{};
   u32 itag = 0;
-  if (q < nU) {
-    int lo = 0, hi = nr;  // roff[lo] <= q < roff[hi]
+  u64 key2 = 0;
+  u32 tag2 = 0;
+  auto run_of = [&](u32 x) {  // roff[lo] <= x < roff[lo + 1]
+    int lo = 0, hi = nr;
     while (hi - lo > 1) {
       const int mid = (lo + hi) >> 1;
-      if (s.roff[mid] <= q)
+      if (s.roff[mid] <= x)
         lo = mid;
       else
         hi = mid;
     }
+    return lo;
+  };
+  if (q < nU) {
+    const int lo = run_of(q);
     const u64 j = (u64)s.rbeg[lo] + (q - s.roff[lo]);
     if (lo < k) {
       const RowsOut& R = s.x.run.d[lo];
@@ -446,6 +462,11 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
       itag = ((u32)(lo - k) << 16) | MARK | q;
     }
   }
+  if (q2 < nU) {
+    const int lo = run_of(q2);
+    key2 = s.x.run.keys[lo - k][(u64)s.rbeg[lo] + (q2 - s.roff[lo])];
+    tag2 = ((u32)(lo - k) << 16) | MARK | q2;
+  }
   if (hs && (u32)tid < nS) {
     s.skey[tid] = sr.key;
     s.sval[tid] = sr.val;
@@ -454,46 +475,58 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
     s.scnt[tid] = sr.cnt;
   }
   if (q < nU) {
-    s.ukey[q] = ir.key;
-    s.utag[q] = itag;
     if (!(itag & MARK)) {
+      s.ukey[q] = ir.key;
       s.dkey[q] = ir.key;
       s.dval[q] = ir.val;
       s.dts[q] = ir.ts;
       s.dnode[q] = ir.node;
       s.dcnt[q] = ir.cnt;
+    } else {
+      s.y.mkey[q - nD] = ir.key;
     }
   }
+  if (q2 < nU) s.y.mkey[q2 - nD] = key2;
   KSTAMP(t, 1);
   __syncthreads();  // (the run pointers in s.x are dead: the histogram takes it)
 
   // ---- a keyset entry of a delta that also has rows of the key is folded into those
   //      rows (KIN on their tags) and dropped from the items: a sync delta's keyset is
   //      mostly its row keys (Map.take(value, keys)), so the sort and every walk below
-  //      see about half the items.  Rows search their delta's keyset slice, entries their
-  //      delta's row slice (both sorted, both staged: slot q holds item q).
-  bool keep = false;
-  if (q < nU) {
-    const u32 src = itag >> 16;
-    const bool mark = itag & MARK;
-    const u32 lo = mark ? s.roff[src] : s.roff[k + src];
-    const u32 hi = mark ? s.roff[src + 1] : s.roff[k + src + 1];
-    const u64* col = mark ? s.dkey : s.ukey;
+  //      see about half the items.  Rows search their delta's keyset slice (y.mkey),
+  //      entries their delta's row slice (dkey; both sorted).
+  auto in_slice = [&](const u64* col, u32 lo, u32 hi, u64 x) {
     u32 a = lo, b = hi;
     while (a < b) {
       const u32 m = (a + b) >> 1;
-      if (col[m] < ir.key)
+      if (col[m] < x)
         a = m + 1;
       else
         b = m;
     }
-    const bool found = a < hi && col[a] == ir.key;
-    if (!mark && found) itag |= KIN;
-    keep = mark && !found;
+    return a < hi && col[a] == x;
+  };
+  bool keep = false, keep2 = false;
+  if (q < nU) {
+    const u32 src = itag >> 16;
+    if (itag & MARK) {
+      keep = !in_slice(s.dkey, s.roff[src], s.roff[src + 1], ir.key);
+    } else if (in_slice(s.y.mkey, s.roff[k + src] - nD, s.roff[k + src + 1] - nD, ir.key)) {
+      itag |= KIN;
+    }
+  }
+  if (q2 < nU) {
+    const u32 src = tag2 >> 16;
+    keep2 = !in_slice(s.dkey, s.roff[src], s.roff[src + 1], key2);
   }
   u32 n_keep;
   // (the scan's barriers come after every search: the entries may move after it)
-  const u32 kpos = block_excl_scan<KB>(keep ? 1u : 0u, s.wave, &n_keep);
+  const u32 kpos = block_excl_scan<KB>((keep ? 1u : 0u) + (keep2 ? 1u : 0u), s.wave, &n_keep);
+  if (nD + n_keep > (u32)CU) {  // more unfolded keyset entries than item slots (uniform)
+    if (tid == 0) atomicOr(p.flag, KF_OVERFLOW);
+    nS = nD = n_keep = 0;
+    keep = keep2 = false;
+  }
   if (q < nD) {
     s.utag[q] = itag;
   } else if (keep) {
@@ -501,8 +534,14 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
     s.ukey[nq] = ir.key;
     s.utag[nq] = (itag & ~SLOT) | nq;
   }
+  if (keep2) {
+    const u32 nq = nD + kpos + (keep ? 1u : 0u);
+    s.ukey[nq] = key2;
+    s.utag[nq] = (tag2 & ~SLOT) | nq;
+  }
   nU = nD + n_keep;
   for (u32 b = tid; b < NSUB; b += KB) s.x.ucnt[b] = 0;
+  KSTAMP(t, 13);
   __syncthreads();
 
   // ---- counting sort of the items by sub-bucket, then (key, tag) within one
@@ -510,23 +549,23 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
   for (u32 i = tid; i < nS; i += KB) {  // state rows: first row of every sub-bucket
     const u32 sb = sub_of(s.skey[i], T, t);
     u32 b = i == 0 ? 0 : sub_of(s.skey[i - 1], T, t) + 1;
-    for (; b <= sb; b++) s.sfirst[b] = (unsigned short)i;
+    for (; b <= sb; b++) s.y.e.sfirst[b] = (unsigned short)i;
     if (i == nS - 1)
-      for (b = sb + 1; b <= (u32)NSUB; b++) s.sfirst[b] = (unsigned short)nS;
+      for (b = sb + 1; b <= (u32)NSUB; b++) s.y.e.sfirst[b] = (unsigned short)nS;
   }
   if (nS == 0)
-    for (u32 b = tid; b <= (u32)NSUB; b += KB) s.sfirst[b] = 0;
+    for (u32 b = tid; b <= (u32)NSUB; b += KB) s.y.e.sfirst[b] = 0;
   KSTAMP(t, 8);
   __syncthreads();
-  scan_excl(s.x.ucnt, NSUB, s.ustart, s.wave);
+  scan_excl(s.x.ucnt, NSUB, s.y.e.ustart, s.wave);
   KSTAMP(t, 9);
   __syncthreads();
   for (u32 b = tid; b < NSUB; b += KB) s.x.ucnt[b] = 0;
   __syncthreads();
-  unsigned short* bin = s.slbu;  // items grouped by sub-bucket (slbu is free until evaluation)
+  unsigned short* bin = s.y.e.slbu;  // items grouped by sub-bucket (slbu is free until evaluation)
   for (u32 q = tid; q < nU; q += KB) {
     const u32 sb = sub_of(s.ukey[q], T, t);
-    bin[s.ustart[sb] + atomicAdd(&s.x.ucnt[sb], 1u)] = (unsigned short)q;
+    bin[s.y.e.ustart[sb] + atomicAdd(&s.x.ucnt[sb], 1u)] = (unsigned short)q;
   }
   KSTAMP(t, 10);
   __syncthreads();
@@ -541,7 +580,7 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
     mp[j] = ~0u;
     if (q >= nU) continue;
     const u64 kq = s.ukey[q];
-    const u32 tq = s.utag[q], sb = sub_of(kq, T, t), lo = s.ustart[sb], hi = s.ustart[sb + 1];
+    const u32 tq = s.utag[q], sb = sub_of(kq, T, t), lo = s.y.e.ustart[sb], hi = s.y.e.ustart[sb + 1];
     u32 rank = 0;
     for (u32 e = lo; e < hi; e++) {
       const u32 w = bin[e];
@@ -573,10 +612,10 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
     const u32 i = tid;
     const Row r = srow(s, i);
     const u32 sb = sub_of(r.key, T, t);
-    u32 e = s.ustart[sb];
-    const u32 qe = s.ustart[sb + 1];
+    u32 e = s.y.e.ustart[sb];
+    const u32 qe = s.y.e.ustart[sb + 1];
     while (e < qe && s.ukey[e] < r.key) e++;
-    s.slbu[i] = (unsigned short)e;
+    s.y.e.slbu[i] = (unsigned short)e;
     for (; e < qe && s.ukey[e] == r.key; e++) {
       const u32 tg = s.utag[e], src = tg >> 16;
       if (tg & (MARK | KIN)) cs.K |= 1ull << src;
@@ -610,8 +649,8 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
     }
     // a tuple the state holds is evaluated (and emitted) as the state's row (the state
     // rows of the sub-bucket are sorted: compare full rows only under the same key)
-    u32 i = s.sfirst[sb];
-    const u32 ie = s.sfirst[sb + 1];
+    u32 i = s.y.e.sfirst[sb];
+    const u32 ie = s.y.e.sfirst[sb + 1];
     while (i < ie && s.skey[i] < r.key) i++;
     for (; first && i < ie && s.skey[i] == r.key; i++)
       if (row_eq(srow(s, i), r)) first = false;
@@ -621,12 +660,12 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
   }
   KSTAMP(t, 7);
   present2(cs, ds, cu, du, p.tabC, p.tabP);
-  if (ds) s.ssurv[tid] = cs.P;
-  if ((u32)tid < nU) s.usurv[tid] = du && cu.P;
+  if (ds) s.y.e.ssurv[tid] = cs.P;
+  if ((u32)tid < nU) s.y.e.usurv[tid] = du && cu.P;
   KSTAMP(t, 3);
   __syncthreads();
-  scan_excl(s.ssurv, nS, s.x.pre.spre, s.wave);
-  scan_excl(s.usurv, nU, s.x.pre.upre, s.wave);
+  scan_excl(s.y.e.ssurv, nS, s.x.pre.spre, s.wave);
+  scan_excl(s.y.e.usurv, nU, s.x.pre.upre, s.wave);
   __syncthreads();
   KSTAMP(t, 4);
 
@@ -646,32 +685,32 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
   for (int j = 0; j < RS; j++) {
     const u32 i = tid + j * KB;
     so[j] = ~0u;
-    if (i >= nS || !s.ssurv[i]) continue;
+    if (i >= nS || !s.y.e.ssurv[i]) continue;
     const Row r = srow(s, i);
-    const u32 lb = s.slbu[i];
+    const u32 lb = s.y.e.slbu[i];
     u32 less = 0;
     for (u32 q = lb; q < nU && s.ukey[q] == r.key; q++)
-      if (s.usurv[q] && row_cmp(drow(s, s.utag[q] & SLOT), r) < 0) less++;
+      if (s.y.e.usurv[q] && row_cmp(drow(s, s.utag[q] & SLOT), r) < 0) less++;
     so[j] = spre[i] + upre[lb] + less;
   }
 #pragma unroll
   for (int j = 0; j < RU; j++) {
     const u32 q = tid + j * KB;
     uo[j] = ~0u;
-    if (q >= nU || !s.usurv[q]) continue;
+    if (q >= nU || !s.y.e.usurv[q]) continue;
     const Row r = drow(s, s.utag[q] & SLOT);
     const u32 sb = sub_of(r.key, T, t);
     u32 gb = q;  // the first item of its key: a few positions back at most
     while (gb > 0 && s.ukey[gb - 1] == r.key) gb--;
     u32 less = 0;
     for (u32 e = gb; e < nU && s.ukey[e] == r.key; e++)
-      if (s.usurv[e] && row_cmp(drow(s, s.utag[e] & SLOT), r) < 0) less++;
-    u32 ls = s.sfirst[sb];
-    const u32 le = s.sfirst[sb + 1];
+      if (s.y.e.usurv[e] && row_cmp(drow(s, s.utag[e] & SLOT), r) < 0) less++;
+    u32 ls = s.y.e.sfirst[sb];
+    const u32 le = s.y.e.sfirst[sb + 1];
     while (ls < le && s.skey[ls] < r.key) ls++;
     u32 sl = 0;
     for (u32 i = ls; i < le && s.skey[i] == r.key; i++)
-      if (s.ssurv[i] && row_cmp(srow(s, i), r) < 0) sl++;
+      if (s.y.e.ssurv[i] && row_cmp(srow(s, i), r) < 0) sl++;
     uo[j] = spre[ls] + sl + upre[gb] + less;
   }
   KSTAMP(t, 5);
