@@ -249,60 +249,79 @@ def resident_delta(eng, torch, sa, ca, cb, ta, tb, b, reps=7):
     """What a NIF caller pays per sync delta against a device-resident state
     (join_delta; the reference's update_state_with_delta,
     causal_crdt.ex:383-404), at wall time on the config-4 shard: H2D of the delta's rows
-    and keyset from pinned host memory, dg_join2_changes (the keyed join as a splice plus
-    the changed keys), dg_merkle_update of those keys, and D2H of the changed keys and
-    their rows (dg_take_keys) for the on_diffs callback."""
+    and keyset from pinned host memory, dg_join_delta (the keyed join applied in place --
+    every differing key keeps its one row -- its changed keys and the MerkleMap update),
+    and D2H of the changed keys and their rows (dg_take_keys) for the on_diffs callback.
+    The state is restored from a pristine copy before each rep (outside the clock)."""
     from delta_crdt_ex_amd import workloads as W
     from delta_crdt_ex_amd.store import Context, Store
     dev = sa.key.device
     keys_np = eng.merkle_diff(ta, tb).cpu().numpy().view(np.uint64)  # the differing keys
     d = W.sync_delta(b, keys_np)
-    n = len(d["rows"][0])
-    cols = [np.ascontiguousarray(c) for c in d["rows"]] + [np.ascontiguousarray(keys_np)]
-    pinned = [torch.from_numpy(c.view(np.int64 if c.dtype.itemsize == 8 else np.int32)).pin_memory()
-              for c in cols]
-    dst = Store.empty(max(n, 1), dev)
-    kdst = torch.empty(max(len(keys_np), 1), dtype=torch.int64, device=dev)
-    out = Store.empty(sa.n + n, dev)
-    octx = Context.empty(0, ca.n + cb.n, dev)
-    back = None
+    n, nk = len(d["rows"][0]), len(keys_np)
+    # the delta as ONE pinned message (key | val | ts | cnt | keyset | node), one H2D copy;
+    # the device store's columns are views into the landed buffer
+    words = 4 * n + nk + (n + 1) // 2
+    msg = torch.empty(words, dtype=torch.int64).pin_memory()
+    m = msg.numpy()
+    k_, v_, t_, nd_, c_ = d["rows"]
+    for i, col in enumerate((k_, v_, t_, c_)):
+        m[i * n:(i + 1) * n] = col.view(np.int64)
+    m[4 * n:4 * n + nk] = keys_np.view(np.int64)
+    m[4 * n + nk:].view(np.int32)[:n] = nd_.view(np.int32)
+    dbuf = torch.empty(words, dtype=torch.int64, device=dev)
+    dst = Store(dbuf[0:n], dbuf[n:2 * n], dbuf[2 * n:3 * n],
+                dbuf[4 * n + nk:].view(torch.int32)[:n], dbuf[3 * n:4 * n], n)
+    kd = dbuf[4 * n:4 * n + nk]
+    # the changed keys' rows come back the same way: one device buffer, one D2H copy
+    rcap = max(nk, 1)  # the changed keys and their rows (one per key here)
+    rhost = torch.empty(5 * rcap + rcap, dtype=torch.int64).pin_memory()
+    st = Store.empty(sa.n + n, dev)
+    spare = Store.empty(sa.n + n, dev)
+    sc = Context.empty(ca.kind, ca.n + cb.n, dev)
+    # (rows: key | val | ts | cnt | node, then the changed keys)
+    cbuf = torch.empty(5 * rcap + rcap, dtype=torch.int64, device=dev)
+    rst = Store(cbuf[0:rcap], cbuf[rcap:2 * rcap], cbuf[2 * rcap:3 * rcap],
+                cbuf[4 * rcap:5 * rcap].view(torch.int32)[:rcap], cbuf[3 * rcap:4 * rcap], 0)
+    changed = cbuf[5 * rcap:]
     ph = {}
+    swaps = 0
     for it in range(reps + 1):
+        for f in ("key", "val", "ts", "node", "cnt"):
+            getattr(st, f)[: sa.n].copy_(getattr(sa, f)[: sa.n])
+        st.n = sa.n
+        sc.node[: ca.n].copy_(ca.node[: ca.n])
+        sc.cnt[: ca.n].copy_(ca.cnt[: ca.n])
+        sc.n, sc.kind = ca.n, ca.kind
         tt = ta.clone()
+        tt.store = st
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for h, t in zip(pinned, (dst.key, dst.val, dst.ts, dst.node, dst.cnt, kdst)):
-            t[: h.numel()].copy_(h, non_blocking=True)
-        dst.n = n
-        kd = kdst[: len(keys_np)]
+        dbuf.copy_(msg, non_blocking=True)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        out, octx, changed = eng.join2_changes(sa, ca, dst, cb, keys=kd, out=out, out_ctx=octx)
+        ch, sw = eng.join_delta(st, sc, dst, cb, kd, spare, tt, changed=changed)
         t2 = time.perf_counter()
-        eng.merkle_update(tt, out, changed)
-        t3 = time.perf_counter()
-        rows = eng.take_keys(out, changed)
-        if back is None:
-            back = [torch.empty(out.n, dtype=c.dtype).pin_memory()
-                    for c in (rows.key, rows.val, rows.ts, rows.node, rows.cnt)]
-        nr = rows.n
-        for h, c in zip(back, (rows.key, rows.val, rows.ts, rows.node, rows.cnt)):
-            h[:nr].copy_(c[:nr], non_blocking=True)
-        ck = changed.cpu()
+        rows = eng.take_keys(st, ch, out=rst)
+        nr, nch = rows.n, int(ch.numel())
+        rhost.copy_(cbuf, non_blocking=True)  # rows and changed keys: one D2H copy
         torch.cuda.synchronize()
-        t4 = time.perf_counter()
+        t3 = time.perf_counter()
+        swaps += int(sw)
         if it:
-            for k, v in (("h2d", t1 - t0), ("join_changes", t2 - t1), ("merkle_update", t3 - t2),
-                         ("d2h_changed_rows", t4 - t3), ("total", t4 - t0)):
+            for k, v in (("h2d", t1 - t0), ("join_delta", t2 - t1), ("d2h_changed_rows", t3 - t2),
+                         ("total", t3 - t0)):
                 ph.setdefault(k, []).append(v)
     med = {k: float(np.median(v)) * 1e6 for k, v in ph.items()}
     return {"metric": "sync delta applied to a device-resident state (config-4 shard), wall time",
-            "us": med, "delta_rows": n, "keyset": int(len(keys_np)), "changed_keys": int(ck.numel()),
-            "rows_back": int(nr), "state_rows": sa.n,
-            "bytes_h2d": 36 * n + 8 * len(keys_np), "bytes_d2h": 36 * int(nr) + 8 * int(ck.numel()),
+            "us": med, "delta_rows": n, "keyset": int(len(keys_np)), "changed_keys": nch,
+            "rows_back": int(nr), "state_rows": sa.n, "in_place": swaps == 0,
+            "bytes_h2d": 8 * words, "bytes_d2h": 8 * (5 * rcap + rcap),
             "deltas_per_s": 1e6 / med["total"],
-            "note": "synchronous calls, pinned host buffers reused, median of reps; the keyed "
-                    "join is the splice (csrc/splice.hip): untouched rows streamed once"}
+            "note": "synchronous calls; the delta travels as one pinned message (one H2D copy) "
+                    "and the changed keys with their rows as one D2H copy; median of reps; join_delta = "
+                    "dg_join_delta: the state's rows of the keyset taken, joined with the delta, "
+                    "written back in place (csrc/splice.hip), changed keys, MerkleMap update"}
 
 
 def _timed(torch, fn, reps):

@@ -377,6 +377,10 @@ int join2_enqueue(dg_engine* e, const dg_store* a, const dg_context* ca, const d
   return DG_OK;
 }
 
+MerkleT merkle_of(const dg_merkle* t);
+int check_merkle(const dg_merkle* t, const char* what);
+int input_error(dg_engine* e, const char* what);
+
 // Engine scratch that persists across calls (the fold's ping-pong states; the splice's
 // taken rows, edit and index), grown on demand.
 int ensure_buf(dg_engine* e, void** buf, size_t* cap, size_t bytes) {
@@ -430,6 +434,92 @@ bool splice_wanted(const dg_engine* e, const dg_store* a, const dg_store* b, con
          pair_aligned(out->key, out->val, out->ts, out->node, out->cnt);
 }
 
+// The splice's scratch (e->spl): the state's rows of the keyset (ak), the edit (ed),
+// the per-key index and the per-tile entry ranges; and a context for the join's union.
+struct Splice {
+  dg_store ak, ed;
+  dg_context uctx;
+  SpliceArgs sp;
+  u64 n_ak = 0;
+};
+
+// Phase 1: take the state's rows of the keyset (with the per-key index) and check that
+// every key of the delta is in the keyset.  *ok = false: the splice does not apply (the
+// full join does).  One host sync.
+int splice_take(dg_engine* e, const dg_store* a, const dg_store* b, const uint64_t* keys,
+                uint64_t n_keys, u64 uctx_cap, Splice* w, bool* ok) {
+  *ok = false;
+  const u64 cap_k = std::min<u64>(a->n, 16 * n_keys + 4096);  // taken rows: a few per key
+  const u64 cap_e = cap_k + b->n;
+  const size_t idx_bytes = ((n_keys + 1) * 8 + 255) / 256 * 256;
+  const size_t tile_bytes = ((splice_tiles(a->n) + 1) * 8 + 255) / 256 * 256;
+  const size_t ctx_bytes = (uctx_cap * 12 + 2 * 256) / 256 * 256 + 256;
+  const size_t bytes = ((cap_k * 36 + 5 * 256) + (cap_e * 36 + 5 * 256) + 5 * idx_bytes +
+                        tile_bytes + ctx_bytes + 256 + 255) / 256 * 256;
+  TRY(ensure_buf(e, &e->spl, &e->spl_cap, bytes));
+  char* p = (char*)e->spl;
+  w->ak = carve_store(p, cap_k);
+  w->ed = carve_store(p, cap_e);
+  SpliceArgs& sp = w->sp;
+  sp = SpliceArgs{};
+  sp.a_lo = (u64*)p;
+  sp.a_off = (u64*)(p + idx_bytes);
+  sp.end = (u64*)(p + 2 * idx_bytes);
+  sp.shift = (i64*)(p + 3 * idx_bytes);
+  sp.gap = (i64*)(p + 4 * idx_bytes);
+  p += 5 * idx_bytes;
+  sp.tile_u0 = (u64*)p;
+  p += tile_bytes;
+  w->uctx = dg_context{};
+  w->uctx.cnt = (uint64_t*)p;
+  w->uctx.node = (uint32_t*)(p + (uctx_cap * 8 + 255) / 256 * 256);
+  w->uctx.cap = uctx_cap;
+  p += ctx_bytes;
+  sp.moved = (u32*)(e->d_counts + 5);  // zeroed with n_ak and bad below
+  TRY(ensure_state(e, take_tiles(n_keys) + 2));
+  Scan sc;
+  TRY(next_scan(e, &sc));
+  HIP_TRY(hipMemsetAsync(e->d_counts + 3, 0, 3 * sizeof(u64), e->stream));  // n_ak, bad, moved
+  // the keyset's rows: one search per key, or -- once the keys are dense enough that the
+  // searches' scattered lines outweigh reading every key -- one streaming pass over the
+  // state's keys (the located ranges go through `end`, which the index overwrites later).
+  // At 1 key in 100 rows (config 4) both take 60 us for 12.5M rows; the searches grow
+  // with the keys, the pass does not.
+  u32* pre_len = nullptr;
+  if (n_keys * 60 >= a->n) {
+    pre_len = (u32*)sp.end;
+    HIP_TRY(launch_splice_locate(rows_of(a), keys, n_keys, (u64*)sp.a_lo, pre_len, e->stream));
+  }
+  HIP_TRY(launch_take_keys(rows_of(a), keys, n_keys, rows_out_of(&w->ak), cap_k, sc,
+                           e->d_counts + 3, e->stream, (u64*)sp.a_lo, (u64*)sp.a_off, pre_len));
+  HIP_TRY(launch_splice_check(b->key, b->n, keys, n_keys, e->d_counts + 4, e->stream));
+  TRY(read_counts(e, 5));
+  w->n_ak = e->h_counts[3];
+  if (e->h_counts[4] != 0 || w->n_ak > cap_k) return DG_OK;
+  w->ak.n = w->n_ak;
+  sp.a = rows_of(a);
+  sp.keys = keys;
+  sp.nk = n_keys;
+  sp.e = rows_of(&w->ed);
+  sp.e.n = w->n_ak + b->n;  // a bound: the kernels read the count
+  sp.d_ne = e->d_counts;
+  *ok = true;
+  return DG_OK;
+}
+
+// Phase 2: the edit E = join(taken rows, delta, keys) (+ its changed keys) and the index.
+int splice_edit(dg_engine* e, Splice* w, const dg_context* ca, const dg_store* b,
+                const dg_context* cb, const uint64_t* keys, uint64_t n_keys, dg_context* out_ctx,
+                bool with_changes, uint64_t* changed, uint64_t cap) {
+  void* chg = nullptr;
+  TRY(join2_enqueue(e, &w->ak, ca, b, cb, keys, n_keys, &w->ed, out_ctx, e->d_counts,
+                    with_changes ? &chg : nullptr));
+  if (with_changes)
+    HIP_TRY(launch_join2_changes(w->ak.n, b->n, chg, changed, cap, e->d_counts + 2, e->stream));
+  HIP_TRY(launch_splice_index(w->sp, e->stream));
+  return DG_OK;
+}
+
 int splice_join(dg_engine* e, const dg_store* a, const dg_context* ca, const dg_store* b,
                 const dg_context* cb, const uint64_t* keys, uint64_t n_keys, dg_store* out,
                 dg_context* out_ctx, bool with_changes, uint64_t* changed, uint64_t cap,
@@ -446,55 +536,15 @@ int splice_join(dg_engine* e, const dg_store* a, const dg_context* ca, const dg_
   if (!out->key || !out->val || !out->ts || !out->node || !out->cnt)
     return fail(DG_E_INVAL, "dg_join2: null output column");
   TRY(set_device(e));
-  const u64 cap_k = std::min<u64>(a->n, 16 * n_keys + 4096);  // taken rows: a few per key
-  const u64 cap_e = cap_k + b->n;
-  const size_t idx_bytes = ((n_keys + 1) * 8 + 255) / 256 * 256;
-  const size_t tile_bytes = ((splice_tiles(a->n) + 1) * 8 + 255) / 256 * 256;
-  const size_t bytes = ((cap_k * 36 + 5 * 256) + (cap_e * 36 + 5 * 256) + 5 * idx_bytes +
-                        tile_bytes + 255) / 256 * 256;
-  TRY(ensure_buf(e, &e->spl, &e->spl_cap, bytes));
-  char* p = (char*)e->spl;
-  dg_store ak = carve_store(p, cap_k);
-  dg_store ed = carve_store(p, cap_e);
-  u64* a_lo = (u64*)p;
-  u64* a_off = (u64*)(p + idx_bytes);
-  u64* end = (u64*)(p + 2 * idx_bytes);
-  i64* shift = (i64*)(p + 3 * idx_bytes);
-  i64* gap = (i64*)(p + 4 * idx_bytes);
-  u64* tile_u0 = (u64*)(p + 5 * idx_bytes);
-  TRY(ensure_state(e, take_tiles(n_keys) + 2));
-  Scan sc;
-  TRY(next_scan(e, &sc));
-  HIP_TRY(hipMemsetAsync(e->d_counts + 3, 0, 2 * sizeof(u64), e->stream));
-  HIP_TRY(launch_take_keys(rows_of(a), keys, n_keys, rows_out_of(&ak), cap_k, sc, e->d_counts + 3,
-                           e->stream, a_lo, a_off));
-  HIP_TRY(launch_splice_check(b->key, b->n, keys, n_keys, e->d_counts + 4, e->stream));
-  TRY(read_counts(e, 5));
-  const u64 n_ak = e->h_counts[3];
-  if (e->h_counts[4] != 0 || n_ak > cap_k) return DG_OK;  // the full join applies
-  ak.n = n_ak;
-  void* chg = nullptr;
-  TRY(join2_enqueue(e, &ak, ca, b, cb, keys, n_keys, &ed, out_ctx, e->d_counts,
-                    with_changes ? &chg : nullptr));
-  if (with_changes)
-    HIP_TRY(launch_join2_changes(ak.n, b->n, chg, changed, cap, e->d_counts + 2, e->stream));
-  SpliceArgs sp{};
-  sp.a = rows_of(a);
-  sp.keys = keys;
-  sp.nk = n_keys;
-  sp.a_lo = a_lo;
-  sp.a_off = a_off;
-  sp.end = end;
-  sp.shift = shift;
-  sp.gap = gap;
-  sp.tile_u0 = tile_u0;
-  sp.e = rows_of(&ed);
-  sp.e.n = ak.n + b->n;  // a bound: the kernels read the count
-  sp.d_ne = e->d_counts;
-  sp.out = rows_out_of(out);
-  HIP_TRY(launch_splice(sp, e->stream));
+  Splice w;
+  bool ok = false;
+  TRY(splice_take(e, a, b, keys, n_keys, 0, &w, &ok));
+  if (!ok) return DG_OK;  // the full join applies
+  TRY(splice_edit(e, &w, ca, b, cb, keys, n_keys, out_ctx, with_changes, changed, cap));
+  w.sp.out = rows_out_of(out);
+  HIP_TRY(launch_splice_copy(w.sp, false, e->stream));
   if (read_counts(e, 3) != DG_OK) return DG_OK;  // a grid aborted: the full join re-runs
-  out->n = a->n - n_ak + e->h_counts[0];
+  out->n = a->n - w.n_ak + e->h_counts[0];
   out_ctx->n = e->h_counts[1];
   if (n_changed) *n_changed = e->h_counts[2];
   *done = true;
@@ -742,6 +792,111 @@ int dg_join2_changes(dg_engine* e, const dg_store* a, const dg_context* ca, cons
   if (*n_changed > cap)
     return fail(DG_E_CAPACITY, "dg_join2_changes: %llu changed keys > cap %llu",
                 (unsigned long long)*n_changed, (unsigned long long)cap);
+  return DG_OK;
+}
+
+int dg_join_delta(dg_engine* e, dg_store* state, dg_context* state_ctx, const dg_store* delta,
+                  const dg_context* delta_ctx, const uint64_t* keys, uint64_t n_keys,
+                  dg_store* spare, dg_merkle* tree, uint64_t* changed, uint64_t cap,
+                  uint64_t* n_changed, int* swapped) {
+  if (!e) return fail(DG_E_INVAL, "null engine");
+  if (!swapped || !n_changed || (cap && !changed) || !spare || !state || !state_ctx)
+    return fail(DG_E_INVAL, "dg_join_delta: null argument");
+  *swapped = 0;
+  *n_changed = 0;
+  TRY(check_store(state, "dg_join_delta state"));
+  TRY(check_store(delta, "dg_join_delta delta"));
+  TRY(check_ctx(state_ctx, "dg_join_delta state_ctx"));
+  TRY(check_ctx(delta_ctx, "dg_join_delta delta_ctx"));
+  if (tree) TRY(check_merkle(tree, "dg_join_delta tree"));
+  if (keys == nullptr && n_keys != 0) return fail(DG_E_INVAL, "dg_join_delta: keys NULL with n_keys>0");
+  if (spare->cap < state->n + delta->n)
+    return fail(DG_E_CAPACITY, "dg_join_delta: spare cap %llu < %llu rows in",
+                (unsigned long long)spare->cap, (unsigned long long)(state->n + delta->n));
+  if (state_ctx->cap < state_ctx->n + delta_ctx->n)
+    return fail(DG_E_CAPACITY, "dg_join_delta: state_ctx cap %llu < %llu",
+                (unsigned long long)state_ctx->cap, (unsigned long long)(state_ctx->n + delta_ctx->n));
+  TRY(set_device(e));
+  TRY(settle(e));
+  const u64 uctx_cap = state_ctx->n + delta_ctx->n;
+  Splice w;
+  bool ok = false;
+  const dg_store old_state = *state;
+  if (splice_wanted(e, state, delta, keys, n_keys, spare) && state->cap >= state->n)
+    TRY(splice_take(e, state, delta, keys, n_keys, uctx_cap, &w, &ok));
+  if (!ok) {
+    // the full keyed join into the spare store (the merge, or a splice into `spare` that
+    // dg_join2_changes picks itself), the context through scratch, then the tree
+    TRY(ensure_buf(e, &e->spl, &e->spl_cap, (uctx_cap * 12 + 1024 + 255) / 256 * 256));
+    dg_context uc{};
+    uc.cnt = (uint64_t*)e->spl;
+    uc.node = (uint32_t*)((char*)e->spl + (uctx_cap * 8 + 255) / 256 * 256);
+    uc.cap = uctx_cap;
+    TRY(dg_join2_changes(e, state, state_ctx, delta, delta_ctx, keys, n_keys, spare, &uc,
+                         changed, cap, n_changed));
+    HIP_TRY(hipMemcpyAsync(state_ctx->node, uc.node, uc.n * 4, hipMemcpyDeviceToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(state_ctx->cnt, uc.cnt, uc.n * 8, hipMemcpyDeviceToDevice, e->stream));
+    state_ctx->n = uc.n;
+    state_ctx->kind = uc.kind;
+    if (tree) TRY(dg_merkle_update(e, tree, &old_state, spare, changed, *n_changed));
+    std::swap(*state, *spare);
+    *swapped = 1;
+    return DG_OK;
+  }
+  TRY(splice_edit(e, &w, state_ctx, delta, delta_ctx, keys, n_keys, &w.uctx, true, changed, cap));
+  TRY(read_counts(e, 6));
+  const bool moved = (u32)e->h_counts[5] != 0;
+  const u64 n_e = e->h_counts[0];
+  w.uctx.n = e->h_counts[1];
+  *n_changed = e->h_counts[2];
+  if (*n_changed > cap)
+    return fail(DG_E_CAPACITY, "dg_join_delta: %llu changed keys > cap %llu",
+                (unsigned long long)*n_changed, (unsigned long long)cap);
+  dg_store* out = state;
+  if (moved) {  // some key's row count changed: the rows outside K move, into `spare`
+    w.sp.out = rows_out_of(spare);
+    HIP_TRY(launch_splice_copy(w.sp, false, e->stream));
+    out = spare;
+  } else {      // every joined key keeps its row count: E's rows in place, nothing else moves
+    w.sp.out = rows_out_of(state);
+    HIP_TRY(launch_splice_copy(w.sp, true, e->stream));
+  }
+  out->n = state->n - w.n_ak + n_e;
+  u32* ctr = nullptr;
+  u32* dirty = nullptr;
+  u64 chunks = 0;
+  if (tree) {
+    const u64 cw = merkle_ctr_words(tree->depth);
+    chunks = merkle_chunks(tree->depth);
+    TRY(ensure_tmp(e, (cw + chunks) * sizeof(u32)));
+    ctr = (u32*)e->tmp;
+    dirty = ctr + cw;
+  }
+  // the union context into the state's, and the tree update's zeroed words: one launch
+  HIP_TRY(launch_splice_finish(w.uctx.node, w.uctx.cnt, w.uctx.n, state_ctx->node, state_ctx->cnt,
+                               dirty, chunks, tree ? e->d_counts : nullptr,
+                               tree ? e->ticket + 3 : nullptr, e->stream));
+  state_ctx->n = w.uctx.n;
+  state_ctx->kind = (state_ctx->kind == DG_CTX_DOTS && delta_ctx->kind == DG_CTX_DOTS) ? DG_CTX_DOTS
+                                                                                          : DG_CTX_VV;
+  if (tree) {
+    // MerkleMap.put/delete of the changed keys: every changed key is a keyset key, so its
+    // old rows are among the taken rows and its new rows among the edit's (both small and
+    // cache-resident: no search of the 12.5M-row state)
+    dg_store ed = w.ed;
+    ed.n = n_e;
+    HIP_TRY(launch_merkle_update(merkle_of(tree), rows_of(&w.ak), rows_of(&ed), changed, *n_changed,
+                                 dirty, e->d_counts, ctr, e->ticket + 3, e->stream));
+    TRY(read_counts(e, 8));
+    TRY(input_error(e, "dg_join_delta"));
+    for (int i = 0; i < 8; i++) tree->n_keys += e->h_counts[i];
+  } else {
+    TRY(read_counts(e, 0));
+  }
+  if (moved) {
+    std::swap(*state, *spare);
+    *swapped = 1;
+  }
   return DG_OK;
 }
 

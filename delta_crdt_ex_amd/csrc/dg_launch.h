@@ -133,9 +133,12 @@ inline u64 take_tiles(u64 n_keys) { return (n_keys + 1023) / 1024; }
 // Uses look-back granules [0, take_tiles(n_keys)).  key_lo / key_off (optional, n_keys and
 // n_keys + 1 entries): per key its first row in s (the first row >= the key) and the
 // output offset of its rows (key_off[n_keys] = *d_count).
+// pre_len (optional, with key_lo): the keys' rows located already (launch_splice_locate:
+// key_lo[u] and pre_len[u] are inputs), so the kernel only scans and copies.
 hipError_t launch_take_keys(const Rows& s, const u64* keys, u64 n_keys, const RowsOut& out,
                             u64 cap, const Scan& scan, u64* d_count, hipStream_t st,
-                            u64* key_lo = nullptr, u64* key_off = nullptr);
+                            u64* key_lo = nullptr, u64* key_off = nullptr,
+                            const u32* pre_len = nullptr);
 
 // ---- splice.hip (a sparse keyed join applied to a large state without merging it)
 // The keyed join of a small delta into a large state, as a splice: the state's rows of the
@@ -152,15 +155,30 @@ struct SpliceArgs {
   i64* shift;          // nk + 1: out - in of the A rows after K[u-1], before K[u] (index)
   i64* gap;            // nk: A rows outside K before K[u]                    (index)
   u64* tile_u0;        // a_tiles + 1: first u with end[u] > the tile's first row (index)
+  u32* moved;          // (index) set when some shift is nonzero: rows outside K move
   Rows e;              // the edit (e.n: an upper bound; the count is *d_ne)
   const u64* d_ne;
   RowsOut out;
   u64 a_tiles, e_tiles;
 };
+// For every key of keys (ascending, n_keys): lo[u] = the first row of s whose key is >=
+// keys[u] and len[u] = its rows, found by streaming s's key column in tiles (each tile's
+// keys searched in the tile staged in LDS) instead of one search per key: cheaper than
+// the searches once more than about 1 key in 150 rows is looked up.
+hipError_t launch_splice_locate(const Rows& s, const u64* keys, u64 n_keys, u64* lo, u32* len,
+                                hipStream_t st);
 // every row of b whose key starts a run and is not in keys: *d_bad += 1
 hipError_t launch_splice_check(const u64* bkey, u64 nb, const u64* keys, u64 nk, u64* d_bad,
                                hipStream_t st);
-hipError_t launch_splice(SpliceArgs p, hipStream_t st);
+// the per-key index (end, shift, gap, tile_u0; *moved |= some shift != 0), then the copy:
+// every state row outside K to its place and E's rows into the holes; e_only: E's rows
+// alone (in place: out is the state itself and no shift is nonzero)
+hipError_t launch_splice_index(SpliceArgs p, hipStream_t st);
+hipError_t launch_splice_copy(SpliceArgs p, bool e_only, hipStream_t st);
+// on[0, nc) = un, oc[0, nc) = uc; dirty[0, n_dirty) = 0; counts[0, 8) = 0 (if non-null);
+// *err_word = 0 (if non-null): one launch instead of two copies and three fills
+hipError_t launch_splice_finish(const u32* un, const u64* uc, u64 nc, u32* on, u64* oc, u32* dirty,
+                                u64 n_dirty, u64* counts, u32* err_word, hipStream_t st);
 u64 splice_tiles(u64 n);  // state tiles of the copy (tile_u0 holds one more entry)
 
 // ---- mutate.hip (a batch of add/remove ops as one delta; see the file header)

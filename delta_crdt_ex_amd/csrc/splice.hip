@@ -11,8 +11,10 @@
 //   2. joins them with the delta on the join kernels (small: the edit E, = the output's
 //      rows of every key of K, sorted),
 //   3. (this file) computes per key where the untouched rows between two keyset keys move
-//      (splice_index_kernel) and writes the output in one streaming pass: the untouched
-//      rows at their new positions and E's rows in the holes (splice_kernel).
+//      (splice_index_kernel), moves E's rows into their holes (splice_erows_kernel, one
+//      thread per key) and the untouched rows to their new positions in one streaming
+//      pass (splice_kernel) -- or not at all when no key's row count changed and the
+//      output is the state itself (dg_join_delta in place).
 // The output is bit-identical to the full keyed join's whenever the delta's keys are a
 // subset of the keyset; the caller checks that first (splice_check_kernel) and otherwise
 // takes the full join.
@@ -64,6 +66,56 @@ __device__ __forceinline__ u64 lower_bound(const u64* a, u64 lo, u64 hi, u64 x) 
   return lo;
 }
 
+// ---- locate (the take's first half by streaming): one workgroup per LT state rows
+// stages the tile's keys in LDS (coalesced, 16 KB) and finds, for every keyset key whose
+// first row >= it lies in the tile -- keys in (key[i0 - 1], key[i1 - 1]], the last tile
+// also the keys above every row -- that row and the key's rows (a run may continue past
+// the tile, read from global memory).
+constexpr int LT = 2048;
+__global__ __launch_bounds__(SB) void splice_locate_kernel(Rows s, const u64* keys, u64 nk, u64* lo,
+                                                           u32* len) {
+  __shared__ u64 s_k[LT];
+  __shared__ u64 s_b[2];
+  const u64 t = blockIdx.x;
+  const u64 i0 = t * LT, i1 = min<u64>(i0 + LT, s.n);
+  if (threadIdx.x < WAVE) {
+    const u64 u = t == 0 ? 0 : wave_upper(keys, nk, s.key[i0 - 1]);
+    if (threadIdx.x == 0) s_b[0] = u;
+  } else if (threadIdx.x < 2 * WAVE) {
+    const u64 u = i1 == s.n ? nk : wave_upper(keys, nk, s.key[i1 - 1]);
+    if ((threadIdx.x & (WAVE - 1)) == 0) s_b[1] = u;
+  }
+  const u32 m = (u32)(i1 - i0);
+  for (u32 j = 2 * threadIdx.x; j < m; j += 2 * SB) {  // 16-byte loads (i0 is even)
+    if (j + 1 < m) {
+      const ulonglong2 v = *(const ulonglong2*)(s.key + i0 + j);
+      s_k[j] = v.x;
+      s_k[j + 1] = v.y;
+    } else {
+      s_k[j] = s.key[i0 + j];
+    }
+  }
+  __syncthreads();
+  for (u64 u = s_b[0] + threadIdx.x; u < s_b[1]; u += SB) {
+    const u64 x = keys[u];
+    u32 a = 0, b = m;
+    while (a < b) {
+      const u32 h = (a + b) >> 1;
+      if (s_k[h] < x)
+        a = h + 1;
+      else
+        b = h;
+    }
+    u32 e = a;
+    while (e < m && s_k[e] == x) e++;
+    u64 g = i0 + e;
+    if (e == m)  // the run may go on into the next tiles
+      while (g < s.n && s.key[g] == x) g++;
+    lo[u] = i0 + a;
+    len[u] = (u32)(g - (i0 + a));
+  }
+}
+
 __global__ __launch_bounds__(SB) void splice_check_kernel(const u64* bkey, u64 nb, const u64* keys,
                                                           u64 nk, u64* d_bad) {
   const u64 j = (u64)blockIdx.x * SB + threadIdx.x;
@@ -84,6 +136,7 @@ __global__ __launch_bounds__(SB) void splice_index_kernel(SpliceArgs p) {
   const u64 pa = p.a_off[u];
   const u64 pe = u < p.nk ? interp_lower_bound(p.e.key, 0, ne, p.keys[u]) : ne;
   p.shift[u] = (i64)pe - (i64)pa;
+  if (pe != pa) atomicOr(p.moved, 1u);
   const u64 end_hi = u < p.nk ? p.a_lo[u] + (p.a_off[u + 1] - pa) : ~0ull;
   const u64 end_lo = u > 0 ? p.a_lo[u - 1] + (pa - p.a_off[u - 1]) : 0ull;
   if (u < p.nk) {
@@ -161,46 +214,32 @@ __device__ __forceinline__ void store_tile(const RowsOut& o, const TileRows& x, 
   }
 }
 
-// Workgroups [0, e_tiles): E's rows (issued first, so their key searches overlap the
-// state's copy); then one workgroup per ST state rows.  Every workgroup issues its rows'
-// loads first: the searches that place them run while the loads are in flight.
+// E's rows: one thread per keyset entry u moves its key's rows [PE[u], PE[u + 1]) of E
+// (PE = shift + a_off) to j + gap[u] -- no search: the index kernel has placed them.
+__global__ __launch_bounds__(SB) void splice_erows_kernel(SpliceArgs p) {
+  const u64 u = (u64)blockIdx.x * SB + threadIdx.x;
+  if (u >= p.nk) return;
+  const u64 j0 = (u64)(p.shift[u] + (i64)p.a_off[u]), j1 = (u64)(p.shift[u + 1] + (i64)p.a_off[u + 1]);
+  const i64 g = p.gap[u];
+  for (u64 j = j0; j < j1; j++) {
+    const u64 o = (u64)((i64)j + g);
+    p.out.key[o] = p.e.key[j];
+    p.out.val[o] = p.e.val[j];
+    p.out.ts[o] = p.e.ts[j];
+    p.out.node[o] = p.e.node[j];
+    p.out.cnt[o] = p.e.cnt[j];
+  }
+}
+
+// One workgroup per ST state rows: every row outside the keyset to its place.  The
+// workgroup issues its rows' loads first: the index entries that place them are staged
+// while the loads are in flight.
 __global__ __launch_bounds__(SB) void splice_kernel(SpliceArgs p) {
   __shared__ u64 s_end[SLC], s_lo[SLC];
   __shared__ i64 s_shift[SLC];
-  __shared__ u64 s_b[2];
   TileRows x;
   i64 to[SR];
-  if (blockIdx.x < p.e_tiles) {
-    const u64 ne = *p.d_ne;
-    const u64 j0 = (u64)blockIdx.x * ST;
-    if (j0 >= ne) return;  // block-uniform
-    const u64 j1 = min<u64>(j0 + ST, ne);
-    load_tile(p.e, j0, j1, x);
-    // the keyset entries of the tile's keys lie in [u0, u1]: E's keys are keyset keys
-    // (clamped into [0, nk): the caller checked that they are, an index stays in bounds
-    // whatever the input)
-    if (threadIdx.x < WAVE) {
-      const u64 u = wave_upper(p.keys, p.nk, p.e.key[j0]);
-      if (threadIdx.x == 0) s_b[0] = u ? u - 1 : 0;
-    } else if (threadIdx.x < 2 * WAVE) {
-      const u64 u = wave_upper(p.keys, p.nk, p.e.key[j1 - 1]);
-      if ((threadIdx.x & (WAVE - 1)) == 0) s_b[1] = u ? u - 1 : 0;
-    }
-    __syncthreads();
-    const u64 u0 = s_b[0], u1 = max(s_b[0], s_b[1]);
-#pragma unroll
-    for (int q = 0; q < SR; q++) {
-      const u64 j = pair_row(j0, q >> 1, q & 1);
-      to[q] = -1;
-      if (j < j1) {
-        const u64 u = min(lower_bound(p.keys, u0, u1 + 1, x.key[q]), u1);
-        to[q] = (i64)j + p.gap[u];
-      }
-    }
-    store_tile(p.out, x, to);
-    return;
-  }
-  const u64 t = blockIdx.x - p.e_tiles;
+  const u64 t = blockIdx.x;
   const u64 i0 = t * ST;
   const u64 i1 = min<u64>(i0 + ST, p.a.n);
   // row i's first keyset entry whose state rows end after it: u*(i) = first u with
@@ -251,6 +290,15 @@ __global__ __launch_bounds__(SB) void splice_kernel(SpliceArgs p) {
 
 }  // namespace
 
+hipError_t launch_splice_locate(const Rows& s, const u64* keys, u64 n_keys, u64* lo, u32* len,
+                                hipStream_t st) {
+  const u64 tiles = (s.n + LT - 1) / LT;
+  if (tiles == 0 || n_keys == 0) return hipSuccess;
+  hipLaunchKernelGGL(splice_locate_kernel, dim3((unsigned)tiles), dim3(SB), 0, st, s, keys, n_keys,
+                     lo, len);
+  return hipGetLastError();
+}
+
 hipError_t launch_splice_check(const u64* bkey, u64 nb, const u64* keys, u64 nk, u64* d_bad,
                                hipStream_t st) {
   if (nb == 0) return hipSuccess;
@@ -261,13 +309,42 @@ hipError_t launch_splice_check(const u64* bkey, u64 nb, const u64* keys, u64 nk,
 
 u64 splice_tiles(u64 n) { return (n + ST - 1) / ST; }
 
-hipError_t launch_splice(SpliceArgs p, hipStream_t st) {
+hipError_t launch_splice_index(SpliceArgs p, hipStream_t st) {
   p.a_tiles = (p.a.n + ST - 1) / ST;
-  p.e_tiles = (p.e.n + ST - 1) / ST;
   hipLaunchKernelGGL(splice_index_kernel, dim3((unsigned)((p.nk + 1 + SB - 1) / SB)), dim3(SB), 0,
                      st, p);
-  if (p.a_tiles + p.e_tiles == 0) return hipGetLastError();
-  hipLaunchKernelGGL(splice_kernel, dim3((unsigned)(p.a_tiles + p.e_tiles)), dim3(SB), 0, st, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_splice_copy(SpliceArgs p, bool e_only, hipStream_t st) {
+  p.a_tiles = (p.a.n + ST - 1) / ST;
+  hipLaunchKernelGGL(splice_erows_kernel, dim3((unsigned)((p.nk + SB - 1) / SB)), dim3(SB), 0, st, p);
+  if (!e_only && p.a_tiles)
+    hipLaunchKernelGGL(splice_kernel, dim3((unsigned)p.a_tiles), dim3(SB), 0, st, p);
+  return hipGetLastError();
+}
+
+// dg_join_delta's epilogue set-up in one launch: the union context copied into the
+// state's, the tree update's dirty flags, key-count shards and input-error word zeroed
+__global__ __launch_bounds__(SB) void splice_finish_kernel(const u32* un, const u64* uc, u64 nc,
+                                                           u32* on, u64* oc, u32* dirty, u64 n_dirty,
+                                                           u64* counts, u32* err_word) {
+  const u64 i = (u64)blockIdx.x * SB + threadIdx.x;
+  if (i < nc) {
+    on[i] = un[i];
+    oc[i] = uc[i];
+  }
+  if (i < n_dirty) dirty[i] = 0;
+  if (i < 8 && counts) counts[i] = 0;
+  if (i == 0 && err_word) *err_word = 0;
+}
+
+hipError_t launch_splice_finish(const u32* un, const u64* uc, u64 nc, u32* on, u64* oc, u32* dirty,
+                                u64 n_dirty, u64* counts, u32* err_word, hipStream_t st) {
+  u64 n = nc > n_dirty ? nc : n_dirty;
+  n = n > 8 ? n : 8;
+  hipLaunchKernelGGL(splice_finish_kernel, dim3((unsigned)((n + SB - 1) / SB)), dim3(SB), 0, st, un,
+                     uc, nc, on, oc, dirty, n_dirty, counts, err_word);
   return hipGetLastError();
 }
 

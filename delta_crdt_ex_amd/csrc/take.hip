@@ -20,7 +20,8 @@ constexpr int TB = 1024, TI = 1, TK = TB * TI;  // one key per thread: the searc
 
 __global__ __launch_bounds__(TB) void take_keys_kernel(Rows s, const u64* keys, u64 n_keys,
                                                       u64 ntiles, RowsOut out, u64 cap, Scan scan,
-                                                      u64* d_count, u64* key_lo, u64* key_off) {
+                                                      u64* d_count, u64* key_lo, u64* key_off,
+                                                      const u32* pre_len) {
   __shared__ u64 s_lo[TK];
   __shared__ u32 s_off[TK + 1];
   __shared__ u32 s_wave[TB / WAVE + 1];
@@ -41,7 +42,10 @@ __global__ __launch_bounds__(TB) void take_keys_kernel(Rows s, const u64* keys, 
     const u32 i = threadIdx.x * TI + q;
     lo[q] = 0;
     len[q] = 0;
-    if (i < nk) {
+    if (i < nk && pre_len) {  // located already (splice_locate_kernel): key_lo, pre_len
+      lo[q] = key_lo[k0 + i];
+      len[q] = pre_len[k0 + i];
+    } else if (i < nk) {
       const u64 key = keys[k0 + i];
       const u64 a = interp_lower_bound(s.key, 0, s.n, key);  // first row with key >= `key`
       u64 e = a;  // a key's rows are few: walk them
@@ -84,7 +88,7 @@ __global__ __launch_bounds__(TB) void take_keys_kernel(Rows s, const u64* keys, 
   const u64 base = s_b[1];
   if (key_lo) {  // the splice's per-key index (splice.hip): first row and output offset
     for (u32 i = threadIdx.x; i < nk; i += TB) {
-      key_lo[k0 + i] = s_lo[i];
+      if (!pre_len) key_lo[k0 + i] = s_lo[i];
       key_off[k0 + i] = base + s_off[i];
     }
   }
@@ -112,11 +116,11 @@ __global__ __launch_bounds__(TB) void take_keys_kernel(Rows s, const u64* keys, 
 
 hipError_t launch_take_keys(const Rows& s, const u64* keys, u64 n_keys, const RowsOut& out,
                             u64 cap, const Scan& scan, u64* d_count, hipStream_t st, u64* key_lo,
-                            u64* key_off) {
+                            u64* key_off, const u32* pre_len) {
   const u64 ntiles = take_tiles(n_keys);
   if (ntiles == 0) return hipMemsetAsync(d_count, 0, sizeof(u64), st);
   hipLaunchKernelGGL(take_keys_kernel, dim3((unsigned)ntiles), dim3(TB), 0, st, s, keys, n_keys,
-                     ntiles, out, cap, scan, d_count, key_lo, key_off);
+                     ntiles, out, cap, scan, d_count, key_lo, key_off, pre_len);
   return hipGetLastError();
 }
 

@@ -574,6 +574,41 @@ class Engine:
         tree.store = s
         return launch
 
+    def join_delta(self, state: Store, state_ctx: Context, delta: Store, delta_ctx: Context,
+                   keys: torch.Tensor, spare: Store, tree: MerkleTree | None = None,
+                   changed: torch.Tensor | None = None):
+        """CausalCrdt.update_state_with_delta on a device-resident state
+        (causal_crdt.ex:383-404, dg_join_delta): `state` and `state_ctx` become the keyed
+        join with the sync delta, `tree` (indexing `state`) is updated for the changed keys.
+        In place when every joined key keeps its row count; otherwise the result lands in
+        `spare` and the two Store objects exchange their columns (so `state` always holds
+        the joined rows).  Returns (changed keys, swapped)."""
+        self._order()
+        if changed is None:
+            changed = torch.empty(max(int(keys.numel()), 1), dtype=_I64, device=self.device)
+        ss, sc, sd, cd, sp = state.abi(), state_ctx.abi(), delta.abi(), delta_ctx.abi(), spare.abi()
+        t = tree.abi() if tree is not None else None
+        kp, nk = self._keys(keys)
+        n = C.c_uint64(0)
+        sw = C.c_int(0)
+        check(self.lib.dg_join_delta(self.h, C.byref(ss), C.byref(sc), C.byref(sd), C.byref(cd),
+                                     kp, nk, C.byref(sp), C.byref(t) if t is not None else None,
+                                     _ptr(changed, _abi.P64), int(changed.numel()), C.byref(n),
+                                     C.byref(sw)))
+        if sw.value:
+            for f in ("key", "val", "ts", "node", "cnt"):
+                a, b = getattr(state, f), getattr(spare, f)
+                setattr(state, f, b)
+                setattr(spare, f, a)
+            spare.n = 0
+        state.n = int(ss.n)
+        state_ctx.n = int(sc.n)
+        state_ctx.kind = int(sc.kind)
+        if tree is not None:
+            tree.n_keys = int(t.n_keys) & ((1 << 64) - 1)
+            tree.store = state
+        return changed[: n.value], bool(sw.value)
+
     def merkle_update(self, tree: MerkleTree, new: Store, keys: torch.Tensor) -> MerkleTree:
         """MerkleMap.put/delete of the changed `keys` + update_hashes: `tree` indexed
         tree.store; afterwards it indexes `new` (causal_crdt.ex:383-394)."""

@@ -218,6 +218,23 @@ int dg_join2_changes(dg_engine* e, const dg_store* a, const dg_context* ca, cons
                      const dg_context* cb, const uint64_t* keys, uint64_t n_keys, dg_store* out,
                      dg_context* out_ctx, uint64_t* changed, uint64_t cap, uint64_t* n_changed);
 
+/* CausalCrdt.update_state_with_delta (causal_crdt.ex:383-404) on a device-resident
+ * state: state = AWLWWMap.join(state, delta, keys) (aw_lww_map.ex:153-209), the keys whose
+ * value changed (diff/3, :343-351) into changed[0, cap) ascending, and the state's
+ * MerkleMap `tree` (NULL: none) updated for them (MerkleMap.put/delete + update_hashes,
+ * :390-394).  state_ctx becomes the union (cap >= state_ctx->n + delta_ctx->n).
+ * The join is applied IN PLACE when every key of the keyset keeps its number of rows (the
+ * rows outside the keyset do not move: only the keyset's rows are rewritten); otherwise
+ * the joined state is written to `spare` (cap >= state->n + delta->n) and the two
+ * dg_store structs are exchanged, *swapped = 1 -- on return *state always describes the
+ * joined state and *spare a free buffer.  A delta with a key outside `keys` (not a sync
+ * delta) takes the full join, also through `spare`; as in the reference, the tree then
+ * follows the changed keys of the keyset only (diff/3 runs over `keys`).  Synchronous. */
+int dg_join_delta(dg_engine* e, dg_store* state, dg_context* state_ctx, const dg_store* delta,
+                  const dg_context* delta_ctx, const uint64_t* keys, uint64_t n_keys,
+                  dg_store* spare, dg_merkle* tree, uint64_t* changed, uint64_t cap,
+                  uint64_t* n_changed, int* swapped);
+
 /* Fold of join/3 over k stores (how CausalCrdt applies k deltas in a row,
  * causal_crdt.ex:86-89,383-384): out = join(...join(join(s0, s1), s2)..., s_{k-1})
  * over all keys.  A row survives iff for every input i it is present in s_i or its
