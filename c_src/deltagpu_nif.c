@@ -24,7 +24,8 @@
  *   join_delta(state, dots, value, keys)      -> {:ok, new_dots, changed}
  *        join/3 (aw_lww_map.ex:153-158) of the resident state with a delta
  *        %{dots: dots, value: value} over `keys`, in place on the device
- *        (dg_join2_changes); changed = [{key, value_map | nil}] for the keys whose raw
+ *        (dg_join_delta: in place when every joined key keeps its row count);
+ *        changed = [{key, value_map | nil}] for the keys whose raw
  *        value maps changed (causal_crdt.ex:344-352), so the caller updates its term
  *        map with Map.merge/Map.drop of those keys only; the Merkle tree, if built,
  *        gets put/delete + update_hashes of them (dg_merkle_update, :390-394).
@@ -264,6 +265,7 @@ typedef struct {
 struct state_res {
   engine_res* eng;
   dg_store rows;
+  dg_store spare; /* dg_join_delta's second buffer (allocated on first need, kept) */
   dg_context ctx;
   dg_merkle tree;
   int has_tree;
@@ -296,6 +298,7 @@ static void state_dtor(ErlNifEnv* env, void* obj) {
   if (s->prev) s->prev->next = s->next; else g->live = s->next;
   if (s->next) s->next->prev = s->prev;
   dg_store_free(g->e, &s->rows);
+  dg_store_free(g->e, &s->spare);
   dg_context_free(g->e, &s->ctx);
   if (s->has_tree) {
     dg_buffer_free(g->e, s->tree.nodes);
@@ -704,34 +707,46 @@ static ERL_NIF_TERM join_delta(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
   enif_mutex_lock(g->lock);
   int rc = DG_OK;
   dgm_rows h;
-  dg_store drows, out, taken;
-  dg_context dctx, octx;
+  dg_store drows, taken;
+  dg_context dctx, nctx;
   uint64_t *d_keys = NULL, n_keys = 0, *changed = NULL, n_changed = 0;
+  int swapped = 0;
   memset(&drows, 0, sizeof drows);
-  memset(&out, 0, sizeof out);
   memset(&taken, 0, sizeof taken);
   memset(&dctx, 0, sizeof dctx);
-  memset(&octx, 0, sizeof octx);
+  memset(&nctx, 0, sizeof nctx);
   ERL_NIF_TERM r, new_dots, changed_terms = enif_make_list(env, 0), values;
   TRY(dgm_rows_init(&h, 256, 16));
   TRY(marshal_dots(env, g, argv[1], &h));
   TRY(marshal_value(env, g, argv[2], &h));
   TRY(upload_sorted(g, &h, &drows, &dctx));
   TRY(marshal_keys(env, g, argv[3], &d_keys, &n_keys));
-  TRY(dg_store_alloc(g->e, s->rows.n + drows.n, &out));
-  TRY(dg_context_alloc(g->e, s->ctx.n + dctx.n, &octx));
-  TRY(dg_buffer_alloc(g->e, (n_keys ? n_keys : 1) * 8, (void**)&changed));
-  TRY(dg_join2_changes(g->e, &s->rows, &s->ctx, &drows, &dctx, d_keys, n_keys, &out, &octx, changed,
-                       n_keys, &n_changed));
-  if (s->has_tree) {
-    TRY(refresh_terms(g));
-    TRY(dg_merkle_update(g->e, &s->tree, &s->rows, &out, changed, n_changed));
+  /* the spare buffer and the context's room for the union, grown on demand */
+  if (s->spare.cap < s->rows.n + drows.n) {
+    dg_store_free(g->e, &s->spare);
+    TRY(dg_store_alloc(g->e, 2 * (s->rows.n + drows.n), &s->spare));
   }
+  if (s->ctx.cap < s->ctx.n + dctx.n) {
+    TRY(dg_context_alloc(g->e, 2 * (s->ctx.n + dctx.n), &nctx));
+    TRY(dg_copy_to_device(g->e, nctx.node, s->ctx.node, s->ctx.n * 4));  /* device to device */
+    TRY(dg_copy_to_device(g->e, nctx.cnt, s->ctx.cnt, s->ctx.n * 8));
+    nctx.n = s->ctx.n;
+    nctx.kind = s->ctx.kind;
+    dg_context_free(g->e, &s->ctx);
+    s->ctx = nctx;
+    memset(&nctx, 0, sizeof nctx);
+  }
+  TRY(dg_buffer_alloc(g->e, (n_keys ? n_keys : 1) * 8, (void**)&changed));
+  if (s->has_tree) TRY(refresh_terms(g));
+  /* update_state_with_delta: the join (in place, or through the spare buffer: the structs
+   * come back exchanged), the changed keys, the MerkleMap put/delete of them */
+  TRY(dg_join_delta(g->e, &s->rows, &s->ctx, &drows, &dctx, d_keys, n_keys, &s->spare,
+                    s->has_tree ? &s->tree : NULL, changed, n_keys, &n_changed, &swapped));
   /* the changed keys' new value maps (dg_take_keys), and the keys that vanished */
-  TRY(dg_store_alloc(g->e, out.n, &taken));
-  TRY(dg_take_keys(g->e, &out, changed, n_changed, &taken));
+  TRY(dg_store_alloc(g->e, s->rows.n ? s->rows.n : 1, &taken));
+  TRY(dg_take_keys(g->e, &s->rows, changed, n_changed, &taken));
   TRY(unmarshal_rows(env, g, &taken, &values));
-  TRY(unmarshal_dots(env, g, &octx, &new_dots));
+  TRY(unmarshal_dots(env, g, &s->ctx, &new_dots));
   {
     uint64_t* hk = (uint64_t*)enif_alloc((n_changed ? n_changed : 1) * 8);
     rc = dg_copy_to_host(g->e, hk, changed, n_changed * 8);
@@ -744,21 +759,13 @@ static ERL_NIF_TERM join_delta(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
     enif_free(hk);
     if (rc) goto out;
   }
-  /* the resource now holds the joined state */
-  dg_store_free(g->e, &s->rows);
-  dg_context_free(g->e, &s->ctx);
-  s->rows = out;
-  s->ctx = octx;
-  memset(&out, 0, sizeof out);
-  memset(&octx, 0, sizeof octx);
 out:
   r = rc ? error_term(env, rc) : enif_make_tuple3(env, A_OK, new_dots, changed_terms);
   dgm_rows_free(&h);
   dg_store_free(g->e, &drows);
-  dg_store_free(g->e, &out);
   dg_store_free(g->e, &taken);
   dg_context_free(g->e, &dctx);
-  dg_context_free(g->e, &octx);
+  dg_context_free(g->e, &nctx);
   dg_buffer_free(g->e, d_keys);
   dg_buffer_free(g->e, changed);
   enif_mutex_unlock(g->lock);

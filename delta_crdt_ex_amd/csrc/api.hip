@@ -1644,7 +1644,8 @@ int dg_copy_to_device(dg_engine* e, void* dst, const void* src, uint64_t bytes) 
   if (!e || (bytes && (!dst || !src))) return fail(DG_E_INVAL, "dg_copy_to_device: null argument");
   if (!bytes) return DG_OK;
   TRY(set_device(e));
-  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, e->stream));
+  // (hipMemcpyDefault: the source may be device memory too -- a device-to-device copy)
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   return DG_OK;
 }

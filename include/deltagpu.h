@@ -175,7 +175,8 @@ int dg_context_alloc(dg_engine* e, uint64_t cap, dg_context* c);
 int dg_context_free(dg_engine* e, dg_context* c);
 int dg_context_upload(dg_engine* e, const dg_context* host, dg_context* dev);
 int dg_context_download(dg_engine* e, const dg_context* dev, dg_context* host);
-/* Raw device memory (key lists, Merkle nodes, continuations) and copies. */
+/* Raw device memory (key lists, Merkle nodes, continuations) and copies
+ * (dg_copy_to_device also copies device to device: its source may be device memory). */
 int dg_buffer_alloc(dg_engine* e, uint64_t bytes, void** p);
 int dg_buffer_free(dg_engine* e, void* p);
 int dg_copy_to_device(dg_engine* e, void* dst, const void* src, uint64_t bytes);
