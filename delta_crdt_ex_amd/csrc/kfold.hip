@@ -360,8 +360,9 @@ __device__ __forceinline__ u32 sub_of(u64 key, u64 T, u64 t) {
 }
 
 // exclusive prefix of n <= PER*KB values into pre[0..n] (pre[n] = total)
-template <class V>
-__device__ __forceinline__ void scan_excl(const V* in, u32 n, unsigned short* pre, u32* wave) {
+// CURSOR: in[i] is also overwritten with pre[i] (each thread rewrites what it read)
+template <bool CURSOR = false, class V>
+__device__ __forceinline__ void scan_excl(V* in, u32 n, unsigned short* pre, u32* wave) {
   const u32 b = threadIdx.x * PER;
   u32 c[PER], sum = 0;
 #pragma unroll
@@ -373,7 +374,10 @@ __device__ __forceinline__ void scan_excl(const V* in, u32 n, unsigned short* pr
   u32 off = block_excl_scan<KB>(sum, wave, &tot);
 #pragma unroll
   for (int q = 0; q < PER; q++) {
-    if (b + q < n) pre[b + q] = (unsigned short)off;
+    if (b + q < n) {
+      pre[b + q] = (unsigned short)off;
+      if (CURSOR) in[b + q] = (V)off;
+    }
     off += c[q];
   }
   if (threadIdx.x == 0) pre[n] = (unsigned short)tot;
@@ -519,6 +523,7 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
     const u32 src = tag2 >> 16;
     keep2 = !in_slice(s.dkey, s.roff[src], s.roff[src + 1], key2);
   }
+  for (u32 b = tid; b < NSUB; b += KB) s.x.ucnt[b] = 0;  // (the scan's barriers order it)
   u32 n_keep;
   // (the scan's barriers come after every search: the entries may move after it)
   const u32 kpos = block_excl_scan<KB>((keep ? 1u : 0u) + (keep2 ? 1u : 0u), s.wave, &n_keep);
@@ -527,25 +532,26 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
     nS = nD = n_keep = 0;
     keep = keep2 = false;
   }
+  // the remaining items in place, each counted in its sub-bucket (the counting sort's
+  // histogram, from the registers)
   if (q < nD) {
     s.utag[q] = itag;
+    atomicAdd(&s.x.ucnt[sub_of(ir.key, T, t)], 1u);
   } else if (keep) {
     const u32 nq = nD + kpos;
     s.ukey[nq] = ir.key;
     s.utag[nq] = (itag & ~SLOT) | nq;
+    atomicAdd(&s.x.ucnt[sub_of(ir.key, T, t)], 1u);
   }
   if (keep2) {
     const u32 nq = nD + kpos + (keep ? 1u : 0u);
     s.ukey[nq] = key2;
     s.utag[nq] = (tag2 & ~SLOT) | nq;
+    atomicAdd(&s.x.ucnt[sub_of(key2, T, t)], 1u);
   }
   nU = nD + n_keep;
-  for (u32 b = tid; b < NSUB; b += KB) s.x.ucnt[b] = 0;
-  KSTAMP(t, 13);
-  __syncthreads();
 
   // ---- counting sort of the items by sub-bucket, then (key, tag) within one
-  for (u32 q = tid; q < nU; q += KB) atomicAdd(&s.x.ucnt[sub_of(s.ukey[q], T, t)], 1u);
   for (u32 i = tid; i < nS; i += KB) {  // state rows: first row of every sub-bucket
     const u32 sb = sub_of(s.skey[i], T, t);
     u32 b = i == 0 ? 0 : sub_of(s.skey[i - 1], T, t) + 1;
@@ -555,17 +561,17 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
   }
   if (nS == 0)
     for (u32 b = tid; b <= (u32)NSUB; b += KB) s.y.e.sfirst[b] = 0;
-  KSTAMP(t, 8);
+  KSTAMP(t, 13);
   __syncthreads();
-  scan_excl(s.x.ucnt, NSUB, s.y.e.ustart, s.wave);
+  // sub-bucket starts; the counts become the scatter's cursors (each thread rewrites the
+  // entries it read)
+  scan_excl<true>(s.x.ucnt, NSUB, s.y.e.ustart, s.wave);
   KSTAMP(t, 9);
-  __syncthreads();
-  for (u32 b = tid; b < NSUB; b += KB) s.x.ucnt[b] = 0;
   __syncthreads();
   unsigned short* bin = s.y.e.slbu;  // items grouped by sub-bucket (slbu is free until evaluation)
   for (u32 q = tid; q < nU; q += KB) {
     const u32 sb = sub_of(s.ukey[q], T, t);
-    bin[s.y.e.ustart[sb] + atomicAdd(&s.x.ucnt[sb], 1u)] = (unsigned short)q;
+    bin[atomicAdd(&s.x.ucnt[sb], 1u)] = (unsigned short)q;
   }
   KSTAMP(t, 10);
   __syncthreads();
@@ -660,12 +666,23 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
   }
   KSTAMP(t, 7);
   present2(cs, ds, cu, du, p.tabC, p.tabP);
-  if (ds) s.y.e.ssurv[tid] = cs.P;
-  if ((u32)tid < nU) s.y.e.usurv[tid] = du && cu.P;
+  const bool ss_ = ds && cs.P, us_ = (u32)tid < nU && du && cu.P;
+  if (ds) s.y.e.ssurv[tid] = ss_;
+  if ((u32)tid < nU) s.y.e.usurv[tid] = us_;
   KSTAMP(t, 3);
-  __syncthreads();
-  scan_excl(s.y.e.ssurv, nS, s.x.pre.spre, s.wave);
-  scan_excl(s.y.e.usurv, nU, s.x.pre.upre, s.wave);
+  // the survivors' exclusive prefixes, state rows (low half) and items (high half) in ONE
+  // block scan of the thread's own flags (one state row and one item per thread); entry n
+  // holds the total (the threads past nS / nU write it too)
+  {
+    u32 tot2;
+    const u32 pre2 = block_excl_scan<KB>((ss_ ? 1u : 0u) | (us_ ? 1u << 16 : 0u), s.wave, &tot2);
+    s.x.pre.spre[tid] = (unsigned short)(pre2 & 0xFFFFu);
+    s.x.pre.upre[tid] = (unsigned short)(pre2 >> 16);
+    if (tid == 0) {
+      s.x.pre.spre[nS] = (unsigned short)(tot2 & 0xFFFFu);
+      s.x.pre.upre[nU] = (unsigned short)(tot2 >> 16);
+    }
+  }
   __syncthreads();
   KSTAMP(t, 4);
 

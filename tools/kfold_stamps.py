@@ -5,9 +5,9 @@ diagnostic build, on config 3 (KF_KEYS keys, 64 keyed deltas).
     python tools/kfold_stamps.py                       # on the GPU box
 
 Stamps (s_memrealtime, 100 MHz) by lane 0 of every bucket at: 0 start (after the
-ticket)  1 slices staged in LDS  13 keyset entries folded into rows  2 delta items sorted  7 key masks built  3 candidates
+ticket)  1 slices staged in LDS  13 keyset entries folded into rows + sub-bucket histogram  2 delta items sorted  7 key masks built  3 candidates
 evaluated (VV tables)  4 survivor scans done  5 survivors ranked  6 offset looked up and
-rows written; 12 run offsets scanned, 8 sub-bucket histogram, 9 its scan, 10 scatter.  Only SHARES are meaningful
+rows written; 12 run offsets scanned, 9 sub-bucket scan, 10 scatter.  Only SHARES are meaningful
 (stamps add barriers)."""
 import ctypes as C
 import os
@@ -46,9 +46,9 @@ def main():
     nb = int(np.nonzero(st[:, 0])[0].max()) + 1
     st = st[:nb]
     t0 = st[:, 0].min()
-    names = ["stage:meta+scan", "stage:rows", "keyset-drop", "sort:histogram", "sort:scan",
+    names = ["stage:meta+scan", "stage:rows", "keyset-drop+histogram", "sort:scan",
              "sort:scatter", "sort:rank+move", "masks", "vv-tables", "scans", "rank", "lookback+write"]
-    d = np.diff(st[:, [0, 12, 1, 13, 8, 9, 10, 2, 7, 3, 4, 5, 6]], axis=1) * 10 / 1000.0  # us
+    d = np.diff(st[:, [0, 12, 1, 13, 9, 10, 2, 7, 3, 4, 5, 6]], axis=1) * 10 / 1000.0  # us
     print(f"buckets={nb} kernel span={(st[:, 6].max() - t0) * 10 / 1000:.1f} us")
     for i, nm in enumerate(names):
         print(f"{nm:16s} median {np.median(d[:, i]):7.2f} us  p90 {np.percentile(d[:, i], 90):7.2f}"
