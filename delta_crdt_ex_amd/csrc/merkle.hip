@@ -400,8 +400,9 @@ __device__ u32 merge_bucket(const Rows& A, const TermH& tha, u64 ia, u64 ie, con
 // ---------------------------------------------------------------- full diff
 // One workgroup per subtree of 2^sub buckets (sub = min(depth, 12)), whose root sits at
 // level Ls = depth - sub.
-//  1. bounds: one wave per subtree boundary finds the boundary's first row in both stores
-//     (a 64-ary wave lower bound: 4 dependent load rounds at 12.5M rows).
+//  1. bounds: two waves of the subtree's workgroup find its first row in both stores
+//     (a 64-ary wave lower bound: 4 dependent load rounds at 12.5M rows), beside the
+//     descent's first loads (no separate launch).
 //  2. count: a subtree whose roots match is skipped.  Otherwise the workgroup descends it
 //     in strides of 4 levels.  Each thread owns 16 consecutive buckets: their ancestors
 //     4 and 8 levels up (one node each), the subtree's root and the buckets' row counts
@@ -439,16 +440,6 @@ struct DiffArgs {
   u64* d_count;
 };
 
-__global__ __launch_bounds__(256) void merkle_diff_bounds_kernel(DiffArgs p) {
-  const u64 i = ((u64)blockIdx.x * 256 + threadIdx.x) / WAVE;  // one wave per boundary
-  const u64 nbnd = p.ntiles + 1;
-  if (i >= 2 * nbnd) return;  // uniform per wave
-  const bool B = i >= nbnd;
-  const u64 t = B ? i - nbnd : i;
-  const Rows& r = B ? p.sb : p.sa;
-  const u64 x = wave_bucket_start(p.ta, r.key, r.n, t << p.sub);
-  if ((threadIdx.x & (WAVE - 1)) == 0) p.bnd[i] = x;
-}
 
 // the counts of a thread's 16 buckets (u16) as 8 words of two halves
 __device__ __forceinline__ void load_counts16(const uint16_t* c, u32 nb, u32 first, u32 w[8]) {
@@ -484,6 +475,17 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
   //      trip; the 16 bucket nodes only below differing ancestors, in a second one
   const bool owns = (u32)tid * OWN < nb;
   const u64 b0 = (tile << sub) + (u64)tid * OWN;  // the first owned bucket (tree-wide)
+  // the subtree's first row in both stores: waves 0 and 1 search while the descent's
+  // loads are in flight (also for the write kernel, which reads them from p.bnd)
+  __shared__ u64 s_bnd[2];
+  if (tid < 2 * WAVE) {
+    const Rows& r = tid < WAVE ? p.sa : p.sb;
+    const u64 x = wave_bucket_start(p.ta, r.key, r.n, tile << sub);
+    if ((tid & (WAVE - 1)) == 0) {
+      s_bnd[tid / WAVE] = x;
+      p.bnd[(tid < WAVE ? 0 : nbnd) + tile] = x;
+    }
+  }
   const u64 ra = p.ta.nodes[root], rb = p.tb.nodes[root];
   u64 ga = 0, gb = 0, qa = 0, qb = 0;
   if (owns && sub >= 8) {
@@ -505,7 +507,7 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
 #pragma unroll
     for (int q = 0; q < 8; q++) ca[q] = cb[q] = 0;
   }
-  if (ra == rb) {  // uniform: the whole subtree matches
+  if (ra == rb) {  // uniform: the whole subtree matches (the bounds are written anyway)
     if (tid == 0) p.cnt[tile] = 0;
     return;
   }
@@ -529,7 +531,6 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
   //      offsets in both stores (from the subtree's first row) and their place among the
   //      staged rows; then every per-bucket step runs one lane per differing bucket, not
   //      every thread over its 16 owned buckets (which ran each step masked 16 times)
-  const u64 a0 = p.bnd[tile], c0 = p.bnd[nbnd + tile];
   u32 ta_ = 0, tb_ = 0, rd = 0;
 #pragma unroll
   for (u32 i = 0; i < OWN; i++) {
@@ -546,6 +547,7 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
   const u32 slot0 = block_excl_scan<DB>(rd, s_wave, &R);
   __syncthreads();
   const u32 d0 = block_excl_scan<DB>((u32)__popc(mine), s_wave, &ND);
+  const u64 a0 = s_bnd[0], c0 = s_bnd[1];  // (the scans' barriers came after the searches)
   const u64 base = a0 + c0;
   const bool lds = R <= RCAP && ND <= DCAP;  // uniform
   if (lds) {
@@ -848,10 +850,9 @@ hipError_t launch_merkle_diff(const MerkleT& a, const Rows& sa, const MerkleT& b
   p.keys = p.cnt + p.ntiles;
   p.bsum = p.keys + sa.n + sb.n + 1;
   p.d_count = d_count;
-  const u64 waves = 2 * (p.ntiles + 1);
   hipError_t e = hipMemsetAsync(p.bsum, 0, grid_of(p.ntiles, DB) * sizeof(u64), st);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(merkle_diff_bounds_kernel, dim3(grid_of(waves * WAVE, 256)), dim3(256), 0, st, p);
+  // (the subtree bounds are searched inside the count kernel)
   hipLaunchKernelGGL(merkle_diff_count_kernel, dim3((unsigned)p.ntiles), dim3(DB), 0, st, p);
   hipLaunchKernelGGL(merkle_diff_write_kernel, dim3((unsigned)p.ntiles), dim3(WAVE), 0, st, p);
   return hipGetLastError();

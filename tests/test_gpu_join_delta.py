@@ -102,3 +102,18 @@ def test_applied_twice_changes_nothing(engine):
     assert c1.numel() == len(want) and c2.numel() == 0 and not sw2 and tree.root() == root
     wr, wc = R.join2(a["rows"], a["ctx"], b["rows"], b["ctx"])
     rows_eq(st, wr)
+
+
+def test_join_delta_edges(engine):
+    """An empty keyset, an empty delta, and a state that is empty."""
+    rng = np.random.default_rng(4)
+    a, b = W.random_pair(rng, 5_000, n_nodes=3)
+    kb = np.unique(b["rows"][0])
+    # empty keyset (the delta's keys all outside it: the right-biased carry replaces them)
+    apply(engine, a, W.sync_delta(b, kb[:10]), np.zeros(0, np.uint64), with_tree=False)
+    # a delta without rows, keyset of present keys: removals only
+    empty = {"rows": tuple(c[:0] for c in b["rows"]), "ctx": b["ctx"]}
+    apply(engine, a, empty, np.unique(a["rows"][0])[::50])
+    # an empty state receiving a sync delta
+    none = {"rows": tuple(c[:0] for c in a["rows"]), "ctx": a["ctx"]}
+    apply(engine, none, W.sync_delta(b, kb[::20]), kb[::20], with_tree=False)
