@@ -220,7 +220,7 @@ def config4_round(eng, torch, dev, rank=0, world=1, keys_per_rank=12_500_000, st
                      "frac": build_alg / (build_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
                      "launch_timing": "HIP events on the engine stream around the async builds"},
         "diff_roofline": {"bound": "hbm",
-                          "kernel": "merkle_diff_bounds + merkle_diff_count (descent) + merkle_diff_write",
+                          "kernel": "merkle_diff_count (subtree bounds + descent) + merkle_diff_write",
                           "alg_bytes_per_call": diff_alg, "avg_call_us": med["diff_ev"] * 1e6,
                           "achieved": diff_alg / med["diff_ev"] / 1e9, "peak": HBM_PEAK_GBS,
                           "unit": "GB/s", "frac": diff_alg / med["diff_ev"] / 1e9 / HBM_PEAK_GBS,

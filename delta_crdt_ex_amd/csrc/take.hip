@@ -16,7 +16,7 @@ namespace dg {
 
 namespace {
 
-constexpr int TB = 1024, TI = 1, TK = TB * TI;  // one key per thread: the searches run side by side
+constexpr int TB = TAKE_TILE, TI = 1, TK = TB * TI;  // one key per thread: the searches run side by side
 
 __global__ __launch_bounds__(TB) void take_keys_kernel(Rows s, const u64* keys, u64 n_keys,
                                                       u64 ntiles, RowsOut out, u64 cap, Scan scan,
