@@ -898,7 +898,7 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   __shared__ StreamLds<KEYED> s;
   const int tid = threadIdx.x;
   const u64 total = p.a.n + p.b.n, ntiles = p.ntiles, w = blockIdx.x;
-  const u64 G = gridDim.x - (p.fused ? 1 : 0);  // tile workgroups
+  const u64 G = gridDim.x - (LATE ? 1 : 0);  // tile workgroups
   u32* cs = p.scan.counts;  // tile-count granules
   const u32 epoch = p.scan.epoch;
   const Rows& A = p.a;
@@ -909,7 +909,7 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   if (w < G) JSTAMP(w, 0);  // (stamps build: slot 0 of a workgroup's first tile = its entry)
   Staged r;
   u64 ga0 = 0, ga1 = 0;  // fused: the first tile's speculative splits
-  if (p.fused) {
+  if (LATE) {
     if (w == G) {  // Dots.union(c1, c2) (aw_lww_map.ex:155), beside the tiles
       ctx_union_block<JB>(p.cu, s.wave);
       return;
@@ -943,20 +943,23 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   }
   if (FAST)
     for (int x = tid; x < 2 * VT; x += JB) (&s.tab[0][0])[x] = 0;
-  if (p.fused) __syncthreads();
+  if (LATE) __syncthreads();
   if (w < G) JSTAMP(w, 8);  // (stamps build: splits searched)
-  // split of boundary `side` (0 start, 1 end) of the tile of iteration k
-  // (a uniform branch between an LDS read and a global read: a select between the two
-  // pointers would make it a flat load, whose wait also drains the previous tile's stores)
+  // split of boundary `side` (0 start, 1 end) of the tile of iteration k.  The fused
+  // launch is exactly the LATE kernel, so the choice between the LDS copy and the
+  // partition's array is made at compile time: a run-time flag let the compiler merge the
+  // two reads into one flat load, whose wait (vmcnt 0) drained the previous tile's output
+  // stores on every iteration (A/B: config 5 0.375-0.379 vs 0.381-0.388 ms per join, config 2
+  // 33-35 vs 34-36 us)
   auto split = [&](u64 tile, int k, int side) -> u64 {
-    if (p.fused) return s.spl[2 * k + side];
+    if (LATE) return s.spl[2 * k + side];
     return p.splits[tile + side];
   };
   // keyed: the keyset slice [kl, kl + km) of the tile of iteration k; its entries are
   // staged with the tile's rows (one per lane) when km <= KS
   auto kslice = [&](u64 tile, int k, u64* kl) -> u64 {
     u64 lo, hi;
-    if (p.fused) {
+    if (LATE) {
       lo = s.kspl[2 * k];
       hi = s.kspl[2 * k + 1];
     } else {
@@ -971,7 +974,7 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   int nat, nbt;
   u64 b0;
   tile_geom(t, a0, a1, total, &nat, &nbt, &b0);
-  if (!p.fused || a0 != ga0 || a1 != ga1) issue_tile(A, B, nat, nbt, a0, b0, r);  // (uniform)
+  if (!LATE || a0 != ga0 || a1 != ga1) issue_tile(A, B, nat, nbt, a0, b0, r);  // (uniform)
   u64 kl = 0, km = 0, kk = 0;
   if (KEYED) {
     km = kslice(t, 0, &kl);
