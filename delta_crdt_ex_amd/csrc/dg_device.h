@@ -316,6 +316,14 @@ __device__ __forceinline__ u32 wave_prev(u32 v) {
   return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
 }
 
+// lane l - 1's value, lane 0 gets `first`.  Pass lane 0's own value here rather than
+// selecting it after the shift (`lane ? wave_prev(v) : x`): the compiler may move the DPP
+// into the `lane != 0` branch of such a select, where lane 0 -- the source of lane 1 --
+// is inactive and lane 1 reads the old value (a wrong Merkle bucket count, seen on gfx950).
+__device__ __forceinline__ u32 wave_prev_or(u32 v, u32 first) {
+  return (u32)__builtin_amdgcn_update_dpp((int)first, (int)v, 0x138, 0xf, 0xf, false);
+}
+
 // Sum of a 32-bit value over the wave (every lane gets it).
 __device__ __forceinline__ u32 wave_sum_u32(u32 v) {
   return (u32)__builtin_amdgcn_readlane((int)wave_incl_scan(v), WAVE - 1);

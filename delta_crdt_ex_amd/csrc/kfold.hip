@@ -262,9 +262,9 @@ __global__ __launch_bounds__(FILL_BLOCK) void kfold_fill_kernel(KFoldArgs p) {
     for (int u = 0; u < FILL_PER; u++) {
       const u64 j = j0 + (u64)u * FILL_BLOCK + threadIdx.x;
       const u32 b = (u32)bucket_of(kc[u], T);  // every lane, for the DPP shift
-      const u32 pb = wave_prev(b);
+      const u32 pb = wave_prev_or(b, (u32)bucket_of(kp[u], T));  // lane 0: its loaded key's
       if (j < jend) {
-        u64 bb = j == 0 ? 0 : (lane ? (u64)pb : bucket_of(kp[u], T)) + 1;
+        u64 bb = j == 0 ? 0 : (u64)pb + 1;
         const u64 end = (j == n - 1) ? T : b;
         for (; bb <= end; bb++) p.dstart[bb * stride + r] = (u32)(bb <= b ? j : n);
       }
