@@ -420,12 +420,15 @@ __global__ __launch_bounds__(PB) void join2_partition_kernel(Rows A, Rows B, u64
                                                              u64* splits, CtxUnionArgs cu,
                                                              const u64* keys, u64 n_keys,
                                                              u64* ksplits) {
-  if (blockIdx.x == gridDim.x - 1) {  // extra workgroup: Dots.union(c1, c2) (aw_lww_map.ex:155)
+  // the extra workgroup computes Dots.union(c1, c2) (aw_lww_map.ex:155); it is the FIRST
+  // of the grid so its latency chain runs beside the searches instead of after the last
+  // of them has been dispatched (config 5: partition 20.4 -> 18.1 us, A/B)
+  if (blockIdx.x == 0) {
     __shared__ u32 s_wave[PB / WAVE + 1];
     ctx_union_block<PB>(cu, s_wave);
     return;
   }
-  const u64 q = (u64)blockIdx.x * (PB / WAVE) + (threadIdx.x >> 6);
+  const u64 q = (u64)(blockIdx.x - 1) * (PB / WAVE) + (threadIdx.x >> 6);
   if (q > ntiles) return;
   const u64 d = min(q * (u64)JT, A.n + B.n);
   const u64 s = mp_split(A, B, d);
