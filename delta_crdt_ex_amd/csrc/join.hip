@@ -15,11 +15,11 @@
 //
 // Kernel shape (HBM-bound integer merge; no MFMA):
 //   1. join2_partition_kernel: one wave per tile boundary finds the merge-path split
-//      of diagonal q*JT.  Key ids are 64-bit hashes, so two interpolation probes on
-//      the key columns land within a few rows of the split and one 128-wide window
+//      of diagonal q*JT.  Key ids are 64-bit hashes, so the key gap at the proportional
+//      split (one probe) lands within a few rows of the split and one 128-wide window
 //      round finishes it (~5 cache lines per array instead of a 21-step search); any
 //      key distribution stays exact through a 128-ary fallback search.  One extra
-//      workgroup computes the context union Dots.union(c1, c2) (:155).
+//      workgroup (the grid's first) computes the context union Dots.union(c1, c2) (:155).
 //   2. join2_stream_kernel (single pass, the default): a persistent grid of G
 //      resident workgroups (occupancy API) walks the tiles statically, t = w + k*G,
 //      so tiles k*G .. k*G+G-1 form "stripe" k.  Per iteration a workgroup commits
