@@ -25,17 +25,14 @@ from .store import u64
 def update_state_with_delta(state: M.AWLWWMap, delta: M.AWLWWMap, keys):
     """Returns (new_state, diffs): diffs is what on_diffs would receive -- None when no
     key's value map changed (diffs_to_callback/3 is not reached), else a list of
-    ("add", key, value) / ("remove", key) in `keys` order (possibly empty).  Keys are
-    deduplicated and values compared exactly (`=:=`: 1, 1.0 and true stay distinct),
-    as the reference's map lookups and `{old, old}` match do."""
+    ("add", key, value) / ("remove", key) in `keys` order (possibly empty).  A key listed
+    twice is reported twice, as diff/3's and diffs_to_callback/3's flat_map over `keys`
+    does (:345,368); values compare exactly (`=:=`: 1, 1.0 and true stay distinct), as
+    the reference's map lookups and `{old, old}` match do, and a nil value reads as an
+    absent key (H9)."""
     U = state.universe
-    order, seen = [], set()
-    for k in keys:  # dedup by interned id, not Python equality
-        kid = U.key(k)
-        if kid not in seen:
-            seen.add(kid)
-            order.append((kid, k))
-    kids = np.array(sorted(seen), dtype=np.uint64)
+    order = [(U.key(k), k) for k in keys]  # keys by interned id, not Python equality
+    kids = np.array(sorted({kid for kid, _ in order}), dtype=np.uint64)
     kt = torch.from_numpy(np.ascontiguousarray(kids).view(np.int64)).to(M._dev())
     out, octx, changed = M.engine().join2_changes(state.rows, state.ctx, delta.rows, delta.ctx,
                                                   keys=kt)
@@ -47,18 +44,30 @@ def update_state_with_delta(state: M.AWLWWMap, delta: M.AWLWWMap, keys):
     old_v, new_v = _read_ids(state, ckeys), _read_ids(new, ckeys)
     diffs = []
     for kid, k in ckeys:
-        o, n = old_v.get(kid), new_v.get(kid)
-        if o == n:  # value ids: equal exactly when the terms are =:=
+        # Map.get(read, key) (:369): nil for an absent key AND for a key whose value is nil
+        o, n = _get(U, old_v, kid), _get(U, new_v, kid)
+        if o == n:  # {old, old} -> []  (value ids: equal exactly when the terms are =:=)
             continue
+        # {_old, nil} -> {:remove, key}  (delta_subscriber_test.exs:26-27); else {:add, ...}
         diffs.append(("remove", k) if n is None else ("add", k, U.value_term(n)))
     return new, diffs
+
+
+def _get(U, ids, kid):
+    """`Map.get(read_result, key)` as a value id: None stands for nil, which the reference
+    returns both for a key read/2 did not return and for one whose value is the atom nil
+    (causal_crdt.ex:369-372)."""
+    v = ids.get(kid)
+    if v is None or U.value_term(v) is None:
+        return None
+    return v
 
 
 def _read_ids(state: M.AWLWWMap, ckeys):
     """read/2 on the device for the (key id, key) pairs: {key id: value id}."""
     if state.rows.n == 0 or not ckeys:
         return {}
-    kids = np.array(sorted(kid for kid, _ in ckeys), dtype=np.uint64)
+    kids = np.array(sorted({kid for kid, _ in ckeys}), dtype=np.uint64)
     kt = torch.from_numpy(np.ascontiguousarray(kids).view(np.int64)).to(M._dev())
     ok, ov = M.engine().read_lww(state.rows, keys=kt)
     return {int(k): int(v) for k, v in zip(u64(ok), u64(ov))}

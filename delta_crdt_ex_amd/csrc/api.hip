@@ -40,6 +40,10 @@ struct dg_engine {
   // splice while their inputs live in `fold`)
   void* spl = nullptr;
   size_t spl_cap = 0;
+  // dg_join_delta's union context on its full-join path (its own: the join it calls may
+  // splice through `spl`)
+  void* ubuf = nullptr;
+  size_t ubuf_cap = 0;
   u32 epoch = 0;
   // small device counters + pinned host mirror.  d_counts[0..8) and ticket[0..16) are one
   // device allocation (ticket == (u32*)(d_counts + 8)), so a synchronous call brings its
@@ -551,6 +555,53 @@ int splice_join(dg_engine* e, const dg_store* a, const dg_context* ca, const dg_
   return DG_OK;
 }
 
+// MerkleMap put/delete + update_hashes of `keys` (the tree indexes `olds`; afterwards
+// `news`), all or nothing: when the update meets an input error (a changed key outside the
+// tree's shard, a bucket over 65535 rows) the same update with the stores exchanged
+// restores every node and count bit for bit, and the error is returned.  `ready`: the
+// dirty flags, key-count shards and error word are zeroed already (dg_join_delta's
+// set-up launch).  `tail` (optional) enqueues work between the update and its host sync
+// that must not take effect after a failed update (it reads the error word as a guard).
+// *d_n_keys = the change in distinct keys (not applied to t->n_keys).
+template <class Tail>
+int tree_update(dg_engine* e, dg_merkle* t, const dg_store* olds, const dg_store* news,
+                const uint64_t* keys, uint64_t n_keys, const char* what, bool ready, Tail tail,
+                u64* d_n_keys) {
+  const u64 chunks = merkle_chunks(t->depth), cw = merkle_ctr_words(t->depth);
+  TRY(ensure_tmp(e, (cw + chunks) * sizeof(u32)));
+  u32* ctr = (u32*)e->tmp;
+  u32* dirty = ctr + cw;
+  if (!ready)
+    HIP_TRY(launch_splice_finish(nullptr, nullptr, 0, nullptr, nullptr, dirty, chunks, e->d_counts,
+                                 e->ticket + 3, e->stream));
+  HIP_TRY(launch_merkle_update(merkle_of(t), rows_of(olds), rows_of(news), keys, n_keys, dirty,
+                               e->d_counts, ctr, e->ticket + 3, e->stream));
+  TRY(tail());
+  TRY(read_counts(e, 8));
+  u64 dk = 0;
+  for (int i = 0; i < 8; i++) dk += e->h_counts[i];  // signed changes, two's complement
+  *d_n_keys = dk;
+  if (!(e->h_ticket[3] & MERKLE_INPUT_ERR)) return DG_OK;
+  const int rc = input_error(e, what);
+  const std::string msg = g_err;
+  HIP_TRY(launch_splice_finish(nullptr, nullptr, 0, nullptr, nullptr, dirty, chunks, e->d_counts,
+                               e->ticket + 3, e->stream));
+  HIP_TRY(launch_merkle_update(merkle_of(t), rows_of(news), rows_of(olds), keys, n_keys, dirty,
+                               e->d_counts, ctr, e->ticket + 3, e->stream));
+  HIP_TRY(hipMemsetAsync(e->ticket + 3, 0, sizeof(u32), e->stream));  // the undo's own bits
+  TRY(read_counts(e, 0));
+  g_err = msg;
+  return rc;
+}
+
+int tree_update(dg_engine* e, dg_merkle* t, const dg_store* olds, const dg_store* news,
+                const uint64_t* keys, uint64_t n_keys, const char* what) {
+  u64 dk = 0;
+  TRY(tree_update(e, t, olds, news, keys, n_keys, what, false, [] { return (int)DG_OK; }, &dk));
+  t->n_keys += dk;
+  return DG_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -643,6 +694,7 @@ int dg_engine_destroy(dg_engine* e) {
   if (e->started) hipFree(e->started);
   if (e->fold) hipFree(e->fold);
   if (e->spl) hipFree(e->spl);
+  if (e->ubuf) hipFree(e->ubuf);
   if (e->h_stage) hipHostFree(e->h_stage);
   if (e->own_stream && e->stream) hipStreamDestroy(e->stream);
   if (e->ev_in || e->ev_out) {  // a registered engine (creation got past the registry)
@@ -818,7 +870,13 @@ int dg_join_delta(dg_engine* e, dg_store* state, dg_context* state_ctx, const dg
                 (unsigned long long)state_ctx->cap, (unsigned long long)(state_ctx->n + delta_ctx->n));
   TRY(set_device(e));
   TRY(settle(e));
+  // All or nothing: nothing of *state, *state_ctx or the tree changes unless the call
+  // succeeds.  Everything that can fail (the join's grid, the capacity of `changed`, the
+  // tree update's input checks) runs on scratch and `spare` first; the state is written
+  // last, by kernels that skip their writes when the tree update reported an error.
   const u64 uctx_cap = state_ctx->n + delta_ctx->n;
+  const dg_context_kind out_kind =
+      (state_ctx->kind == DG_CTX_DOTS && delta_ctx->kind == DG_CTX_DOTS) ? DG_CTX_DOTS : DG_CTX_VV;
   Splice w;
   bool ok = false;
   const dg_store old_state = *state;
@@ -826,25 +884,38 @@ int dg_join_delta(dg_engine* e, dg_store* state, dg_context* state_ctx, const dg
     TRY(splice_take(e, state, delta, keys, n_keys, uctx_cap, &w, &ok));
   if (!ok) {
     // the full keyed join into the spare store (the merge, or a splice into `spare` that
-    // dg_join2_changes picks itself), the context through scratch, then the tree
-    TRY(ensure_buf(e, &e->spl, &e->spl_cap, (uctx_cap * 12 + 1024 + 255) / 256 * 256));
+    // dg_join2_changes picks itself), the context into its own scratch, then the tree
+    TRY(ensure_buf(e, &e->ubuf, &e->ubuf_cap, (uctx_cap * 12 + 1024 + 255) / 256 * 256));
     dg_context uc{};
-    uc.cnt = (uint64_t*)e->spl;
-    uc.node = (uint32_t*)((char*)e->spl + (uctx_cap * 8 + 255) / 256 * 256);
+    uc.cnt = (uint64_t*)e->ubuf;
+    uc.node = (uint32_t*)((char*)e->ubuf + (uctx_cap * 8 + 255) / 256 * 256);
     uc.cap = uctx_cap;
     TRY(dg_join2_changes(e, state, state_ctx, delta, delta_ctx, keys, n_keys, spare, &uc,
                          changed, cap, n_changed));
+    if (tree) TRY(tree_update(e, tree, &old_state, spare, changed, *n_changed, "dg_join_delta"));
     HIP_TRY(hipMemcpyAsync(state_ctx->node, uc.node, uc.n * 4, hipMemcpyDeviceToDevice, e->stream));
     HIP_TRY(hipMemcpyAsync(state_ctx->cnt, uc.cnt, uc.n * 8, hipMemcpyDeviceToDevice, e->stream));
+    TRY(read_counts(e, 0));
     state_ctx->n = uc.n;
     state_ctx->kind = uc.kind;
-    if (tree) TRY(dg_merkle_update(e, tree, &old_state, spare, changed, *n_changed));
     std::swap(*state, *spare);
     *swapped = 1;
     return DG_OK;
   }
   TRY(splice_edit(e, &w, state_ctx, delta, delta_ctx, keys, n_keys, &w.uctx, true, changed, cap));
-  TRY(read_counts(e, 6));
+  if (read_counts(e, 6) != DG_OK) {
+    // the join grid could not become resident (another process's persistent kernels) or
+    // timed out: nothing of the state is written yet, so re-run the edit on a grid small
+    // enough to find room beside other work, as dg_join2_changes does
+    const int workers = e->join_workers;
+    e->join_workers = RETRY_WORKERS;
+    HIP_TRY(hipMemsetAsync(e->d_counts + 5, 0, sizeof(u64), e->stream));  // `moved`
+    const int rc = splice_edit(e, &w, state_ctx, delta, delta_ctx, keys, n_keys, &w.uctx, true,
+                               changed, cap);
+    e->join_workers = workers;
+    TRY(rc);
+    TRY(read_counts(e, 6));
+  }
   const bool moved = (u32)e->h_counts[5] != 0;
   const u64 n_e = e->h_counts[0];
   w.uctx.n = e->h_counts[1];
@@ -852,47 +923,34 @@ int dg_join_delta(dg_engine* e, dg_store* state, dg_context* state_ctx, const dg
   if (*n_changed > cap)
     return fail(DG_E_CAPACITY, "dg_join_delta: %llu changed keys > cap %llu",
                 (unsigned long long)*n_changed, (unsigned long long)cap);
-  dg_store* out = state;
-  if (moved) {  // some key's row count changed: the rows outside K move, into `spare`
-    w.sp.out = rows_out_of(spare);
-    HIP_TRY(launch_splice_copy(w.sp, false, e->stream));
-    out = spare;
-  } else {      // every joined key keeps its row count: E's rows in place, nothing else moves
-    w.sp.out = rows_out_of(state);
-    HIP_TRY(launch_splice_copy(w.sp, true, e->stream));
-  }
-  out->n = state->n - w.n_ak + n_e;
-  u32* ctr = nullptr;
-  u32* dirty = nullptr;
-  u64 chunks = 0;
-  if (tree) {
-    const u64 cw = merkle_ctr_words(tree->depth);
-    chunks = merkle_chunks(tree->depth);
-    TRY(ensure_tmp(e, (cw + chunks) * sizeof(u32)));
-    ctr = (u32*)e->tmp;
-    dirty = ctr + cw;
-  }
-  // the union context into the state's, and the tree update's zeroed words: one launch
-  HIP_TRY(launch_splice_finish(w.uctx.node, w.uctx.cnt, w.uctx.n, state_ctx->node, state_ctx->cnt,
-                               dirty, chunks, tree ? e->d_counts : nullptr,
-                               tree ? e->ticket + 3 : nullptr, e->stream));
-  state_ctx->n = w.uctx.n;
-  state_ctx->kind = (state_ctx->kind == DG_CTX_DOTS && delta_ctx->kind == DG_CTX_DOTS) ? DG_CTX_DOTS
-                                                                                          : DG_CTX_VV;
+  dg_store* out = moved ? spare : state;
+  w.sp.out = rows_out_of(out);
+  // the copy: into `spare` (scratch until the swap) when rows move, else E's rows in place,
+  // guarded by the tree update's error word; then the union context, guarded the same way
+  const u32* guard = tree ? e->ticket + 3 : nullptr;
+  w.sp.guard = moved ? nullptr : guard;
+  auto copy = [&]() -> int {
+    HIP_TRY(launch_splice_copy(w.sp, !moved, e->stream));
+    HIP_TRY(launch_splice_finish(w.uctx.node, w.uctx.cnt, w.uctx.n, state_ctx->node, state_ctx->cnt,
+                                 nullptr, 0, nullptr, nullptr, e->stream, guard));
+    return DG_OK;
+  };
   if (tree) {
     // MerkleMap.put/delete of the changed keys: every changed key is a keyset key, so its
     // old rows are among the taken rows and its new rows among the edit's (both small and
     // cache-resident: no search of the 12.5M-row state)
     dg_store ed = w.ed;
     ed.n = n_e;
-    HIP_TRY(launch_merkle_update(merkle_of(tree), rows_of(&w.ak), rows_of(&ed), changed, *n_changed,
-                                 dirty, e->d_counts, ctr, e->ticket + 3, e->stream));
-    TRY(read_counts(e, 8));
-    TRY(input_error(e, "dg_join_delta"));
-    for (int i = 0; i < 8; i++) tree->n_keys += e->h_counts[i];
+    u64 dk = 0;
+    TRY(tree_update(e, tree, &w.ak, &ed, changed, *n_changed, "dg_join_delta", false, copy, &dk));
+    tree->n_keys += dk;
   } else {
+    TRY(copy());
     TRY(read_counts(e, 0));
   }
+  out->n = old_state.n - w.n_ak + n_e;
+  state_ctx->n = w.uctx.n;
+  state_ctx->kind = out_kind;
   if (moved) {
     std::swap(*state, *spare);
     *swapped = 1;
@@ -1402,19 +1460,7 @@ int dg_merkle_update(dg_engine* e, dg_merkle* t, const dg_store* old_s, const dg
   if (n_keys && !keys) return fail(DG_E_INVAL, "dg_merkle_update: null keys");
   TRY(set_device(e));
   TRY(settle(e));
-  const u64 chunks = merkle_chunks(t->depth), cw = merkle_ctr_words(t->depth);
-  TRY(ensure_tmp(e, (cw + chunks) * sizeof(u32)));
-  u32* ctr = (u32*)e->tmp;
-  u32* dirty = ctr + cw;
-  HIP_TRY(hipMemsetAsync(dirty, 0, chunks * sizeof(u32), e->stream));
-  HIP_TRY(hipMemsetAsync(e->ticket + 3, 0, sizeof(u32), e->stream));
-  HIP_TRY(hipMemsetAsync(e->d_counts, 0, 8 * sizeof(u64), e->stream));
-  HIP_TRY(launch_merkle_update(merkle_of(t), rows_of(old_s), rows_of(new_s), keys, n_keys, dirty,
-                               e->d_counts, ctr, e->ticket + 3, e->stream));
-  TRY(read_counts(e, 8));
-  TRY(input_error(e, "dg_merkle_update"));
-  for (int i = 0; i < 8; i++) t->n_keys += e->h_counts[i];  // signed changes, two's complement
-  return DG_OK;
+  return tree_update(e, t, old_s, new_s, keys, n_keys, "dg_merkle_update");
 }
 
 int dg_merkle_diff(dg_engine* e, const dg_merkle* a, const dg_store* sa, const dg_merkle* b,

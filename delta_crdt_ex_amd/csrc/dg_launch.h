@@ -164,6 +164,9 @@ struct SpliceArgs {
   const u64* d_ne;
   RowsOut out;
   u64 a_tiles, e_tiles;
+  // (optional) an input-error word: when it has a MERKLE_INPUT_ERR bit set, E's rows are
+  // not written (dg_join_delta's in-place copy runs after the tree update it depends on)
+  const u32* guard;
 };
 // For every key of keys (ascending, n_keys): lo[u] = the first row of s whose key is >=
 // keys[u] and len[u] = its rows, found by streaming s's key column in tiles (each tile's
@@ -179,10 +182,12 @@ hipError_t launch_splice_check(const u64* bkey, u64 nb, const u64* keys, u64 nk,
 // alone (in place: out is the state itself and no shift is nonzero)
 hipError_t launch_splice_index(SpliceArgs p, hipStream_t st);
 hipError_t launch_splice_copy(SpliceArgs p, bool e_only, hipStream_t st);
-// on[0, nc) = un, oc[0, nc) = uc; dirty[0, n_dirty) = 0; counts[0, 8) = 0 (if non-null);
+// on[0, nc) = un, oc[0, nc) = uc (skipped when `guard` is non-null and holds a
+// MERKLE_INPUT_ERR bit); dirty[0, n_dirty) = 0; counts[0, 8) = 0 (if non-null);
 // *err_word = 0 (if non-null): one launch instead of two copies and three fills
 hipError_t launch_splice_finish(const u32* un, const u64* uc, u64 nc, u32* on, u64* oc, u32* dirty,
-                                u64 n_dirty, u64* counts, u32* err_word, hipStream_t st);
+                                u64 n_dirty, u64* counts, u32* err_word, hipStream_t st,
+                                const u32* guard = nullptr);
 u64 splice_tiles(u64 n);  // state tiles of the copy (tile_u0 holds one more entry)
 
 // ---- mutate.hip (a batch of add/remove ops as one delta; see the file header)
@@ -255,6 +260,10 @@ struct MerkleT {
   TermH th;
 };
 constexpr u32 MERKLE_UPL = 11;  // levels reduced per upsweep workgroup
+// input-error bits a build / update leaves in its error word: a key outside the tree's
+// shard (2), a bucket over 65535 rows (4)
+constexpr u32 MERKLE_ERR_SHARD = 2u, MERKLE_ERR_COUNT = 4u;
+constexpr u32 MERKLE_INPUT_ERR = MERKLE_ERR_SHARD | MERKLE_ERR_COUNT;
 inline u64 merkle_chunks(u32 depth) { return 1ull << (depth - (depth < MERKLE_UPL ? depth : MERKLE_UPL)); }
 // scratch u32 words of a build / update: the arrival counter (16 words) + a u64 chunk
 // root and a u64 key count per chunk (the in-launch hand-off)
@@ -265,7 +274,10 @@ inline u64 merkle_ctr_words(u32 depth) { return 16 + 4 * merkle_chunks(depth); }
 hipError_t launch_merkle_build(const Rows& s, const MerkleT& t, u64* d_keys, u32* ctr, u32* err,
                                hipStream_t st);
 // put/delete of the changed keys + update_hashes; dirty: merkle_chunks(depth) u32, zero
-// on entry; d_keys[0, 8) (zero on entry) sum to the change in distinct keys.
+// on entry; d_keys[0, 8) (zero on entry) sum to the change in distinct keys.  The update
+// adds (new leaf - old leaf) and (new rows - old rows) per key, so the same launch with
+// olds and news exchanged undoes it bit for bit (keys outside the shard are skipped both
+// ways; counts wrap mod 2^32 and unwrap).
 hipError_t launch_merkle_update(const MerkleT& t, const Rows& olds, const Rows& news, const u64* keys,
                                 u64 n_keys, u32* dirty, u64* d_keys, u32* ctr, u32* err,
                                 hipStream_t st);

@@ -134,8 +134,7 @@ constexpr int UPB = 512;   // threads per chunk workgroup
 constexpr int UPL = MERKLE_UPL;  // levels reduced per workgroup (2048 nodes in LDS)
 constexpr u32 UPW = 1u << UPL;
 constexpr u32 NHL = 1024;  // node hashes staged in LDS by the build (more: read from global)
-constexpr u32 ERR_SHARD = 2u, ERR_COUNT = 4u;  // input-error bits: key outside the shard,
-                                               // a bucket over 65535 rows
+constexpr u32 ERR_SHARD = MERKLE_ERR_SHARD, ERR_COUNT = MERKLE_ERR_COUNT;  // input-error bits
 
 __device__ __forceinline__ void wait_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 

@@ -225,6 +225,7 @@ __device__ __forceinline__ void store_tile(const RowsOut& o, const TileRows& x, 
 __global__ __launch_bounds__(SB) void splice_erows_kernel(SpliceArgs p) {
   const u64 u = (u64)blockIdx.x * SB + threadIdx.x;
   if (u >= p.nk) return;
+  if (p.guard && (*p.guard & MERKLE_INPUT_ERR)) return;  // the tree update failed: no write
   const u64 j0 = (u64)(p.shift[u] + (i64)p.a_off[u]), j1 = (u64)(p.shift[u + 1] + (i64)p.a_off[u + 1]);
   const i64 g = p.gap[u];
   for (u64 j = j0; j < j1; j++) {
@@ -330,13 +331,15 @@ hipError_t launch_splice_copy(SpliceArgs p, bool e_only, hipStream_t st) {
   return hipGetLastError();
 }
 
-// dg_join_delta's epilogue set-up in one launch: the union context copied into the
-// state's, the tree update's dirty flags, key-count shards and input-error word zeroed
+// dg_join_delta's set-up and epilogue launches: the tree update's dirty flags, key-count
+// shards and input-error word zeroed; the union context copied into the state's (unless
+// the guard word reports a failed tree update)
 __global__ __launch_bounds__(SB) void splice_finish_kernel(const u32* un, const u64* uc, u64 nc,
                                                            u32* on, u64* oc, u32* dirty, u64 n_dirty,
-                                                           u64* counts, u32* err_word) {
+                                                           u64* counts, u32* err_word,
+                                                           const u32* guard) {
   const u64 i = (u64)blockIdx.x * SB + threadIdx.x;
-  if (i < nc) {
+  if (i < nc && !(guard && (*guard & MERKLE_INPUT_ERR))) {
     on[i] = un[i];
     oc[i] = uc[i];
   }
@@ -346,11 +349,12 @@ __global__ __launch_bounds__(SB) void splice_finish_kernel(const u32* un, const 
 }
 
 hipError_t launch_splice_finish(const u32* un, const u64* uc, u64 nc, u32* on, u64* oc, u32* dirty,
-                                u64 n_dirty, u64* counts, u32* err_word, hipStream_t st) {
+                                u64 n_dirty, u64* counts, u32* err_word, hipStream_t st,
+                                const u32* guard) {
   u64 n = nc > n_dirty ? nc : n_dirty;
   n = n > 8 ? n : 8;
   hipLaunchKernelGGL(splice_finish_kernel, dim3((unsigned)((n + SB - 1) / SB)), dim3(SB), 0, st, un,
-                     uc, nc, on, oc, dirty, n_dirty, counts, err_word);
+                     uc, nc, on, oc, dirty, n_dirty, counts, err_word, guard);
   return hipGetLastError();
 }
 

@@ -16,7 +16,7 @@ kind, the byte length and xxh64 of each column, and the exact interning tables o
 the state's Universe (keys, values and nodes as tagged terms), so `read` restores the
 same terms, ids and rows.  Columns are the raw SoA arrays (key, val, ts, node, cnt,
 ctx node, ctx cnt, and the Merkle tree's nodes and per-bucket row counts when one is
-persisted): 36 B per dot + 12 B per context entry + 8 B per tree node + 2 B per bucket,
+persisted; the header records whether the tree hashed terms or ids): 36 B per dot + 12 B per context entry + 8 B per tree node + 2 B per bucket,
 copied device -> host by one D2H copy each.  A persisted tree hashes terms (the
 Universe's term hashes, interning.py), so it is valid for the restored ids.  The header names the tree's depth and key-hash shard.  A checksum mismatch
 raises; the file is written to a temporary name, fsynced and renamed over the old one.
@@ -124,7 +124,8 @@ def _universe_from(tables) -> interning.Universe:
 def write_arrays(path, node_id, sequence_number: int, rows, ctx, universe, merkle=None) -> None:
     """The snapshot file from host arrays: rows = (key, val, ts, node, cnt) numpy columns,
     ctx = (kind, node, cnt), merkle = None or (depth, shard_bits, shard, nodes uint64,
-    counts uint16)."""
+    counts uint16[, terms]) -- `terms` (default True): the tree hashed the rows' terms
+    (the Universe's term hashes) rather than their ids; the reader restores it so."""
     cols = [np.ascontiguousarray(c, dt) for c, (_, dt) in zip(rows, _COLS)]
     cols += [np.ascontiguousarray(ctx[1], np.uint32), np.ascontiguousarray(ctx[2], np.uint64)]
     if merkle is not None:
@@ -137,7 +138,8 @@ def write_arrays(path, node_id, sequence_number: int, rows, ctx, universe, merkl
         "rows": int(len(cols[0])),
         "ctx_kind": int(ctx[0]),
         "ctx_n": int(len(cols[5])),
-        "merkle": None if merkle is None else [int(merkle[0]), int(merkle[1]), str(int(merkle[2]))],
+        "merkle": None if merkle is None else [int(merkle[0]), int(merkle[1]), str(int(merkle[2])),
+                                               bool(merkle[5]) if len(merkle) > 5 else True],
         "columns": [[len(b), xxhash.xxh64_intdigest(b)] for b in blobs],
         "universe": _universe_tables(universe),
     }
@@ -177,7 +179,9 @@ def read_arrays(path):
                 raise ValueError(f"{path}: column checksum mismatch")
             arrays.append(np.frombuffer(b, dtype=dt).copy())
     m = header.get("merkle")
-    merkle = None if m is None else (int(m[0]), int(m[1]), int(m[2]), arrays[7], arrays[8])
+    # the 4th entry: term-hashed tree (files without it hold term-hashed trees)
+    merkle = None if m is None else (int(m[0]), int(m[1]), int(m[2]), arrays[7], arrays[8],
+                                     bool(m[3]) if len(m) > 3 else True)
     return (_unpack(header["node_id"]), header["sequence_number"], tuple(arrays[:5]),
             (header["ctx_kind"], arrays[5], arrays[6]), _universe_from(header["universe"]), merkle)
 
@@ -189,7 +193,8 @@ def write(path, node_id, sequence_number: int, state, merkle_map=None) -> None:
     m = None
     if merkle_map is not None:
         m = (merkle_map.depth, merkle_map.shard_bits, merkle_map.shard,
-             merkle_map.nodes.cpu().numpy().view(np.uint64), merkle_map.bucket_counts())
+             merkle_map.nodes.cpu().numpy().view(np.uint64), merkle_map.bucket_counts(),
+             merkle_map.terms is not None)
     write_arrays(path, node_id, sequence_number, state.rows.to_numpy(),
                  (state.ctx.kind,) + tuple(state.ctx.to_numpy()), state.universe, m)
 
@@ -212,8 +217,10 @@ def read(path, device=None):
     if merkle is None:
         tree = None
     else:
-        depth, sb, shard, nodes, counts = merkle
-        tree = MerkleTree.empty(depth, dev, sb, shard, TermHashes.of(U, dev))
+        depth, sb, shard, nodes, counts, terms = merkle
+        # a tree over ids stays one: mixing term-hashed buckets into it after
+        # the next update would leave its nodes matching neither kind of rebuild
+        tree = MerkleTree.empty(depth, dev, sb, shard, TermHashes.of(U, dev) if terms else None)
         tree.nodes.copy_(torch.from_numpy(nodes.view(np.int64).copy()))
         tree.counts[: 1 << depth].copy_(torch.from_numpy(counts.view(np.int16).copy()))
         tree.store = st

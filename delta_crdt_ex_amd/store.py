@@ -8,6 +8,7 @@ include/deltagpu.h (u64 ids are reinterpreted, never compared in torch).
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 from dataclasses import dataclass
 
 import numpy as np
@@ -141,6 +142,9 @@ class TermHashes:
         self.nh, self.vid, self.vh = dev(node_hash), dev(val_id), dev(val_hash)
         self.c = _abi.dg_term_hashes(self.nh.data_ptr(), len(node_hash), self.vid.data_ptr(),
                                      self.vh.data_ptr(), len(val_id))
+        self.device = device
+        self._universe = None  # set by `of`: tables that follow a Universe
+        self.version = None
 
     @staticmethod
     def of(universe, device) -> "TermHashes":
@@ -149,8 +153,20 @@ class TermHashes:
         if cached is not None and cached[0] == universe.terms_version and cached[1] == str(device):
             return cached[2]
         th = TermHashes(*universe.term_tables(), device)
+        th._universe = weakref.ref(universe)
+        th.version = universe.terms_version
         universe._dev_terms = (universe.terms_version, str(device), th)
         return th
+
+    def current(self) -> "TermHashes":
+        """These tables, or their Universe's newer ones once it has interned new values or
+        nodes or relabelled: ids missing from stale tables would hash as
+        themselves, and the tree would stop matching a rebuild and a peer's tree.  Tables
+        made from explicit arrays follow nothing and are returned as they are."""
+        u = self._universe() if self._universe is not None else None
+        if u is None or u.terms_version == self.version:
+            return self
+        return TermHashes.of(u, self.device)
 
 
 @dataclass(eq=False)
@@ -180,6 +196,8 @@ class MerkleTree:
                           self.store, self.counts.clone(), self.terms)
 
     def abi(self) -> _abi.dg_merkle:
+        if self.terms is not None:  # follow the Universe's newest tables
+            self.terms = self.terms.current()
         t = _abi.dg_merkle()
         t.depth = self.depth
         t.shard_bits = self.shard_bits

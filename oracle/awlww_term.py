@@ -29,7 +29,7 @@ from __future__ import annotations
 import itertools
 from dataclasses import dataclass, field
 
-from .erlterm import term_sorted, sort_key
+from .erlterm import term_sorted, sort_key, tg
 
 
 class TieOrderUnpinned(Exception):
@@ -267,4 +267,35 @@ def causal_diff(old, new, keys):
             continue
         out.append(("remove", key) if n is None else ("add", key, n))
     return out
+
+
+def diffs_to_callback(old, new, keys):
+    """causal_crdt.ex:361-381: what the `on_diffs` subscriber receives for the keys diff/3
+    reported -- None when that list is empty (:361, the callback is not called), else per
+    key, in order, from read/2 of both states (:364-365):
+        {old, old} -> []              (exact match, `=:=`; nil/absent on both sides too)
+        {_old, nil} -> {:remove, key} (Map.get gives nil for an absent key AND a nil value)
+        {_old, new} -> {:add, key, new}
+    `None` stands for the atom nil."""
+    if len(keys) == 0:
+        return None
+    ro, rn = read(old, list(keys)), read(new, list(keys))
+    out = []
+    for key in keys:
+        o, n = ro.get(key), rn.get(key)
+        if tg(o) == tg(n):  # an absent key reads as None, i.e. as tg(nil)
+            continue
+        out.append(("remove", key) if tg(n) == _NIL else ("add", key, n))
+    return out
+
+
+_NIL = tg(None)
+
+
+def update_state_with_delta(state, delta, keys):
+    """causal_crdt.ex:383-404, the CRDT half: (joined state, what on_diffs receives):
+    join/3 (:384), diff/3 (:388), diffs_to_callback/3 over diffs_keys (:354-359,400)."""
+    new = join(state, delta, keys)
+    diffs = causal_diff(state, new, keys)
+    return new, diffs_to_callback(state, new, [d[1] for d in diffs])
 

@@ -1,17 +1,23 @@
 """dg_join2_changes on cuda:0: the join's rows and context equal
 dg_join2's, and its changed keys equal the C oracle's exact per-key row-set diff
 restricted to `keys` (ref.changed_keys; tests/test_configs.py pins that to the term
-oracle's diff/3 of causal_crdt.ex:343-351).  Plus delta_subscriber_test.exs:11-29
-restated through the CausalCrdt mirror."""
+oracle's diff/3 of causal_crdt.ex:343-351).  Plus delta_subscriber_test.exs:20-27
+restated step for step through the CausalCrdt mirror, and op histories with nil values
+against the oracle's diffs_to_callback/3."""
 import numpy as np
 import pytest
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as hst
 
 from delta_crdt_ex_amd import aw_lww_map as M
 from delta_crdt_ex_amd import causal_crdt as CC
 from delta_crdt_ex_amd import workloads as W
 from delta_crdt_ex_amd.store import u64
+from delta_crdt_ex_amd.terms import Atom
 from kfold_cases import random_fold
+from oracle import awlww_term as T
 from oracle import ref as R
+from oracle.erlterm import tg
 from test_gpu_configs import keys_dev
 from test_gpu_parity import ctx_eq, rows_eq, up
 
@@ -77,19 +83,56 @@ def test_changes_large_properties(engine):
 
 
 def test_delta_subscriber_scenario():
-    """delta_subscriber_test.exs:11-29: the first add reports {:add, k, v}; adding the
-    same value again changes the key's dots but not its value, so no {:add}; removing it
-    reports {:remove, k}."""
+    """delta_subscriber_test.exs:20-27 step for step: the first add reports {:add, k, v};
+    adding the same value again changes the key's dots but not its value, so on_diffs
+    receives []; `add "Derek" nil` reports {:remove, "Derek"} (H9: Map.get of a nil value
+    is nil); removing the nil value then reports [] ({nil, nil} matches {old, old})."""
     st = M.compress_dots(M.new())
     st, diffs = CC.update_state_with_delta(st, M.add("Derek", "Kraan", 1, st), ["Derek"])
     assert diffs == [("add", "Derek", "Kraan")]
     st, diffs = CC.update_state_with_delta(st, M.add("Derek", "Kraan", 1, st), ["Derek"])
     assert diffs == []
-    st, diffs = CC.update_state_with_delta(st, M.remove("Derek", 1, st), ["Derek"])
+    st, diffs = CC.update_state_with_delta(st, M.add("Derek", None, 1, st), ["Derek"])
     assert diffs == [("remove", "Derek")]
+    assert M.read(st) == {"Derek": None}
+    st, diffs = CC.update_state_with_delta(st, M.remove("Derek", 1, st), ["Derek"])
+    assert diffs == []
+    # removing an absent key changes no raw value map: on_diffs is not called
+    st, diffs = CC.update_state_with_delta(st, M.remove("Derek", 1, st), ["Derek"])
+    assert diffs is None
     # a key the delta does not touch: no diff at all
     st, diffs = CC.update_state_with_delta(st, M.add("Other", 1, 1, st), ["Nope"])
     assert diffs is None
+
+
+_VALS = [None, 0, 1, 1.0, -0.0, True, Atom("nil_not"), "Kraan", b"x", (1, None)]
+
+
+@settings(max_examples=40, deadline=None, suppress_health_check=list(HealthCheck))
+@given(hst.lists(hst.tuples(hst.sampled_from(["add", "remove"]), hst.integers(0, 3),
+                            hst.integers(0, len(_VALS) - 1), hst.integers(0, 2)),
+                 min_size=1, max_size=14))
+def test_on_diffs_histories_match_oracle(ops):
+    """Op histories with nil values (and 1 / 1.0 / true, which BEAM keeps apart) through
+    the mirror's update_state_with_delta equal the term oracle's diffs_to_callback
+    (causal_crdt.ex:361-404) call for call."""
+    st = M.compress_dots(M.new())
+    ref = T.compress_dots(T.new())
+    t = 1000
+    for op, k, v, node in ops:
+        key, val = f"k{k}", _VALS[v]
+        t += 1
+        if op == "add":
+            d, rd = M.add(key, val, node, st, ts=t), T.add(tg(key), tg(val), node, ref, t)
+        else:
+            d, rd = M.remove(key, node, st), T.remove(tg(key), node, ref)
+        st, got = CC.update_state_with_delta(st, d, [key])
+        ref, want = T.update_state_with_delta(ref, rd, [tg(key)])
+        norm = None if got is None else [tuple(tg(x) for x in g) for g in got]
+        wnorm = None if want is None else [tuple(tg(x) if i else x for i, x in enumerate(w))
+                                           for w in want]
+        assert norm == wnorm, (op, key, val)
+    assert {tg(k): tg(v) for k, v in M.read(st).items()} == T.read(ref)
 
 
 def test_changes_sparse_keyed_multichunk(engine):

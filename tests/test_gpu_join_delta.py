@@ -117,3 +117,203 @@ def test_join_delta_edges(engine):
     # an empty state receiving a sync delta
     none = {"rows": tuple(c[:0] for c in a["rows"]), "ctx": a["ctx"]}
     apply(engine, none, W.sync_delta(b, kb[::20]), kb[::20], with_tree=False)
+
+
+# ---------------------------------------------------------------- local mutations
+# handle_operation (causal_crdt.ex:337-342): every mutate is a one-key delta whose context
+# is a MapSet (aw_lww_map.ex:124-146), joined into the replica's VV state with keys = [key]
+# through update_state_with_delta (:383-404) -- the path INTEGRATION.md routes to
+# dg_join_delta on a GPU-attached state.
+
+def _mutation_state(n_keys=20_000, seed=31):
+    rng = np.random.default_rng(seed)
+    a, _ = W.random_pair(rng, n_keys, n_nodes=4, max_entries=2)
+    return a, rng
+
+
+@pytest.mark.parametrize("case", ["update", "new_key", "remove", "remove_absent", "nil_value",
+                                  "same_value"])
+def test_one_key_mutation_delta(engine, case):
+    """A one-key add/remove delta with a dot-set context into a VV state: rows, context,
+    changed keys and the tree against the C oracle and a fresh build.  `update` keeps the
+    key's row count (in place when the key held one row), `new_key` and `remove` move rows
+    (through the spare store), `remove_absent` changes nothing."""
+    a, rng = _mutation_state()
+    keys = np.unique(a["rows"][0])
+    counts = np.bincount(np.searchsorted(keys, a["rows"][0]), minlength=len(keys))
+    one = keys[counts == 1]
+    node = int(a["ctx"][1][0])
+    nil_id = (1 << 63) - 12345  # the interned id of :nil (any value id; the join never reads it)
+    if case == "update":
+        ops = [("add", int(one[17]), 424242, 10 ** 12)]
+    elif case == "same_value":
+        k = int(one[3])
+        v = int(a["rows"][1][np.searchsorted(a["rows"][0], k)])
+        ops = [("add", k, v, 10 ** 12)]
+    elif case == "nil_value":
+        ops = [("add", int(one[5]), nil_id, 10 ** 12)]
+    elif case == "new_key":
+        k = int(keys[100]) + 1
+        assert k not in set(keys.tolist())
+        ops = [("add", k, 7, 10 ** 12)]
+    elif case == "remove":
+        ops = [("remove", int(keys[len(keys) // 2]), 0, 0)]
+    else:
+        ops = [("remove", int(keys[200]) + 1, 0, 0)]
+    drows, dctx, dkeys = R.mutate_batch(a["rows"], a["ctx"], node, ops)
+    d = {"rows": drows, "ctx": dctx}
+    st, sc, swapped, wr = apply(engine, a, d, dkeys, depth=12)
+    assert swapped == (case in ("new_key", "remove"))
+    assert sc.kind == 0  # map ⊔ MapSet folds the dots into the VV (aw_lww_map.ex:45-52)
+
+
+def test_mutation_sequence_matches_the_oracle(engine):
+    """200 mutations in a row (adds of new and existing keys, removes, re-adds), each its
+    own dg_join_delta on one resident state + tree, against the oracle's fold."""
+    a, rng = _mutation_state(n_keys=30_000, seed=32)
+    st, sc = state_of(a, extra_ctx=4)
+    spare = Store.empty(st.n + 8, DEV)
+    tree = engine.merkle_build(st, 12)
+    rows, ctx = a["rows"], a["ctx"]
+    node = int(ctx[1][1])
+    keys = np.unique(rows[0])
+    for i in range(200):
+        r = rng.random()
+        if r < 0.4:
+            op = ("add", int(rng.choice(keys)), int(rng.integers(1 << 40)), 10 ** 12 + i)
+        elif r < 0.7:
+            op = ("add", int(rng.integers(1 << 63)) | 1, int(rng.integers(1 << 40)), 10 ** 12 + i)
+        else:
+            op = ("remove", int(rng.choice(keys)), 0, 0)
+        drows, dctx, dkeys = R.mutate_batch(rows, ctx, node, [op])
+        sd, cd = up({"rows": drows, "ctx": dctx})
+        if spare.cap < st.n + sd.n:
+            spare = Store.empty(st.n + sd.n + 64, DEV)
+        changed, _ = engine.join_delta(st, sc, sd, cd, kdev(dkeys), spare, tree)
+        wr, wc = R.join2(rows, ctx, drows, dctx, keys=dkeys)
+        assert np.array_equal(u64(changed), R.changed_keys(rows, wr, dkeys))
+        rows, ctx = wr, wc
+    rows_eq(st, rows)
+    ctx_eq(sc, ctx)
+    fresh = engine.merkle_build(st, 12)
+    assert np.array_equal(tree.nodes.cpu().numpy(), fresh.nodes.cpu().numpy())
+    assert tree.n_keys == fresh.n_keys
+
+
+# ---------------------------------------------------------------- all or nothing (ADVICE r3)
+
+def _snapshot(st, sc, tree):
+    return ([c.copy() for c in st.to_numpy()], [c.copy() for c in sc.to_numpy()], sc.kind,
+            tree.nodes.cpu().numpy().copy(), tree.bucket_counts().copy(), tree.n_keys)
+
+
+def _assert_unchanged(st, sc, tree, snap):
+    rows, ctx, kind, nodes, counts, nk = snap
+    for x, y in zip(st.to_numpy(), rows):
+        assert np.array_equal(x, y)
+    for x, y in zip(sc.to_numpy(), ctx):
+        assert np.array_equal(x, y)
+    assert sc.kind == kind
+    assert np.array_equal(tree.nodes.cpu().numpy(), nodes)
+    assert np.array_equal(tree.bucket_counts(), counts)
+    assert tree.n_keys == nk
+
+
+def _rows(keys, node, cnt0):
+    n = len(keys)
+    return (np.asarray(keys, np.uint64), np.arange(n, dtype=np.uint64) + 5, np.full(n, 1, np.int64),
+            np.full(n, node, np.uint32), np.arange(n, dtype=np.uint64) + cnt0)
+
+
+def test_failed_tree_update_leaves_the_state_alone(engine):
+    """A delta whose joined rows overflow a bucket's 16-bit row count (depth-1 tree,
+    65530 rows in bucket 0, 10 new keys there): DG_E_CAPACITY, and the state's rows,
+    context and tree are exactly what they were (the moved path: rows go to the spare)."""
+    from delta_crdt_ex_amd._abi import CapacityError
+    rng = np.random.default_rng(5)
+    keys = np.unique(rng.integers(0, 1 << 63, 65540, dtype=np.uint64))
+    low, extra = keys[:65530], keys[65530:65540]
+    a = {"rows": _rows(low, 0, 1), "ctx": (0, np.array([0], np.uint32), np.array([65530], np.uint64))}
+    d = {"rows": _rows(extra, 1, 1), "ctx": (0, np.array([1], np.uint32), np.array([10], np.uint64))}
+    st, sc = state_of(a, extra_ctx=1)
+    sd, cd = up(d)
+    spare = Store.empty(st.n + sd.n, DEV)
+    tree = engine.merkle_build(st, 1)
+    snap = _snapshot(st, sc, tree)
+    with pytest.raises(CapacityError, match="65535"):
+        engine.join_delta(st, sc, sd, cd, kdev(extra), spare, tree)
+    _assert_unchanged(st, sc, tree, snap)
+    # the engine is usable afterwards: a deeper tree takes the same delta
+    apply(engine, a, d, extra, depth=8)
+
+
+def test_failed_tree_update_full_join_path(engine):
+    """A keyset key outside the tree's key-hash shard changes (DG_E_INVAL), on the path of
+    a delta with a key outside its keyset (the full join into the spare store)."""
+    from delta_crdt_ex_amd._abi import DeltaGpuError
+    rng = np.random.default_rng(6)
+    low = np.unique(rng.integers(0, 1 << 63, 5000, dtype=np.uint64))      # shard 0 of 2
+    out_key = np.array([(1 << 63) + 77], np.uint64)                        # shard 1
+    stray = np.array([int(low[10]) + 1], np.uint64)                        # outside the keyset
+    dk = np.sort(np.concatenate([out_key, stray]))
+    a = {"rows": _rows(low, 0, 1), "ctx": (0, np.array([0], np.uint32), np.array([5000], np.uint64))}
+    d = {"rows": _rows(dk, 1, 1), "ctx": (0, np.array([1], np.uint32), np.array([2], np.uint64))}
+    st, sc = state_of(a, extra_ctx=1)
+    sd, cd = up(d)
+    spare = Store.empty(st.n + sd.n, DEV)
+    tree = engine.merkle_build(st, 8, shard_bits=1, shard=0)
+    snap = _snapshot(st, sc, tree)
+    with pytest.raises(DeltaGpuError, match="shard"):
+        engine.join_delta(st, sc, sd, cd, kdev(out_key), spare, tree)
+    _assert_unchanged(st, sc, tree, snap)
+
+
+def test_failed_tree_update_in_place_path(engine):
+    """The in-place path: a key outside the tree's shard keeps its row count but changes
+    (the tree was built over the shard's rows only); E's rows and the context are written
+    by kernels that see the failed update and skip, so nothing changes."""
+    from delta_crdt_ex_amd._abi import DeltaGpuError
+    rng = np.random.default_rng(7)
+    low = np.unique(rng.integers(0, 1 << 63, 5000, dtype=np.uint64))
+    x = np.array([(1 << 63) + 99], np.uint64)
+    allk = np.concatenate([low, x])
+    a = {"rows": _rows(allk, 0, 1), "ctx": (0, np.array([0], np.uint32), np.array([5001], np.uint64))}
+    inside = {"rows": tuple(c[:-1] for c in a["rows"]), "ctx": a["ctx"]}
+    d = {"rows": (x, np.array([999], np.uint64), np.array([2], np.int64), np.array([1], np.uint32),
+                  np.array([1], np.uint64)),
+         "ctx": (0, np.array([0, 1], np.uint32), np.array([5001, 1], np.uint64))}
+    st, sc = state_of(a, extra_ctx=2)
+    sd, cd = up(d)
+    spare = Store.empty(st.n + sd.n, DEV)
+    si, _ = up(inside)
+    tree = engine.merkle_build(si, 8, shard_bits=1, shard=0)
+    snap = _snapshot(st, sc, tree)
+    with pytest.raises(DeltaGpuError, match="shard"):
+        engine.join_delta(st, sc, sd, cd, kdev(x), spare, tree)
+    _assert_unchanged(st, sc, tree, snap)
+
+
+def test_join_delta_retries_an_aborted_grid(monkeypatch):
+    """the splice's edit join on an over-sized persistent grid
+    (DG_JOIN_WORKERS=1024, 512 fit) aborts; dg_join_delta re-runs the edit on a small grid
+    (nothing of the state is written before) and ends equal to a co-resident engine."""
+    from delta_crdt_ex_amd.store import Engine
+    a, b = W.config4_shard(1, 8, keys_per_rank=5_000_000, diff_frac=0.06)
+    want = R.store_diff(a["rows"], b["rows"])
+    d = W.sync_delta(b, want)
+    results = []
+    for workers in (None, "1024"):
+        if workers:
+            monkeypatch.setenv("DG_JOIN_WORKERS", workers)
+        eng = Engine(0)
+        st, sc = state_of(a, extra_ctx=8)
+        sd, cd = up(d)
+        spare = Store.empty(st.n + sd.n, DEV)
+        tree = eng.merkle_build(st, 16)
+        changed, _ = eng.join_delta(st, sc, sd, cd, kdev(want), spare, tree)
+        results.append(([c.copy() for c in st.to_numpy()], u64(changed).copy(), tree.root()))
+        eng.close()
+    (r0, c0, t0), (r1, c1, t1) = results
+    assert len(c0) > 200_000 and np.array_equal(c0, c1) and t0 == t1
+    for x, y in zip(r0, r1):
+        assert np.array_equal(x, y)

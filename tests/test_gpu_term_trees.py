@@ -105,3 +105,27 @@ def test_tree_survives_a_relabel(M):
     # equal as Erlang terms (the Universe holds "a" as the binary b"a": tg normalises)
     from oracle.erlterm import tg
     assert {k: tg(v) for k, v in T.read(A).items()} == {k: tg(v) for k, v in M.read(st).items()}
+
+
+def test_tree_follows_new_terms_after_build(M):
+    """a tree built, then values and a node interned (new terms the tree's
+    tables lack), then updated through Engine.merkle_update: the update picks up the
+    Universe's current tables, so the tree equals a fresh build and the C oracle's."""
+    from oracle.erlterm import tg
+    A = G.history(230, Universe(), values=G.TERM_VALUES)[0]
+    U = _shuffled_universe(A, 4)
+    st = M.from_terms(A.value, A.dots, U)
+    tree = M.merkle_map(st, 9)
+    v0 = U.terms_version
+    nxt = st
+    for i, (k, v) in enumerate([("fresh-1", ("a", "tuple", 1)), ("fresh-2", b"\x01new"),
+                                 (next(iter(A.value)), 3.75)]):
+        nxt = M.join(nxt, M.add(k, v, ("a new node", i), nxt, ts=10 ** 15 + i), [k])
+    assert U.terms_version != v0  # the build's tables are stale now
+    changed = M.engine().join2_changes(st.rows, st.ctx, nxt.rows, nxt.ctx)[2]
+    M.engine().merkle_update(tree, nxt.rows, changed)
+    fresh = M.merkle_map(nxt, 9)
+    assert np.array_equal(tree.nodes.cpu().numpy(), fresh.nodes.cpu().numpy())
+    r = R.merkle_build(nxt.rows.to_numpy(), 9, terms=R.Terms(*U.term_tables()))
+    assert np.array_equal(tree.nodes.cpu().numpy().view(np.uint64), r.nodes)
+    assert {tg(k): tg(v) for k, v in M.read(nxt).items()}[tg("fresh-2")] == tg(b"\x01new")

@@ -295,3 +295,76 @@ def test_random_histories_converge(steps):
     reads = [x.read() for x in reps]
     assert reads[0] == reads[1] == reads[2]
     assert T.canon(reps[0].state)[1] == T.canon(reps[1].state)[1] == T.canon(reps[2].state)[1]
+
+
+# ------------------------------------------------------------- on_diffs (delta_subscriber_test.exs)
+
+class Subscribed(Replica):
+    """A replica whose mutations go through update_state_with_delta/3 and collect what
+    its on_diffs subscriber receives (causal_crdt.ex:337-342,361-404)."""
+
+    def __init__(self, node, clock):
+        super().__init__(node, clock)
+        self.received = []  # each on_diffs call's list (None calls are not made)
+
+    def apply(self, delta, keys):
+        self.state, got = T.update_state_with_delta(self.state, delta, keys)
+        if got is not None:
+            self.received.append(got)
+        return got
+
+    def mutate(self, f, *args):
+        key = args[0]
+        if f == "add":
+            delta = T.add(key, args[1], self.node, self.state, self.clock())
+        else:
+            delta = T.remove(key, self.node, self.state)
+        return self.apply(delta, [key])
+
+
+def test_subscriber_receives_diffs():  # delta_subscriber_test.exs:11-28 (and :30-47)
+    r = Subscribed(1, Clock())
+    assert r.mutate("add", "Derek", "Kraan") == [("add", "Derek", "Kraan")]
+    # the same value again: the raw map changed (fresh dot and ts), the read did not
+    assert r.mutate("add", "Derek", "Kraan") == []
+    # add k nil reports {:remove, k} (:26-27): Map.get of a nil value is nil
+    assert r.mutate("add", "Derek", None) == [("remove", "Derek")]
+    # and removing the nil value reports nothing: {nil, nil} matches {old, old}
+    assert r.mutate("remove", "Derek") == []
+    # removing an absent key changes no raw map: the callback is not called
+    assert r.mutate("remove", "Derek") is None
+
+
+def test_subscriber_updates_are_bundled():  # delta_subscriber_test.exs:49-77
+    c = Clock()
+    c1, c2 = Replica(1, c), Subscribed(2, c)
+    for k in ("Derek", "Andrew", "Nathan"):
+        c1.mutate("add", k, "Kraan")
+    keys = diff_keys(c1.state, c2.state)
+    delta = T.AW(c1.state.dots, {k: c1.state.value[k] for k in keys if k in c1.state.value})
+    got = c2.apply(delta, keys)
+    assert {k: v for _, k, v in got} == {"Derek": "Kraan", "Andrew": "Kraan", "Nathan": "Kraan"}
+
+
+def _replay(received):
+    m = {}
+    for diffs in received:
+        for d in diffs:
+            if d[0] == "add":
+                m[d[1]] = d[2]
+            else:
+                m.pop(d[1], None)
+    return m
+
+
+@settings(max_examples=150, deadline=None)
+@given(st.lists(st.tuples(st.sampled_from(["add", "remove"]), terms(), terms()), max_size=25))
+def test_property_diff_stream_replays_to_the_model(ops):  # delta_subscriber_test.exs:79-117
+    """The on_diffs stream, replayed into a map, equals Map.put/Map.delete over the ops
+    -- with nil values dropped, since an add of nil is reported as a remove."""
+    r = Subscribed(1, Clock())
+    for op, key, val in ops:
+        r.mutate(op, key, val)
+    want = {k: v for k, v in model([(o, k, v, None) for o, k, v in ops]).items()
+            if v != tg(None)}
+    assert _replay(r.received) == want

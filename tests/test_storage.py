@@ -61,8 +61,8 @@ def test_golden_snapshot_matches_the_oracle():
     ok, ov = R.read_lww(rows)
     got = {U.key_term(int(k)): U.value_term(int(v)) for k, v in zip(ok, ov)}
     assert {k: repr(v) for k, v in got.items()} == {k: repr(v) for k, v in T.read(A).items()}
-    depth, sb, shard, nodes, counts = merkle
-    assert (depth, sb, shard) == (6, 0, 0)
+    depth, sb, shard, nodes, counts, terms = merkle
+    assert (depth, sb, shard, terms) == (6, 0, 0, True)
     want = R.merkle_build(rows, 6, terms=R.Terms(*U.term_tables()))  # a tree over terms
     assert np.array_equal(nodes, want.nodes) and np.array_equal(counts, want.counts)
 
@@ -86,6 +86,22 @@ def test_snapshot_write_is_atomic(tmp_path):
     assert storage.read_arrays(p)[1] == 1
     storage.write_arrays(p, 1, 2, rows, (0, np.zeros(0, np.uint32), np.zeros(0, np.uint64)), U)
     assert storage.read_arrays(p)[1] == 2 and not (tmp_path / "r.dgsnap.tmp").exists()
+
+
+def test_snapshot_records_the_tree_kind(tmp_path):
+    """the header says whether the persisted tree hashed terms or ids, and the
+    reader restores that kind (a tree over ids must not come back term-hashed)."""
+    U = interning.Universe()
+    rows = tuple(np.zeros(0, dt) for dt in (np.uint64, np.uint64, np.int64, np.uint32, np.uint64))
+    ctx = (0, np.zeros(0, np.uint32), np.zeros(0, np.uint64))
+    nodes, counts = np.zeros(7, np.uint64), np.zeros(4, np.uint16)
+    for terms in (True, False):
+        p = tmp_path / f"t{terms}.dgsnap"
+        storage.write_arrays(p, 1, 1, rows, ctx, U, (2, 0, 0, nodes, counts, terms))
+        assert storage.read_arrays(p)[5][5] is terms
+    # a 5-tuple (no flag) is a term-hashed tree, as every earlier DGSNAP02 file is
+    storage.write_arrays(tmp_path / "d.dgsnap", 1, 1, rows, ctx, U, (2, 0, 0, nodes, counts))
+    assert storage.read_arrays(tmp_path / "d.dgsnap")[5][5] is True
 
 
 @pytest.mark.gpu
@@ -135,3 +151,22 @@ def test_snapshot_round_trip(tmp_path):
     with pytest.raises(ValueError, match="checksum"):
         storage.read(p)
     assert storage.read(tmp_path / "absent") is None
+
+
+@pytest.mark.gpu
+def test_snapshot_keeps_an_id_tree(tmp_path):
+    """A tree built over ids (terms=None) comes back as one: after an update it still
+    equals a fresh id-hashed build of the new rows."""
+    from delta_crdt_ex_amd import aw_lww_map as M
+    st = M.compress_dots(M.new())
+    for i in range(40):
+        st = M.join(st, M.add(i, f"v{i}", 1, st, ts=10 + i), [i])
+    tree = M.engine().merkle_build(st.rows, 6)  # terms=None: ids
+    p = tmp_path / "ids.dgsnap"
+    storage.write(p, 1, 1, st, tree)
+    _, _, back, bt = storage.read(p)
+    assert bt.terms is None and bt.root() == tree.root()
+    nxt = M.join(back, M.add(3, "new value", 1, back, ts=99), [3])
+    changed = M.engine().join2_changes(back.rows, back.ctx, nxt.rows, nxt.ctx)[2]
+    M.engine().merkle_update(bt, nxt.rows, changed)
+    assert bt.root() == M.engine().merkle_build(nxt.rows, 6).root()
