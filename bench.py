@@ -202,6 +202,11 @@ def config4_round(eng, torch, dev, rank=0, world=1, keys_per_rank=12_500_000, st
     one_round()
     rounds = [one_round() for _ in range(5)]
     resident = resident_delta(eng, torch, sa, ca, cb, ta, tb, b)
+    partial = {"max_sync_size_200": partial_round(eng, torch, ta, tb, max_sync_size=200),
+               "infinite": partial_round(eng, torch, ta, tb, max_sync_size=None, reps=3),
+               "note": "prepare on A, continue on B, A, B, A ...: the message exchange of "
+                       "causal_crdt.ex:91-110,252-270 with both replicas on this GPU (between "
+                       "BEAM nodes each hop is one message); synchronous calls, wall time"}
     med = {k: float(np.median([r[k] for r in rounds]))
            for k in ("diff", "take", "join", "update", "total", "diff_ev")}
     last = rounds[-1]
@@ -233,6 +238,7 @@ def config4_round(eng, torch, dev, rank=0, world=1, keys_per_rank=12_500_000, st
         "round_delta_rows": last["rows"], "round_changed_keys": last["changed"],
         "update_equals_rebuild": all(r["ok"] for r in rounds),
         "resident_delta": resident,
+        "partial": partial,
         "round_note": "synchronous calls: merkle_diff -> take_keys -> join2_changes (keyed) -> "
                       "merkle_update (incremental put/delete + update_hashes of the changed keys)",
     }
@@ -243,6 +249,58 @@ def config4_round(eng, torch, dev, rank=0, world=1, keys_per_rank=12_500_000, st
         res["collectives_us"] = (time.perf_counter() - t0) * 1e6
         res["replica_root"] = hex(root_a)
     return res, (2 * n_keys, 2 * build_us * 1e-6 + med["diff"])
+
+
+def partial_round(eng, torch, ta, tb, levels=8, max_sync_size=200, reps=5):
+    """CausalCrdt's anti-entropy message exchange as the reference runs it between two
+    replicas that never hold each other's tree (causal_crdt.ex:91-110,252-270): the
+    originator's prepare_partial_diff(mm, 8), then continue_partial_diff(cont, mm, 8)
+    ping-pong, every {:continue, c} truncated to max_sync_size (default 200,
+    delta_crdt.ex:32) before it is sent, until {:ok, keys} (truncated too, :105).  Per hop:
+    wall time of the synchronous calls (continue + truncate) and the message the hop sends
+    -- node form 16 B per entry (position, hash), leaf form 8 B per bucket + 16 B per
+    (key, leaf) pair; keys 8 B each.  Median over reps."""
+    hops_all = []
+    for _ in range(reps + 1):
+        hops = []
+        t0 = time.perf_counter()
+        cont = eng.merkle_prepare(ta, levels)
+        hops.append({"call": "prepare", "us": (time.perf_counter() - t0) * 1e6, "level": cont.level,
+                     "entries": cont.n, "bytes": 16 * cont.n})
+        side = (tb, ta)
+        i = 0
+        while True:
+            t = side[i % 2]
+            t0 = time.perf_counter()
+            res = eng.merkle_continue(t, cont, levels)
+            if res[0] == "ok":
+                keys = res[1][:max_sync_size] if max_sync_size else res[1]
+                torch.cuda.synchronize()
+                hops.append({"call": "continue -> ok", "us": (time.perf_counter() - t0) * 1e6,
+                             "keys": int(keys.numel()), "total_keys": int(res[2]),
+                             "bytes": 8 * int(keys.numel())})
+                break
+            cont = res[1]
+            if max_sync_size:
+                eng.merkle_truncate(t, cont, max_sync_size)
+            el = (time.perf_counter() - t0) * 1e6
+            h = {"call": "continue", "us": el, "level": cont.level, "entries": cont.n}
+            if cont.leaf:
+                h.update(buckets=cont.n_buckets, bytes=8 * cont.n_buckets + 16 * cont.n)
+            else:
+                h["bytes"] = 16 * cont.n
+            hops.append(h)
+            i += 1
+        hops_all.append(hops)
+    hops_all = hops_all[1:]
+    out = []
+    for j, h in enumerate(hops_all[0]):
+        h = dict(h)
+        h["us"] = float(np.median([hs[j]["us"] for hs in hops_all]))
+        out.append(h)
+    return {"max_sync_size": max_sync_size if max_sync_size else "infinite", "levels": levels,
+            "hops": out, "total_us": sum(h["us"] for h in out),
+            "total_bytes": sum(h["bytes"] for h in out)}
 
 
 def resident_delta(eng, torch, sa, ca, cb, ta, tb, b, reps=7):
@@ -563,6 +621,44 @@ def read_runs_rate(eng, torch, dev, n_keys=1_000_000, max_entries=32, reps=5):
             "note": "dg_read_lww synchronous (three launches + one count readback)"}
 
 
+MUTATE_EXE = os.path.join(ROOT, "c_src", "_build", "bench_mutate")
+
+
+def _run_json(cmd, timeout=300):
+    import subprocess
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+    if r.returncode != 0:
+        raise RuntimeError(f"{cmd[0]} failed ({r.returncode}): {r.stderr[-2000:]}")
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def mutate_rate(sizes=(1000, 10_000), reps=300):
+    """The reference's own benchmark shape (bench/basic_operations.exs:25-41): per-op
+    latency of read / add / update / remove on replicas of 1k and 10k keys, each mutation
+    a one-key delta with a MapSet context joined into the GPU-resident state through
+    dg_join_delta (H2D of the delta, the join + changed keys + MerkleMap update, D2H of the
+    changed keys' rows), timed from C over the C-ABI (c_src/bench_mutate.c: no Python in
+    the loop -- what a NIF pays).  `batch_us_per_op`: the trace workload (1000 adds of new
+    keys, :9-23) as ONE delta through one dg_join_delta."""
+    if not os.path.exists(MUTATE_EXE):
+        raise RuntimeError(f"{MUTATE_EXE} is missing: built by __graft_entry__.build()")
+    out = {"metric": "per-op latency of a local mutation on a GPU-resident replica "
+                     "(basic_operations.exs shape), microseconds, median",
+           "unit": "us"}
+    for n in sizes:
+        out[f"keys_{n}"] = _run_json([MUTATE_EXE, str(n), str(reps)])
+    return out
+
+
+def mutate_cpu_baseline(sizes=(1000, 10_000), reps=300):
+    """The same ops on the C restatement (oracle/deltaref.c ref_join2 + ref_store_diff per
+    op on host rows, one thread; c_src/bench_mutate.c built with -DDG_REF)."""
+    exe = MUTATE_EXE + "_ref"
+    if not os.path.exists(exe):
+        return None
+    return {f"keys_{n}": _run_json([exe, str(n), str(reps)]) for n in sizes}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -759,10 +855,13 @@ def main():
         secondaries["config5"] = aggregate(*config5_rate(eng, torch, dev, rank, world))
         if world == 1:
             secondaries["read_runs32"] = read_runs_rate(eng, torch, dev)
+            secondaries["mutate"] = mutate_rate()
     if rank == 0:
         res.update(secondaries)
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(a, b)
+            if not args.no_configs:
+                res["cpu_baseline"]["mutate"] = mutate_cpu_baseline()
         elif not args.no_cpu_baseline:
             res["cpu_baseline"] = None
         print(json.dumps(res), flush=True)

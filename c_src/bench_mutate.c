@@ -1,0 +1,467 @@
+/*
+ * bench_mutate.c — per-operation latency of a local mutation applied to a device-resident
+ * replica state through the C-ABI, the shape of the reference's own benchmark
+ * (bench/basic_operations.exs:25-41): a replica set up with `n` adds of key x -> x
+ * (1..n, one mutate each, so node 0's counter ends at n), then
+ *   read    DeltaCrdt.read(crdt)                  read/1 of every key (dg_read_lww + D2H)
+ *   add     mutate(crdt, :add, ["key4", "value"])  a new key              (rows move)
+ *   update  mutate(crdt, :add, [10, 12])           key 10: one row -> one (in place)
+ *   remove  mutate(crdt, :remove, [10])            key 10's row removed   (rows move)
+ * with the reference's before_each (add [10, 10], remove ["key4"]) before every op.
+ *
+ * A mutation is handle_operation (causal_crdt.ex:337-342): AWLWWMap.add/remove builds a
+ * one-key delta with a MapSet context (aw_lww_map.ex:99-146) from the replica's terms,
+ * and update_state_with_delta (:383-404) joins it with keys = [key].  The delta is built
+ * on the host here, as the Elixir side builds it from its own `value` map (INTEGRATION.md
+ * §3), and one op costs what a NIF's join_delta costs on a GPU-attached state:
+ *   h2d   the delta (rows, dot-list context, keyset) as ONE packed copy into the
+ *         state's scratch (no allocation per op)
+ *   join  dg_join_delta: the keyed join in place or through the spare store, the changed
+ *         keys, the MerkleMap put/delete (the state's tree)
+ *   d2h   the changed keys' rows (dg_take_keys) and the keys, back for on_diffs
+ * Also `batch`: the reference's trace workload (1000 x mutate(:add, ["key#{x}", "value"]),
+ * :9-23) as ONE delta through one dg_join_delta -- how mutate_async batches amortize.
+ *
+ * Built twice from this file: bench_mutate (the GPU path, links libdeltagpu) and, with
+ * -DDG_REF, bench_mutate_ref (the CPU restatement's keyed join per op, oracle/deltaref.c
+ * ref_join2 on host rows -- bench.py's cpu_baseline leg only).  Prints one JSON line.
+ *     bench_mutate N_KEYS [REPS]
+ */
+#define _POSIX_C_SOURCE 200809L
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "marshal.h"
+
+#ifdef DG_REF
+int ref_join2(const dg_store* a, const dg_context* ca, const dg_store* b, const dg_context* cb,
+              const uint64_t* keys, uint64_t n_keys, dg_store* out, dg_context* out_ctx);
+int ref_read_lww(const dg_store* s, const uint64_t* keys, uint64_t n_keys, uint64_t* out_key,
+                 uint64_t* out_val, uint64_t cap, uint64_t* n_out);
+int ref_store_diff(const dg_store* a, const dg_store* b, uint64_t* out, uint64_t cap, uint64_t* n);
+#endif
+
+#define DG(x)                                                                          \
+  do {                                                                                 \
+    int rc_ = (x);                                                                     \
+    if (rc_ != DG_OK) {                                                                \
+      fprintf(stderr, "FAIL %s:%d: %s -> %d (%s)\n", __FILE__, __LINE__, #x, rc_,        \
+              dg_last_error());                                                        \
+      exit(1);                                                                         \
+    }                                                                                  \
+  } while (0)
+
+static double now_us(void) {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return t.tv_sec * 1e6 + t.tv_nsec * 1e-3;
+}
+
+static int cmp_d(const void* a, const void* b) {
+  const double x = *(const double*)a, y = *(const double*)b;
+  return x < y ? -1 : x > y;
+}
+
+static double median(double* v, int n) {
+  qsort(v, (size_t)n, sizeof *v, cmp_d);
+  return n ? v[n / 2] : 0.0;
+}
+
+static uint64_t key_int(int64_t k) {
+  dgm_buf b = {0};
+  dgm_enc_i64(&b, k);
+  const uint64_t id = dgm_key_id(b.p, b.n);
+  dgm_buf_free(&b);
+  return id;
+}
+
+static uint64_t key_bin(const char* s) {
+  dgm_buf b = {0};
+  dgm_enc_binary(&b, s, strlen(s));
+  const uint64_t id = dgm_key_id(b.p, b.n);
+  dgm_buf_free(&b);
+  return id;
+}
+
+static uint64_t val_int(int64_t v) { return (uint64_t)v + (UINT64_C(1) << 62); }
+static const uint64_t VAL_VALUE = (UINT64_C(1) << 63) + 4096;  /* "value": a table id */
+
+/* ---------------------------------------------------------------- host rows */
+typedef struct {
+  uint64_t *key, *val, *cnt;
+  int64_t* ts;
+  uint32_t* node;
+  uint64_t n, cap;
+} hrows;
+
+static void hrows_init(hrows* r, uint64_t cap) {
+  r->key = calloc(cap, 8);
+  r->val = calloc(cap, 8);
+  r->cnt = calloc(cap, 8);
+  r->ts = calloc(cap, 8);
+  r->node = calloc(cap, 4);
+  r->n = 0;
+  r->cap = cap;
+}
+
+static dg_store hview(hrows* r) {
+  dg_store s = {r->key, r->val, r->ts, r->node, r->cnt, r->n, r->cap};
+  return s;
+}
+
+/* the replica after `n` adds of x -> x: rows sorted by (key id, ...), dot (0, x) */
+typedef struct {
+  uint64_t key;
+  uint64_t x;
+} kx;
+
+static int cmp_kx(const void* a, const void* b) {
+  const uint64_t x = ((const kx*)a)->key, y = ((const kx*)b)->key;
+  return x < y ? -1 : x > y;
+}
+
+static void setup_rows(hrows* r, int64_t n) {
+  kx* v = malloc((size_t)n * sizeof *v);
+  for (int64_t x = 1; x <= n; x++) {
+    v[x - 1].key = key_int(x);
+    v[x - 1].x = (uint64_t)x;
+  }
+  qsort(v, (size_t)n, sizeof *v, cmp_kx);
+  for (int64_t i = 0; i < n; i++) {
+    r->key[i] = v[i].key;
+    r->val[i] = val_int((int64_t)v[i].x);
+    r->ts[i] = (int64_t)v[i].x;
+    r->node[i] = 0;
+    r->cnt[i] = v[i].x;
+  }
+  r->n = (uint64_t)n;
+  free(v);
+}
+
+static int cmp_u64(const void* a, const void* b) {
+  const uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
+  return x < y ? -1 : x > y;
+}
+
+/* ---------------------------------------------------------------- one-key deltas */
+/* A delta as the reference's add/remove builds it (aw_lww_map.ex:99-146): the key's old
+ * dots plus (add) the fresh dot {0, c + 1} as a MapSet context, and (add) one row. */
+typedef struct {
+  uint64_t key, val, cnt;
+  int64_t ts;
+  int has_row;
+  uint32_t dnode[2];
+  uint64_t dcnt[2];
+  int nd;
+} delta1;
+
+typedef struct {
+  uint64_t c;        /* node 0's counter (its VV entry) */
+  int64_t clock;     /* the add timestamps */
+  uint64_t dot10;    /* key 10's current dot counter (0: absent) */
+  uint64_t dot_k4;   /* "key4"'s */
+} replica;
+
+static delta1 mk_add(replica* R, uint64_t key, uint64_t val, uint64_t* cur) {
+  delta1 d;
+  memset(&d, 0, sizeof d);
+  d.key = key;
+  d.val = val;
+  d.ts = ++R->clock;
+  d.cnt = ++R->c;
+  d.has_row = 1;
+  if (*cur) { /* the old dot, then the new one (both node 0: ascending counters) */
+    d.dnode[d.nd] = 0;
+    d.dcnt[d.nd++] = *cur;
+  }
+  d.dnode[d.nd] = 0;
+  d.dcnt[d.nd++] = d.cnt;
+  *cur = d.cnt;
+  return d;
+}
+
+static delta1 mk_remove(uint64_t key, uint64_t* cur) {
+  delta1 d;
+  memset(&d, 0, sizeof d);
+  d.key = key;
+  if (*cur) {
+    d.dnode[d.nd] = 0;
+    d.dcnt[d.nd++] = *cur;
+  }
+  *cur = 0;
+  return d;
+}
+
+enum { OP_READ = 0, OP_ADD, OP_UPDATE, OP_REMOVE, N_OPS };
+static const char* OP_NAMES[N_OPS] = {"read", "add", "update", "remove"};
+
+#ifndef DG_REF
+/* ================================================================ the GPU path */
+typedef struct {
+  dg_engine* e;
+  dg_store st, spare, taken;
+  dg_context ctx;
+  dg_merkle tree;
+  uint64_t* d_msg;    /* the packed delta: key | val | ts | cnt | dcnt | keyset | node | dnode */
+  uint64_t* h_msg;
+  uint64_t msg_words;
+  uint64_t *changed, *h_back;  /* the changed keys; host copy of keys + rows */
+  uint64_t back_cap;
+  uint64_t *rk, *rv, *h_rk;    /* read/1 output */
+} gpu;
+
+static void gpu_upload(gpu* g, hrows* r) {
+  DG(dg_store_alloc(g->e, r->n + 16384, &g->st));
+  DG(dg_store_alloc(g->e, r->n + 16384, &g->spare));
+  dg_store hs = hview(r);
+  DG(dg_store_upload(g->e, &hs, &g->st));
+  DG(dg_context_alloc(g->e, 64, &g->ctx));
+  uint32_t n0 = 0;
+  uint64_t c0 = r->n;
+  dg_context hc = {DG_CTX_VV, 0, &n0, &c0, 1, 1};
+  DG(dg_context_upload(g->e, &hc, &g->ctx));
+  g->ctx.kind = DG_CTX_VV;
+  /* the MerkleMap: ~3 keys per bucket (the bench's config-4 rule) */
+  uint32_t depth = 8;
+  while (depth < 28 && (UINT64_C(3) << depth) < r->n) depth++;
+  memset(&g->tree, 0, sizeof g->tree);
+  g->tree.depth = depth;
+  DG(dg_buffer_alloc(g->e, ((UINT64_C(2) << depth) - 1) * 8, (void**)&g->tree.nodes));
+  DG(dg_buffer_alloc(g->e, ((UINT64_C(1) << depth) + 8) * 2, (void**)&g->tree.counts));
+  DG(dg_merkle_build(g->e, &g->st, &g->tree));
+  g->msg_words = 8 * 2048;
+  DG(dg_buffer_alloc(g->e, g->msg_words * 8, (void**)&g->d_msg));
+  g->h_msg = calloc(g->msg_words, 8);
+  g->back_cap = 2048;
+  DG(dg_buffer_alloc(g->e, g->back_cap * 8, (void**)&g->changed));
+  DG(dg_store_alloc(g->e, g->back_cap, &g->taken));
+  g->h_back = calloc(g->back_cap * 6, 8);
+  DG(dg_buffer_alloc(g->e, (r->n + 16384) * 8, (void**)&g->rk));
+  DG(dg_buffer_alloc(g->e, (r->n + 16384) * 8, (void**)&g->rv));
+  g->h_rk = calloc((r->n + 16384) * 2, 8);
+}
+
+/* one mutation: h2d, dg_join_delta, d2h of the changed keys' rows; phases in t[3] (us) */
+static void gpu_apply(gpu* g, const uint64_t* key, const uint64_t* val, const int64_t* ts,
+                      const uint64_t* cnt, uint64_t n_rows, const uint32_t* dnode,
+                      const uint64_t* dcnt, uint64_t nd, const uint64_t* keys, uint64_t nk,
+                      double* t) {
+  const double t0 = now_us();
+  /* pack: 8-byte columns, then the u32 columns two to a word */
+  uint64_t* m = g->h_msg;
+  uint64_t o = 0;
+  const uint64_t o_key = o; memcpy(m + o, key, n_rows * 8); o += n_rows;
+  const uint64_t o_val = o; memcpy(m + o, val, n_rows * 8); o += n_rows;
+  const uint64_t o_ts = o; memcpy(m + o, ts, n_rows * 8); o += n_rows;
+  const uint64_t o_cnt = o; memcpy(m + o, cnt, n_rows * 8); o += n_rows;
+  const uint64_t o_dcnt = o; memcpy(m + o, dcnt, nd * 8); o += nd;
+  const uint64_t o_keys = o; memcpy(m + o, keys, nk * 8); o += nk;
+  const uint64_t o_node = o; memset(m + o, 0, (n_rows + 1) / 2 * 8);
+  o += (n_rows + 1) / 2;
+  const uint64_t o_dnode = o; o += (nd + 1) / 2;
+  (void)ts;  /* (every row of these deltas is node 0's: the node column stays zero) */
+  memcpy(m + o_dnode, dnode, nd * 4);
+  if (o > g->msg_words) {
+    fprintf(stderr, "delta too large\n");
+    exit(1);
+  }
+  DG(dg_copy_to_device(g->e, g->d_msg, m, o * 8));
+  uint64_t* d = g->d_msg;
+  dg_store ds = {d + o_key, d + o_val, (int64_t*)(d + o_ts), (uint32_t*)(d + o_node), d + o_cnt,
+                 n_rows, n_rows};
+  dg_context dc = {DG_CTX_DOTS, 0, (uint32_t*)(d + o_dnode), d + o_dcnt, nd, nd};
+  const double t1 = now_us();
+  uint64_t n_changed = 0;
+  int swapped = 0;
+  DG(dg_join_delta(g->e, &g->st, &g->ctx, &ds, &dc, d + o_keys, nk, &g->spare, &g->tree,
+                   g->changed, g->back_cap, &n_changed, &swapped));
+  const double t2 = now_us();
+  if (n_changed) {
+    g->taken.n = 0;
+    DG(dg_take_keys(g->e, &g->st, g->changed, n_changed, &g->taken));
+    const uint64_t nt = g->taken.n;
+    DG(dg_copy_to_host(g->e, g->h_back, g->changed, n_changed * 8));
+    if (nt) {
+      dg_store hb = {g->h_back + g->back_cap, g->h_back + 2 * g->back_cap,
+                     (int64_t*)(g->h_back + 3 * g->back_cap), (uint32_t*)(g->h_back + 5 * g->back_cap),
+                     g->h_back + 4 * g->back_cap, 0, g->back_cap};
+      DG(dg_store_download(g->e, &g->taken, &hb));
+    }
+  }
+  const double t3 = now_us();
+  t[0] = t1 - t0;
+  t[1] = t2 - t1;
+  t[2] = t3 - t2;
+}
+
+static void gpu_read(gpu* g) {
+  uint64_t n = 0;
+  DG(dg_read_lww(g->e, &g->st, NULL, 0, g->rk, g->rv, g->st.cap, &n));
+  DG(dg_copy_to_host(g->e, g->h_rk, g->rk, n * 8));
+  DG(dg_copy_to_host(g->e, g->h_rk + n, g->rv, n * 8));
+}
+#else
+/* ================================================================ the CPU restatement */
+typedef struct {
+  hrows st, out;
+  uint32_t vv_node;
+  uint64_t vv_cnt;
+  uint64_t *rk, *rv, *diff;
+} cpu;
+
+static void cpu_apply(cpu* c, const uint64_t* key, const uint64_t* val, const int64_t* ts,
+                      const uint64_t* cnt, uint64_t n_rows, const uint32_t* dnode,
+                      const uint64_t* dcnt, uint64_t nd, const uint64_t* keys, uint64_t nk,
+                      double* t) {
+  const double t0 = now_us();
+  uint32_t* node = calloc(n_rows ? n_rows : 1, 4);
+  dg_store ds = {(uint64_t*)key, (uint64_t*)val, (int64_t*)ts, node, (uint64_t*)cnt, n_rows, n_rows};
+  dg_context dc = {DG_CTX_DOTS, 0, (uint32_t*)dnode, (uint64_t*)dcnt, nd, nd};
+  dg_store sa = hview(&c->st);
+  dg_context ca = {DG_CTX_VV, 0, &c->vv_node, &c->vv_cnt, 1, 1};
+  uint32_t* on = malloc((nd + 2) * 4);
+  uint64_t* oc = malloc((nd + 2) * 8);
+  dg_context octx = {DG_CTX_VV, 0, on, oc, 0, nd + 2};
+  if (c->out.cap < c->st.n + n_rows) exit(2);
+  dg_store so = hview(&c->out);
+  if (ref_join2(&sa, &ca, &ds, &dc, keys, nk, &so, &octx) != 0) exit(3);
+  /* diff/3's changed keys: the join's rows against the state's (causal_crdt.ex:344-352) */
+  uint64_t n_diff = 0;
+  if (ref_store_diff(&sa, &so, c->diff, c->st.n + so.n + 1, &n_diff) != 0) exit(4);
+  c->out.n = so.n;
+  hrows tmp = c->st;
+  c->st = c->out;
+  c->out = tmp;
+  c->vv_cnt = oc[0];
+  free(node);
+  free(on);
+  free(oc);
+  const double t1 = now_us();
+  t[0] = 0;
+  t[1] = t1 - t0;
+  t[2] = 0;
+}
+#endif
+
+int main(int argc, char** argv) {
+  const int64_t n = argc > 1 ? atoll(argv[1]) : 1000;
+  const int reps = argc > 2 ? atoi(argv[2]) : 200;
+  hrows r;
+  hrows_init(&r, (uint64_t)n + 16384);
+  setup_rows(&r, n);
+  replica R = {(uint64_t)n, n, 10, 0};
+  const uint64_t K10 = key_int(10), K4 = key_bin("key4");
+#ifndef DG_REF
+  gpu g;
+  memset(&g, 0, sizeof g);
+  DG(dg_engine_create(0, NULL, &g.e));
+  gpu_upload(&g, &r);
+#define APPLY(...) gpu_apply(&g, __VA_ARGS__)
+#else
+  cpu c;
+  memset(&c, 0, sizeof c);
+  c.st = r;
+  hrows_init(&c.out, (uint64_t)n + 16384);
+  c.vv_node = 0;
+  c.vv_cnt = (uint64_t)n;
+  c.rk = calloc((size_t)n + 16384, 8);
+  c.rv = calloc((size_t)n + 16384, 8);
+  c.diff = calloc(2 * ((size_t)n + 16384), 8);
+#define APPLY(...) cpu_apply(&c, __VA_ARGS__)
+#endif
+  double* ts[N_OPS][3];
+  for (int o = 0; o < N_OPS; o++)
+    for (int p = 0; p < 3; p++) ts[o][p] = calloc((size_t)reps, sizeof(double));
+  double* tot[N_OPS];
+  for (int o = 0; o < N_OPS; o++) tot[o] = calloc((size_t)reps, sizeof(double));
+
+#define RUN_DELTA(dd, out3)                                                                \
+  do {                                                                                     \
+    const delta1 d_ = (dd);                                                                \
+    APPLY(&d_.key, &d_.val, &d_.ts, &d_.cnt, (uint64_t)d_.has_row, d_.dnode, d_.dcnt,       \
+          (uint64_t)d_.nd, &d_.key, 1, (out3));                                            \
+  } while (0)
+
+  double scratch[3];
+  for (int it = -5; it < reps; it++) {
+    for (int o = 0; o < N_OPS; o++) {
+      /* before_each: add [10, 10], remove ["key4"] */
+      RUN_DELTA(mk_add(&R, K10, val_int(10), &R.dot10), scratch);
+      RUN_DELTA(mk_remove(K4, &R.dot_k4), scratch);
+      double t3[3] = {0, 0, 0};
+      const double t0 = now_us();
+      if (o == OP_READ) {
+#ifndef DG_REF
+        gpu_read(&g);
+#else
+        uint64_t nr = 0;
+        dg_store sa = hview(&c.st);
+        if (ref_read_lww(&sa, NULL, 0, c.rk, c.rv, c.st.n + 1, &nr) != 0) exit(5);
+#endif
+      } else if (o == OP_ADD) {
+        RUN_DELTA(mk_add(&R, K4, VAL_VALUE, &R.dot_k4), t3);
+      } else if (o == OP_UPDATE) {
+        RUN_DELTA(mk_add(&R, K10, val_int(12), &R.dot10), t3);
+      } else {
+        RUN_DELTA(mk_remove(K10, &R.dot10), t3);
+      }
+      const double el = now_us() - t0;
+      if (it >= 0) {
+        tot[o][it] = el;
+        for (int p = 0; p < 3; p++) ts[o][p][it] = t3[p];
+      }
+    }
+  }
+  /* the trace workload as one batched delta: 1000 adds of new keys "key<x>" */
+  const int nb = 1000;
+  uint64_t* bk = malloc(nb * 8);
+  uint64_t *bv = malloc(nb * 8), *bc = malloc(nb * 8), *bd = malloc(nb * 8);
+  int64_t* bt = malloc(nb * 8);
+  uint32_t* bn = calloc(nb, 4);
+  double bt_us[16];
+  int n_batch = 0;
+  for (int rep = 0; rep < 6; rep++) {
+    for (int i = 0; i < nb; i++) {
+      char s[32];
+      snprintf(s, sizeof s, "key%d_%d", i, rep);
+      bk[i] = key_bin(s);
+    }
+    /* sorted keys; every add's fresh dot {0, c + 1 + i} (new keys: no old dots) */
+    qsort(bk, nb, 8, cmp_u64);
+    for (int i = 0; i < nb; i++) {
+      bv[i] = VAL_VALUE;
+      bt[i] = ++R.clock;
+      bc[i] = R.c + 1 + (uint64_t)i;
+      bd[i] = bc[i];
+    }
+    R.c += nb;
+    double t3[3];
+    const double t0 = now_us();
+    APPLY(bk, bv, bt, bc, nb, bn, bd, nb, bk, nb, t3);
+    const double el = now_us() - t0;
+    if (rep) bt_us[n_batch++] = el;
+  }
+  printf("{\"n_keys\": %lld, \"reps\": %d, \"path\": \"%s\", \"us\": {", (long long)n, reps,
+#ifndef DG_REF
+         "gpu"
+#else
+         "cpu_restatement"
+#endif
+  );
+  for (int o = 0; o < N_OPS; o++) {
+    printf("%s\"%s\": %.2f", o ? ", " : "", OP_NAMES[o], median(tot[o], reps));
+  }
+  printf("}, \"phases_us\": {");
+  for (int o = 1; o < N_OPS; o++) {
+    printf("%s\"%s\": {\"h2d\": %.2f, \"join_delta\": %.2f, \"d2h_changed\": %.2f}", o > 1 ? ", " : "",
+           OP_NAMES[o], median(ts[o][0], reps), median(ts[o][1], reps), median(ts[o][2], reps));
+  }
+  const double bmed = median(bt_us, n_batch);
+  printf("}, \"batch_1000_adds_us\": %.2f, \"batch_us_per_op\": %.3f}\n", bmed, bmed / nb);
+#ifndef DG_REF
+  dg_engine_destroy(g.e);
+#endif
+  return 0;
+}

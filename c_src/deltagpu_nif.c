@@ -262,6 +262,19 @@ typedef struct {
   uint64_t th_nodes, th_vals; /* the table sizes uploaded; a relabel clears th_vals */
 } engine_res;
 
+/* A delta's device buffers, kept per state and grown on demand: a local mutation (a
+ * one-key delta, causal_crdt.ex:337-342) then allocates nothing -- a hipMalloc / hipFree
+ * pair per call cost more than the join itself (c_src/bench_mutate.c). */
+typedef struct {
+  dg_store raw, rows;       /* as marshalled (map-walk order), and sorted */
+  dg_context rawc, ctx;
+  uint64_t* keys;           /* the keyset */
+  uint64_t keys_cap;
+  uint64_t* changed;        /* dg_join_delta's changed keys */
+  uint64_t changed_cap;
+  dg_store taken;           /* their rows (dg_take_keys) */
+} delta_buf;
+
 struct state_res {
   engine_res* eng;
   dg_store rows;
@@ -269,6 +282,7 @@ struct state_res {
   dg_context ctx;
   dg_merkle tree;
   int has_tree;
+  delta_buf d;
   state_res *prev, *next;
 };
 
@@ -300,6 +314,13 @@ static void state_dtor(ErlNifEnv* env, void* obj) {
   dg_store_free(g->e, &s->rows);
   dg_store_free(g->e, &s->spare);
   dg_context_free(g->e, &s->ctx);
+  dg_store_free(g->e, &s->d.raw);
+  dg_store_free(g->e, &s->d.rows);
+  dg_store_free(g->e, &s->d.taken);
+  dg_context_free(g->e, &s->d.rawc);
+  dg_context_free(g->e, &s->d.ctx);
+  dg_buffer_free(g->e, s->d.keys);
+  dg_buffer_free(g->e, s->d.changed);
   if (s->has_tree) {
     dg_buffer_free(g->e, s->tree.nodes);
     dg_buffer_free(g->e, s->tree.counts);
@@ -504,9 +525,83 @@ static int upload_sorted(engine_res* g, const dgm_rows* h, dg_store* rows, dg_co
   return rc;
 }
 
+/* grow a kept device store / context / buffer to at least n entries (doubling) */
+static int grow_store(engine_res* g, dg_store* s, uint64_t n) {
+  if (s->key && s->cap >= n) return DG_OK;
+  const uint64_t want = n > 2 * s->cap ? n : 2 * s->cap + 16;
+  dg_store_free(g->e, s);
+  memset(s, 0, sizeof *s);
+  return dg_store_alloc(g->e, want, s);
+}
+static int grow_ctx(engine_res* g, dg_context* c, uint64_t n) {
+  if (c->node && c->cap >= n) return DG_OK;
+  dg_context_free(g->e, c);
+  memset(c, 0, sizeof *c);
+  return dg_context_alloc(g->e, n + 16, c);
+}
+static int grow_buf(engine_res* g, uint64_t** p, uint64_t* cap, uint64_t n) {
+  if (*p && *cap >= n) return DG_OK;
+  dg_buffer_free(g->e, *p);
+  *p = NULL;
+  *cap = 0;
+  const uint64_t c = n + 16;
+  int rc = dg_buffer_alloc(g->e, c * 8, (void**)p);
+  if (!rc) *cap = c;
+  return rc;
+}
+
+/* rows already in (key, val, ts, node, cnt) order without duplicates, a context in
+ * (node, cnt) order: a delta built by add/remove (one key, its dots) usually is */
+static int rows_sorted(const dg_store* s) {
+  for (uint64_t i = 1; i < s->n; i++) {
+    const uint64_t a[5] = {s->key[i - 1], s->val[i - 1], (uint64_t)s->ts[i - 1] ^ (1ull << 63),
+                           s->node[i - 1], s->cnt[i - 1]};
+    const uint64_t b[5] = {s->key[i], s->val[i], (uint64_t)s->ts[i] ^ (1ull << 63), s->node[i],
+                           s->cnt[i]};
+    int c = 0;
+    for (int f = 0; f < 5 && !c; f++) c = a[f] < b[f] ? -1 : a[f] > b[f];
+    if (c >= 0) return 0;
+  }
+  return 1;
+}
+static int ctx_sorted(const dg_context* c) {
+  for (uint64_t i = 1; i < c->n; i++) {
+    if (c->node[i - 1] > c->node[i]) return 0;
+    if (c->node[i - 1] == c->node[i] && (c->kind == DG_CTX_VV || c->cnt[i - 1] >= c->cnt[i])) return 0;
+  }
+  return 1;
+}
+
+/* host rows -> the state's kept delta buffers, sorted on the device only when the map
+ * walk did not already produce the order */
+static int upload_delta(engine_res* g, const dgm_rows* h, delta_buf* d) {
+  int rc;
+  if ((rc = grow_store(g, &d->rows, h->s.n ? h->s.n : 1))) return rc;
+  if (rows_sorted(&h->s)) {
+    if ((rc = dg_store_upload(g->e, &h->s, &d->rows))) return rc;
+  } else {
+    if ((rc = grow_store(g, &d->raw, h->s.n))) return rc;
+    if ((rc = dg_store_upload(g->e, &h->s, &d->raw))) return rc;
+    if ((rc = dg_sort_store(g->e, &d->raw, &d->rows))) return rc;
+  }
+  if ((rc = grow_ctx(g, &d->ctx, h->c.n ? h->c.n : 1))) return rc;
+  if (ctx_sorted(&h->c)) {
+    rc = dg_context_upload(g->e, &h->c, &d->ctx);
+  } else {
+    if ((rc = grow_ctx(g, &d->rawc, h->c.n))) return rc;
+    if ((rc = dg_context_upload(g->e, &h->c, &d->rawc))) return rc;
+    rc = dg_sort_context(g->e, &d->rawc, &d->ctx);
+  }
+  d->ctx.kind = h->c.kind;
+  return rc;
+}
+
 /* a key list -> its ids, ascending unique, on the device */
+static int grow_buf(engine_res* g, uint64_t** p, uint64_t* cap, uint64_t n);
+
+/* keep: *d_keys is a kept buffer of *keep_cap entries, grown as needed (else allocated) */
 static int marshal_keys(ErlNifEnv* env, engine_res* g, ERL_NIF_TERM keys, uint64_t** d_keys,
-                        uint64_t* n_keys) {
+                        uint64_t* n_keys, int keep, uint64_t* keep_cap) {
   unsigned len;
   if (!enif_get_list_length(env, keys, &len)) return DG_E_INVAL;
   uint64_t* ids = (uint64_t*)enif_alloc((len ? len : 1) * sizeof *ids);
@@ -529,7 +624,8 @@ static int marshal_keys(ErlNifEnv* env, engine_res* g, ERL_NIF_TERM keys, uint64
   unsigned m = 0;
   for (unsigned i = 0; i < n; i++)
     if (!m || ids[m - 1] != ids[i]) ids[m++] = ids[i];
-  int rc = dg_buffer_alloc(g->e, (m ? m : 1) * 8, (void**)d_keys);
+  int rc = keep ? grow_buf(g, d_keys, keep_cap, m ? m : 1)
+                : dg_buffer_alloc(g->e, (m ? m : 1) * 8, (void**)d_keys);
   if (!rc) rc = dg_copy_to_device(g->e, *d_keys, ids, m * 8);
   *n_keys = m;
   enif_free(ids);
@@ -707,27 +803,25 @@ static ERL_NIF_TERM join_delta(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
   enif_mutex_lock(g->lock);
   int rc = DG_OK;
   dgm_rows h;
-  dg_store drows, taken;
-  dg_context dctx, nctx;
-  uint64_t *d_keys = NULL, n_keys = 0, *changed = NULL, n_changed = 0;
+  delta_buf* d = &s->d;
+  dg_context nctx;
+  uint64_t n_keys = 0, n_changed = 0;
   int swapped = 0;
-  memset(&drows, 0, sizeof drows);
-  memset(&taken, 0, sizeof taken);
-  memset(&dctx, 0, sizeof dctx);
   memset(&nctx, 0, sizeof nctx);
   ERL_NIF_TERM r, new_dots, changed_terms = enif_make_list(env, 0), values;
   TRY(dgm_rows_init(&h, 256, 16));
   TRY(marshal_dots(env, g, argv[1], &h));
   TRY(marshal_value(env, g, argv[2], &h));
-  TRY(upload_sorted(g, &h, &drows, &dctx));
-  TRY(marshal_keys(env, g, argv[3], &d_keys, &n_keys));
+  /* the delta into the state's kept buffers (no allocation once they are big enough) */
+  TRY(upload_delta(g, &h, d));
+  TRY(marshal_keys(env, g, argv[3], &d->keys, &n_keys, 1, &d->keys_cap));
   /* the spare buffer and the context's room for the union, grown on demand */
-  if (s->spare.cap < s->rows.n + drows.n) {
+  if (s->spare.cap < s->rows.n + d->rows.n) {
     dg_store_free(g->e, &s->spare);
-    TRY(dg_store_alloc(g->e, 2 * (s->rows.n + drows.n), &s->spare));
+    TRY(dg_store_alloc(g->e, 2 * (s->rows.n + d->rows.n), &s->spare));
   }
-  if (s->ctx.cap < s->ctx.n + dctx.n) {
-    TRY(dg_context_alloc(g->e, 2 * (s->ctx.n + dctx.n), &nctx));
+  if (s->ctx.cap < s->ctx.n + d->ctx.n) {
+    TRY(dg_context_alloc(g->e, 2 * (s->ctx.n + d->ctx.n), &nctx));
     TRY(dg_copy_to_device(g->e, nctx.node, s->ctx.node, s->ctx.n * 4));  /* device to device */
     TRY(dg_copy_to_device(g->e, nctx.cnt, s->ctx.cnt, s->ctx.n * 8));
     nctx.n = s->ctx.n;
@@ -736,20 +830,28 @@ static ERL_NIF_TERM join_delta(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
     s->ctx = nctx;
     memset(&nctx, 0, sizeof nctx);
   }
-  TRY(dg_buffer_alloc(g->e, (n_keys ? n_keys : 1) * 8, (void**)&changed));
+  TRY(grow_buf(g, &d->changed, &d->changed_cap, n_keys ? n_keys : 1));
   if (s->has_tree) TRY(refresh_terms(g));
   /* update_state_with_delta: the join (in place, or through the spare buffer: the structs
-   * come back exchanged), the changed keys, the MerkleMap put/delete of them */
-  TRY(dg_join_delta(g->e, &s->rows, &s->ctx, &drows, &dctx, d_keys, n_keys, &s->spare,
-                    s->has_tree ? &s->tree : NULL, changed, n_keys, &n_changed, &swapped));
-  /* the changed keys' new value maps (dg_take_keys), and the keys that vanished */
-  TRY(dg_store_alloc(g->e, s->rows.n ? s->rows.n : 1, &taken));
-  TRY(dg_take_keys(g->e, &s->rows, changed, n_changed, &taken));
-  TRY(unmarshal_rows(env, g, &taken, &values));
+   * come back exchanged), the changed keys, the MerkleMap put/delete of them -- all or
+   * nothing: on an error the state, its context and tree are as they were */
+  TRY(dg_join_delta(g->e, &s->rows, &s->ctx, &d->rows, &d->ctx, d->keys, n_keys, &s->spare,
+                    s->has_tree ? &s->tree : NULL, d->changed, d->changed_cap, &n_changed, &swapped));
+  /* the changed keys' new value maps (dg_take_keys into the kept buffer, grown to the
+   * size the first try reports), and the keys that vanished */
+  TRY(grow_store(g, &d->taken, 2 * n_changed + 16));
+  rc = dg_take_keys(g->e, &s->rows, d->changed, n_changed, &d->taken);
+  if (rc == DG_E_CAPACITY) {
+    const uint64_t need = d->taken.n;
+    TRY(grow_store(g, &d->taken, need));
+    rc = dg_take_keys(g->e, &s->rows, d->changed, n_changed, &d->taken);
+  }
+  TRY(rc);
+  TRY(unmarshal_rows(env, g, &d->taken, &values));
   TRY(unmarshal_dots(env, g, &s->ctx, &new_dots));
   {
     uint64_t* hk = (uint64_t*)enif_alloc((n_changed ? n_changed : 1) * 8);
-    rc = dg_copy_to_host(g->e, hk, changed, n_changed * 8);
+    rc = dg_copy_to_host(g->e, hk, d->changed, n_changed * 8);
     for (uint64_t i = n_changed; !rc && i-- > 0;) {
       const boxed* b = (const boxed*)dgm_key_term(g->u, hk[i]);
       ERL_NIF_TERM k = enif_make_copy(env, b->t), v;
@@ -762,12 +864,7 @@ static ERL_NIF_TERM join_delta(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
 out:
   r = rc ? error_term(env, rc) : enif_make_tuple3(env, A_OK, new_dots, changed_terms);
   dgm_rows_free(&h);
-  dg_store_free(g->e, &drows);
-  dg_store_free(g->e, &taken);
-  dg_context_free(g->e, &dctx);
   dg_context_free(g->e, &nctx);
-  dg_buffer_free(g->e, d_keys);
-  dg_buffer_free(g->e, changed);
   enif_mutex_unlock(g->lock);
   return r;
 }
@@ -783,7 +880,7 @@ static ERL_NIF_TERM read_nif(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]
   uint64_t *hk = NULL, *hv = NULL;
   ERL_NIF_TERM r, m = enif_make_new_map(env);
   const int all = enif_is_identical(argv[1], A_ALL);
-  if (!all) TRY(marshal_keys(env, g, argv[1], &d_keys, &n_keys));
+  if (!all) TRY(marshal_keys(env, g, argv[1], &d_keys, &n_keys, 0, NULL));
   const uint64_t cap = s->rows.n ? s->rows.n : 1;
   TRY(dg_buffer_alloc(g->e, cap * 8, (void**)&dk));
   TRY(dg_buffer_alloc(g->e, cap * 8, (void**)&dv));
@@ -821,7 +918,7 @@ static ERL_NIF_TERM take_nif(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]
   dg_store taken;
   memset(&taken, 0, sizeof taken);
   ERL_NIF_TERM r, values = enif_make_new_map(env);
-  TRY(marshal_keys(env, g, argv[1], &d_keys, &n_keys));
+  TRY(marshal_keys(env, g, argv[1], &d_keys, &n_keys, 0, NULL));
   TRY(dg_store_alloc(g->e, s->rows.n, &taken));
   TRY(dg_take_keys(g->e, &s->rows, d_keys, n_keys, &taken));
   TRY(unmarshal_rows(env, g, &taken, &values));

@@ -130,6 +130,10 @@ __device__ __forceinline__ u64 wave_bucket_start(const MT& t, const u64* keys, u
 // them, then adds to ONE arrival counter; the workgroup whose add returns last reads the
 // roots and counts with sc1 loads.  No release fence per workgroup: an agent release
 // in each of 2048 workgroups cost 75 us of a 219 us build (rocprofv3 A/B).
+#ifndef DG_MERKLE_VEC  // the build's 4-consecutive-rows loop (0: the strided loop, for A/B)
+#define DG_MERKLE_VEC 1
+#endif
+constexpr bool MERKLE_VEC = DG_MERKLE_VEC;
 constexpr int UPB = 512;   // threads per chunk workgroup
 constexpr int UPL = MERKLE_UPL;  // levels reduced per workgroup (2048 nodes in LDS)
 constexpr u32 UPW = 1u << UPL;
@@ -169,8 +173,8 @@ __device__ void lds_upsweep(u64* nodes, u32 hi, u64 g0, u32 width, u64* s) {
 
 // scratch: ctr[0] the arrival counter (zeroed before the launch), then per chunk its
 // root and its distinct-key count (u64 each, at hand[0, G) and hand[G, 2G)).
-template <bool BUILD>
-__global__ __launch_bounds__(UPB) void merkle_chunk_kernel(Rows rows, MT t, const u32* dirty,
+template <bool BUILD, bool VEC = false>
+__global__ __launch_bounds__(UPB, 4) void merkle_chunk_kernel(Rows rows, MT t, const u32* dirty,
                                                            u32* ctr, u64* hand, u64* d_keys,
                                                            u32* err) {
   __shared__ u64 s[UPW];
@@ -202,34 +206,105 @@ __global__ __launch_bounds__(UPB) void merkle_chunk_kernel(Rows rows, MT t, cons
     u32 heads = 0;
     // rows outside the tree's key range (before the first chunk, after the last one)
     bool bad = tid == 0 && ((g == 0 && lo > 0) || (g == G - 1 && hi < rows.n));
-    for (u64 i0 = lo; i0 < hi; i0 += 4 * UPB) {
-      u64 key[4], h[4];
-      bool head[4];
+    if (VEC) {
+      // each thread hashes 4 CONSECUTIVE rows (16-byte loads: 2 per 8-byte column, 1 for
+      // the node column), sums the rows of one bucket in registers and adds each run once
+      // to LDS: ~1.4 LDS atomics per 4 rows instead of 8, and no two lanes of a wave add to
+      // one bucket in the same instruction unless a bucket straddles them
+      const u64 a0 = lo & ~3ull;
+      const int lane_ = tid & (WAVE - 1);
+      for (u64 base = a0; base < hi; base += 4 * UPB) {  // block-uniform trip count
+        const u64 gb = base + 4 * (u64)tid;
+        const bool any = gb < hi;
+        u64 key[4] = {0, 0, 0, 0}, val[4] = {0, 0, 0, 0}, cnt[4] = {0, 0, 0, 0};
+        i64 ts[4] = {0, 0, 0, 0};
+        u32 nd[4] = {0, 0, 0, 0};
+        if (any && gb + 3 < rows.n) {
+          const ulonglong2 k0 = *(const ulonglong2*)(rows.key + gb), k1 = *(const ulonglong2*)(rows.key + gb + 2);
+          const ulonglong2 v0 = *(const ulonglong2*)(rows.val + gb), v1 = *(const ulonglong2*)(rows.val + gb + 2);
+          const longlong2 t0 = *(const longlong2*)(rows.ts + gb), t1 = *(const longlong2*)(rows.ts + gb + 2);
+          const ulonglong2 c0 = *(const ulonglong2*)(rows.cnt + gb), c1 = *(const ulonglong2*)(rows.cnt + gb + 2);
+          const uint4 n4 = *(const uint4*)(rows.node + gb);
+          key[0] = k0.x, key[1] = k0.y, key[2] = k1.x, key[3] = k1.y;
+          val[0] = v0.x, val[1] = v0.y, val[2] = v1.x, val[3] = v1.y;
+          ts[0] = t0.x, ts[1] = t0.y, ts[2] = t1.x, ts[3] = t1.y;
+          cnt[0] = c0.x, cnt[1] = c0.y, cnt[2] = c1.x, cnt[3] = c1.y;
+          nd[0] = n4.x, nd[1] = n4.y, nd[2] = n4.z, nd[3] = n4.w;
+        } else if (any) {  // the store's last rows: no 16-byte load past its end
 #pragma unroll
-      for (int q = 0; q < 4; q++) {  // four rows in flight per thread
-        const u64 i = i0 + (u64)q * UPB + tid;
-        key[q] = 0;
-        h[q] = 0;
-        head[q] = false;
-        if (i < hi) {
-          key[q] = rows.key[i];
-          const u32 nd = rows.node[i];
-          const u64 nt = nh_lds ? (nd < (u32)t.th.nn ? s_nh[nd] : (u64)nd) : th_node(t.th, nd);
-          h[q] = row_hash(key[q], th_val(t.th, rows.val[i]), rows.ts[i], nt, rows.cnt[i]);
-          head[q] = i == lo || rows.key[i - 1] != key[q];
+          for (int q = 0; q < 4; q++)
+            if (gb + q < rows.n) {
+              key[q] = rows.key[gb + q];
+              val[q] = rows.val[gb + q];
+              ts[q] = rows.ts[gb + q];
+              cnt[q] = rows.cnt[gb + q];
+              nd[q] = rows.node[gb + q];
+            }
+        }
+        // the row before this thread's first: the previous lane's last key (lane 0: memory)
+        u64 prev = __shfl_up(key[3], 1, WAVE);
+        if (lane_ == 0) prev = (any && gb > 0) ? rows.key[gb - 1] : ~key[0];
+        u64 run_h = 0;
+        u32 run_c = 0;
+        u64 run_b = ~0ull;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const u64 i = gb + (u64)q;
+          if (i >= lo && i < hi) {
+            const u64 nt = nh_lds ? (nd[q] < (u32)t.th.nn ? s_nh[nd[q]] : (u64)nd[q]) : th_node(t.th, nd[q]);
+            const u64 h = row_hash(key[q], th_val(t.th, val[q]), ts[q], nt, cnt[q]);
+            const u64 pk = q ? key[q - 1] : prev;
+            heads += (i == lo || pk != key[q]) ? 1u : 0u;
+            if (t.sb && (key[q] >> (64 - t.sb)) != t.shard) bad = true;
+            const u64 b = bucket_of(t, key[q]) - g0;
+            if (b != run_b) {
+              if (run_b < width) {
+                atomicAdd((unsigned long long*)&s[run_b], (unsigned long long)run_h);
+                atomicAdd(&s_c[run_b], run_c);
+              }
+              run_b = b;
+              run_h = 0;
+              run_c = 0;
+            }
+            run_h += h;
+            run_c++;
+          }
+        }
+        if (run_b < width) {
+          atomicAdd((unsigned long long*)&s[run_b], (unsigned long long)run_h);
+          atomicAdd(&s_c[run_b], run_c);
         }
       }
+    } else {
+      for (u64 i0 = lo; i0 < hi; i0 += 4 * UPB) {
+        u64 key[4], h[4];
+        bool head[4];
 #pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const u64 i = i0 + (u64)q * UPB + tid;
-        if (i < hi) {
-          if (t.sb && (key[q] >> (64 - t.sb)) != t.shard) bad = true;
-          const u64 b = bucket_of(t, key[q]) - g0;
-          if (b < width) {
-            atomicAdd((unsigned long long*)&s[b], (unsigned long long)h[q]);
-            atomicAdd(&s_c[b], 1u);
+        for (int q = 0; q < 4; q++) {  // four rows in flight per thread
+          const u64 i = i0 + (u64)q * UPB + tid;
+          key[q] = 0;
+          h[q] = 0;
+          head[q] = false;
+          if (i < hi) {
+            key[q] = rows.key[i];
+            const u32 nd = rows.node[i];
+            const u64 nt = nh_lds ? (nd < (u32)t.th.nn ? s_nh[nd] : (u64)nd) : th_node(t.th, nd);
+            h[q] = row_hash(key[q], th_val(t.th, rows.val[i]), rows.ts[i], nt, rows.cnt[i]);
+            head[q] = i == lo || rows.key[i - 1] != key[q];
           }
-          heads += head[q] ? 1u : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const u64 i = i0 + (u64)q * UPB + tid;
+          if (i < hi) {
+            if (t.sb && (key[q] >> (64 - t.sb)) != t.shard) bad = true;
+            const u64 b = bucket_of(t, key[q]) - g0;
+            if (b < width) {
+              atomicAdd((unsigned long long*)&s[b], (unsigned long long)h[q]);
+              atomicAdd(&s_c[b], 1u);
+            }
+            heads += head[q] ? 1u : 0u;
+          }
         }
       }
     }
@@ -813,8 +888,15 @@ hipError_t launch_merkle_build(const Rows& s, const MerkleT& m, u64* d_keys, u32
   // scratch: the arrival counter (zeroed before EVERY launch), then the hand-off words
   hipError_t e = hipMemsetAsync(ctr, 0, 16 * sizeof(u32), st);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(merkle_chunk_kernel<true>, dim3((unsigned)G), dim3(UPB), 0, st, s, t,
-                     (const u32*)nullptr, ctr, (u64*)(ctr + 16), d_keys, err);
+  // 16-byte row loads need 16-byte aligned columns (a view into a packed buffer may not be)
+  const bool vec = MERKLE_VEC && !(((uintptr_t)s.key | (uintptr_t)s.val | (uintptr_t)s.ts |
+                                    (uintptr_t)s.node | (uintptr_t)s.cnt) & 15);
+  if (vec)
+    hipLaunchKernelGGL((merkle_chunk_kernel<true, true>), dim3((unsigned)G), dim3(UPB), 0, st, s, t,
+                       (const u32*)nullptr, ctr, (u64*)(ctr + 16), d_keys, err);
+  else
+    hipLaunchKernelGGL((merkle_chunk_kernel<true, false>), dim3((unsigned)G), dim3(UPB), 0, st, s, t,
+                       (const u32*)nullptr, ctr, (u64*)(ctr + 16), d_keys, err);
   return hipGetLastError();
 }
 

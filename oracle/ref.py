@@ -351,6 +351,20 @@ def merkle_continue(t: Tree, rows, cont, levels):
     return ("continue", ("leaf", dpos, pk, ph))
 
 
+def merkle_truncate(t: Tree, cont, max_entries):
+    """truncate_diff(cont, max_sync_size) (causal_crdt.ex:98,212-214) on the oracle's
+    continuations: a node form keeps its first `max_entries` entries, a leaf form its first
+    `max_entries` buckets and the (key, leaf) pairs of those buckets (include/deltagpu.h
+    dg_merkle_truncate)."""
+    if cont[0] == "node":
+        _, L, pos, hs = cont
+        return ("node", L, pos[:max_entries], hs[:max_entries])
+    _, buckets, pk, ph = cont
+    keep = np.asarray(buckets)[:max_entries]
+    m = np.isin(t.bucket_of(pk), keep.astype(np.int64))
+    return ("leaf", keep, np.asarray(pk)[m], np.asarray(ph)[m])
+
+
 def store_diff(ra, rb):
     sa, ra = _store(ra)
     sb, rb = _store(rb)

@@ -258,3 +258,62 @@ def test_config4_shard_full_size(engine):
     fresh = engine.merkle_build(out, depth, shard_bits=3, shard=0)
     assert np.array_equal(nodes(ta), nodes(fresh))
     assert np.array_equal(ta.bucket_counts(), fresh.bucket_counts())
+
+
+@pytest.mark.parametrize("max_sync_size", [200, None])
+def test_partial_diff_config4_shard(engine, max_sync_size):
+    """The partial-diff protocol at the scale and shape CausalCrdt runs it:
+    a config-4 shard (12.5M keys, 1 % differing, depth 22), prepare_partial_diff(mm, 8) on
+    the originator (causal_crdt.ex:255), then continue_partial_diff(cont, mm, 8) ping-pong
+    between the replicas (:96), each {:continue, c} truncated to max_sync_size before it
+    is sent (:98, default 200: delta_crdt.ex:32; None: :infinite), and the final keys
+    truncated too (:105).  Every hop's continuation equals the C oracle's, hashes and
+    all; the keys are the first differing keys of the buckets the truncations kept."""
+    a, b = W.config4_shard(3, 8, keys_per_rank=12_500_000, diff_frac=0.01)
+    sa, _ = up(a)
+    sb, _ = up(b)
+    depth, levels = 22, 8
+    ta = engine.merkle_build(sa, depth, shard_bits=3, shard=3)
+    tb = engine.merkle_build(sb, depth, shard_bits=3, shard=3)
+    ra = R.merkle_build(a["rows"], depth, 3, 3)
+    rb = R.merkle_build(b["rows"], depth, 3, 3)
+    cont, rc = engine.merkle_prepare(ta, levels), R.merkle_prepare(ra, levels)
+    assert cont.n == rc[2].size == 256
+    side = [(tb, rb, b["rows"]), (ta, ra, a["rows"])]
+    hops, sizes = 0, []
+    while True:
+        t, r, rows = side[hops % 2]
+        res = engine.merkle_continue(t, cont, levels)
+        rres = R.merkle_continue(r, rows, rc, levels)
+        hops += 1
+        assert res[0] == rres[0]
+        if res[0] == "ok":
+            break
+        cont, rc = res[1], rres[1]
+        if max_sync_size is not None:
+            engine.merkle_truncate(t, cont, max_sync_size)
+            rc = R.merkle_truncate(r, rc, max_sync_size)
+        sizes.append((cont.n, cont.n_buckets))
+        if rc[0] == "node":
+            assert cont.level == rc[1] and not cont.leaf
+        else:
+            assert cont.level == depth + 1
+            assert np.array_equal(u64(cont.bucket[: cont.n_buckets]), rc[1])
+        assert np.array_equal(u64(cont.pos[: cont.n]), rc[2])
+        assert np.array_equal(u64(cont.hash[: cont.n]), rc[3])
+    assert hops == 4  # level 8 -> 16 -> 22 -> leaf form -> keys
+    keys = u64(res[1])
+    assert np.array_equal(keys, rres[1])
+    full = R.store_diff(a["rows"], b["rows"])
+    if max_sync_size is None:
+        assert np.array_equal(keys, full)
+        assert sizes[0][0] == 256 * 256  # every level-8 subtree differs at 1 %
+    else:
+        # the keys of the kept buckets: a subset of the diff, every one of them differing
+        assert all(n <= max_sync_size for n, nb in sizes[:2])
+        assert sizes[2][1] <= max_sync_size
+        assert 0 < len(keys) and np.all(np.isin(keys, full))
+        want = full[np.isin(R.Tree(depth, 3, 3).bucket_of(full),
+                            u64(cont.bucket[: cont.n_buckets]).astype(np.int64))]
+        assert np.array_equal(keys, want)
+        assert len(keys[:max_sync_size]) <= max_sync_size  # send_diff's truncate (:105)
