@@ -217,7 +217,7 @@ static void gpu_upload(gpu* g, hrows* r) {
   DG(dg_store_alloc(g->e, r->n + 16384, &g->spare));
   dg_store hs = hview(r);
   DG(dg_store_upload(g->e, &hs, &g->st));
-  DG(dg_context_alloc(g->e, 64, &g->ctx));
+  DG(dg_context_alloc(g->e, 4096, &g->ctx));  /* room for the union with a delta's dot list */
   uint32_t n0 = 0;
   uint64_t c0 = r->n;
   dg_context hc = {DG_CTX_VV, 0, &n0, &c0, 1, 1};

@@ -1056,9 +1056,13 @@ int kfold_pass(dg_engine* e, const dg_store* state, const dg_context* ctx, int k
                const uint64_t* n_keys, dg_store* out, dg_context* out_ctx, bool* stepwise) {
   *stepwise = true;
   if (k < 1 || k > KFOLD_MAX_K || ctx->kind != DG_CTX_VV) return DG_OK;
-  u64 m_rows = 0, m_keys = 0, allmask = 0;
+  u64 m_rows = 0, m_keys = 0, allmask = 0, dotsmask = 0, n_dots = 0;
   for (int i = 0; i < k; i++) {
-    if (dctxs[i].kind != DG_CTX_VV || deltas[i].n >= (1ull << 32)) return DG_OK;
+    if (deltas[i].n >= (1ull << 32)) return DG_OK;
+    if (dctxs[i].kind == DG_CTX_DOTS) {  // a mutation delta's MapSet context
+      dotsmask |= 1ull << i;
+      n_dots += dctxs[i].n;
+    }
     const bool full = !keys || !keys[i];
     const u64 nk = full ? 0 : n_keys[i];
     if (nk >= (1ull << 32)) return DG_OK;
@@ -1075,14 +1079,18 @@ int kfold_pass(dg_engine* e, const dg_store* state, const dg_context* ctx, int k
   for (int attempt = 0; attempt < 2; attempt++) {
     const u64 T = T0 << (3 * attempt);
     if (T >= (1ull << 31)) return DG_OK;
-    // device scratch: runs | flat | sstart | dstart | tabC | tabP | flag
+    // device scratch: runs | flat | cflat | sstart | dstart | tabC | tabP | flag | dset
     auto al = [](size_t b) { return (b + 255) / 256 * 256; };
     const size_t b_runs = al(k * sizeof(KRun)), b_flat = al((2 * k + 2) * sizeof(u64));
+    const size_t b_cf = al((k + 1) * sizeof(u64));
     const size_t b_ss = al((T + 1) * 8), b_ds = al((T + 1) * 2 * k * 4), b_tab = al((size_t)k * KNT * 8);
-    const size_t bytes = b_runs + b_flat + b_ss + b_ds + 2 * b_tab + 256;
+    u64 dset_n = 1024;  // a power of two at least twice the dots: probes stay short
+    while (dset_n < 2 * n_dots) dset_n <<= 1;
+    const size_t b_dset = dotsmask ? al(dset_n * 8) : 0;
+    const size_t bytes = b_runs + b_flat + b_cf + b_ss + b_ds + 2 * b_tab + 256 + b_dset;
     TRY(ensure_state(e, T + 2));
     TRY(ensure_tmp(e, bytes));
-    const size_t hb = b_runs + b_flat;
+    const size_t hb = b_runs + b_flat + b_cf;
     if (hb > e->h_stage_cap) {
       HIP_TRY(hipStreamSynchronize(e->stream));
       if (e->h_stage) HIP_TRY(hipHostFree(e->h_stage));
@@ -1106,17 +1114,26 @@ int kfold_pass(dg_engine* e, const dg_store* state, const dg_context* ctx, int k
     for (int i = 0; i < k; i++) hf[i + 1] = hf[i] + chunks(deltas[i].n);
     for (int i = 0; i < k; i++) hf[k + i + 1] = hf[k + i] + chunks(hr[i].n_keys);
     hf[2 * k + 1] = hf[2 * k] + chunks(state->n);
+    u64* hc = (u64*)((char*)e->h_stage + b_runs + b_flat);
+    hc[0] = 0;
+    for (int i = 0; i < k; i++) hc[i + 1] = hc[i] + (((dotsmask >> i) & 1) ? dctxs[i].n : 0);
     char* d = (char*)e->tmp;
     KFoldArgs p{};
     p.s = rows_of(state);
     p.c0 = ctx_of(ctx);
     p.runs = (const KRun*)d;
     p.flat = (const u64*)(d + b_runs);
-    p.sstart = (u64*)(d + b_runs + b_flat);
-    p.dstart = (u32*)(d + b_runs + b_flat + b_ss);
-    p.tabC = (u64*)(d + b_runs + b_flat + b_ss + b_ds);
-    p.tabP = (u64*)(d + b_runs + b_flat + b_ss + b_ds + b_tab);
-    p.flag = (u32*)(d + b_runs + b_flat + b_ss + b_ds + 2 * b_tab);
+    p.cflat = (const u64*)(d + b_runs + b_flat);
+    char* d2 = d + b_runs + b_flat + b_cf;
+    p.sstart = (u64*)d2;
+    p.dstart = (u32*)(d2 + b_ss);
+    p.tabC = (u64*)(d2 + b_ss + b_ds);
+    p.tabP = (u64*)(d2 + b_ss + b_ds + b_tab);
+    p.flag = (u32*)(d2 + b_ss + b_ds + 2 * b_tab);
+    p.dotsmask = dotsmask;
+    p.dset = dotsmask ? (u64*)(d2 + b_ss + b_ds + 2 * b_tab + 256) : nullptr;
+    p.dset_mask = dset_n - 1;
+    p.dset_n = hc[k];
     p.k = k;
     p.allmask = allmask;
     p.T = T;
@@ -1127,8 +1144,10 @@ int kfold_pass(dg_engine* e, const dg_store* state, const dg_context* ctx, int k
     p.out_ctx_cnt = out_ctx->cnt;
     p.d_counts = e->d_counts;
     HIP_TRY(hipMemcpyAsync(d, e->h_stage, hb, hipMemcpyHostToDevice, e->stream));
-    // start tables (empty runs keep 0), VV tables (absent node = 0) and the flag
+    // start tables (empty runs keep 0), VV tables (absent node = 0) and the flag; the
+    // dot set's slots empty (all ones)
     HIP_TRY(hipMemsetAsync(p.sstart, 0, b_ss + b_ds + 2 * b_tab + 256, e->stream));
+    if (dotsmask) HIP_TRY(hipMemsetAsync(p.dset, 0xFF, dset_n * 8, e->stream));
     TRY(next_scan(e, &p.scan));
     HIP_TRY(launch_kfold(p, e->stream));
     HIP_TRY(hipMemcpyAsync(&e->h_counts[10], p.flag, sizeof(u32), hipMemcpyDeviceToHost, e->stream));

@@ -124,7 +124,19 @@ struct KFoldArgs {
   Scan scan;
   u64* d_counts;       // [0] output rows, [1] output context entries
   u32* flag;           // KF_* bits: the caller must re-run the fold step by step
+  // dot-set contexts (MapSet deltas of add/remove, aw_lww_map.ex:124-146): bit i of
+  // dotsmask = c_i is a dot set; its dots go to an open-addressing hash set of
+  // (i, node, counter) keys (kfold_dset_kernel), so "c_i covers the dot" stays one
+  // probe -- tabC[i] then holds c_i's per-node max, which is what Dots.union folds into
+  // the VV prefix unions (aw_lww_map.ex:45-52)
+  u64 dotsmask;
+  u64* dset;           // dset_mask + 1 entries, KF_EMPTY when unused
+  u64 dset_mask;
+  const u64* cflat;    // k + 1: prefix sums of the dot-set contexts' sizes (VV: 0)
+  u64 dset_n;          // their total (host copy of cflat[k])
 };
+constexpr u64 KF_EMPTY = ~0ull;
+constexpr u64 KF_CNT_LIMIT = (1ull << 48) - 1;  // dot-set counters below this pack into a key
 hipError_t launch_kfold(const KFoldArgs& p, hipStream_t st);
 
 // ---- take.hip (sync-delta values: Map.take(value, keys))

@@ -59,6 +59,29 @@ __device__ __forceinline__ u64 vv_at(const u64* tab, u32 i, u32 node) {
   return node < (u32)KNT ? tab[(u64)i * KNT + node] : 0ull;
 }
 
+// the hash set of the dot-set contexts' dots: key (cnt << 16) | (node << 6) | i
+__device__ __forceinline__ u64 dset_key(u32 i, u32 node, u64 cnt) {
+  return (cnt << 16) | ((u64)node << 6) | (u64)i;
+}
+__device__ __forceinline__ u64 dset_slot(u64 key, u64 mask) {
+  u64 x = key * 0x9E3779B97F4A7C15ull;
+  return (x ^ (x >> 29)) & mask;
+}
+// c_i covers (node, cnt): a VV entry >= cnt, or the dot in c_i's set (one probe, more
+// only on a collision: the table is at most half full)
+template <bool DOTS>
+__device__ __forceinline__ bool covers(const u64* tabC, const KFoldArgs& p, u32 i, u32 node, u64 cnt,
+                                       u64 vv) {
+  if (!DOTS || !((p.dotsmask >> i) & 1)) return vv >= cnt;
+  if (node >= (u32)KNT || cnt >= KF_CNT_LIMIT) return false;  // never inserted
+  const u64 key = dset_key(i, node, cnt);
+  for (u64 h = dset_slot(key, p.dset_mask);; h = (h + 1) & p.dset_mask) {
+    const u64 x = p.dset[h];
+    if (x == key) return true;
+    if (x == KF_EMPTY) return false;
+  }
+}
+
 // P after the touching deltas (bits of K | R, in delta order; see the header), for a
 // thread's two candidates (its state row and its item) at once: the
 // table reads of both are issued before either is evaluated, so the two candidates cost
@@ -71,8 +94,9 @@ struct Cand {
   u32 node;
   u64 cnt;
 };
+template <bool DOTS>
 __device__ __forceinline__ void present2(Cand& a, bool da, Cand& b, bool db, const u64* tabC,
-                                         const u64* tabP) {
+                                         const u64* tabP, const KFoldArgs& p) {
   u64 ba = da ? (a.K | a.R) : 0ull, bb = db ? (b.K | b.R) : 0ull;
   while (ba | bb) {
     u32 ia[PB2], ib[PB2];
@@ -99,12 +123,16 @@ __device__ __forceinline__ void present2(Cand& a, bool da, Cand& b, bool db, con
       if (j < na) {
         const u32 i = ia[j];
         const bool inD = (a.M >> i) & 1;
-        a.P = ((a.K >> i) & 1) ? (a.P ? (inD || ca[j] < a.cnt) : (inD && qa[j] < a.cnt)) : inD;
+        a.P = ((a.K >> i) & 1) ? (a.P ? (inD || !covers<DOTS>(tabC, p, i, a.node, a.cnt, ca[j]))
+                                      : (inD && qa[j] < a.cnt))
+                               : inD;
       }
       if (j < nb) {
         const u32 i = ib[j];
         const bool inD = (b.M >> i) & 1;
-        b.P = ((b.K >> i) & 1) ? (b.P ? (inD || cb[j] < b.cnt) : (inD && qb[j] < b.cnt)) : inD;
+        b.P = ((b.K >> i) & 1) ? (b.P ? (inD || !covers<DOTS>(tabC, p, i, b.node, b.cnt, cb[j]))
+                                      : (inD && qb[j] < b.cnt))
+                               : inD;
       }
     }
   }
@@ -132,13 +160,19 @@ __device__ __forceinline__ void kfold_prep(const KFoldArgs& p) {
   }
   for (int i = n / WAVE; i < k; i += KNT / WAVE) {  // one wave per delta context
     const Ctx c = p.runs[i].ctx;
+    const bool dots = (p.dotsmask >> i) & 1;  // a dot set: its per-node max (several lanes
+                                              // may meet one node: atomicMax)
     for (u64 e = n % WAVE; e < c.n; e += WAVE) {
       const u32 nd = c.node[e];
-      if (nd >= (u32)KNT) {
+      const u64 cn = c.cnt[e];
+      if (nd >= (u32)KNT || (dots && cn >= KF_CNT_LIMIT)) {
         atomicOr(p.flag, KF_PREP_FAIL);
         continue;
       }
-      p.tabC[(u64)i * KNT + nd] = c.cnt[e];
+      if (dots)
+        atomicMax((unsigned long long*)&p.tabC[(u64)i * KNT + nd], (unsigned long long)cn);
+      else
+        p.tabC[(u64)i * KNT + nd] = cn;
       pres[nd] = 1;
     }
   }
@@ -272,6 +306,37 @@ __global__ __launch_bounds__(FILL_BLOCK) void kfold_fill_kernel(KFoldArgs p) {
   }
 }
 
+// ------------------------------------------------------------------------ dot sets
+// Every dot of the dot-set contexts into the hash set (one thread per dot; the context of
+// dot j by a search of the k + 1 prefix sums).  Linear probing with atomicCAS; a dot is
+// inserted once (a MapSet holds it once; a duplicate would find itself).
+constexpr int DSB = 256;
+__global__ __launch_bounds__(DSB) void kfold_dset_kernel(KFoldArgs p) {
+  const u64 j = (u64)blockIdx.x * DSB + threadIdx.x;
+  const u64 total = p.cflat[p.k];
+  if (j >= total) return;
+  int lo = 0, hi = p.k;  // cflat[lo] <= j < cflat[lo + 1]
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (p.cflat[mid] <= j)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  while (p.cflat[lo + 1] <= j) lo++;  // empty contexts between
+  const Ctx c = p.runs[lo].ctx;
+  const u64 e = j - p.cflat[lo];
+  const u32 nd = c.node[e];
+  const u64 cn = c.cnt[e];
+  if (nd >= (u32)KNT || cn >= KF_CNT_LIMIT) return;  // the prep flags it: stepwise
+  const u64 key = dset_key((u32)lo, nd, cn);
+  for (u64 h = dset_slot(key, p.dset_mask);; h = (h + 1) & p.dset_mask) {
+    const u64 old = atomicCAS((unsigned long long*)&p.dset[h], (unsigned long long)KF_EMPTY,
+                              (unsigned long long)key);
+    if (old == KF_EMPTY || old == key) return;
+  }
+}
+
 // ------------------------------------------------------------------------ main
 #ifdef DG_STAMPS
 // Diagnostic build only (DG_STAMPS=1): per-bucket phase timestamps (s_memrealtime) by
@@ -383,7 +448,9 @@ __device__ __forceinline__ void scan_excl(V* in, u32 n, unsigned short* pre, u32
   if (threadIdx.x == 0) pre[n] = (unsigned short)tot;
 }
 
-// two 1024-thread buckets per CU: 8 waves per SIMD, so at most 64 VGPRs
+// two 1024-thread buckets per CU: 8 waves per SIMD, so at most 64 VGPRs.  DOTS: some delta
+// contexts are dot sets (their coverage through the hash set)
+template <bool DOTS>
 __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256, 8))) void kfold_kernel(KFoldArgs p) {
   __shared__ KLds s;
   if (*p.flag & KF_PREP_FAIL) return;  // every workgroup leaves: no ticket is taken
@@ -665,7 +732,7 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
     cu.cnt = r.cnt;
   }
   KSTAMP(t, 7);
-  present2(cs, ds, cu, du, p.tabC, p.tabP);
+  present2<DOTS>(cs, ds, cu, du, p.tabC, p.tabP, p);
   const bool ss_ = ds && cs.P, us_ = (u32)tid < nU && du && cu.P;
   if (ds) s.y.e.ssurv[tid] = ss_;
   if ((u32)tid < nU) s.y.e.usurv[tid] = us_;
@@ -762,10 +829,17 @@ extern "C" int dg_debug_kfold_stamps(unsigned long long* host, size_t n) {
 #endif
 
 hipError_t launch_kfold(const KFoldArgs& p, hipStream_t st) {
+  if (p.dotsmask) {  // the host set p.dset to KF_EMPTY and passes the contexts' total in dset_n
+    const u64 n = p.dset_n;
+    if (n) hipLaunchKernelGGL(kfold_dset_kernel, dim3((u32)((n + DSB - 1) / DSB)), dim3(DSB), 0, st, p);
+  }
   // prep + delta fill + the state's starts
   const u64 g = 1 + fill_blocks(p.n_fill_chunks) + (p.T + FILL_WAVES) / FILL_WAVES;
   hipLaunchKernelGGL(kfold_fill_kernel, dim3((u32)g), dim3(FILL_BLOCK), 0, st, p);
-  hipLaunchKernelGGL(kfold_kernel, dim3((u32)p.T), dim3(KB), 0, st, p);
+  if (p.dotsmask)
+    hipLaunchKernelGGL(kfold_kernel<true>, dim3((u32)p.T), dim3(KB), 0, st, p);
+  else
+    hipLaunchKernelGGL(kfold_kernel<false>, dim3((u32)p.T), dim3(KB), 0, st, p);
   return hipGetLastError();
 }
 

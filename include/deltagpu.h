@@ -251,8 +251,9 @@ int dg_joink(dg_engine* e, int k, const dg_store* stores, const dg_context* ctxs
  * keys[i] (device, ascending unique, n_keys[i] entries) or keys == NULL / keys[i] ==
  * NULL for a full-state join of that delta.  out->cap >= state->n + Σ deltas[i].n,
  * out_ctx->cap >= ctx->n + Σ dctxs[i].n.  Synchronous.
- * Runs as ONE pass over the state per 64 deltas when every context is a VV with node
- * ids < 1024 and the key ids are spread like hashes (the interned form); otherwise,
+ * Runs as ONE pass over the state per 64 deltas when the state's context is a VV, every
+ * context names node ids < 1024 only, dot-set contexts (mutation deltas) have counters
+ * below 2^48 - 1, and the key ids are spread like hashes (the interned form); otherwise,
  * and always with DG_APPLY_MODE=fold in the environment at engine creation, as k
  * dg_join2 steps through engine scratch.  Both give the same rows. */
 int dg_apply_deltas(dg_engine* e, const dg_store* state, const dg_context* ctx, int k,

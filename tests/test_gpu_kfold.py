@@ -12,7 +12,7 @@ import pytest
 from delta_crdt_ex_amd import workloads as W
 from delta_crdt_ex_amd._abi import DeltaGpuError
 from delta_crdt_ex_amd.store import Engine
-from kfold_cases import random_fold
+from kfold_cases import mutation_fold, random_fold
 from oracle import ref as R
 from test_gpu_configs import keys_dev
 from test_gpu_parity import DEV, ctx_eq, rows_eq, up
@@ -138,6 +138,29 @@ def test_stepwise_fallback(engine, strict, case):
     with pytest.raises(DeltaGpuError, match="one-pass fold not applicable"):
         run(strict, st, ds)
     check(engine, st, ds)
+
+
+@pytest.mark.parametrize("seed,k", [(40, 1), (41, 5), (42, 16), (43, 64)])
+def test_onepass_dot_set_contexts(strict, seed, k):
+    """Mutation deltas (MapSet contexts, aw_lww_map.ex:124-146) folded in ONE pass (the
+    strict engine refuses the stepwise fold): their dots go to the device hash set, their
+    per-node maxima into the VV prefix unions (they used to fall back)."""
+    st, ds = mutation_fold(seed, n_keys=20_000, k=k, ops=400)
+    assert all(d["ctx"][0] == 1 for d in ds)
+    check(strict, st, ds)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_onepass_mixed_contexts(strict, seed):
+    """Random folds whose deltas carry dot sets, and dot sets mixed with version vectors
+    (sync deltas and mutation deltas in one batch), crowded keys included."""
+    st, ds = random_fold(50 + seed, n_keys=2000, k=12, delta_dots=True)
+    check(strict, st, ds)
+    st2, ds2 = random_fold(60 + seed, n_keys=600, k=20, rows_per_key=6, p_keys=0.3, p_take=0.7)
+    _, dd = random_fold(70 + seed, n_keys=600, k=20, rows_per_key=6, p_keys=0.3, p_take=0.7,
+                        delta_dots=True)
+    mixed = [ds2[i] if i % 2 else dict(ds2[i], ctx=dd[i]["ctx"]) for i in range(20)]
+    check(strict, st2, mixed)
 
 
 def test_config3_onepass(strict):
