@@ -201,13 +201,14 @@ static const char* OP_NAMES[N_OPS] = {"read", "add", "update", "remove"};
 /* ================================================================ the GPU path */
 typedef struct {
   dg_engine* e;
-  dg_store st, spare, taken;
+  dg_store st, spare;
   dg_context ctx;
   dg_merkle tree;
   uint64_t* d_msg;    /* the packed delta: key | val | ts | cnt | dcnt | keyset | node | dnode */
   uint64_t* h_msg;
   uint64_t msg_words;
   uint64_t *changed, *h_back;  /* the changed keys; host copy of keys + rows */
+  uint64_t* d_back;            /* rows + keys, packed for one copy home */
   uint64_t back_cap;
   uint64_t *rk, *rv, *h_rk;    /* read/1 output */
 } gpu;
@@ -235,8 +236,8 @@ static void gpu_upload(gpu* g, hrows* r) {
   DG(dg_buffer_alloc(g->e, g->msg_words * 8, (void**)&g->d_msg));
   g->h_msg = calloc(g->msg_words, 8);
   g->back_cap = 2048;
-  DG(dg_buffer_alloc(g->e, g->back_cap * 8, (void**)&g->changed));
-  DG(dg_store_alloc(g->e, g->back_cap, &g->taken));
+  DG(dg_buffer_alloc(g->e, g->back_cap * 6 * 8, (void**)&g->d_back));
+  g->changed = g->d_back;  /* the changed keys open the block */
   g->h_back = calloc(g->back_cap * 6, 8);
   DG(dg_buffer_alloc(g->e, (r->n + 16384) * 8, (void**)&g->rk));
   DG(dg_buffer_alloc(g->e, (r->n + 16384) * 8, (void**)&g->rv));
@@ -279,16 +280,14 @@ static void gpu_apply(gpu* g, const uint64_t* key, const uint64_t* val, const in
                    g->changed, g->back_cap, &n_changed, &swapped));
   const double t2 = now_us();
   if (n_changed) {
-    g->taken.n = 0;
-    DG(dg_take_keys(g->e, &g->st, g->changed, n_changed, &g->taken));
-    const uint64_t nt = g->taken.n;
-    DG(dg_copy_to_host(g->e, g->h_back, g->changed, n_changed * 8));
-    if (nt) {
-      dg_store hb = {g->h_back + g->back_cap, g->h_back + 2 * g->back_cap,
-                     (int64_t*)(g->h_back + 3 * g->back_cap), (uint32_t*)(g->h_back + 5 * g->back_cap),
-                     g->h_back + 4 * g->back_cap, 0, g->back_cap};
-      DG(dg_store_download(g->e, &g->taken, &hb));
-    }
+    /* the changed keys (written there by dg_join_delta) and their rows (dg_take_keys) in
+     * ONE device block -- keys | key | val | ts | cnt | node, the row columns at stride S
+     * (64 for a few keys, back_cap otherwise) -- and one copy of it home */
+    const uint64_t S = n_changed <= 16 ? 64 : g->back_cap;
+    uint64_t* b = g->d_back + g->back_cap;
+    dg_store tk = {b, b + S, (int64_t*)(b + 2 * S), (uint32_t*)(b + 4 * S), b + 3 * S, 0, S};
+    DG(dg_take_keys(g->e, &g->st, g->changed, n_changed, &tk));
+    DG(dg_copy_to_host(g->e, g->h_back, g->d_back, (g->back_cap + 5 * S) * 8));
   }
   const double t3 = now_us();
   t[0] = t1 - t0;

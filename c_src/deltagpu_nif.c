@@ -270,9 +270,12 @@ typedef struct {
   dg_context rawc, ctx;
   uint64_t* keys;           /* the keyset */
   uint64_t keys_cap;
-  uint64_t* changed;        /* dg_join_delta's changed keys */
-  uint64_t changed_cap;
-  dg_store taken;           /* their rows (dg_take_keys) */
+  /* the return block: dg_join_delta's changed keys [0, back_cap), then their rows
+   * (dg_take_keys) as key | val | ts | cnt | node columns at stride back_cap -- brought
+   * home with ONE copy */
+  uint64_t* back;
+  uint64_t back_cap;
+  uint64_t* h_back;         /* its host copy (enif_alloc) */
 } delta_buf;
 
 struct state_res {
@@ -316,11 +319,11 @@ static void state_dtor(ErlNifEnv* env, void* obj) {
   dg_context_free(g->e, &s->ctx);
   dg_store_free(g->e, &s->d.raw);
   dg_store_free(g->e, &s->d.rows);
-  dg_store_free(g->e, &s->d.taken);
   dg_context_free(g->e, &s->d.rawc);
   dg_context_free(g->e, &s->d.ctx);
   dg_buffer_free(g->e, s->d.keys);
-  dg_buffer_free(g->e, s->d.changed);
+  dg_buffer_free(g->e, s->d.back);
+  if (s->d.h_back) enif_free(s->d.h_back);
   if (s->has_tree) {
     dg_buffer_free(g->e, s->tree.nodes);
     dg_buffer_free(g->e, s->tree.counts);
@@ -550,6 +553,23 @@ static int grow_buf(engine_res* g, uint64_t** p, uint64_t* cap, uint64_t n) {
   return rc;
 }
 
+/* the return block for n changed keys and up to `rows` of their rows (6 x cap words) */
+static int grow_back(engine_res* g, delta_buf* d, uint64_t n) {
+  if (d->back && d->back_cap >= n) return DG_OK;
+  dg_buffer_free(g->e, d->back);
+  if (d->h_back) enif_free(d->h_back);
+  d->back = NULL;
+  d->h_back = NULL;
+  const uint64_t c = n + 64;
+  d->back_cap = 0;
+  int rc = dg_buffer_alloc(g->e, 6 * c * 8, (void**)&d->back);
+  if (rc) return rc;
+  d->h_back = (uint64_t*)enif_alloc(6 * c * 8);
+  if (!d->h_back) return DG_E_NOMEM;
+  d->back_cap = c;
+  return DG_OK;
+}
+
 /* rows already in (key, val, ts, node, cnt) order without duplicates, a context in
  * (node, cnt) order: a delta built by add/remove (one key, its dots) usually is */
 static int rows_sorted(const dg_store* s) {
@@ -708,22 +728,26 @@ static int u_dot(void* ud, uint32_t node, uint64_t cnt) {
   return 0;
 }
 
+/* host rows -> %{key => value map} */
+static int unmarshal_host_rows(ErlNifEnv* env, engine_res* g, const dg_store* h, ERL_NIF_TERM* out) {
+  unm u;
+  memset(&u, 0, sizeof u);
+  u.env = env;
+  u.g = g;
+  u.out = enif_make_new_map(env);
+  dgm_walk w = {u_key, u_entry, u_dot};
+  const int rc = dgm_walk_rows(h, &w, &u);
+  close_key(&u);
+  *out = u.out;
+  return rc;
+}
+
 /* device rows -> %{key => value map} (host copy of just those rows) */
 static int unmarshal_rows(ErlNifEnv* env, engine_res* g, const dg_store* dev, ERL_NIF_TERM* out) {
   dgm_rows h;
   int rc = dgm_rows_init(&h, dev->n, 1);
   if (rc) return rc;
-  if (!(rc = dg_store_download(g->e, dev, &h.s))) {
-    unm u;
-    memset(&u, 0, sizeof u);
-    u.env = env;
-    u.g = g;
-    u.out = enif_make_new_map(env);
-    dgm_walk w = {u_key, u_entry, u_dot};
-    rc = dgm_walk_rows(&h.s, &w, &u);
-    close_key(&u);
-    *out = u.out;
-  }
+  if (!(rc = dg_store_download(g->e, dev, &h.s))) rc = unmarshal_host_rows(env, g, &h.s, out);
   dgm_rows_free(&h);
   return rc;
 }
@@ -830,36 +854,43 @@ static ERL_NIF_TERM join_delta(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
     s->ctx = nctx;
     memset(&nctx, 0, sizeof nctx);
   }
-  TRY(grow_buf(g, &d->changed, &d->changed_cap, n_keys ? n_keys : 1));
+  TRY(grow_back(g, d, n_keys ? n_keys : 1));
   if (s->has_tree) TRY(refresh_terms(g));
   /* update_state_with_delta: the join (in place, or through the spare buffer: the structs
    * come back exchanged), the changed keys, the MerkleMap put/delete of them -- all or
    * nothing: on an error the state, its context and tree are as they were */
   TRY(dg_join_delta(g->e, &s->rows, &s->ctx, &d->rows, &d->ctx, d->keys, n_keys, &s->spare,
-                    s->has_tree ? &s->tree : NULL, d->changed, d->changed_cap, &n_changed, &swapped));
-  /* the changed keys' new value maps (dg_take_keys into the kept buffer, grown to the
-   * size the first try reports), and the keys that vanished */
-  TRY(grow_store(g, &d->taken, 2 * n_changed + 16));
-  rc = dg_take_keys(g->e, &s->rows, d->changed, n_changed, &d->taken);
-  if (rc == DG_E_CAPACITY) {
-    const uint64_t need = d->taken.n;
-    TRY(grow_store(g, &d->taken, need));
-    rc = dg_take_keys(g->e, &s->rows, d->changed, n_changed, &d->taken);
-  }
-  TRY(rc);
-  TRY(unmarshal_rows(env, g, &d->taken, &values));
-  TRY(unmarshal_dots(env, g, &s->ctx, &new_dots));
-  {
-    uint64_t* hk = (uint64_t*)enif_alloc((n_changed ? n_changed : 1) * 8);
-    rc = dg_copy_to_host(g->e, hk, d->changed, n_changed * 8);
-    for (uint64_t i = n_changed; !rc && i-- > 0;) {
-      const boxed* b = (const boxed*)dgm_key_term(g->u, hk[i]);
-      ERL_NIF_TERM k = enif_make_copy(env, b->t), v;
-      if (!enif_get_map_value(env, values, k, &v)) v = A_NIL;
-      changed_terms = enif_make_list_cell(env, enif_make_tuple2(env, k, v), changed_terms);
+                    s->has_tree ? &s->tree : NULL, d->back, d->back_cap, &n_changed, &swapped));
+  /* the changed keys' new value maps: their rows taken into the return block (grown and
+   * retaken if a key holds more rows than the block's stride), the block copied home once */
+  for (int attempt = 0;; attempt++) {
+    const uint64_t S = d->back_cap;
+    uint64_t* b = d->back + S;
+    dg_store tk = {b, b + S, (int64_t*)(b + 2 * S), (uint32_t*)(b + 4 * S), b + 3 * S, 0, S};
+    rc = dg_take_keys(g->e, &s->rows, d->back, n_changed, &tk);
+    if (rc == DG_E_CAPACITY && attempt == 0) {
+      /* grow keeping the changed keys: move them through the host */
+      uint64_t* keep = (uint64_t*)enif_alloc((n_changed ? n_changed : 1) * 8);
+      TRY(dg_copy_to_host(g->e, keep, d->back, n_changed * 8));
+      rc = grow_back(g, d, tk.n > n_changed ? tk.n : n_changed);
+      if (!rc) rc = dg_copy_to_device(g->e, d->back, keep, n_changed * 8);
+      enif_free(keep);
+      TRY(rc);
+      continue;
     }
-    enif_free(hk);
-    if (rc) goto out;
+    TRY(rc);
+    TRY(dg_copy_to_host(g->e, d->h_back, d->back, (S + 5 * S) * 8));
+    uint64_t* hb = d->h_back + S;
+    dg_store hs = {hb, hb + S, (int64_t*)(hb + 2 * S), (uint32_t*)(hb + 4 * S), hb + 3 * S, tk.n, S};
+    TRY(unmarshal_host_rows(env, g, &hs, &values));
+    break;
+  }
+  TRY(unmarshal_dots(env, g, &s->ctx, &new_dots));
+  for (uint64_t i = n_changed; i-- > 0;) {
+    const boxed* b = (const boxed*)dgm_key_term(g->u, d->h_back[i]);
+    ERL_NIF_TERM k = enif_make_copy(env, b->t), v;
+    if (!enif_get_map_value(env, values, k, &v)) v = A_NIL;
+    changed_terms = enif_make_list_cell(env, enif_make_tuple2(env, k, v), changed_terms);
   }
 out:
   r = rc ? error_term(env, rc) : enif_make_tuple3(env, A_OK, new_dots, changed_terms);

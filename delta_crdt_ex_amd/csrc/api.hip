@@ -27,7 +27,7 @@ struct dg_engine {
   u64* state = nullptr;
   u64 state_cap = 0;
   u32* ticket = nullptr;  // [0] ticket, [1] error bits, [2] store_check flag, [3] op order flag,
-                          // [4] join abort epoch
+                          // [4] join abort epoch, [6] the Merkle build/update arrival counter
                           // (16 words right behind d_counts: one allocation, see below)
   u32* counts = nullptr;  // single-pass join tile-count granules
   u32* started = nullptr;  // single-pass join start flags (JOIN_MAX_GRID epochs)
@@ -250,6 +250,8 @@ int sync_words(dg_engine* e) {
   return DG_OK;
 }
 
+constexpr int MERKLE_ARRIVE = 6;  // ticket word: the Merkle kernels' arrival counter
+
 int read_counts(dg_engine* e, int n) {
   (void)n;
   const int rc = sync_words(e);
@@ -258,6 +260,7 @@ int read_counts(dg_engine* e, int n) {
   memcpy(&err, (const char*)&e->h_counts[8] + sizeof(u32), sizeof(u32));
   if (err) {
     HIP_TRY(hipMemsetAsync(e->ticket, 0, 4 * sizeof(u32), e->stream));
+    HIP_TRY(hipMemsetAsync(e->ticket + MERKLE_ARRIVE, 0, sizeof(u32), e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
     return fail(DG_E_DEVICE, "a kernel timed out or a join grid aborted (error bits 0x%x)", err);
   }
@@ -569,13 +572,13 @@ int tree_update(dg_engine* e, dg_merkle* t, const dg_store* olds, const dg_store
                 u64* d_n_keys) {
   const u64 chunks = merkle_chunks(t->depth), cw = merkle_ctr_words(t->depth);
   TRY(ensure_tmp(e, (cw + chunks) * sizeof(u32)));
-  u32* ctr = (u32*)e->tmp;
-  u32* dirty = ctr + cw;
+  u64* hand = (u64*)e->tmp;
+  u32* dirty = (u32*)e->tmp + cw;
   if (!ready)
     HIP_TRY(launch_splice_finish(nullptr, nullptr, 0, nullptr, nullptr, dirty, chunks, e->d_counts,
                                  e->ticket + 3, e->stream));
   HIP_TRY(launch_merkle_update(merkle_of(t), rows_of(olds), rows_of(news), keys, n_keys, dirty,
-                               e->d_counts, ctr, e->ticket + 3, e->stream));
+                               e->d_counts, e->ticket + MERKLE_ARRIVE, hand, e->ticket + 3, e->stream));
   TRY(tail());
   TRY(read_counts(e, 8));
   u64 dk = 0;
@@ -587,7 +590,7 @@ int tree_update(dg_engine* e, dg_merkle* t, const dg_store* olds, const dg_store
   HIP_TRY(launch_splice_finish(nullptr, nullptr, 0, nullptr, nullptr, dirty, chunks, e->d_counts,
                                e->ticket + 3, e->stream));
   HIP_TRY(launch_merkle_update(merkle_of(t), rows_of(news), rows_of(olds), keys, n_keys, dirty,
-                               e->d_counts, ctr, e->ticket + 3, e->stream));
+                               e->d_counts, e->ticket + MERKLE_ARRIVE, hand, e->ticket + 3, e->stream));
   HIP_TRY(hipMemsetAsync(e->ticket + 3, 0, sizeof(u32), e->stream));  // the undo's own bits
   TRY(read_counts(e, 0));
   g_err = msg;
@@ -1437,8 +1440,8 @@ int merkle_build_enqueue(dg_engine* e, const dg_store* s, dg_merkle* t, uint64_t
   TRY(set_device(e));
   TRY(ensure_tmp(e, merkle_ctr_words(t->depth) * sizeof(u32)));
   HIP_TRY(hipMemsetAsync(e->ticket + 3, 0, sizeof(u32), e->stream));
-  HIP_TRY(launch_merkle_build(rows_of(s), merkle_of(t), d_n_keys, (u32*)e->tmp, e->ticket + 3,
-                              e->stream));
+  HIP_TRY(launch_merkle_build(rows_of(s), merkle_of(t), d_n_keys, e->ticket + MERKLE_ARRIVE,
+                              (u64*)e->tmp, e->ticket + 3, e->stream));
   return DG_OK;
 }
 

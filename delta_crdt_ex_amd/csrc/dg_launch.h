@@ -277,21 +277,22 @@ constexpr u32 MERKLE_UPL = 11;  // levels reduced per upsweep workgroup
 constexpr u32 MERKLE_ERR_SHARD = 2u, MERKLE_ERR_COUNT = 4u;
 constexpr u32 MERKLE_INPUT_ERR = MERKLE_ERR_SHARD | MERKLE_ERR_COUNT;
 inline u64 merkle_chunks(u32 depth) { return 1ull << (depth - (depth < MERKLE_UPL ? depth : MERKLE_UPL)); }
-// scratch u32 words of a build / update: the arrival counter (16 words) + a u64 chunk
-// root and a u64 key count per chunk (the in-launch hand-off)
-inline u64 merkle_ctr_words(u32 depth) { return 16 + 4 * merkle_chunks(depth); }
+// scratch words of a build / update: a u64 chunk root and a u64 key count per chunk (the
+// in-launch hand-off), in u32 units
+inline u64 merkle_ctr_words(u32 depth) { return 4 * merkle_chunks(depth); }
 // one fused launch: rows hashed into LDS bucket sums per chunk, levels reduced, the last
-// chunk reduces to the root; *d_keys = distinct keys; ctr: merkle_ctr_words(depth) u32
-// of scratch; err bit 1: a row outside the tree's shard.
-hipError_t launch_merkle_build(const Rows& s, const MerkleT& t, u64* d_keys, u32* ctr, u32* err,
-                               hipStream_t st);
+// chunk reduces to the root; *d_keys = distinct keys; arrive: a persistent counter, zero
+// on entry and left zero; hand: merkle_ctr_words(depth) u32 of scratch; err bit 1: a row
+// outside the tree's shard.
+hipError_t launch_merkle_build(const Rows& s, const MerkleT& t, u64* d_keys, u32* arrive, u64* hand,
+                               u32* err, hipStream_t st);
 // put/delete of the changed keys + update_hashes; dirty: merkle_chunks(depth) u32, zero
 // on entry; d_keys[0, 8) (zero on entry) sum to the change in distinct keys.  The update
 // adds (new leaf - old leaf) and (new rows - old rows) per key, so the same launch with
 // olds and news exchanged undoes it bit for bit (keys outside the shard are skipped both
 // ways; counts wrap mod 2^32 and unwrap).
 hipError_t launch_merkle_update(const MerkleT& t, const Rows& olds, const Rows& news, const u64* keys,
-                                u64 n_keys, u32* dirty, u64* d_keys, u32* ctr, u32* err,
+                                u64 n_keys, u32* dirty, u64* d_keys, u32* arrive, u64* hand, u32* err,
                                 hipStream_t st);
 constexpr int DIFF_BLOCK = 256;
 constexpr u32 DIFF_SUB = 12;  // levels a diff workgroup descends: subtrees of 4096 buckets

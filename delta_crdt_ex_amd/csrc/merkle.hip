@@ -171,8 +171,9 @@ __device__ void lds_upsweep(u64* nodes, u32 hi, u64 g0, u32 width, u64* s) {
   }
 }
 
-// scratch: ctr[0] the arrival counter (zeroed before the launch), then per chunk its
-// root and its distinct-key count (u64 each, at hand[0, G) and hand[G, 2G)).
+// ctr: the arrival counter, zero on entry and left zero (the last workgroup resets it: a
+// persistent engine word, no fill launch per build); scratch: per chunk its root and its
+// distinct-key count (u64 each, at hand[0, G) and hand[G, 2G)).
 template <bool BUILD, bool VEC = false>
 __global__ __launch_bounds__(UPB, 4) void merkle_chunk_kernel(Rows rows, MT t, const u32* dirty,
                                                            u32* ctr, u64* hand, u64* d_keys,
@@ -341,6 +342,7 @@ __global__ __launch_bounds__(UPB, 4) void merkle_chunk_kernel(Rows rows, MT t, c
     if (BUILD) st_sc1(hand + G + g, chunk_keys);
     wait_vmem();
     s_last = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1;
+    if (s_last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // all G arrived
   }
   __syncthreads();
   if (!s_last) return;
@@ -495,8 +497,9 @@ __device__ u32 merge_bucket(const Rows& A, const TermH& tha, u64 ia, u64 ie, con
 constexpr int DB = DIFF_BLOCK;
 constexpr u32 XSUB = 1u << DIFF_SUB;  // buckets per subtree (at most)
 constexpr u32 OWN = XSUB / DB;        // buckets per thread
-constexpr u32 RCAP = 1792;            // rows of the differing buckets staged in LDS
-constexpr u32 DCAP = 512;             // differing buckets listed in LDS (36.9 KB in all:
+constexpr u32 RCAP = 1664;            // rows of the differing buckets staged in LDS
+constexpr u32 DCAP = 512;             // differing buckets listed in LDS
+constexpr u32 NHD = 128;              // node term hashes staged per tree (38.9 KB in all:
                                       // 4 workgroups per CU)
 static_assert(OWN == 16, "a thread owns 16 buckets: two 16-byte count loads per tree");
 
@@ -538,9 +541,15 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
   __shared__ u32 s_dp[DCAP + 1];          // its first staged row
   __shared__ u32 s_dn[DCAP];              // its rows in A (high half) and B (low half)
   __shared__ u64 s_k[RCAP], s_h[RCAP];    // the staged rows' keys and row hashes
+  __shared__ u64 s_nha[NHD], s_nhb[NHD];  // the trees' node term hashes (<= NHD nodes)
   const u32 depth = p.ta.depth, sub = p.sub, Ls = depth - sub, nb = 1u << sub;
   const u64 tile = blockIdx.x;
   const int tid = threadIdx.x;
+  const bool nha_lds = p.ta.th.on && p.ta.th.nn <= NHD, nhb_lds = p.tb.th.on && p.tb.th.nn <= NHD;
+  if (nha_lds)
+    for (u32 x = tid; x < (u32)p.ta.th.nn; x += DB) s_nha[x] = p.ta.th.nh[x];
+  if (nhb_lds)
+    for (u32 x = tid; x < (u32)p.tb.th.nn; x += DB) s_nhb[x] = p.tb.th.nh[x];
   const u64 root = ((1ull << Ls) - 1) + tile;
   const u64 nbnd = p.ntiles + 1;
   // ---- descent in strides of 4 levels: thread tid owns buckets [16 tid, 16 tid + 16) of
@@ -643,28 +652,54 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
     if (tid == 0) s_dp[ND] = R;
     __syncthreads();
     // hash the staged rows, all at once: row q belongs to the last differing bucket whose
-    // first staged row is <= q (a search of the LDS list), A's rows first
+    // first staged row is <= q (a search of the LDS list), A's rows first.  A thread's rows
+    // go in batches of RB: every column load of the batch is issued before any row is
+    // hashed (one round trip per batch, not one per row), and the node term hashes come
+    // from LDS (staged above), not from a dependent global load
+    constexpr int RB = 4;
+    for (u32 u0 = 0; u0 < (RCAP + DB - 1) / DB; u0 += RB) {
+      if (u0 * DB >= R) break;  // uniform
+      u64 key[RB], val[RB], cnt[RB];
+      i64 ts[RB];
+      u32 nd[RB];
+      bool fromb[RB];
 #pragma unroll
-    for (u32 u = 0; u < (RCAP + DB - 1) / DB; u++) {
-      const u32 q = u * DB + tid;
-      if (q < R) {
-        u32 lo = 0, hi = ND;  // s_dp[lo] <= q < s_dp[hi]
-        while (hi - lo > 1) {
-          const u32 m = (lo + hi) >> 1;
-          if (s_dp[m] <= q)
-            lo = m;
-          else
-            hi = m;
+      for (int j = 0; j < RB; j++) {
+        const u32 q = (u0 + j) * DB + tid;
+        fromb[j] = false;
+        key[j] = val[j] = cnt[j] = 0;
+        ts[j] = 0;
+        nd[j] = 0;
+        if (q < R) {
+          u32 lo = 0, hi = ND;  // s_dp[lo] <= q < s_dp[hi]
+          while (hi - lo > 1) {
+            const u32 m = (lo + hi) >> 1;
+            if (s_dp[m] <= q)
+              lo = m;
+            else
+              hi = m;
+          }
+          const u32 r = q - s_dp[lo], na = s_dn[lo] >> 16;
+          fromb[j] = r >= na;
+          const Rows& S = fromb[j] ? p.sb : p.sa;
+          const u64 i = fromb[j] ? c0 + s_db[lo] + (r - na) : a0 + s_da[lo] + r;
+          key[j] = S.key[i];
+          val[j] = S.val[i];
+          ts[j] = S.ts[i];
+          nd[j] = S.node[i];
+          cnt[j] = S.cnt[i];
         }
-        const u32 r = q - s_dp[lo], na = s_dn[lo] >> 16;
-        if (r < na) {
-          const u64 i = a0 + s_da[lo] + r;
-          s_k[q] = p.sa.key[i];
-          s_h[q] = rh(p.sa, i, p.ta.th);
-        } else {
-          const u64 i = c0 + s_db[lo] + (r - na);
-          s_k[q] = p.sb.key[i];
-          s_h[q] = rh(p.sb, i, p.tb.th);
+      }
+#pragma unroll
+      for (int j = 0; j < RB; j++) {
+        const u32 q = (u0 + j) * DB + tid;
+        if (q < R) {
+          const TermH& th = fromb[j] ? p.tb.th : p.ta.th;
+          const u64* snh = fromb[j] ? s_nhb : s_nha;
+          const bool lds_ok = fromb[j] ? nhb_lds : nha_lds;
+          const u64 nt = lds_ok ? (nd[j] < (u32)th.nn ? snh[nd[j]] : (u64)nd[j]) : th_node(th, nd[j]);
+          s_k[q] = key[j];
+          s_h[q] = row_hash(key[j], th_val(th, val[j]), ts[j], nt, cnt[j]);
         }
       }
     }
@@ -717,7 +752,10 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
     }
     u32 k2 = 0, ra = offa, rb = offb;
     for (u32 i = 0; i < OWN; i++) {
-      const u32 x = half16(ca, i), y = half16(cb, i);
+      // (the counts re-read from memory: indexing the registers by a loop variable here
+      // would put them in scratch for the whole kernel)
+      const u64 bi = bucket0 + (u64)tid * OWN + i;
+      const u32 x = bi - bucket0 < nb ? p.ta.counts[bi] : 0u, y = bi - bucket0 < nb ? p.tb.counts[bi] : 0u;
       if (mine >> i & 1u) {
         if (pass == 0)
           k2 += merge_bucket<false, false>(p.sa, p.ta.th, a0 + ra, a0 + ra + x, p.sb, p.tb.th,
@@ -881,37 +919,32 @@ inline unsigned grid_of(u64 n, int b) { return (unsigned)((n + b - 1) / b); }
 
 }  // namespace
 
-hipError_t launch_merkle_build(const Rows& s, const MerkleT& m, u64* d_keys, u32* ctr, u32* err,
-                               hipStream_t st) {
+hipError_t launch_merkle_build(const Rows& s, const MerkleT& m, u64* d_keys, u32* arrive, u64* hand,
+                               u32* err, hipStream_t st) {
   const MT t = mt_of(m);
   const u64 G = merkle_chunks(t.depth);
-  // scratch: the arrival counter (zeroed before EVERY launch), then the hand-off words
-  hipError_t e = hipMemsetAsync(ctr, 0, 16 * sizeof(u32), st);
-  if (e != hipSuccess) return e;
   // 16-byte row loads need 16-byte aligned columns (a view into a packed buffer may not be)
   const bool vec = MERKLE_VEC && !(((uintptr_t)s.key | (uintptr_t)s.val | (uintptr_t)s.ts |
                                     (uintptr_t)s.node | (uintptr_t)s.cnt) & 15);
   if (vec)
     hipLaunchKernelGGL((merkle_chunk_kernel<true, true>), dim3((unsigned)G), dim3(UPB), 0, st, s, t,
-                       (const u32*)nullptr, ctr, (u64*)(ctr + 16), d_keys, err);
+                       (const u32*)nullptr, arrive, hand, d_keys, err);
   else
     hipLaunchKernelGGL((merkle_chunk_kernel<true, false>), dim3((unsigned)G), dim3(UPB), 0, st, s, t,
-                       (const u32*)nullptr, ctr, (u64*)(ctr + 16), d_keys, err);
+                       (const u32*)nullptr, arrive, hand, d_keys, err);
   return hipGetLastError();
 }
 
 hipError_t launch_merkle_update(const MerkleT& m, const Rows& olds, const Rows& news, const u64* keys,
-                                u64 n_keys, u32* dirty, u64* d_keys, u32* ctr, u32* err,
+                                u64 n_keys, u32* dirty, u64* d_keys, u32* arrive, u64* hand, u32* err,
                                 hipStream_t st) {
   const MT t = mt_of(m);
   const u64 G = merkle_chunks(t.depth);
-  hipError_t e = hipMemsetAsync(ctr, 0, 16 * sizeof(u32), st);
-  if (e != hipSuccess) return e;
   if (n_keys)
     hipLaunchKernelGGL(merkle_update_kernel, dim3(grid_of(n_keys, UB)), dim3(UB), 0, st, t, olds, news,
                        keys, n_keys, dirty, d_keys, err);
   hipLaunchKernelGGL(merkle_chunk_kernel<false>, dim3((unsigned)G), dim3(UPB), 0, st, news, t, dirty,
-                     ctr, (u64*)(ctr + 16), (u64*)nullptr, err);
+                     arrive, hand, (u64*)nullptr, err);
   return hipGetLastError();
 }
 
