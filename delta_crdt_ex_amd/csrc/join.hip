@@ -748,6 +748,10 @@ __device__ __forceinline__ void commit_tile(const Staged& r, Buf& s) {
 // earlier, so step 4 rarely waits; its cost is one G-word read per iteration, issued
 // before the merge.  Spins stay bounded (scan.err bit 0 on timeout).
 constexpr int FUSE_IT = JB / WAVE / 2;  // fused splits: one wave per boundary, 2 per tile
+#ifndef DG_JOIN_RED2
+#define DG_JOIN_RED2 1  // stripe_sums' partials double-buffered (0: one buffer + a barrier)
+#endif
+constexpr bool JOIN_RED2 = DG_JOIN_RED2;
 
 template <bool KEYED>
 struct StreamLds {
@@ -757,7 +761,7 @@ struct StreamLds {
   u64 kslice[2][KEYED ? KS : 1];    // keyed: the tile's keyset slice (<= KS entries)
   u64 kspl[KEYED ? 2 * FUSE_IT : 1];  // keyed + fused: keyset splits of this workgroup's tiles
   u32 wave[JB / WAVE + 1];
-  u64 red[2 * (JB / WAVE)];
+  u64 red[2][2 * (JB / WAVE)];  // stripe_sums' wave partials, double-buffered by iteration parity
   u64 spl[2 * FUSE_IT];  // fused: splits of this workgroup's tiles (start, end per tile)
   u64 chk[JB / WAVE];    // CHG: each wave's last change event, and 1 + its lane (0: none)
   int chf[JB / WAVE];
@@ -880,7 +884,10 @@ __device__ __forceinline__ void stripe_sums(const u32* cs, u32 epoch, u32* err, 
   lo = wave_sum_u32((u32)lo);
   tot = wave_sum_u32((u32)tot);
   constexpr int NW = JB / WAVE;
-  __syncthreads();  // every wave is done reading s_red from the previous call
+  // (no barrier before the writes: the caller alternates two s_red buffers by iteration
+  // parity, and the previous reader of this buffer finished two iterations ago, behind the
+  // iterations' own barriers)
+  if (!JOIN_RED2) __syncthreads();  // (A/B: one buffer, every wave done reading it)
   if ((tid & (WAVE - 1)) == 0) {
     s_red[tid / WAVE] = lo;
     s_red[NW + tid / WAVE] = tot;
@@ -1101,7 +1108,7 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     JSTAMP(t, 4);
     if (k > 0) {  // stripe k-1: this workgroup's tile t - G
       u64 below, all;
-      stripe_sums(cs, epoch, p.scan.err, t - G - w, G, w, true, sc, s.red, &below, &all);
+      stripe_sums(cs, epoch, p.scan.err, t - G - w, G, w, true, sc, s.red[JOIN_RED2 ? (k & 1) : 0], &below, &all);
       JSTAMP(t, 5);
       write_tile(p, s, bi ^ 1, base + below, np);
       base += all;
@@ -1112,7 +1119,7 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       u64 below, all;
       StripeCounts last;
       stripe_load(cs, t - w, G, ntiles, epoch, last);
-      stripe_sums(cs, epoch, p.scan.err, t - w, G, w, false, last, s.red, &below, &all);
+      stripe_sums(cs, epoch, p.scan.err, t - w, G, w, false, last, s.red[JOIN_RED2 ? ((k + 1) & 1) : 0], &below, &all);
       write_tile(p, s, bi, base + below, np);
       if (tid == 0 && t == ntiles - 1) p.d_count[0] = base + below + np;
       break;
