@@ -175,8 +175,25 @@ def config4_round(eng, torch, dev, rank=0, world=1, keys_per_rank=12_500_000, st
     eng.merkle_build(sb, depth, tb, sbits, rank if sbits else 0)
     cap = max_sync_size or (ta.n_keys + tb.n_keys)
 
+    # the round as CausalCrdt runs it on the receiving replica: update_state_with_delta
+    # REPLACES A's state (causal_crdt.ex:383-404), so the keyed join is applied in place
+    # (dg_join_delta, with its MerkleMap update); A's state and tree are restored from a
+    # pristine copy before each round, outside the clock
+    st = Store.empty(sa.n + sb.n, dev)
+    spare = Store.empty(sa.n + sb.n, dev)
+    sc = Context.empty(ca.kind, ca.n + cb.n, dev)
+
     def one_round():
         t = {}
+        for f in ("key", "val", "ts", "node", "cnt"):
+            getattr(st, f)[: sa.n].copy_(getattr(sa, f)[: sa.n])
+        st.n = sa.n
+        sc.node[: ca.n].copy_(ca.node[: ca.n])
+        sc.cnt[: ca.n].copy_(ca.cnt[: ca.n])
+        sc.n, sc.kind = ca.n, ca.kind
+        tt = ta.clone()
+        tt.store = st
+        torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         e0.record(eng.stream)
@@ -185,17 +202,13 @@ def config4_round(eng, torch, dev, rank=0, world=1, keys_per_rank=12_500_000, st
         t1 = time.perf_counter()
         delta = eng.take_keys(sb, keys)
         t2 = time.perf_counter()
-        out, octx, changed = eng.join2_changes(sa, ca, delta, cb, keys=keys)
-        t3 = time.perf_counter()
-        tt = ta.clone()
-        t4 = time.perf_counter()
-        eng.merkle_update(tt, out, changed)
+        changed, swapped = eng.join_delta(st, sc, delta, cb, keys, spare, tt)
         torch.cuda.synchronize()
-        t5 = time.perf_counter()
-        t.update(diff=t1 - t0, take=t2 - t1, join=t3 - t2, update=t5 - t4, total=(t5 - t4) + (t3 - t0),
-                 diff_ev=e0.elapsed_time(e1) * 1e-3,
-                 keys=int(keys.numel()), total_keys=total, rows=delta.n, changed=int(changed.numel()))
-        t["ok"] = tt.root() == eng.merkle_build(out, depth, None, sbits, rank if sbits else 0,
+        t3 = time.perf_counter()
+        t.update(diff=t1 - t0, take=t2 - t1, join_delta=t3 - t2, total=t3 - t0,
+                 diff_ev=e0.elapsed_time(e1) * 1e-3, keys=int(keys.numel()), total_keys=total,
+                 rows=delta.n, changed=int(changed.numel()), in_place=not swapped)
+        t["ok"] = tt.root() == eng.merkle_build(st, depth, None, sbits, rank if sbits else 0,
                                                 terms=terms).root()
         return t
 
@@ -208,7 +221,7 @@ def config4_round(eng, torch, dev, rank=0, world=1, keys_per_rank=12_500_000, st
                        "causal_crdt.ex:91-110,252-270 with both replicas on this GPU (between "
                        "BEAM nodes each hop is one message); synchronous calls, wall time"}
     med = {k: float(np.median([r[k] for r in rounds]))
-           for k in ("diff", "take", "join", "update", "total", "diff_ev")}
+           for k in ("diff", "take", "join_delta", "total", "diff_ev")}
     last = rounds[-1]
     acc = _diff_accounting(ta, tb)
     diff_alg = acc["bytes_no_keys"] + 8 * last["total_keys"]
@@ -237,10 +250,12 @@ def config4_round(eng, torch, dev, rank=0, world=1, keys_per_rank=12_500_000, st
         "round_keys": last["keys"], "round_total_keys": last["total_keys"],
         "round_delta_rows": last["rows"], "round_changed_keys": last["changed"],
         "update_equals_rebuild": all(r["ok"] for r in rounds),
+        "round_in_place": all(r["in_place"] for r in rounds),
         "resident_delta": resident,
         "partial": partial,
-        "round_note": "synchronous calls: merkle_diff -> take_keys -> join2_changes (keyed) -> "
-                      "merkle_update (incremental put/delete + update_hashes of the changed keys)",
+        "round_note": "synchronous calls: merkle_diff -> take_keys (the sync delta from B) -> "
+                      "join_delta (update_state_with_delta on A: the keyed join in place, its "
+                      "changed keys, the MerkleMap put/delete + update_hashes)",
     }
     if world > 1:
         t0 = time.perf_counter()

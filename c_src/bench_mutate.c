@@ -209,6 +209,9 @@ typedef struct {
   uint64_t msg_words;
   uint64_t *changed, *h_back;  /* the changed keys; host copy of keys + rows */
   uint64_t* d_back;            /* rows + keys, packed for one copy home */
+  dg_store mb_rows;            /* dg_mutate_batch's delta, its dot list and touched keys */
+  dg_context mb_ctx;
+  uint64_t* mb_keys;
   uint64_t back_cap;
   uint64_t *rk, *rv, *h_rk;    /* read/1 output */
 } gpu;
@@ -238,6 +241,10 @@ static void gpu_upload(gpu* g, hrows* r) {
   g->back_cap = 2048;
   DG(dg_buffer_alloc(g->e, g->back_cap * 6 * 8, (void**)&g->d_back));
   g->changed = g->d_back;  /* the changed keys open the block */
+  DG(dg_store_alloc(g->e, 2048, &g->mb_rows));
+  DG(dg_context_alloc(g->e, 8 * 2048, &g->mb_ctx));
+  g->mb_ctx.kind = DG_CTX_DOTS;
+  DG(dg_buffer_alloc(g->e, 2048 * 8, (void**)&g->mb_keys));
   g->h_back = calloc(g->back_cap * 6, 8);
   DG(dg_buffer_alloc(g->e, (r->n + 16384) * 8, (void**)&g->rk));
   DG(dg_buffer_alloc(g->e, (r->n + 16384) * 8, (void**)&g->rv));
@@ -293,6 +300,43 @@ static void gpu_apply(gpu* g, const uint64_t* key, const uint64_t* val, const in
   t[0] = t1 - t0;
   t[1] = t2 - t1;
   t[2] = t3 - t2;
+}
+
+/* a batch of m adds (keys ascending) by node 0 built ON THE DEVICE (dg_mutate_batch: the
+ * NIF's mutate_batch) and applied with dg_join_delta, the changed rows back: one op list
+ * upload, the delta's dots from the state, the join, the return block */
+static void gpu_mutate_batch(gpu* g, const uint64_t* key, const uint64_t* val, const int64_t* ts,
+                             uint64_t m) {
+  uint64_t* h = g->h_msg;
+  const uint64_t words = 4 * m + (m + 7) / 8 + 1;
+  if (words > g->msg_words) {
+    fprintf(stderr, "batch too large\n");
+    exit(1);
+  }
+  memcpy(h, key, m * 8);
+  memcpy(h + m, val, m * 8);
+  memcpy(h + 2 * m, ts, m * 8);
+  for (uint64_t i = 0; i < m; i++) h[3 * m + i] = i;  /* add_rank: every op an add */
+  uint8_t* kinds = (uint8_t*)(h + 4 * m);
+  memset(kinds, 1, m);
+  DG(dg_copy_to_device(g->e, g->d_msg, h, words * 8));
+  uint64_t* d = g->d_msg;
+  dg_store delta = {g->mb_rows.key, g->mb_rows.val, g->mb_rows.ts, g->mb_rows.node, g->mb_rows.cnt, 0,
+                    g->mb_rows.cap};
+  dg_context dots = g->mb_ctx;
+  uint64_t n_keys = 0, n_changed = 0;
+  int swapped = 0;
+  DG(dg_mutate_batch(g->e, &g->st, &g->ctx, 0, m, (const uint8_t*)(d + 4 * m), d, d + m,
+                     (const int64_t*)(d + 2 * m), d + 3 * m, m, &delta, &dots, g->mb_keys, m, &n_keys));
+  DG(dg_join_delta(g->e, &g->st, &g->ctx, &delta, &dots, g->mb_keys, n_keys, &g->spare, &g->tree,
+                   g->changed, g->back_cap, &n_changed, &swapped));
+  if (n_changed) {
+    uint64_t* b = g->d_back + g->back_cap;
+    const uint64_t S = g->back_cap;
+    dg_store tk = {b, b + S, (int64_t*)(b + 2 * S), (uint32_t*)(b + 4 * S), b + 3 * S, 0, S};
+    DG(dg_take_keys(g->e, &g->st, g->changed, n_changed, &tk));
+    DG(dg_copy_to_host(g->e, g->h_back, g->d_back, 6 * S * 8));
+  }
 }
 
 static void gpu_read(gpu* g) {
@@ -442,6 +486,28 @@ int main(int argc, char** argv) {
     const double el = now_us() - t0;
     if (rep) bt_us[n_batch++] = el;
   }
+  double dmb[16];
+  int n_dmb = 0;
+#ifndef DG_REF
+  /* the same workload with the delta built on the device (the NIF's mutate_batch) */
+  for (int rep = 0; rep < 6; rep++) {
+    for (int i = 0; i < nb; i++) {
+      char s[32];
+      snprintf(s, sizeof s, "mkey%d_%d", i, rep);
+      bk[i] = key_bin(s);
+    }
+    qsort(bk, nb, 8, cmp_u64);
+    for (int i = 0; i < nb; i++) {
+      bv[i] = VAL_VALUE;
+      bt[i] = ++R.clock;
+    }
+    R.c += nb;
+    const double t0 = now_us();
+    gpu_mutate_batch(&g, bk, bv, bt, nb);
+    const double el = now_us() - t0;
+    if (rep) dmb[n_dmb++] = el;
+  }
+#endif
   printf("{\"n_keys\": %lld, \"reps\": %d, \"path\": \"%s\", \"us\": {", (long long)n, reps,
 #ifndef DG_REF
          "gpu"
@@ -458,7 +524,12 @@ int main(int argc, char** argv) {
            OP_NAMES[o], median(ts[o][0], reps), median(ts[o][1], reps), median(ts[o][2], reps));
   }
   const double bmed = median(bt_us, n_batch);
-  printf("}, \"batch_1000_adds_us\": %.2f, \"batch_us_per_op\": %.3f}\n", bmed, bmed / nb);
+  printf("}, \"batch_1000_adds_us\": %.2f, \"batch_us_per_op\": %.3f", bmed, bmed / nb);
+  if (n_dmb) {
+    const double m2 = median(dmb, n_dmb);
+    printf(", \"mutate_batch_1000_adds_us\": %.2f, \"mutate_batch_us_per_op\": %.3f", m2, m2 / nb);
+  }
+  printf("}\n");
 #ifndef DG_REF
   dg_engine_destroy(g.e);
 #endif

@@ -29,6 +29,10 @@
  *        value maps changed (causal_crdt.ex:344-352), so the caller updates its term
  *        map with Map.merge/Map.drop of those keys only; the Merkle tree, if built,
  *        gets put/delete + update_hashes of them (dg_merkle_update, :390-394).
+ *   mutate_batch(state, node, ops)            -> {:ok, new_dots, changed}
+ *        a batch of {:add, key, value, ts} / {:remove, key} ops by `node` as ONE delta
+ *        (dg_mutate_batch, aw_lww_map.ex:99-146) applied like join_delta with the
+ *        touched keys (the queued mutate_async calls of a GPU-attached replica)
  *   read(state, keys | :all)                  -> %{key => value}       (read/1,2, :211-224)
  *   take(state, keys)                         -> value map of those keys (Map.take, :118,331)
  *   merkle_build(state, depth)                -> :ok
@@ -37,6 +41,7 @@
  *   (a continuation is an opaque binary; `max` is max_sync_size, :98,105,206-214)
  */
 #include <erl_nif.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "../include/deltagpu.h"
@@ -819,6 +824,72 @@ static ERL_NIF_TERM state_load(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
   return r;
 }
 
+/* The keys a dg_join_delta changed (in d->back[0, n_changed)) as [{key, value_map | nil}]
+ * and the state's new context: their rows taken into the return block (grown and retaken
+ * if a key holds more rows than the block's stride), the block copied home ONCE. */
+static int changed_result(ErlNifEnv* env, engine_res* g, state_res* s, uint64_t n_changed,
+                          ERL_NIF_TERM* new_dots, ERL_NIF_TERM* changed_terms) {
+  delta_buf* d = &s->d;
+  ERL_NIF_TERM values = enif_make_new_map(env);
+  int rc = DG_OK;
+  for (int attempt = 0;; attempt++) {
+    const uint64_t S = d->back_cap;
+    uint64_t* b = d->back + S;
+    dg_store tk = {b, b + S, (int64_t*)(b + 2 * S), (uint32_t*)(b + 4 * S), b + 3 * S, 0, S};
+    rc = dg_take_keys(g->e, &s->rows, d->back, n_changed, &tk);
+    if (rc == DG_E_CAPACITY && attempt == 0) {
+      /* grow, keeping the changed keys: they pass through the host */
+      uint64_t* keep = (uint64_t*)enif_alloc((n_changed ? n_changed : 1) * 8);
+      if (!keep) return DG_E_NOMEM;
+      rc = dg_copy_to_host(g->e, keep, d->back, n_changed * 8);
+      if (!rc) rc = grow_back(g, d, tk.n > n_changed ? tk.n : n_changed);
+      if (!rc) rc = dg_copy_to_device(g->e, d->back, keep, n_changed * 8);
+      enif_free(keep);
+      if (rc) return rc;
+      continue;
+    }
+    if (rc) return rc;
+    if ((rc = dg_copy_to_host(g->e, d->h_back, d->back, 6 * S * 8))) return rc;
+    uint64_t* hb = d->h_back + S;
+    dg_store hs = {hb, hb + S, (int64_t*)(hb + 2 * S), (uint32_t*)(hb + 4 * S), hb + 3 * S, tk.n, S};
+    if ((rc = unmarshal_host_rows(env, g, &hs, &values))) return rc;
+    break;
+  }
+  if ((rc = unmarshal_dots(env, g, &s->ctx, new_dots))) return rc;
+  for (uint64_t i = n_changed; i-- > 0;) {
+    const boxed* b = (const boxed*)dgm_key_term(g->u, d->h_back[i]);
+    ERL_NIF_TERM k = enif_make_copy(env, b->t), v;
+    if (!enif_get_map_value(env, values, k, &v)) v = A_NIL;
+    *changed_terms = enif_make_list_cell(env, enif_make_tuple2(env, k, v), *changed_terms);
+  }
+  return DG_OK;
+}
+
+/* The spare buffer and the context's room for a union with `dn` more entries, grown. */
+static int room_for(engine_res* g, state_res* s, uint64_t rows, uint64_t dn) {
+  int rc = DG_OK;
+  if (s->spare.cap < s->rows.n + rows) {
+    dg_store_free(g->e, &s->spare);
+    if ((rc = dg_store_alloc(g->e, 2 * (s->rows.n + rows), &s->spare))) return rc;
+  }
+  if (s->ctx.cap < s->ctx.n + dn) {
+    dg_context nctx;
+    memset(&nctx, 0, sizeof nctx);
+    if ((rc = dg_context_alloc(g->e, 2 * (s->ctx.n + dn), &nctx))) return rc;
+    rc = dg_copy_to_device(g->e, nctx.node, s->ctx.node, s->ctx.n * 4); /* device to device */
+    if (!rc) rc = dg_copy_to_device(g->e, nctx.cnt, s->ctx.cnt, s->ctx.n * 8);
+    if (rc) {
+      dg_context_free(g->e, &nctx);
+      return rc;
+    }
+    nctx.n = s->ctx.n;
+    nctx.kind = s->ctx.kind;
+    dg_context_free(g->e, &s->ctx);
+    s->ctx = nctx;
+  }
+  return rc;
+}
+
 static ERL_NIF_TERM join_delta(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
   (void)argc;
   state_res* s;
@@ -828,32 +899,16 @@ static ERL_NIF_TERM join_delta(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
   int rc = DG_OK;
   dgm_rows h;
   delta_buf* d = &s->d;
-  dg_context nctx;
   uint64_t n_keys = 0, n_changed = 0;
   int swapped = 0;
-  memset(&nctx, 0, sizeof nctx);
-  ERL_NIF_TERM r, new_dots, changed_terms = enif_make_list(env, 0), values;
+  ERL_NIF_TERM r, new_dots = A_NIL, changed_terms = enif_make_list(env, 0);
   TRY(dgm_rows_init(&h, 256, 16));
   TRY(marshal_dots(env, g, argv[1], &h));
   TRY(marshal_value(env, g, argv[2], &h));
   /* the delta into the state's kept buffers (no allocation once they are big enough) */
   TRY(upload_delta(g, &h, d));
   TRY(marshal_keys(env, g, argv[3], &d->keys, &n_keys, 1, &d->keys_cap));
-  /* the spare buffer and the context's room for the union, grown on demand */
-  if (s->spare.cap < s->rows.n + d->rows.n) {
-    dg_store_free(g->e, &s->spare);
-    TRY(dg_store_alloc(g->e, 2 * (s->rows.n + d->rows.n), &s->spare));
-  }
-  if (s->ctx.cap < s->ctx.n + d->ctx.n) {
-    TRY(dg_context_alloc(g->e, 2 * (s->ctx.n + d->ctx.n), &nctx));
-    TRY(dg_copy_to_device(g->e, nctx.node, s->ctx.node, s->ctx.n * 4));  /* device to device */
-    TRY(dg_copy_to_device(g->e, nctx.cnt, s->ctx.cnt, s->ctx.n * 8));
-    nctx.n = s->ctx.n;
-    nctx.kind = s->ctx.kind;
-    dg_context_free(g->e, &s->ctx);
-    s->ctx = nctx;
-    memset(&nctx, 0, sizeof nctx);
-  }
+  TRY(room_for(g, s, d->rows.n, d->ctx.n));
   TRY(grow_back(g, d, n_keys ? n_keys : 1));
   if (s->has_tree) TRY(refresh_terms(g));
   /* update_state_with_delta: the join (in place, or through the spare buffer: the structs
@@ -861,41 +916,146 @@ static ERL_NIF_TERM join_delta(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
    * nothing: on an error the state, its context and tree are as they were */
   TRY(dg_join_delta(g->e, &s->rows, &s->ctx, &d->rows, &d->ctx, d->keys, n_keys, &s->spare,
                     s->has_tree ? &s->tree : NULL, d->back, d->back_cap, &n_changed, &swapped));
-  /* the changed keys' new value maps: their rows taken into the return block (grown and
-   * retaken if a key holds more rows than the block's stride), the block copied home once */
-  for (int attempt = 0;; attempt++) {
-    const uint64_t S = d->back_cap;
-    uint64_t* b = d->back + S;
-    dg_store tk = {b, b + S, (int64_t*)(b + 2 * S), (uint32_t*)(b + 4 * S), b + 3 * S, 0, S};
-    rc = dg_take_keys(g->e, &s->rows, d->back, n_changed, &tk);
-    if (rc == DG_E_CAPACITY && attempt == 0) {
-      /* grow keeping the changed keys: move them through the host */
-      uint64_t* keep = (uint64_t*)enif_alloc((n_changed ? n_changed : 1) * 8);
-      TRY(dg_copy_to_host(g->e, keep, d->back, n_changed * 8));
-      rc = grow_back(g, d, tk.n > n_changed ? tk.n : n_changed);
-      if (!rc) rc = dg_copy_to_device(g->e, d->back, keep, n_changed * 8);
-      enif_free(keep);
-      TRY(rc);
-      continue;
-    }
-    TRY(rc);
-    TRY(dg_copy_to_host(g->e, d->h_back, d->back, (S + 5 * S) * 8));
-    uint64_t* hb = d->h_back + S;
-    dg_store hs = {hb, hb + S, (int64_t*)(hb + 2 * S), (uint32_t*)(hb + 4 * S), hb + 3 * S, tk.n, S};
-    TRY(unmarshal_host_rows(env, g, &hs, &values));
-    break;
-  }
-  TRY(unmarshal_dots(env, g, &s->ctx, &new_dots));
-  for (uint64_t i = n_changed; i-- > 0;) {
-    const boxed* b = (const boxed*)dgm_key_term(g->u, d->h_back[i]);
-    ERL_NIF_TERM k = enif_make_copy(env, b->t), v;
-    if (!enif_get_map_value(env, values, k, &v)) v = A_NIL;
-    changed_terms = enif_make_list_cell(env, enif_make_tuple2(env, k, v), changed_terms);
-  }
+  TRY(changed_result(env, g, s, n_changed, &new_dots, &changed_terms));
 out:
   r = rc ? error_term(env, rc) : enif_make_tuple3(env, A_OK, new_dots, changed_terms);
   dgm_rows_free(&h);
-  dg_context_free(g->e, &nctx);
+  enif_mutex_unlock(g->lock);
+  return r;
+}
+
+/* mutate_batch(state, node, ops): a batch of mutations by replica `node` -- ops =
+ * [{:add, key, value, ts} | {:remove, key}] in the order they were made (the queued
+ * mutate_async calls of one CausalCrdt, causal_crdt.ex:196-198,337-342) -- applied to
+ * the resident state as ONE delta: dg_mutate_batch builds it on the device exactly as
+ * the ops' add/remove deltas would compose (aw_lww_map.ex:99-146: per touched key the last
+ * op's row if it is an add, context = the touched keys' dots plus every add's dot), then
+ * dg_join_delta applies it with the touched keys.  -> {:ok, new_dots, changed} as
+ * join_delta.  A one-key mutate costs ~0.1-0.2 ms on the device and a few us on the BEAM
+ * (bench.py `mutate`), so the Elixir side applies single ops with join_cpu and ships them
+ * here in batches. */
+typedef struct {
+  uint64_t key, val, rank;
+  int64_t ts;
+  uint32_t idx;
+  uint8_t kind;
+} mop;
+
+static int mop_cmp(const void* a, const void* b) {  /* by key, then batch order: stable */
+  const mop *x = (const mop*)a, *y = (const mop*)b;
+  if (x->key != y->key) return x->key < y->key ? -1 : 1;
+  return x->idx < y->idx ? -1 : x->idx > y->idx;
+}
+
+static ERL_NIF_TERM mutate_batch_nif(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  (void)argc;
+  state_res* s;
+  unsigned m;
+  if (!enif_get_resource(env, argv[0], STATE_RT, (void**)&s) || !enif_get_list_length(env, argv[2], &m))
+    return enif_make_badarg(env);
+  engine_res* g = s->eng;
+  enif_mutex_lock(g->lock);
+  int rc = DG_OK, swapped = 0;
+  delta_buf* d = &s->d;
+  uint64_t n_keys = 0, n_changed = 0, n_adds = 0;
+  uint32_t node = 0;
+  ERL_NIF_TERM r, new_dots = A_NIL, changed_terms = enif_make_list(env, 0), head, tail = argv[2];
+  mop* ops = (mop*)enif_alloc((m ? m : 1) * sizeof *ops);
+  uint64_t* h = NULL;
+  uint64_t* dev = NULL;
+  if (!ops) {
+    rc = DG_E_NOMEM;
+    goto out;
+  }
+  {
+    boxed bn = {argv[1]};
+    TRY(dgm_node(g->u, &bn, &node));
+  }
+  /* intern every op (values first: a relabel re-spaces ids already handed out) */
+  for (unsigned i = 0; i < m; i++) {
+    int ar;
+    const ERL_NIF_TERM* e;
+    if (!enif_get_list_cell(env, tail, &head, &tail) || !enif_get_tuple(env, head, &ar, &e) || ar < 2) {
+      rc = DG_E_INVAL;
+      goto out;
+    }
+    ops[i].idx = i;
+    ops[i].kind = ar == 4;
+    ops[i].val = 0;
+    ops[i].ts = 0;
+    if (ar == 4) {
+      ErlNifSInt64 ts;
+      if (!enif_get_int64(env, e[3], &ts)) {
+        rc = DG_E_INVAL;
+        goto out;
+      }
+      ops[i].ts = ts;
+      TRY(intern_value(env, g, e[2], &ops[i].val));
+    } else if (ar != 2) {
+      rc = DG_E_INVAL;
+      goto out;
+    }
+  }
+  tail = argv[2];
+  for (unsigned i = 0; i < m; i++) {
+    int ar;
+    const ERL_NIF_TERM* e;
+    enif_get_list_cell(env, tail, &head, &tail);
+    enif_get_tuple(env, head, &ar, &e);
+    boxed bk = {e[1]};
+    TRY(dgm_key(g->u, &bk, &ops[i].key));
+    if (ar == 4) {  /* a later relabel may have moved this value's id: take it again */
+      boxed bv = {e[2]};
+      int relabeled = 0;
+      TRY(dgm_value(g->u, &bv, &ops[i].val, &relabeled));
+      if (relabeled) TRY(remap_live(g));
+      ops[i].rank = n_adds++;
+    }
+  }
+  qsort(ops, m, sizeof *ops, mop_cmp);
+  /* kind | key | val | ts | add_rank, one upload (the u8 kinds packed at the end) */
+  {
+    const uint64_t words = 4 * (uint64_t)m + (m + 7) / 8 + 1;
+    h = (uint64_t*)enif_alloc(words * 8);
+    if (!h) {
+      rc = DG_E_NOMEM;
+      goto out;
+    }
+    uint8_t* kinds = (uint8_t*)(h + 4 * (uint64_t)m);
+    for (unsigned i = 0; i < m; i++) {
+      h[i] = ops[i].key;
+      h[m + i] = ops[i].val;
+      h[2 * (uint64_t)m + i] = (uint64_t)ops[i].ts;
+      h[3 * (uint64_t)m + i] = ops[i].rank;
+      kinds[i] = ops[i].kind;
+    }
+    TRY(dg_buffer_alloc(g->e, words * 8, (void**)&dev));
+    TRY(dg_copy_to_device(g->e, dev, h, words * 8));
+  }
+  /* the delta in the state's kept buffers: one row per touched key, a dot list of at most
+   * the touched keys' rows + the adds (retried with the exact sizes when short) */
+  TRY(grow_store(g, &d->rows, m ? m : 1));
+  TRY(grow_buf(g, &d->keys, &d->keys_cap, m ? m : 1));
+  for (int attempt = 0;; attempt++) {
+    TRY(grow_ctx(g, &d->ctx, attempt ? s->rows.n + n_adds + 1 : 8 * (uint64_t)m + n_adds + 1));
+    rc = dg_mutate_batch(g->e, &s->rows, &s->ctx, node, m, (const uint8_t*)(dev + 4 * (uint64_t)m), dev,
+                         dev + m, (const int64_t*)(dev + 2 * (uint64_t)m), dev + 3 * (uint64_t)m, n_adds,
+                         &d->rows, &d->ctx, d->keys, d->keys_cap, &n_keys);
+    if (rc == DG_E_CAPACITY && attempt == 0) continue;
+    TRY(rc);
+    break;
+  }
+  TRY(room_for(g, s, d->rows.n, d->ctx.n));
+  TRY(grow_back(g, d, n_keys ? n_keys : 1));
+  if (s->has_tree) TRY(refresh_terms(g));
+  TRY(dg_join_delta(g->e, &s->rows, &s->ctx, &d->rows, &d->ctx, d->keys, n_keys, &s->spare,
+                    s->has_tree ? &s->tree : NULL, d->back, d->back_cap, &n_changed, &swapped));
+  TRY(changed_result(env, g, s, n_changed, &new_dots, &changed_terms));
+out:
+  r = rc ? error_term(env, rc) : enif_make_tuple3(env, A_OK, new_dots, changed_terms);
+  if (ops) enif_free(ops);
+  if (h) enif_free(h);
+  dg_buffer_free(g->e, dev);
   enif_mutex_unlock(g->lock);
   return r;
 }
@@ -1139,6 +1299,7 @@ static ErlNifFunc funcs[] = {
     {"engine_open", 1, engine_open, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"state_load", 3, state_load, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"join_delta", 4, join_delta, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"mutate_batch", 3, mutate_batch_nif, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"read", 2, read_nif, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"take", 2, take_nif, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"merkle_build", 2, merkle_build_nif, ERL_NIF_DIRTY_JOB_CPU_BOUND},

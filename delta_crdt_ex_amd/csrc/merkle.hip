@@ -497,6 +497,9 @@ __device__ u32 merge_bucket(const Rows& A, const TermH& tha, u64 ia, u64 ie, con
 constexpr int DB = DIFF_BLOCK;
 constexpr u32 XSUB = 1u << DIFF_SUB;  // buckets per subtree (at most)
 constexpr u32 OWN = XSUB / DB;        // buckets per thread
+#ifndef DG_DIFF_EXP
+#define DG_DIFF_EXP 0
+#endif
 constexpr u32 RCAP = 1664;            // rows of the differing buckets staged in LDS
 constexpr u32 DCAP = 512;             // differing buckets listed in LDS
 constexpr u32 NHD = 128;              // node term hashes staged per tree (38.9 KB in all:
@@ -563,7 +566,11 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
   __shared__ u64 s_bnd[2];
   if (tid < 2 * WAVE) {
     const Rows& r = tid < WAVE ? p.sa : p.sb;
+#if DG_DIFF_EXP == 1  // diagnostic build only (timing, wrong keys): no bounds search
+    const u64 x = r.n * tile / p.ntiles;
+#else
     const u64 x = wave_bucket_start(p.ta, r.key, r.n, tile << sub);
+#endif
     if ((tid & (WAVE - 1)) == 0) {
       s_bnd[tid / WAVE] = x;
       p.bnd[(tid < WAVE ? 0 : nbnd) + tile] = x;
@@ -683,11 +690,19 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
           fromb[j] = r >= na;
           const Rows& S = fromb[j] ? p.sb : p.sa;
           const u64 i = fromb[j] ? c0 + s_db[lo] + (r - na) : a0 + s_da[lo] + r;
+#if DG_DIFF_EXP == 2  // diagnostic build only (timing, wrong keys): no row loads
+          key[j] = i;
+          val[j] = i ^ 5;
+          ts[j] = (i64)i;
+          nd[j] = (u32)i & 3;
+          cnt[j] = i;
+#else
           key[j] = S.key[i];
           val[j] = S.val[i];
           ts[j] = S.ts[i];
           nd[j] = S.node[i];
           cnt[j] = S.cnt[i];
+#endif
         }
       }
 #pragma unroll

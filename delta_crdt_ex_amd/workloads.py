@@ -317,9 +317,11 @@ def shard_keys(rank: int, world: int, n_total: int) -> np.ndarray:
 
 def config5_shard(rank: int, world: int, keys_per_rank: int = 12_500_000, seed: int = 5):
     """Config 5 at weak scaling: key-hash shard `rank` of world * keys_per_rank keys (100M
-    over 8 GPUs), each rank's pair drawn with the config-5 distribution (seed per rank)."""
-    return config5(keys=shard_keys(rank, world, world * keys_per_rank), n_nodes=64,
-                   seed=seed + 1000 * rank if world > 1 else seed)
+    over 8 GPUs).  config5 draws every choice from the key alone, so the shards are exact
+    slices of ONE replica pair of world * keys_per_rank keys (they used to be
+    independent pairs)."""
+    n_total = world * keys_per_rank
+    return config5(keys=shard_keys(rank, world, n_total), n_nodes=64, seed=seed, n_total=n_total)
 
 
 def config3_shard(rank: int, world: int, n_keys: int = 10_000_000, seed: int = 3):
@@ -336,57 +338,63 @@ def sync_delta(rep, keys):
     return {"rows": _take_rows(rep["rows"], keys), "ctx": rep["ctx"], "keys": keys}
 
 
+def _draw(k, seed, salt):
+    """A per-key pseudo-random u64: splitmix64 of (key, seed, salt) -- every choice of a
+    generator that must give the same rows for a key however the key space is sharded."""
+    return splitmix64_np(splitmix64_np(k ^ np.uint64((seed * 0x9E3779B97F4A7C15 + salt) & (2**64 - 1)))
+                         ^ np.uint64(salt))
+
+
 def config5(n_keys: int = 100_000_000, n_nodes: int = 64, remove_frac: float = 0.5,
             readd_frac: float = 0.2, ts_range: int = 16, max_entries: int = 3, seed: int = 5,
-            nodes: NodeTable | None = None, keys=None):
+            nodes: NodeTable | None = None, keys=None, n_total: int | None = None):
     """Config 5, remove-heavy adversarial pair.  Base: every key holds 1..max_entries
-    concurrent entries written by random nodes 0..n_nodes-3 (dots {node, c}, c
-    counting per node in key order), small values and ts in [0, ts_range) so LWW ties
-    are everywhere.  Replicas A (node n_nodes-2) and B (node n_nodes-1) each saw the
-    whole base (dense VVs: they cover every dot they hold) and then independently
-    removed `remove_frac` of the keys and re-added (add/4: the key's entries replaced
-    by one new entry) `readd_frac` of the rest.  `keys` (uint64 array of k) overrides
-    the key range (a key-hash shard).  Returns (A, B)."""
+    concurrent entries written by distinct nodes of 0..n_nodes-3 (dots {node, c} with
+    c = k * max_entries + j + 1 for entry j of key k: unique per node), small values and ts
+    in [0, ts_range) so LWW ties are everywhere.  Replicas A (node n_nodes-2) and B (node
+    n_nodes-1) each saw the whole base (dense VVs: they cover every dot they hold) and then
+    independently removed `remove_frac` of the keys and re-added (add/4: the key's entries
+    replaced by one new entry, dot {A or B, k}) `readd_frac` of the rest.  Every choice is
+    a function of the key (and seed), so a key-hash shard (`keys`, a subset of
+    1..n_total) is exactly that shard's slice of the whole pair, with the pair's full VVs.
+    Returns (A, B)."""
     N = nodes or NodeTable(n_nodes, seed)
-    rng = np.random.default_rng(seed)
     k = np.arange(1, n_keys + 1, dtype=np.uint64) if keys is None else np.asarray(keys, np.uint64)
+    total = int(n_total if n_total is not None else (int(k.max()) if len(k) else 0))
     n_keys = len(k)
     key = splitmix64_np(k)
-    ne = rng.integers(1, min(max_entries, n_nodes - 2) + 1, n_keys)
+    W = n_nodes - 2  # base writers
+    me = min(max_entries, W)
+    ne = (_draw(k, seed, 1) % np.uint64(me)).astype(np.int64) + 1
     ekey = np.repeat(key, ne)
     E = len(ekey)
     kidx = np.repeat(np.arange(n_keys), ne)
-    # entry j of key x comes from writer (h_x + j) mod (n_nodes - 2): distinct writers
-    # per key (a writer's second add to a key would replace its first)
+    # entry j of key x comes from writer (h_x + j) mod W: distinct writers per key (a
+    # writer's second add to a key would replace its first)
     first = np.r_[0, np.cumsum(ne)[:-1]]
-    j = np.arange(E) - np.repeat(first, ne)
-    h = rng.integers(0, n_nodes - 2, n_keys)
-    enode = ((h[kidx] + j) % (n_nodes - 2)).astype(np.uint32)  # logical writer
-    # counters per node in generation order (key index, then entry)
-    order = np.argsort(enode, kind="stable")
-    cnt = np.empty(E, np.uint64)
-    sn = enode[order]
-    starts = np.r_[0, np.flatnonzero(sn[1:] != sn[:-1]) + 1]
-    ranks = np.arange(E) - np.repeat(starts, np.diff(np.r_[starts, E]))
-    cnt[order] = ranks.astype(np.uint64) + 1
-    eval_ = encode_int_value(rng.integers(0, 4, E))
-    ets = rng.integers(0, ts_range, E).astype(np.int64)
-    base_vv = {}
-    for nd, c in zip(*np.unique(enode, return_counts=True)):
-        base_vv[N[int(nd)]] = int(c)
+    j = (np.arange(E) - np.repeat(first, ne)).astype(np.uint64)
+    h = (_draw(k, seed, 2) % np.uint64(W))
+    enode = ((h[kidx] + j) % np.uint64(W)).astype(np.uint32)  # logical writer
+    cnt = k[kidx] * np.uint64(me) + j + np.uint64(1)
+    ek = k[kidx] * np.uint64(me) + j  # per-entry draws
+    eval_ = encode_int_value((_draw(ek, seed, 3) % np.uint64(4)).astype(np.int64))
+    ets = (_draw(ek, seed, 4) % np.uint64(ts_range)).astype(np.int64)
+    base_vv = {N[w]: total * me + me for w in range(W)}  # covers every base dot
     enode = N.ids(enode).astype(np.uint32)  # the interned (dense) ids of the writers
     reps = []
-    for node_id in (n_nodes - 2, n_nodes - 1):
-        removed = rng.random(n_keys) < remove_frac
-        readd = (~removed) & (rng.random(n_keys) < readd_frac)
+    for r, node_id in enumerate((n_nodes - 2, n_nodes - 1)):
+        u = _draw(k, seed, 10 + r)
+        removed = (u % np.uint64(1 << 20)).astype(np.float64) < remove_frac * (1 << 20)
+        v = _draw(k, seed, 20 + r)
+        readd = (~removed) & ((v % np.uint64(1 << 20)).astype(np.float64) < readd_frac * (1 << 20))
         keep_e = ~(removed | readd)[kidx]
         na = int(readd.sum())
         ak = key[readd]
-        av = encode_int_value(rng.integers(0, 4, na))
-        at = rng.integers(0, ts_range, na).astype(np.int64)
+        av = encode_int_value((_draw(k[readd], seed, 30 + r) % np.uint64(4)).astype(np.int64))
+        at = (_draw(k[readd], seed, 40 + r) % np.uint64(ts_range)).astype(np.int64)
         rows = sort_rows(np.concatenate([ekey[keep_e], ak]), np.concatenate([eval_[keep_e], av]),
                          np.concatenate([ets[keep_e], at]),
                          np.concatenate([enode[keep_e], np.full(na, N[node_id], np.uint32)]),
-                         np.concatenate([cnt[keep_e], np.arange(1, na + 1, dtype=np.uint64)]))
-        reps.append({"rows": rows, "ctx": vv({**base_vv, N[node_id]: na}), "nodes": N})
+                         np.concatenate([cnt[keep_e], k[readd]]))
+        reps.append({"rows": rows, "ctx": vv({**base_vv, N[node_id]: total}), "nodes": N})
     return reps[0], reps[1]

@@ -86,49 +86,53 @@ def test_config3_keys_outside_keyset_are_right_biased():
 # ------------------------------------------------------------------ config 5
 
 def test_config5_generator_matches_term_replay():
-    n, nn = 50, 8
-    a, b = W.config5(n_keys=n, n_nodes=nn, seed=3)
+    """The config-5 generator's rows are what the reference's own mutators produce: every
+    base writer adds its entries in key order (aw_lww_map.ex:99-112), replicas A and B
+    re-add (add/4) and remove (remove/3) keys.  A writer's counter before an add is set
+    to the generator's counter - 1 in its context, as its adds to keys elsewhere (other
+    shards; later removed) would have left it -- next_dot takes vv[node] + 1 (:30-37)."""
+    n, nn, seed = 50, 8, 3
+    a, b = W.config5(n_keys=n, n_nodes=nn, seed=seed)
     N = a["nodes"]
-    # the base: every writer node's own adds (the generator's draws, replayed in its
-    # order), joined -- concurrent entries of one key survive
-    rng = np.random.default_rng(3)
-    ne = rng.integers(1, 4, n)
-    E = int(ne.sum())
-    kidx = np.repeat(np.arange(n), ne)
-    first = np.r_[0, np.cumsum(ne)[:-1]]
-    h = rng.integers(0, nn - 2, n)
-    enode = (h[kidx] + np.arange(E) - np.repeat(first, ne)) % (nn - 2)
-    # counters per node in generation order
-    seen = {}
-    cnt = []
-    for x in enode:
-        seen[int(x)] = seen.get(int(x), 0) + 1
-        cnt.append(seen[int(x)])
-    evals = rng.integers(0, 4, E)
-    ets = rng.integers(0, 16, E)
+    me, Wn = 3, nn - 2
+    k = np.arange(1, n + 1, dtype=np.uint64)
+    ne = (W._draw(k, seed, 1) % np.uint64(me)).astype(np.int64) + 1
+    h = W._draw(k, seed, 2) % np.uint64(Wn)
     writers = {}
-    for e in range(E):
-        writers.setdefault(int(enode[e]), []).append(e)
+    for x in range(n):
+        for j in range(int(ne[x])):
+            w = int((h[x] + np.uint64(j)) % np.uint64(Wn))
+            ek = np.array([(x + 1) * me + j], np.uint64)
+            val = int(W._draw(ek, seed, 3)[0] % np.uint64(4))
+            ts = int(W._draw(ek, seed, 4)[0] % np.uint64(16))
+            writers.setdefault(w, []).append((x + 1, (x + 1) * me + j + 1, val, ts))
     base = T.compress_dots(T.new())
-    for nd, es in writers.items():
+    for w, adds in writers.items():
         st = T.compress_dots(T.new())
-        for e in es:
-            key = int(kidx[e]) + 1
-            st = T.join(st, T.add(key, int(evals[e]), int(N.raw[nd]), st, int(ets[e])), [key])
+        term = int(N.raw[w])
+        for key, cnt, val, ts in adds:
+            st = T.AW({**st.dots, term: cnt - 1}, st.value)  # its adds elsewhere
+            st = T.join(st, T.add(key, val, term, st, ts), [key])
         base = T.join(base, st, sorted(set(base.value) | set(st.value)))
-    for node_id, gen in ((nn - 2, a), (nn - 1, b)):
-        removed = rng.random(n) < 0.5
-        readd = (~removed) & (rng.random(n) < 0.2)
-        na = int(readd.sum())
-        av = rng.integers(0, 4, na)
-        at = rng.integers(0, 16, na)
+    base = T.AW({**base.dots, **{int(N.raw[w]): n * me + me for w in range(Wn)}}, base.value)
+    for r, (node_id, gen) in enumerate(((nn - 2, a), (nn - 1, b))):
+        term = int(N.raw[node_id])
+        u = W._draw(k, seed, 10 + r)
+        removed = (u % np.uint64(1 << 20)).astype(np.float64) < 0.5 * (1 << 20)
+        v = W._draw(k, seed, 20 + r)
+        readd = (~removed) & ((v % np.uint64(1 << 20)).astype(np.float64) < 0.2 * (1 << 20))
         st = base
-        for j, kk in enumerate(np.flatnonzero(readd)):
-            key = int(kk) + 1
-            st = T.join(st, T.add(key, int(av[j]), int(N.raw[node_id]), st, int(at[j])), [key])
-        for kk in np.flatnonzero(removed):
-            key = int(kk) + 1
-            st = T.join(st, T.remove(key, int(N.raw[node_id]), st), [key])
+        for x in np.flatnonzero(readd):
+            key = int(x) + 1
+            kk = np.array([key], np.uint64)
+            val = int(W._draw(kk, seed, 30 + r)[0] % np.uint64(4))
+            ts = int(W._draw(kk, seed, 40 + r)[0] % np.uint64(16))
+            st = T.AW({**st.dots, term: key - 1}, st.value)
+            st = T.join(st, T.add(key, val, term, st, ts), [key])
+        for x in np.flatnonzero(removed):
+            key = int(x) + 1
+            st = T.join(st, T.remove(key, term, st), [key])
+        st = T.AW({**st.dots, term: n}, st.value)  # its VV entry: the whole key space's
         rows, ctx = CV.state_to_soa_ints(st, N)
         assert rows_equal(rows, gen["rows"]), node_id
         assert ctx_equal(ctx, gen["ctx"]), node_id

@@ -105,6 +105,31 @@ def test_config5_properties_large(engine):
     engine.store_check(j1)
 
 
+def test_config5_shards_join_to_the_unsharded_join(engine):
+    """Config 5 at weak scaling: the 8 key-hash shards of a 4M-key pair are
+    exact slices of the unsharded pair, and their 8 independent device joins (as the ranks
+    of bench.py --gpus 8 run them, no data-path collective) concatenate to the unsharded
+    device join, row for row, with equal contexts and reads."""
+    from delta_crdt_ex_amd.sharding import shard_of
+    world, per = 8, 500_000
+    a, b = W.config5(n_keys=world * per, n_nodes=64, seed=5)
+    whole, wctx = engine.join2(*up(a), *up(b))
+    wrows = whole.to_numpy()
+    sh = shard_of(wrows[0], world)
+    for r in range(world):
+        pa, pb = W.config5_shard(r, world, keys_per_rank=per)
+        for x, y in zip(pa["rows"], tuple(c[shard_of(a["rows"][0], world) == r] for c in a["rows"])):
+            assert np.array_equal(x, y)  # the shard is the pair's slice
+        out, octx = engine.join2(*up(pa), *up(pb))
+        for x, y in zip(out.to_numpy(), (c[sh == r] for c in wrows)):
+            assert np.array_equal(x, y)
+        ctx_eq(octx, (0,) + tuple(wctx.to_numpy()))
+        k1, v1 = engine.read_lww(out)
+        k0, v0 = engine.read_lww(whole)
+        m = shard_of(u64(k0), world) == r
+        assert np.array_equal(u64(k1), u64(k0)[m]) and np.array_equal(u64(v1), u64(v0)[m])
+
+
 @pytest.mark.timeout(600)
 def test_config5_full_share_parity(engine):
     """The bench's config-5 workload itself (one GPU's share of 100M keys: 12.5M keys,

@@ -9,15 +9,23 @@ rc=$?
 tail -1 $O/pytest_gpu.log
 if [ $rc -ne 0 ]; then
   echo "TESTS rc=$rc"; grep -E "^(FAILED|ERROR)" $O/pytest_gpu.log | head -20
-  [ $rc -eq 1 ] || fi
+  [ $rc -eq 1 ] || exit $rc
+fi
 for n in 1000 10000; do timeout -k 10 120 $R/c_src/_build/bench_mutate $n 300 > $O/mutate_$n.json 2> $O/mutate_$n.err || { echo MUTATE_FAILED; cat $O/mutate_$n.err; exit 1; }; cat $O/mutate_$n.json; done
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/mk -o mk -- python3 $R/tools/prof_merkle.py > $O/mk.log 2>&1 || { echo PROF_MK_FAILED; tail -5 $O/mk.log; exit 1; }
 python3 $R/tools/kernel_timeline.py $O/mk 0 > $O/mk_stats.txt; head -14 $O/mk_stats.txt
+# diagnostic diff builds (timing only): no bounds search (EXP1), no row loads (EXP2)
+for x in 1 2; do
+  export DG_LIB_PATH=$R/delta_crdt_ex_amd/libdeltagpu_DG_DIFF_EXP$x.so
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/mkx$x -o mk -- python3 $R/tools/prof_merkle.py > $O/mkx$x.log 2>&1 || { echo PROF_MKX_FAILED; tail -5 $O/mkx$x.log; exit 1; }
+  echo "EXP$x: $(python3 $R/tools/kernel_timeline.py $O/mkx$x 0 | grep -E 'diff_count' | head -1)"
+  rm -f $O/mkx$x/*kernel_trace.csv
+done
+unset DG_LIB_PATH
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c5 -o c5 -- python3 $R/tools/bench_c5_line.py > $O/c5.log 2>&1 || { echo PROF_C5_FAILED; tail -5 $O/c5.log; exit 1; }
 python3 $R/tools/kernel_timeline.py $O/c5 0 > $O/c5_stats.txt; head -6 $O/c5_stats.txt
 grep '^{"metric"' $O/c5.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('c5 events avg_launch_us', d['roofline']['avg_launch_us'], 'frac', d['roofline']['frac'])"
-exit $rc
 # A/B: stripe_sums' partials double-buffered (base) vs one buffer + barrier (var), config 5
 # and config 2 joins back to back (tools/prof_c5.py), rocprofv3 kernel averages
 for v in base var base var; do
