@@ -332,6 +332,7 @@ static void state_dtor(ErlNifEnv* env, void* obj) {
   if (s->has_tree) {
     dg_buffer_free(g->e, s->tree.nodes);
     dg_buffer_free(g->e, s->tree.counts);
+    dg_buffer_free(g->e, s->tree.starts);
   }
   enif_mutex_unlock(g->lock);
   enif_release_resource(g);
@@ -1141,6 +1142,7 @@ static ERL_NIF_TERM merkle_build_nif(ErlNifEnv* env, int argc, const ERL_NIF_TER
   s->tree.terms = &g->th; /* rows hashed through their terms: comparable across nodes */
   TRY(dg_buffer_alloc(g->e, ((2ull << depth) - 1) * 8, (void**)&s->tree.nodes));
   TRY(dg_buffer_alloc(g->e, ((1ull << depth) > 8 ? (1ull << depth) : 8) * 2, (void**)&s->tree.counts));
+  TRY(dg_buffer_alloc(g->e, (dg_merkle_chunks(depth) + 1) * 8, (void**)&s->tree.starts));
   s->has_tree = 1;
   TRY(dg_merkle_build(g->e, &s->rows, &s->tree));
 out:;

@@ -95,6 +95,7 @@ class dg_merkle(C.Structure):
         ("n_keys", C.c_uint64),
         ("counts", VP),
         ("terms", C.POINTER(dg_term_hashes)),
+        ("starts", VP),
     ]
 
 
@@ -181,6 +182,7 @@ _SIGS = {
     "dg_sort_store": (C.c_int, [C.c_void_p, C.POINTER(dg_store), C.POINTER(dg_store)]),
     "dg_sort_context": (C.c_int, [C.c_void_p, C.POINTER(dg_context), C.POINTER(dg_context)]),
     "dg_remap_values": (C.c_int, [C.c_void_p, C.POINTER(dg_store), P64, P64, C.c_uint64]),
+    "dg_merkle_chunks": (C.c_uint64, [C.c_uint32]),
     "dg_merkle_build": (C.c_int, [C.c_void_p, C.POINTER(dg_store), C.POINTER(dg_merkle)]),
     "dg_merkle_build_async": (C.c_int, [C.c_void_p, C.POINTER(dg_store), C.POINTER(dg_merkle),
                                         P64]),

@@ -570,15 +570,20 @@ template <class Tail>
 int tree_update(dg_engine* e, dg_merkle* t, const dg_store* olds, const dg_store* news,
                 const uint64_t* keys, uint64_t n_keys, const char* what, bool ready, Tail tail,
                 u64* d_n_keys) {
+  // scratch: the hand-off words | dirty flags (u32, padded to even) | the per-chunk
+  // row-count changes (i64, for the chunk starts); dirty and cdelta zeroed in one launch
   const u64 chunks = merkle_chunks(t->depth), cw = merkle_ctr_words(t->depth);
-  TRY(ensure_tmp(e, (cw + chunks) * sizeof(u32)));
+  const u64 cpad = (chunks + 1) & ~1ull, zw = cpad + 2 * chunks;
+  TRY(ensure_tmp(e, (cw + zw) * sizeof(u32)));
   u64* hand = (u64*)e->tmp;
   u32* dirty = (u32*)e->tmp + cw;
+  i64* cdelta = (i64*)(dirty + cpad);
   if (!ready)
-    HIP_TRY(launch_splice_finish(nullptr, nullptr, 0, nullptr, nullptr, dirty, chunks, e->d_counts,
+    HIP_TRY(launch_splice_finish(nullptr, nullptr, 0, nullptr, nullptr, dirty, zw, e->d_counts,
                                  e->ticket + 3, e->stream));
   HIP_TRY(launch_merkle_update(merkle_of(t), rows_of(olds), rows_of(news), keys, n_keys, dirty,
-                               e->d_counts, e->ticket + MERKLE_ARRIVE, hand, e->ticket + 3, e->stream));
+                               e->d_counts, e->ticket + MERKLE_ARRIVE, hand, cdelta, e->ticket + 3,
+                               e->stream));
   TRY(tail());
   TRY(read_counts(e, 8));
   u64 dk = 0;
@@ -587,10 +592,11 @@ int tree_update(dg_engine* e, dg_merkle* t, const dg_store* olds, const dg_store
   if (!(e->h_ticket[3] & MERKLE_INPUT_ERR)) return DG_OK;
   const int rc = input_error(e, what);
   const std::string msg = g_err;
-  HIP_TRY(launch_splice_finish(nullptr, nullptr, 0, nullptr, nullptr, dirty, chunks, e->d_counts,
+  HIP_TRY(launch_splice_finish(nullptr, nullptr, 0, nullptr, nullptr, dirty, zw, e->d_counts,
                                e->ticket + 3, e->stream));
   HIP_TRY(launch_merkle_update(merkle_of(t), rows_of(news), rows_of(olds), keys, n_keys, dirty,
-                               e->d_counts, e->ticket + MERKLE_ARRIVE, hand, e->ticket + 3, e->stream));
+                               e->d_counts, e->ticket + MERKLE_ARRIVE, hand, cdelta, e->ticket + 3,
+                               e->stream));
   HIP_TRY(hipMemsetAsync(e->ticket + 3, 0, sizeof(u32), e->stream));  // the undo's own bits
   TRY(read_counts(e, 0));
   g_err = msg;
@@ -1393,6 +1399,7 @@ MerkleT merkle_of(const dg_merkle* t) {
     m.th.nv = (t->terms->val_id && t->terms->val_hash) ? t->terms->n_vals : 0;
     m.th.on = 1;
   }
+  m.starts = t->starts;
   return m;
 }
 
@@ -1618,6 +1625,8 @@ int dg_merkle_truncate(dg_engine* e, const dg_merkle* t, dg_merkle_cont* cont, u
   cont->n_buckets = max;
   return DG_OK;
 }
+
+uint64_t dg_merkle_chunks(uint32_t depth) { return merkle_chunks(depth); }
 
 int dg_merkle_fold_roots(const uint64_t* roots, uint32_t shard_bits, uint64_t* root) {
   if (!roots || !root || shard_bits > 16) return fail(DG_E_INVAL, "dg_merkle_fold_roots: bad arguments");

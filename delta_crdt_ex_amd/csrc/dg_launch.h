@@ -270,6 +270,7 @@ struct MerkleT {
   u64* nodes;     // heap, 2^(depth+1) - 1
   uint16_t* counts;  // rows per bucket, 2^depth
   TermH th;
+  u64* starts;    // optional: first row of each 2^MERKLE_UPL-bucket chunk (+ the end)
 };
 constexpr u32 MERKLE_UPL = 11;  // levels reduced per upsweep workgroup
 // input-error bits a build / update leaves in its error word: a key outside the tree's
@@ -280,6 +281,7 @@ inline u64 merkle_chunks(u32 depth) { return 1ull << (depth - (depth < MERKLE_UP
 // scratch words of a build / update: a u64 chunk root and a u64 key count per chunk (the
 // in-launch hand-off), in u32 units
 inline u64 merkle_ctr_words(u32 depth) { return 4 * merkle_chunks(depth); }
+// an update's per-chunk row-count changes (i64, zero on entry): how the chunk starts move
 // one fused launch: rows hashed into LDS bucket sums per chunk, levels reduced, the last
 // chunk reduces to the root; *d_keys = distinct keys; arrive: a persistent counter, zero
 // on entry and left zero; hand: merkle_ctr_words(depth) u32 of scratch; err bit 1: a row
@@ -292,8 +294,8 @@ hipError_t launch_merkle_build(const Rows& s, const MerkleT& t, u64* d_keys, u32
 // olds and news exchanged undoes it bit for bit (keys outside the shard are skipped both
 // ways; counts wrap mod 2^32 and unwrap).
 hipError_t launch_merkle_update(const MerkleT& t, const Rows& olds, const Rows& news, const u64* keys,
-                                u64 n_keys, u32* dirty, u64* d_keys, u32* arrive, u64* hand, u32* err,
-                                hipStream_t st);
+                                u64 n_keys, u32* dirty, u64* d_keys, u32* arrive, u64* hand, i64* cdelta,
+                                u32* err, hipStream_t st);
 constexpr int DIFF_BLOCK = 256;
 constexpr u32 DIFF_SUB = 12;  // levels a diff workgroup descends: subtrees of 4096 buckets
 inline u32 diff_sub(u32 depth) { return depth < DIFF_SUB ? depth : DIFF_SUB; }

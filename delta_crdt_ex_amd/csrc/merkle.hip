@@ -54,6 +54,7 @@ struct MT {
   u64* nodes;
   uint16_t* counts;
   TermH th;
+  u64* starts;  // optional (nullptr): each chunk's first row, then the end (dg_merkle.starts)
 };
 
 // The value's and the node's terms in a row hash (dg_term_hashes): a canonical integer
@@ -177,7 +178,7 @@ __device__ void lds_upsweep(u64* nodes, u32 hi, u64 g0, u32 width, u64* s) {
 template <bool BUILD, bool VEC = false>
 __global__ __launch_bounds__(UPB, 4) void merkle_chunk_kernel(Rows rows, MT t, const u32* dirty,
                                                            u32* ctr, u64* hand, u64* d_keys,
-                                                           u32* err) {
+                                                           u32* err, const i64* cdelta) {
   __shared__ u64 s[UPW];
   __shared__ u32 s_c[BUILD ? UPW : 1];  // rows per bucket
   __shared__ u64 s_nh[BUILD ? NHL : 1]; // node term hashes
@@ -204,6 +205,10 @@ __global__ __launch_bounds__(UPB, 4) void merkle_chunk_kernel(Rows rows, MT t, c
     }
     __syncthreads();
     const u64 lo = s_rng[0], hi = s_rng[1];
+    if (t.starts && tid == 0) {  // the chunk index (dg_merkle.starts): its first row, and the end
+      t.starts[g] = lo;
+      if (g == G - 1) t.starts[G] = hi;
+    }
     u32 heads = 0;
     // rows outside the tree's key range (before the first chunk, after the last one)
     bool bad = tid == 0 && ((g == 0 && lo > 0) || (g == G - 1 && hi < rows.n));
@@ -365,6 +370,32 @@ __global__ __launch_bounds__(UPB, 4) void merkle_chunk_kernel(Rows rows, MT t, c
     hl -= nlev;
     first = false;
   }
+  if (!BUILD && t.starts && cdelta) {
+    // the update moved rows: chunk g's first row shifts by the row-count changes of the
+    // chunks before it (an exclusive scan of cdelta, UPB chunks per round; the end by all)
+    i64 carry = 0;
+    for (u64 c0 = 0; c0 <= G; c0 += UPB) {
+      const u64 x = c0 + tid;
+      const i64 v = x < G ? cdelta[x] : 0;
+      i64 incl = v;
+#pragma unroll
+      for (int d = 1; d < WAVE; d <<= 1) {
+        const i64 y = __shfl_up(incl, d, WAVE);
+        if (lane >= d) incl += y;
+      }
+      __syncthreads();
+      if (lane == WAVE - 1) s[w] = (u64)incl;
+      __syncthreads();
+      i64 before = 0, tot = 0;
+      for (int q = 0; q < UPB / WAVE; q++) {
+        const i64 y = (i64)s[q];
+        before += q < w ? y : 0;
+        tot += y;
+      }
+      if (x <= G) t.starts[x] = (u64)((i64)t.starts[x] + carry + before + incl - v);
+      carry += tot;
+    }
+  }
   if (BUILD) {
     u64 sum = 0;
     for (u64 x = tid; x < G; x += UPB) sum += ld_sc1(hand + G + x);
@@ -397,7 +428,7 @@ __device__ __forceinline__ u64 key_leaf(const Rows& s, u64 x, const TermH& th, u
 
 __global__ __launch_bounds__(UB) void merkle_update_kernel(MT t, Rows olds, Rows news, const u64* keys,
                                                            u64 n_keys, u32* dirty, u64* d_keys,
-                                                           u32* err) {
+                                                           u32* err, i64* cdelta) {
   const u64 i = (u64)blockIdx.x * UB + threadIdx.x;
   int dk = 0;
   bool bad = false, over = false;
@@ -426,6 +457,8 @@ __global__ __launch_bounds__(UB) void merkle_update_kernel(MT t, Rows olds, Rows
         }
         const u32 L1 = t.depth < (u32)UPL ? t.depth : (u32)UPL;
         dirty[b >> L1] = 1u;
+        if (cdelta && rn != ro)  // the chunk's rows changed in number: later chunks' starts move
+          atomicAdd((unsigned long long*)&cdelta[b >> L1], (unsigned long long)((i64)rn - (i64)ro));
       }
     }
   }
@@ -566,10 +599,12 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
   __shared__ u64 s_bnd[2];
   if (tid < 2 * WAVE) {
     const Rows& r = tid < WAVE ? p.sa : p.sb;
+    const u64* st = tid < WAVE ? p.ta.starts : p.tb.starts;  // the trees' chunk index, if kept
+    const u32 L1 = depth < (u32)UPL ? depth : (u32)UPL;
 #if DG_DIFF_EXP == 1  // diagnostic build only (timing, wrong keys): no bounds search
     const u64 x = r.n * tile / p.ntiles;
 #else
-    const u64 x = wave_bucket_start(p.ta, r.key, r.n, tile << sub);
+    const u64 x = st ? st[(tile << sub) >> L1] : wave_bucket_start(p.ta, r.key, r.n, tile << sub);
 #endif
     if ((tid & (WAVE - 1)) == 0) {
       s_bnd[tid / WAVE] = x;
@@ -927,6 +962,7 @@ MT mt_of(const MerkleT& m) {
   t.nodes = m.nodes;
   t.counts = m.counts;
   t.th = m.th;
+  t.starts = m.starts;
   return t;
 }
 
@@ -943,23 +979,24 @@ hipError_t launch_merkle_build(const Rows& s, const MerkleT& m, u64* d_keys, u32
                                     (uintptr_t)s.node | (uintptr_t)s.cnt) & 15);
   if (vec)
     hipLaunchKernelGGL((merkle_chunk_kernel<true, true>), dim3((unsigned)G), dim3(UPB), 0, st, s, t,
-                       (const u32*)nullptr, arrive, hand, d_keys, err);
+                       (const u32*)nullptr, arrive, hand, d_keys, err, (const i64*)nullptr);
   else
     hipLaunchKernelGGL((merkle_chunk_kernel<true, false>), dim3((unsigned)G), dim3(UPB), 0, st, s, t,
-                       (const u32*)nullptr, arrive, hand, d_keys, err);
+                       (const u32*)nullptr, arrive, hand, d_keys, err, (const i64*)nullptr);
   return hipGetLastError();
 }
 
 hipError_t launch_merkle_update(const MerkleT& m, const Rows& olds, const Rows& news, const u64* keys,
-                                u64 n_keys, u32* dirty, u64* d_keys, u32* arrive, u64* hand, u32* err,
-                                hipStream_t st) {
+                                u64 n_keys, u32* dirty, u64* d_keys, u32* arrive, u64* hand, i64* cdelta,
+                                u32* err, hipStream_t st) {
   const MT t = mt_of(m);
   const u64 G = merkle_chunks(t.depth);
+  i64* cd = t.starts ? cdelta : nullptr;
   if (n_keys)
     hipLaunchKernelGGL(merkle_update_kernel, dim3(grid_of(n_keys, UB)), dim3(UB), 0, st, t, olds, news,
-                       keys, n_keys, dirty, d_keys, err);
+                       keys, n_keys, dirty, d_keys, err, cd);
   hipLaunchKernelGGL(merkle_chunk_kernel<false>, dim3((unsigned)G), dim3(UPB), 0, st, news, t, dirty,
-                     arrive, hand, (u64*)nullptr, err);
+                     arrive, hand, (u64*)nullptr, err, (const i64*)cd);
   return hipGetLastError();
 }
 

@@ -224,6 +224,7 @@ def read(path, device=None):
         tree.nodes.copy_(torch.from_numpy(nodes.view(np.int64).copy()))
         tree.counts[: 1 << depth].copy_(torch.from_numpy(counts.view(np.int16).copy()))
         tree.store = st
+        tree.starts = None  # the chunk index is not persisted: the diff searches until a build
         tree.n_keys = int(len(np.unique(rows[0])))
     return node_id, seq, state, tree
 

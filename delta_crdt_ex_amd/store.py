@@ -183,17 +183,21 @@ class MerkleTree:
     store: Store | None = None
     counts: torch.Tensor | None = None
     terms: TermHashes | None = None
+    starts: torch.Tensor | None = None  # the chunk index (dg_merkle.starts); None: not kept
 
     @staticmethod
     def empty(depth: int, device, shard_bits: int = 0, shard: int = 0,
               terms: TermHashes | None = None) -> "MerkleTree":
+        chunks = 1 << max(depth - 11, 0)
         return MerkleTree(depth, torch.empty(2 * (1 << depth) - 1, dtype=_I64, device=device), 0,
                           shard_bits, shard, None,
-                          torch.empty(max(1 << depth, 8), dtype=torch.int16, device=device), terms)
+                          torch.empty(max(1 << depth, 8), dtype=torch.int16, device=device), terms,
+                          torch.empty(chunks + 1, dtype=_I64, device=device))
 
     def clone(self) -> "MerkleTree":
         return MerkleTree(self.depth, self.nodes.clone(), self.n_keys, self.shard_bits, self.shard,
-                          self.store, self.counts.clone(), self.terms)
+                          self.store, self.counts.clone(), self.terms,
+                          self.starts.clone() if self.starts is not None else None)
 
     def abi(self) -> _abi.dg_merkle:
         if self.terms is not None:  # follow the Universe's newest tables
@@ -206,6 +210,7 @@ class MerkleTree:
         t.n_keys = self.n_keys
         t.counts = self.counts.data_ptr()
         t.terms = C.pointer(self.terms.c) if self.terms is not None else None
+        t.starts = self.starts.data_ptr() if self.starts is not None else None
         return t
 
     def bucket_counts(self) -> np.ndarray:

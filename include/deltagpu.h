@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define DG_ABI_VERSION 3
+#define DG_ABI_VERSION 4
 
 enum dg_status {
   DG_OK = 0,
@@ -116,7 +116,16 @@ typedef struct dg_merkle {
   uint64_t n_keys;     /* distinct keys indexed (set by build / update) */
   uint16_t* counts;    /* 2^depth entries (caller-allocated, device; set by build / update) */
   const dg_term_hashes* terms; /* host pointer (its arrays: device); NULL: hash the ids */
+  uint64_t* starts;    /* optional (NULL: none): dg_merkle_chunks(depth) + 1 entries (device),
+                          the first row of every 2^11-bucket chunk in the indexed store and,
+                          last, the end of the tree's rows; set by build, kept by update (they
+                          move with the rows).  The diff reads a subtree's rows from it instead
+                          of searching the store's keys. */
 } dg_merkle;
+
+/* The number of 2^11-bucket chunks of a depth-`depth` tree (1 up to depth 11): `starts`
+ * holds one more entry.  Host only. */
+uint64_t dg_merkle_chunks(uint32_t depth);
 
 /* A partial-diff continuation (the `continuation` of CausalCrdt's %Diff{},
  * causal_crdt.ex:29,96,255): either NODE form -- the sender's hashes of the nodes

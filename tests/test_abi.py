@@ -30,7 +30,7 @@ def test_every_header_function_is_exported(lib):
 
 
 def test_abi_version(lib):
-    assert lib.dg_abi_version() == 3
+    assert lib.dg_abi_version() == 4
 
 
 LAYOUT_C = r"""
@@ -46,7 +46,7 @@ int main(void) {
   F(dg_context, kind) F(dg_context, node) F(dg_context, cnt) F(dg_context, n) F(dg_context, cap)
   printf("dg_merkle %zu\n", sizeof(dg_merkle));
   F(dg_merkle, depth) F(dg_merkle, shard_bits) F(dg_merkle, shard) F(dg_merkle, nodes)
-  F(dg_merkle, n_keys) F(dg_merkle, counts) F(dg_merkle, terms)
+  F(dg_merkle, n_keys) F(dg_merkle, counts) F(dg_merkle, terms) F(dg_merkle, starts)
   printf("dg_term_hashes %zu\n", sizeof(dg_term_hashes));
   F(dg_term_hashes, node_hash) F(dg_term_hashes, n_nodes) F(dg_term_hashes, val_id)
   F(dg_term_hashes, val_hash) F(dg_term_hashes, n_vals)

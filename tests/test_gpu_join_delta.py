@@ -50,6 +50,8 @@ def apply(engine, a, d, keys, depth=10, terms=None, with_tree=True):
         assert np.array_equal(tree.nodes.cpu().numpy(), fresh.nodes.cpu().numpy())
         assert np.array_equal(tree.bucket_counts(), fresh.bucket_counts())
         assert tree.n_keys == fresh.n_keys
+        # the chunk index moved with the rows (dg_merkle.starts)
+        assert np.array_equal(tree.starts.cpu().numpy(), fresh.starts.cpu().numpy())
     return st, sc, swapped, wr
 
 
@@ -204,11 +206,13 @@ def test_mutation_sequence_matches_the_oracle(engine):
 
 def _snapshot(st, sc, tree):
     return ([c.copy() for c in st.to_numpy()], [c.copy() for c in sc.to_numpy()], sc.kind,
-            tree.nodes.cpu().numpy().copy(), tree.bucket_counts().copy(), tree.n_keys)
+            tree.nodes.cpu().numpy().copy(), tree.bucket_counts().copy(), tree.n_keys,
+            tree.starts.cpu().numpy().copy())
 
 
 def _assert_unchanged(st, sc, tree, snap):
-    rows, ctx, kind, nodes, counts, nk = snap
+    rows, ctx, kind, nodes, counts, nk, starts = snap
+    assert np.array_equal(tree.starts.cpu().numpy(), starts)
     for x, y in zip(st.to_numpy(), rows):
         assert np.array_equal(x, y)
     for x, y in zip(sc.to_numpy(), ctx):

@@ -317,3 +317,31 @@ def test_partial_diff_config4_shard(engine, max_sync_size):
                             u64(cont.bucket[: cont.n_buckets]).astype(np.int64))]
         assert np.array_equal(keys, want)
         assert len(keys[:max_sync_size]) <= max_sync_size  # send_diff's truncate (:105)
+
+
+def test_chunk_index_follows_the_rows(engine):
+    """dg_merkle.starts (each 2^11-bucket chunk's first row): the build's equals the host's
+    search of the store; an update that changes rows per key (adds, removes) moves it
+    exactly as a fresh build would; and a diff reads the same keys with the index as
+    without it (starts = NULL: the key-column search)."""
+    rng = np.random.default_rng(17)
+    a, b = W.random_pair(rng, 60_000, n_nodes=4, max_entries=3)
+    sa, ca = up(a)
+    sb, cb = up(b)
+    depth = 14
+    ta, tb = engine.merkle_build(sa, depth), engine.merkle_build(sb, depth)
+    keys = a["rows"][0]
+    chunk_first = (np.arange(1 << (depth - 11), dtype=np.uint64) << np.uint64(64 - depth + 11))
+    want = np.r_[np.searchsorted(keys, chunk_first), len(keys)].astype(np.uint64)
+    assert np.array_equal(u64(ta.starts), want)
+    out, octx, changed = engine.join2_changes(sa, ca, sb, cb)
+    assert out.n != sa.n  # rows moved
+    engine.merkle_update(ta, out, changed)
+    fresh = engine.merkle_build(out, depth)
+    assert np.array_equal(u64(ta.starts), u64(fresh.starts))
+    assert np.array_equal(nodes(ta), nodes(fresh))
+    ta2, tb2 = engine.merkle_build(out, depth), engine.merkle_build(sb, depth)
+    with_index = u64(engine.merkle_diff(ta2, tb2))
+    ta2.starts = tb2.starts = None
+    assert np.array_equal(u64(engine.merkle_diff(ta2, tb2)), with_index)
+    assert np.array_equal(with_index, R.store_diff(out.to_numpy(), b["rows"]))

@@ -146,3 +146,24 @@ def test_universe_tracks_device_stores_weakly():
     del s
     gc.collect()
     assert U.tracked() == []
+
+
+def test_term_hash_tables_follow_their_universe():
+    """tables made by TermHashes.of follow their Universe -- after new values
+    or nodes are interned (or a relabel) `current()` hands out the new tables, so a tree
+    never hashes a fresh id as itself; tables made from explicit arrays stay as they are."""
+    from delta_crdt_ex_amd.store import TermHashes
+    U = Universe()
+    U.value("a")
+    U.node("n1")
+    th = TermHashes.of(U, "cpu")
+    assert th.current() is th
+    U.value(("a", "tuple"))
+    U.node("n2")
+    th2 = th.current()
+    assert th2 is not th and th2.version == U.terms_version
+    ids, _ = U.value_ids()
+    assert len(th2.vid) >= len(ids) and th2.c.n_nodes == 2
+    fixed = TermHashes(*U.term_tables(), "cpu")
+    U.value("b")
+    assert fixed.current() is fixed
