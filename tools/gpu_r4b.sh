@@ -16,7 +16,7 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/mk -o mk -- python3 $R/tools/prof_merkle.py > $O/mk.log 2>&1 || { echo PROF_MK_FAILED; tail -5 $O/mk.log; exit 1; }
 python3 $R/tools/kernel_timeline.py $O/mk 0 > $O/mk_stats.txt; head -14 $O/mk_stats.txt
 # diagnostic diff builds (timing only): no bounds search (EXP1), no row loads (EXP2)
-for x in 1 2; do
+for x in 2; do
   export DG_LIB_PATH=$R/delta_crdt_ex_amd/libdeltagpu_DG_DIFF_EXP$x.so
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/mkx$x -o mk -- python3 $R/tools/prof_merkle.py > $O/mkx$x.log 2>&1 || { echo PROF_MKX_FAILED; tail -5 $O/mkx$x.log; exit 1; }
   echo "EXP$x: $(python3 $R/tools/kernel_timeline.py $O/mkx$x 0 | grep -E 'diff_count' | head -1)"
