@@ -38,4 +38,6 @@ for v in base var base var; do
   done
 done
 unset DG_LIB_PATH C5_CONFIG C5_REPS
+timeout -k 10 400 bash $R/tools/pmc_diff.sh > $O/pmc_diff.txt 2>&1 || { echo PMC_DIFF_FAILED; tail -5 $O/pmc_diff.txt; exit 1; }
+grep -E "diff_count|chunk_kernel<true" $O/pmc_diff.txt
 exit $rc
