@@ -3,6 +3,10 @@ boundary is a plain C-ABI library, include/deltagpu.h).
 
     python -m delta_crdt_ex_amd.build          # incremental
     python -m delta_crdt_ex_amd.build --force
+
+Experiment builds (DG_VARIANT="-DNAME=V", DG_STAMPS=1) go to ab/libdeltagpu_<NAME>.so, a
+directory that exists only while an A/B runs (tools/build_base.sh puts a build of an
+earlier commit there too); select one with DG_LIB_PATH.
 """
 from __future__ import annotations
 
@@ -19,7 +23,7 @@ STAMPS = os.environ.get("DG_STAMPS") == "1"  # diagnostic build with in-kernel p
 VARIANT = os.environ.get("DG_VARIANT", "")     # experiment builds: extra -D flags, own .so
 _SUFFIX = ("_stamps" if STAMPS else "") + (("_" + VARIANT.replace("=", "").replace("-D", "").replace(" ", "_")) if VARIANT else "")
 OBJ = os.path.join(HERE, "_build" + _SUFFIX)
-LIB = os.path.join(HERE, "libdeltagpu" + _SUFFIX + ".so")
+LIB = os.path.join(HERE, "ab", "libdeltagpu" + _SUFFIX + ".so") if _SUFFIX else os.path.join(HERE, "libdeltagpu.so")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 SOURCES = ["join.hip", "kfold.hip", "take.hip", "splice.hip", "mutate.hip", "segred.hip", "merkle.hip", "remap.hip", "sort.hip", "api.hip"]
 ARCH = os.environ.get("DG_OFFLOAD_ARCH", "gfx950")
@@ -66,6 +70,7 @@ def _digest_object(hipcc: str, run) -> str:
 
 def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(OBJ, exist_ok=True)
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
     hipcc = _hipcc()
     deps = _deps()
     flags = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall",

@@ -1088,18 +1088,18 @@ int kfold_pass(dg_engine* e, const dg_store* state, const dg_context* ctx, int k
   for (int attempt = 0; attempt < 2; attempt++) {
     const u64 T = T0 << (3 * attempt);
     if (T >= (1ull << 31)) return DG_OK;
-    // device scratch: runs | flat | cflat | sstart | dstart | tabC | tabP | flag | dset
+    // device scratch: runs | cflat | sstart | dstart | tabC | tabP | flag | dset
     auto al = [](size_t b) { return (b + 255) / 256 * 256; };
-    const size_t b_runs = al(k * sizeof(KRun)), b_flat = al((2 * k + 2) * sizeof(u64));
+    const size_t b_runs = al(k * sizeof(KRun));
     const size_t b_cf = al((k + 1) * sizeof(u64));
     const size_t b_ss = al((T + 1) * 8), b_ds = al((T + 1) * 2 * k * 4), b_tab = al((size_t)k * KNT * 8);
     u64 dset_n = 1024;  // a power of two at least twice the dots: probes stay short
     while (dset_n < 2 * n_dots) dset_n <<= 1;
     const size_t b_dset = dotsmask ? al(dset_n * 8) : 0;
-    const size_t bytes = b_runs + b_flat + b_cf + b_ss + b_ds + 2 * b_tab + 256 + b_dset;
+    const size_t bytes = b_runs + b_cf + b_ss + b_ds + 2 * b_tab + 256 + b_dset;
     TRY(ensure_state(e, T + 2));
     TRY(ensure_tmp(e, bytes));
-    const size_t hb = b_runs + b_flat + b_cf;
+    const size_t hb = b_runs + b_cf;
     if (hb > e->h_stage_cap) {
       HIP_TRY(hipStreamSynchronize(e->stream));
       if (e->h_stage) HIP_TRY(hipHostFree(e->h_stage));
@@ -1110,7 +1110,6 @@ int kfold_pass(dg_engine* e, const dg_store* state, const dg_context* ctx, int k
       e->h_stage_cap = hb;
     }
     KRun* hr = (KRun*)e->h_stage;
-    u64* hf = (u64*)((char*)e->h_stage + b_runs);
     for (int i = 0; i < k; i++) {
       hr[i].rows = rows_of(&deltas[i]);
       const bool full = !keys || !keys[i];
@@ -1118,12 +1117,11 @@ int kfold_pass(dg_engine* e, const dg_store* state, const dg_context* ctx, int k
       hr[i].n_keys = full ? 0 : n_keys[i];
       hr[i].ctx = ctx_of(&dctxs[i]);
     }
-    auto chunks = [&](u64 n) { return ceil_div(n, KFOLD_FILL_CHUNK); };
-    hf[0] = 0;
-    for (int i = 0; i < k; i++) hf[i + 1] = hf[i] + chunks(deltas[i].n);
-    for (int i = 0; i < k; i++) hf[k + i + 1] = hf[k + i] + chunks(hr[i].n_keys);
-    hf[2 * k + 1] = hf[2 * k] + chunks(state->n);
-    u64* hc = (u64*)((char*)e->h_stage + b_runs + b_flat);
+    u64 max_run = 0;  // the fill's slices per run: a multiple of 8, each <= KFOLD_FILL_SLICE
+    for (int i = 0; i < k; i++) max_run = std::max<u64>({max_run, deltas[i].n, hr[i].n_keys});
+    const u64 fill_p = 8 * std::max<u64>(1, ceil_div(max_run, 8 * KFOLD_FILL_SLICE));
+    if (fill_p >= (1ull << 31)) return DG_OK;
+    u64* hc = (u64*)((char*)e->h_stage + b_runs);
     hc[0] = 0;
     for (int i = 0; i < k; i++) hc[i + 1] = hc[i] + (((dotsmask >> i) & 1) ? dctxs[i].n : 0);
     char* d = (char*)e->tmp;
@@ -1131,9 +1129,8 @@ int kfold_pass(dg_engine* e, const dg_store* state, const dg_context* ctx, int k
     p.s = rows_of(state);
     p.c0 = ctx_of(ctx);
     p.runs = (const KRun*)d;
-    p.flat = (const u64*)(d + b_runs);
-    p.cflat = (const u64*)(d + b_runs + b_flat);
-    char* d2 = d + b_runs + b_flat + b_cf;
+    p.cflat = (const u64*)(d + b_runs);
+    char* d2 = d + b_runs + b_cf;
     p.sstart = (u64*)d2;
     p.dstart = (u32*)(d2 + b_ss);
     p.tabC = (u64*)(d2 + b_ss + b_ds);
@@ -1146,8 +1143,8 @@ int kfold_pass(dg_engine* e, const dg_store* state, const dg_context* ctx, int k
     p.k = k;
     p.allmask = allmask;
     p.T = T;
-    p.n_fill_chunks = hf[2 * k];  // the delta runs; the state's starts: kfold_fill_kernel's
-                                  // trailing workgroups (state_start, one wave per bucket)
+    p.fill_p = (u32)fill_p;  // the delta runs; the state's starts: kfold_fill_kernel's
+                             // trailing workgroups (state_start, one wave per bucket)
     p.out = rows_out_of(out);
     p.out_ctx_node = out_ctx->node;
     p.out_ctx_cnt = out_ctx->cnt;

@@ -88,7 +88,7 @@ constexpr int KFOLD_CAP_M = 512 >> DG_KFOLD_SCALE;   //   keyset entries
 constexpr int KFOLD_MAX_K = 64;    // deltas per pass (delta masks are u64)
 constexpr int KNT = 1024;          // VV tables cover node ids < KNT
 constexpr u32 KF_PREP_FAIL = 1, KF_OVERFLOW = 2;
-constexpr u64 KFOLD_FILL_CHUNK = 1024 * 8;  // elements per workgroup of the bucket fill
+constexpr u64 KFOLD_FILL_SLICE = 2048;  // the fill cuts every delta run into slices of at most this
 // mean fill per bucket the host sizes T for, each >= 5.5 sigma below its LDS capacity:
 // state rows (cap 1024), delta rows (their payload slots: cap 512), keyset entries as
 // staged (cap 1024: a thread stages two items) and all staged items (delta rows + keyset
@@ -111,9 +111,7 @@ struct KFoldArgs {
   int k;
   u64 allmask;         // bit i: delta i joins every key (keys_i == NULL)
   u64 T;               // key buckets
-  const u64* flat;     // 2k+2 prefix sums of run lengths in KFOLD_FILL_CHUNKs: delta
-                       // rows, keysets, state
-  u64 n_fill_chunks;   // flat[2k]: the delta runs' chunks
+  u32 fill_p;          // slices per delta run in the fill: a multiple of 8 (kfold.hip)
   u64* sstart;         // T+1
   u32* dstart;         // (T+1) x 2k
   u64* tabC;           // k x KNT: c_i

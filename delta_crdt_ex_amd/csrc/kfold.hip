@@ -240,17 +240,27 @@ __device__ __forceinline__ void state_start(const KFoldArgs& p, u64 t) {
 }
 
 // One launch of KNT-thread workgroups: workgroup 0 builds the VV tables (kfold_prep);
-// workgroups [1, 1 + fill_blocks) walk the delta runs, one chunk of FILL_CHUNK elements of
-// ONE run at a time (chunk prefix sums per run in p.flat), so the run's key pointer is
-// uniform and the key loads coalesce; each thread issues all of its chunk's loads before
-// any store. The workgroups past them search the state's starts, one bucket per wave.
+// workgroups [1, 1 + fill_blocks) walk the delta runs; the workgroups past them search the
+// state's starts, one bucket per wave.
+//
+// The delta walk writes the (T+1) x 2k start table, bucket-major: the entry of (bucket,
+// run) is one u32 of the 512-B row the bucket's workgroup reads in one go.  Every run is
+// cut into the same number P of equal slices (P = fill_p, a multiple of 8), and slice i of
+// EVERY run goes to a workgroup of XCD i mod 8 (workgroups are dealt to the XCDs
+// round-robin by index).  Keys are uniform hashes, so slice i of every run covers about
+// the same bucket range: a row of the table is written, 4 bytes at a time, by the 2k runs
+// all from one XCD, and the pieces merge in that XCD's L2 before they go to HBM (6.5 MB
+// written for config 3's 6.5 MB table; chunks dealt to any XCD wrote 64 MB: every piece a
+// partial line of its own).  Within a slice each thread issues its elements' loads before
+// any store; the previous key comes from the neighbour lane by DPP.
 constexpr int FILL_BLOCK = KNT;
-constexpr u64 FILL_CHUNK = KFOLD_FILL_CHUNK;
-constexpr int FILL_PER = (int)(FILL_CHUNK / FILL_BLOCK);
-static_assert(FILL_CHUNK % FILL_BLOCK == 0, "whole rounds per chunk");
+constexpr int FILL_PER = 2;  // elements per thread per round (slices are <= 2048 long)
 constexpr int FILL_WAVES = FILL_BLOCK / WAVE;
-__host__ __device__ __forceinline__ u32 fill_blocks(u64 n_fill_chunks) {
-  return (u32)(n_fill_chunks < 2048 ? n_fill_chunks : 2048);
+constexpr u32 FILL_XCD = 8;
+__host__ __device__ __forceinline__ u32 fill_blocks(u32 fill_p, int k) {
+  const u64 items = (u64)fill_p * 2 * (u64)k;  // (run, slice) pairs
+  const u64 g = items < 2048 ? items : 2048;
+  return (u32)((g + FILL_XCD - 1) / FILL_XCD * FILL_XCD);
 }
 
 __global__ __launch_bounds__(FILL_BLOCK) void kfold_fill_kernel(KFoldArgs p) {
@@ -258,49 +268,43 @@ __global__ __launch_bounds__(FILL_BLOCK) void kfold_fill_kernel(KFoldArgs p) {
     kfold_prep(p);
     return;
   }
-  const u32 g = fill_blocks(p.n_fill_chunks);
+  const u32 g = fill_blocks(p.fill_p, p.k);
   const u32 blk = blockIdx.x - 1;
   if (blk >= g) {  // block-uniform
     const u64 t = (u64)(blk - g) * FILL_WAVES + threadIdx.x / WAVE;  // wave-uniform
     if (t <= p.T) state_start(p, t);
     return;
   }
-  __shared__ u64 flat[2 * KFOLD_MAX_K + 2];
   const int nr = 2 * p.k;  // the delta runs
-  for (int i = threadIdx.x; i <= nr; i += FILL_BLOCK) flat[i] = p.flat[i];
-  __syncthreads();
   const u64 T = p.T, stride = 2 * (u64)p.k;
+  const u32 P = p.fill_p, per_x = P / FILL_XCD;
+  const u32 x = blockIdx.x % FILL_XCD;        // this workgroup's XCD
+  const u32 w = blk / FILL_XCD, nw = g / FILL_XCD;  // its index among the XCD's workgroups
   const int lane = threadIdx.x & (WAVE - 1);
-  for (u64 c = blk; c < p.n_fill_chunks; c += g) {
-    int lo = 0, hi = nr;  // flat[lo] <= c < flat[hi]; empty runs are skipped
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (flat[mid] <= c)
-        lo = mid;
-      else
-        hi = mid;
-    }
-    const int r = lo;
+  for (u64 m = w; m < (u64)nr * per_x; m += nw) {
+    const int r = (int)(m / per_x);
+    const u64 i = (m % per_x) * FILL_XCD + x;  // slice i of run r
     u64 n;
     const u64* keys = run_keys(p, r, &n);
-    const u64 j0 = (c - flat[r]) * FILL_CHUNK;
-    const u64 jend = min<u64>(j0 + FILL_CHUNK, n);
-    u64 kc[FILL_PER], kp[FILL_PER];
+    const u64 j0 = n * i / P, jend = n * (i + 1) / P;
+    for (u64 jb = j0; jb < jend; jb += (u64)FILL_PER * FILL_BLOCK) {
+      u64 kc[FILL_PER], kp[FILL_PER];
 #pragma unroll
-    for (int u = 0; u < FILL_PER; u++) {
-      const u64 j = j0 + (u64)u * FILL_BLOCK + threadIdx.x;
-      kc[u] = j < jend ? keys[j] : 0;
-      kp[u] = (lane == 0 && j > 0 && j < jend) ? keys[j - 1] : 0;  // lanes > 0: DPP
-    }
+      for (int u = 0; u < FILL_PER; u++) {
+        const u64 j = jb + (u64)u * FILL_BLOCK + threadIdx.x;
+        kc[u] = j < jend ? keys[j] : 0;
+        kp[u] = (lane == 0 && j > 0 && j < jend) ? keys[j - 1] : 0;  // lanes > 0: DPP
+      }
 #pragma unroll
-    for (int u = 0; u < FILL_PER; u++) {
-      const u64 j = j0 + (u64)u * FILL_BLOCK + threadIdx.x;
-      const u32 b = (u32)bucket_of(kc[u], T);  // every lane, for the DPP shift
-      const u32 pb = wave_prev_or(b, (u32)bucket_of(kp[u], T));  // lane 0: its loaded key's
-      if (j < jend) {
-        u64 bb = j == 0 ? 0 : (u64)pb + 1;
-        const u64 end = (j == n - 1) ? T : b;
-        for (; bb <= end; bb++) p.dstart[bb * stride + r] = (u32)(bb <= b ? j : n);
+      for (int u = 0; u < FILL_PER; u++) {
+        const u64 j = jb + (u64)u * FILL_BLOCK + threadIdx.x;
+        const u32 b = (u32)bucket_of(kc[u], T);  // every lane, for the DPP shift
+        const u32 pb = wave_prev_or(b, (u32)bucket_of(kp[u], T));  // lane 0: its loaded key's
+        if (j < jend) {
+          u64 bb = j == 0 ? 0 : (u64)pb + 1;
+          const u64 end = (j == n - 1) ? T : b;
+          for (; bb <= end; bb++) p.dstart[bb * stride + r] = (u32)(bb <= b ? j : n);
+        }
       }
     }
   }
@@ -834,7 +838,7 @@ hipError_t launch_kfold(const KFoldArgs& p, hipStream_t st) {
     if (n) hipLaunchKernelGGL(kfold_dset_kernel, dim3((u32)((n + DSB - 1) / DSB)), dim3(DSB), 0, st, p);
   }
   // prep + delta fill + the state's starts
-  const u64 g = 1 + fill_blocks(p.n_fill_chunks) + (p.T + FILL_WAVES) / FILL_WAVES;
+  const u64 g = 1 + fill_blocks(p.fill_p, p.k) + (p.T + FILL_WAVES) / FILL_WAVES;
   hipLaunchKernelGGL(kfold_fill_kernel, dim3((u32)g), dim3(FILL_BLOCK), 0, st, p);
   if (p.dotsmask)
     hipLaunchKernelGGL(kfold_kernel<true>, dim3((u32)p.T), dim3(KB), 0, st, p);

@@ -20,7 +20,7 @@ sys.path.insert(0, ROOT)
 
 from delta_crdt_ex_amd import _abi  # noqa: E402
 
-_abi.LIB_PATH = os.environ.get("KF_STAMPS_LIB") or os.path.join(ROOT, "delta_crdt_ex_amd", "libdeltagpu_stamps.so")
+_abi.LIB_PATH = os.environ.get("KF_STAMPS_LIB") or os.path.join(ROOT, "delta_crdt_ex_amd", "ab", "libdeltagpu_stamps.so")
 
 
 def main():

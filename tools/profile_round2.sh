@@ -50,13 +50,13 @@ for k, d in agg.items():
         print(f"   {c:28s} {sum(v)/len(v):16.1f}  (n={len(v)})")
 PY
 # config-5 join stamps
-if [ -e delta_crdt_ex_amd/libdeltagpu_stamps.so ]; then
-  C5_STAMPS=gpurun_out/c5_stamps.npy DG_LIB_PATH=$PWD/delta_crdt_ex_amd/libdeltagpu_stamps.so timeout -k 10 200 python -u tools/prof_c5.py > $OUT/c5_stamps_run.log 2>&1 || { tail -20 $OUT/c5_stamps_run.log; exit 1; }
+if [ -e delta_crdt_ex_amd/ab/libdeltagpu_stamps.so ]; then
+  C5_STAMPS=gpurun_out/c5_stamps.npy DG_LIB_PATH=$PWD/delta_crdt_ex_amd/ab/libdeltagpu_stamps.so timeout -k 10 200 python -u tools/prof_c5.py > $OUT/c5_stamps_run.log 2>&1 || { tail -20 $OUT/c5_stamps_run.log; exit 1; }
   python tools/stamps_report.py gpurun_out/c5_stamps.npy > $OUT/c5_stamps.txt
 fi
 # config-2 join stamps (the bench's fused path)
-if [ -e delta_crdt_ex_amd/libdeltagpu_stamps.so ]; then
-  C5_CONFIG=2 C5_STAMPS=gpurun_out/c2_stamps.npy DG_LIB_PATH=$PWD/delta_crdt_ex_amd/libdeltagpu_stamps.so timeout -k 10 200 python -u tools/prof_c5.py > $OUT/c2_stamps_run.log 2>&1 || { tail -20 $OUT/c2_stamps_run.log; exit 1; }
+if [ -e delta_crdt_ex_amd/ab/libdeltagpu_stamps.so ]; then
+  C5_CONFIG=2 C5_STAMPS=gpurun_out/c2_stamps.npy DG_LIB_PATH=$PWD/delta_crdt_ex_amd/ab/libdeltagpu_stamps.so timeout -k 10 200 python -u tools/prof_c5.py > $OUT/c2_stamps_run.log 2>&1 || { tail -20 $OUT/c2_stamps_run.log; exit 1; }
   python tools/stamps_report.py gpurun_out/c2_stamps.npy > $OUT/c2_stamps.txt
 fi
 # read/1 (segmented reduction) on config 5's joined state + a Merkle build/diff
