@@ -664,15 +664,41 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
     tb_ += y;
     if (mine >> i & 1u) rd += x + y;
   }
-  u32 tot, ND, R;
-  const u32 offa = block_excl_scan<DB>(ta_, s_wave, &tot);
-  __syncthreads();
-  const u32 offb = block_excl_scan<DB>(tb_, s_wave, &tot);
-  __syncthreads();
-  const u32 slot0 = block_excl_scan<DB>(rd, s_wave, &R);
-  __syncthreads();
-  const u32 d0 = block_excl_scan<DB>((u32)__popc(mine), s_wave, &ND);
-  const u64 a0 = s_bnd[0], c0 = s_bnd[1];  // (the scans' barriers came after the searches)
+  // the four exclusive prefixes (rows in A, rows in B, staged rows, differing buckets) in
+  // ONE barrier: four wave scans, the wave totals to LDS, each thread adds up the totals of
+  // the waves before its own (4 waves) -- four block scans took 12 barriers
+  constexpr int NW = DB / WAVE;
+  __shared__ u32 s_w4[4 * NW];
+  u32 offa, offb, slot0, d0, ND, R;
+  {
+    const u32 v[4] = {ta_, tb_, rd, (u32)__popc(mine)};
+    u32 inc[4];
+    const int lane = tid & (WAVE - 1), w = tid / WAVE;
+#pragma unroll
+    for (int j = 0; j < 4; j++) inc[j] = wave_incl_scan(v[j]);
+    if (lane == WAVE - 1)
+#pragma unroll
+      for (int j = 0; j < 4; j++) s_w4[j * NW + w] = inc[j];
+    __syncthreads();
+    u32 below[4], total[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      below[j] = total[j] = 0;
+#pragma unroll
+      for (int i = 0; i < NW; i++) {
+        const u32 x = s_w4[j * NW + i];
+        below[j] += i < w ? x : 0u;
+        total[j] += x;
+      }
+    }
+    offa = below[0] + inc[0] - v[0];
+    offb = below[1] + inc[1] - v[1];
+    slot0 = below[2] + inc[2] - v[2];
+    d0 = below[3] + inc[3] - v[3];
+    R = total[2];
+    ND = total[3];
+  }
+  const u64 a0 = s_bnd[0], c0 = s_bnd[1];  // (the barrier above came after the searches)
   const u64 base = a0 + c0;
   const bool lds = R <= RCAP && ND <= DCAP;  // uniform
   if (lds) {

@@ -21,6 +21,11 @@ cp $R/gpurun_out/prof_kfold/kf_kernel_stats.csv $O/kfold_kernel_stats.csv 2>/dev
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/mk -o mk -- python3 $R/tools/prof_merkle.py > $O/mk.log 2>&1 || { echo PROF_MK_FAILED; tail -5 $O/mk.log; exit 1; }
 python3 $R/tools/kernel_timeline.py $O/mk 0 > $O/mk_stats.txt; head -14 $O/mk_stats.txt
+# the same round on the base build (one-barrier scans and XCD-sliced kfold fill absent)
+DG_LIB_ANY_DIGEST=1 DG_LIB_PATH=$R/delta_crdt_ex_amd/ab/libdeltagpu_base.so timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/mkbase -o mk -- python3 $R/tools/prof_merkle.py > $O/mkbase.log 2>&1 || { echo PROF_MKBASE_FAILED; tail -5 $O/mkbase.log; exit 1; }
+echo "base: $(python3 $R/tools/kernel_timeline.py $O/mkbase 0 | grep -E 'diff_count' | head -1)"
+echo "head: $(grep -E 'diff_count' $O/mk_stats.txt | head -1)"
+rm -f $O/mkbase/*kernel_trace.csv
 # diagnostic diff builds (timing only): no bounds search (EXP1), no row loads (EXP2)
 for x in 2; do
   export DG_LIB_PATH=$R/delta_crdt_ex_amd/ab/libdeltagpu_DG_DIFF_EXP$x.so
