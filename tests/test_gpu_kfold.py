@@ -112,6 +112,21 @@ def test_onepass_small_states(strict, n_keys, keep):
     check(strict, st, ds)
 
 
+@pytest.mark.parametrize("seed", range(2))
+def test_onepass_unequal_runs(strict, seed):
+    """Runs of very unequal lengths: one delta with rows of most keys (its run is cut into
+    more than 8 slices by the fill, P > 8) beside deltas of a few hundred rows, an empty delta and
+    an empty keyset -- most (run, slice) pairs of the fill are empty, and slice i of a long
+    run and of a short one cover different bucket ranges."""
+    n = 30_000
+    st, ds = random_fold(50 + seed, n_keys=n, k=9, p_keys=0.002)
+    _, big = random_fold(50 + seed, n_keys=n, k=1, p_keys=0.9, p_take=0.9)
+    assert len(big[0]["rows"][0]) > 8 * 2048
+    empty = dict(ds[1], rows=tuple(c[:0] for c in ds[1]["rows"]))
+    nokeys = dict(ds[2], keys=np.zeros(0, np.uint64))
+    check(strict, st, ds[:1] + [empty, nokeys] + ds[3:5] + big + ds[5:])
+
+
 def test_onepass_large_node_ids_in_rows(strict):
     """Row node ids >= the VV table width that no context names: never covered."""
     st, ds = random_fold(22, n_keys=2000, k=8, n_nodes=40, node_base=1000, ctx_node_max=1024)
