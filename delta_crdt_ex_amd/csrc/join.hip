@@ -748,10 +748,9 @@ __device__ __forceinline__ void commit_tile(const Staged& r, Buf& s) {
 // earlier, so step 4 rarely waits; its cost is one G-word read per iteration, issued
 // before the merge.  Spins stay bounded (scan.err bit 0 on timeout).
 constexpr int FUSE_IT = JB / WAVE / 2;  // fused splits: one wave per boundary, 2 per tile
-#ifndef DG_JOIN_RED2
-#define DG_JOIN_RED2 1  // stripe_sums' partials double-buffered (0: one buffer + a barrier)
-#endif
-constexpr bool JOIN_RED2 = DG_JOIN_RED2;
+// (stripe_sums' partials are double-buffered by iteration parity, which drops the barrier
+// a single buffer needs before its writes: measured neutral, config 5 356-360 vs 358-360 us
+// and config 2 34.5-35.4 vs 34.6-34.7 us, rocprofv3 on one box; kept, one barrier fewer)
 
 template <bool KEYED>
 struct StreamLds {
@@ -887,7 +886,6 @@ __device__ __forceinline__ void stripe_sums(const u32* cs, u32 epoch, u32* err, 
   // (no barrier before the writes: the caller alternates two s_red buffers by iteration
   // parity, and the previous reader of this buffer finished two iterations ago, behind the
   // iterations' own barriers)
-  if (!JOIN_RED2) __syncthreads();  // (A/B: one buffer, every wave done reading it)
   if ((tid & (WAVE - 1)) == 0) {
     s_red[tid / WAVE] = lo;
     s_red[NW + tid / WAVE] = tot;
@@ -1108,7 +1106,7 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     JSTAMP(t, 4);
     if (k > 0) {  // stripe k-1: this workgroup's tile t - G
       u64 below, all;
-      stripe_sums(cs, epoch, p.scan.err, t - G - w, G, w, true, sc, s.red[JOIN_RED2 ? (k & 1) : 0], &below, &all);
+      stripe_sums(cs, epoch, p.scan.err, t - G - w, G, w, true, sc, s.red[k & 1], &below, &all);
       JSTAMP(t, 5);
       write_tile(p, s, bi ^ 1, base + below, np);
       base += all;
@@ -1119,7 +1117,7 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       u64 below, all;
       StripeCounts last;
       stripe_load(cs, t - w, G, ntiles, epoch, last);
-      stripe_sums(cs, epoch, p.scan.err, t - w, G, w, false, last, s.red[JOIN_RED2 ? ((k + 1) & 1) : 0], &below, &all);
+      stripe_sums(cs, epoch, p.scan.err, t - w, G, w, false, last, s.red[(k + 1) & 1], &below, &all);
       write_tile(p, s, bi, base + below, np);
       if (tid == 0 && t == ntiles - 1) p.d_count[0] = base + below + np;
       break;

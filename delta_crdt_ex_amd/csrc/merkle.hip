@@ -571,6 +571,23 @@ __device__ __forceinline__ void load_counts16(const uint16_t* c, u32 nb, u32 fir
 
 __device__ __forceinline__ u32 half16(const u32 w[8], u32 i) { return (w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu; }
 
+#ifdef DG_STAMPS
+// Diagnostic build only (DG_STAMPS=1): per-subtree phase timestamps (s_memrealtime) by
+// thread 0 of each count workgroup, read back with dg_debug_diff_stamps
+// (tools/diff_stamps.py).  Each stamp is behind a barrier, so only shares are meaningful.
+__device__ u64 g_df_stamps[4096 * 8];
+#define DSTAMP(k)                                                                    \
+  do {                                                                               \
+    __syncthreads();                                                                 \
+    if (threadIdx.x == 0 && tile < 4096)                                             \
+      g_df_stamps[tile * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                \
+  } while (0)
+#else
+#define DSTAMP(k) \
+  do {            \
+  } while (0)
+#endif
+
 __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) {  // 4 per CU: all resident
   __shared__ u32 s_wave[DB / WAVE + 1];
   __shared__ u32 s_da[DCAP], s_db[DCAP];  // a differing bucket's first row in A / B (from the subtree's)
@@ -581,6 +598,7 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
   const u32 depth = p.ta.depth, sub = p.sub, Ls = depth - sub, nb = 1u << sub;
   const u64 tile = blockIdx.x;
   const int tid = threadIdx.x;
+  DSTAMP(0);
   const bool nha_lds = p.ta.th.on && p.ta.th.nn <= NHD, nhb_lds = p.tb.th.on && p.tb.th.nn <= NHD;
   if (nha_lds)
     for (u32 x = tid; x < (u32)p.ta.th.nn; x += DB) s_nha[x] = p.ta.th.nh[x];
@@ -636,6 +654,7 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
     if (tid == 0) p.cnt[tile] = 0;
     return;
   }
+  DSTAMP(1);
   u32 mine = 0;  // the owned buckets that differ (bit i: bucket 16 tid + i)
   if (owns && (sub < 8 || ga != gb) && (sub < 4 || qa != qb)) {
     const u64 lv = ((1ull << depth) - 1) + b0;
@@ -698,6 +717,7 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
     R = total[2];
     ND = total[3];
   }
+  DSTAMP(2);
   const u64 a0 = s_bnd[0], c0 = s_bnd[1];  // (the barrier above came after the searches)
   const u64 base = a0 + c0;
   const bool lds = R <= RCAP && ND <= DCAP;  // uniform
@@ -719,6 +739,7 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
     }
     if (tid == 0) s_dp[ND] = R;
     __syncthreads();
+    DSTAMP(3);
     // hash the staged rows, all at once: row q belongs to the last differing bucket whose
     // first staged row is <= q (a search of the LDS list), A's rows first.  A thread's rows
     // go in batches of RB: every column load of the batch is issued before any row is
@@ -780,11 +801,13 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
       }
     }
     __syncthreads();
+    DSTAMP(4);
     // merge each differing bucket's keys (one lane per bucket): count, scan, write
     u32 c = 0;
     for (int pass = 0; pass < 2; pass++) {
       u32 o = 0;
       if (pass == 1) {
+        DSTAMP(5);
         u32 t2;
         o = block_excl_scan<DB>(c, s_wave, &t2);
         if (tid == 0) {
@@ -811,6 +834,7 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
       }
       c = k2;
     }
+    DSTAMP(6);
     return;
   }
   // more differing rows or buckets than the LDS lists hold: each thread merges its owned
@@ -847,6 +871,15 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
     c = k2;
   }
 }
+
+#ifdef DG_STAMPS
+}  // namespace
+extern "C" int dg_debug_diff_stamps(unsigned long long* host, size_t n) {
+  if (n > 4096 * 8) n = 4096 * 8;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_df_stamps), n * 8) == hipSuccess ? 0 : -3;
+}
+namespace {
+#endif
 
 constexpr int DSB = 1024;
 __global__ __launch_bounds__(DSB) void tile_scan_kernel(const u64* cnt, u64* off, u64 ntiles,
