@@ -233,7 +233,7 @@ static void gpu_upload(gpu* g, hrows* r) {
   memset(&g->tree, 0, sizeof g->tree);
   g->tree.depth = depth;
   DG(dg_buffer_alloc(g->e, ((UINT64_C(2) << depth) - 1) * 8, (void**)&g->tree.nodes));
-  DG(dg_buffer_alloc(g->e, ((UINT64_C(1) << depth) + 8) * 2, (void**)&g->tree.counts));
+  DG(dg_buffer_alloc(g->e, ((UINT64_C(1) << depth) + 16) * 2, (void**)&g->tree.counts));
   DG(dg_buffer_alloc(g->e, (dg_merkle_chunks(depth) + 1) * 8, (void**)&g->tree.starts));
   DG(dg_merkle_build(g->e, &g->st, &g->tree));
   g->msg_words = 8 * 2048;

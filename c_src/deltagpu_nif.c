@@ -1141,7 +1141,7 @@ static ERL_NIF_TERM merkle_build_nif(ErlNifEnv* env, int argc, const ERL_NIF_TER
   TRY(refresh_terms(g));
   s->tree.terms = &g->th; /* rows hashed through their terms: comparable across nodes */
   TRY(dg_buffer_alloc(g->e, ((2ull << depth) - 1) * 8, (void**)&s->tree.nodes));
-  TRY(dg_buffer_alloc(g->e, ((1ull << depth) > 8 ? (1ull << depth) : 8) * 2, (void**)&s->tree.counts));
+  TRY(dg_buffer_alloc(g->e, ((1ull << depth) > 16 ? (1ull << depth) : 16) * 2, (void**)&s->tree.counts));
   TRY(dg_buffer_alloc(g->e, (dg_merkle_chunks(depth) + 1) * 8, (void**)&s->tree.starts));
   s->has_tree = 1;
   TRY(dg_merkle_build(g->e, &s->rows, &s->tree));

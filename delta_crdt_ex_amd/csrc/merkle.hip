@@ -554,22 +554,38 @@ struct DiffArgs {
 };
 
 
-// the counts of a thread's 16 buckets (u16) as 8 words of two halves
-__device__ __forceinline__ void load_counts16(const uint16_t* c, u32 nb, u32 first, u32 w[8]) {
-  if (nb >= OWN) {  // aligned: 32 bytes per thread
-    const uint4* v = (const uint4*)(c + first);
-    const uint4 x = v[0], y = v[1];
-    w[0] = x.x, w[1] = x.y, w[2] = x.z, w[3] = x.w, w[4] = y.x, w[5] = y.y, w[6] = y.z, w[7] = y.w;
-  } else {  // a subtree of fewer than 16 buckets (depth < 4): thread 0 only
+// the counts of a thread's 16 buckets (u16) as 8 words of two halves: 32 bytes at
+// c + first, one path for every subtree size (the counts array holds at least 16 entries,
+// deltagpu.h); mask_counts16 zeroes what the thread does not own, AFTER the round trip's
+// other loads are issued (any use of a loaded value -- a second load path for small
+// subtrees, a mask -- makes the compiler wait for it right there)
+__device__ __forceinline__ void load_counts16(const uint16_t* c, u32 first, u32 w[8]) {
+  const uint4* v = (const uint4*)(c + first);
+  const uint4 x = v[0], y = v[1];
+  w[0] = x.x, w[1] = x.y, w[2] = x.z, w[3] = x.w, w[4] = y.x, w[5] = y.y, w[6] = y.z, w[7] = y.w;
+}
+__device__ __forceinline__ void mask_counts16(u32 w[8], u32 nb, bool owns) {
 #pragma unroll
-    for (u32 q = 0; q < 8; q++) {
-      const u32 lo = 2 * q < nb ? c[first + 2 * q] : 0u, hi = 2 * q + 1 < nb ? c[first + 2 * q + 1] : 0u;
-      w[q] = lo | (hi << 16);
-    }
+  for (u32 q = 0; q < 8; q++) {  // (nb < 16: a tree of fewer than 16 buckets, thread 0's)
+    const u32 keep = (2 * q + 1 < nb ? 0xFFFF0000u : 0u) | (2 * q < nb ? 0xFFFFu : 0u);
+    w[q] &= owns ? keep : 0u;
   }
 }
 
 __device__ __forceinline__ u32 half16(const u32 w[8], u32 i) { return (w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu; }
+
+// a buffer descriptor over [base, base + bytes) for a wave-uniform base (the halves go
+// through readfirstlane so the compiler can keep the descriptor in SGPRs; gfx950 flags)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const u64* base, u32 bytes) {
+  const u32 lo = __builtin_amdgcn_readfirstlane((u32)(uintptr_t)base);
+  const u32 hi = __builtin_amdgcn_readfirstlane((u32)((uintptr_t)base >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uintptr_t)hi << 32) | lo), 0, (int)bytes, 0x00020000);
+}
+// one u64 through a descriptor; an offset past its range reads 0 without an access
+__device__ __forceinline__ u64 buf_load_u64(__amdgpu_buffer_rsrc_t r, int off) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+  return ((u64)v[1] << 32) | v[0];
+}
 
 #ifdef DG_STAMPS
 // Diagnostic build only (DG_STAMPS=1): per-subtree phase timestamps (s_memrealtime) by
@@ -600,20 +616,32 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
   const int tid = threadIdx.x;
   DSTAMP(0);
   const bool nha_lds = p.ta.th.on && p.ta.th.nn <= NHD, nhb_lds = p.tb.th.on && p.tb.th.nn <= NHD;
-  if (nha_lds)
-    for (u32 x = tid; x < (u32)p.ta.th.nn; x += DB) s_nha[x] = p.ta.th.nh[x];
-  if (nhb_lds)
-    for (u32 x = tid; x < (u32)p.tb.th.nn; x += DB) s_nhb[x] = p.tb.th.nh[x];
   const u64 root = ((1ull << Ls) - 1) + tile;
   const u64 nbnd = p.ntiles + 1;
   // ---- descent in strides of 4 levels: thread tid owns buckets [16 tid, 16 tid + 16) of
   //      the subtree, and their common ancestors 4 and 8 levels up (one node each) are
-  //      loaded with the subtree's root and the owned buckets' row counts in ONE round
-  //      trip; the 16 bucket nodes only below differing ancestors, in a second one
+  //      loaded with the subtree's root, the owned buckets' row counts and the node term
+  //      hashes in ONE round trip (every load unconditional at a clamped index, the
+  //      unused ones selected away: a load under a divergent branch is waited for at the
+  //      branch's join, one round trip each); the 16 bucket nodes only below differing
+  //      ancestors, in a second one
   const bool owns = (u32)tid * OWN < nb;
-  const u64 b0 = (tile << sub) + (u64)tid * OWN;  // the first owned bucket (tree-wide)
-  // the subtree's first row in both stores: waves 0 and 1 search while the descent's
-  // loads are in flight (also for the write kernel, which reads them from p.bnd)
+  const u64 bucket0 = tile << sub;
+  const u64 b0 = bucket0 + (u64)tid * OWN;  // the first owned bucket (tree-wide)
+  const u64 b0c = owns ? b0 : bucket0;      // (clamped: the loads stay inside the subtree)
+  const u64 ra = p.ta.nodes[root], rb = p.tb.nodes[root];
+  const u64 gi = sub >= 8 ? ((1ull << (depth - 8)) - 1) + (b0c >> 8) : root;
+  const u64 qi = sub >= 4 ? ((1ull << (depth - 4)) - 1) + (b0c >> 4) : root;
+  const u64 ga = p.ta.nodes[gi], gb = p.tb.nodes[gi], qa = p.ta.nodes[qi], qb = p.tb.nodes[qi];
+  u32 ca[8], cb[8];
+  load_counts16(p.ta.counts + bucket0, owns ? (u32)tid * OWN : 0u, ca);
+  load_counts16(p.tb.counts + bucket0, owns ? (u32)tid * OWN : 0u, cb);
+  const u32 nna = nha_lds ? (u32)p.ta.th.nn : 0u, nnb = nhb_lds ? (u32)p.tb.th.nn : 0u;
+  const u64 hna = nna ? p.ta.th.nh[(u32)tid < nna ? (u32)tid : 0u] : 0ull;
+  const u64 hnb = nnb ? p.tb.th.nh[(u32)tid < nnb ? (u32)tid : 0u] : 0ull;
+  // the subtree's first row in both stores: waves 0 and 1 look it up (the chunk index) or
+  // search while the descent's loads are in flight (also for the write kernel, which
+  // reads them from p.bnd)
   __shared__ u64 s_bnd[2];
   if (tid < 2 * WAVE) {
     const Rows& r = tid < WAVE ? p.sa : p.sb;
@@ -629,34 +657,44 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
       p.bnd[(tid < WAVE ? 0 : nbnd) + tile] = x;
     }
   }
-  const u64 ra = p.ta.nodes[root], rb = p.tb.nodes[root];
-  u64 ga = 0, gb = 0, qa = 0, qb = 0;
-  if (owns && sub >= 8) {
-    const u64 g = ((1ull << (depth - 8)) - 1) + (b0 >> 8);
-    ga = p.ta.nodes[g];
-    gb = p.tb.nodes[g];
-  }
-  if (owns && sub >= 4) {
-    const u64 q = ((1ull << (depth - 4)) - 1) + (b0 >> 4);
-    qa = p.ta.nodes[q];
-    qb = p.tb.nodes[q];
-  }
-  const u64 bucket0 = tile << sub;
-  u32 ca[8], cb[8];
-  if (owns) {
-    load_counts16(p.ta.counts + bucket0, nb, (u32)tid * OWN, ca);
-    load_counts16(p.tb.counts + bucket0, nb, (u32)tid * OWN, cb);
-  } else {
-#pragma unroll
-    for (int q = 0; q < 8; q++) ca[q] = cb[q] = 0;
-  }
+  static_assert(NHD <= DB, "one node term hash per thread");
+  if ((u32)tid < nna) s_nha[tid] = hna;
+  if ((u32)tid < nnb) s_nhb[tid] = hnb;
   if (ra == rb) {  // uniform: the whole subtree matches (the bounds are written anyway)
     if (tid == 0) p.cnt[tile] = 0;
     return;
   }
   DSTAMP(1);
   u32 mine = 0;  // the owned buckets that differ (bit i: bucket 16 tid + i)
-  if (owns && (sub < 8 || ga != gb) && (sub < 4 || qa != qb)) {
+  const bool anc = owns && (sub < 8 || ga != gb) && (sub < 4 || qa != qb);
+  if (nb >= (u32)(WAVE * OWN)) {
+    // the wave's 1024 buckets' nodes, loaded by the wave together: load i of a lane reads
+    // node 64 i + lane (owner lane 4 i + lane / 16, only under its differing ancestors),
+    // so each load instruction reads 512 contiguous bytes instead of one 8-B node from
+    // each of 64 lines (a lane's own 16 nodes); every load is issued before any compare,
+    // and the ballot of load i hands each of its four owner lanes its 16 bits
+    // (buffer loads: a lane that must not load passes an offset past the descriptor's
+    // range, which the hardware answers with 0 and no memory access -- a conditional
+    // global load would be a branch, and the compiler waits for each load at its join)
+    const int lane = tid & (WAVE - 1);
+    const u64 amask = __ballot(anc);
+    const u64 lv = ((1ull << depth) - 1) + (tile << sub) + (u64)(tid - lane) * OWN;
+    const __amdgpu_buffer_rsrc_t na = wave_rsrc(p.ta.nodes + lv, WAVE * OWN * 8);
+    const __amdgpu_buffer_rsrc_t nbr = wave_rsrc(p.tb.nodes + lv, WAVE * OWN * 8);
+    u64 x[OWN], y[OWN];
+#pragma unroll
+    for (u32 i = 0; i < OWN; i++) {
+      const bool ld = (amask >> (4 * i + lane / 16)) & 1;
+      const int off = ld ? (int)((64 * i + lane) * 8) : 0x7ffffff0;
+      x[i] = buf_load_u64(na, off);
+      y[i] = buf_load_u64(nbr, off);
+    }
+#pragma unroll
+    for (u32 i = 0; i < OWN; i++) {
+      const u64 bal = __ballot(x[i] != y[i]);
+      if ((u32)(lane >> 2) == i) mine = (u32)(bal >> (16 * (lane & 3))) & 0xFFFFu;
+    }
+  } else if (anc) {  // a subtree of fewer than 1024 buckets: a thread loads its own nodes
     const u64 lv = ((1ull << depth) - 1) + b0;
     const u32 m = nb < OWN ? nb : OWN;
 #pragma unroll
@@ -675,6 +713,8 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
   //      offsets in both stores (from the subtree's first row) and their place among the
   //      staged rows; then every per-bucket step runs one lane per differing bucket, not
   //      every thread over its 16 owned buckets (which ran each step masked 16 times)
+  mask_counts16(ca, nb, owns);
+  mask_counts16(cb, nb, owns);
   u32 ta_ = 0, tb_ = 0, rd = 0;
 #pragma unroll
   for (u32 i = 0; i < OWN; i++) {
@@ -754,12 +794,10 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
       bool fromb[RB];
 #pragma unroll
       for (int j = 0; j < RB; j++) {
-        const u32 q = (u0 + j) * DB + tid;
-        fromb[j] = false;
-        key[j] = val[j] = cnt[j] = 0;
-        ts[j] = 0;
-        nd[j] = 0;
-        if (q < R) {
+        // (every lane loads: a lane past the staged rows reads the last one again, so
+        // no load sits under a divergent branch and all of them go out before any wait)
+        const u32 q = min((u0 + j) * DB + tid, R - 1);
+        {
           u32 lo = 0, hi = ND;  // s_dp[lo] <= q < s_dp[hi]
           while (hi - lo > 1) {
             const u32 m = (lo + hi) >> 1;

@@ -191,7 +191,7 @@ class MerkleTree:
         chunks = 1 << max(depth - 11, 0)
         return MerkleTree(depth, torch.empty(2 * (1 << depth) - 1, dtype=_I64, device=device), 0,
                           shard_bits, shard, None,
-                          torch.empty(max(1 << depth, 8), dtype=torch.int16, device=device), terms,
+                          torch.empty(max(1 << depth, 16), dtype=torch.int16, device=device), terms,
                           torch.empty(chunks + 1, dtype=_I64, device=device))
 
     def clone(self) -> "MerkleTree":

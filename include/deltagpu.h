@@ -114,7 +114,8 @@ typedef struct dg_merkle {
   uint64_t shard;      /* < 2^shard_bits */
   uint64_t* nodes;     /* 2^(depth+1) - 1 entries (caller-allocated, device) */
   uint64_t n_keys;     /* distinct keys indexed (set by build / update) */
-  uint16_t* counts;    /* 2^depth entries (caller-allocated, device; set by build / update) */
+  uint16_t* counts;    /* max(2^depth, 16) entries, 16-B aligned (caller-allocated, device;
+                          set by build / update) */
   const dg_term_hashes* terms; /* host pointer (its arrays: device); NULL: hash the ids */
   uint64_t* starts;    /* optional (NULL: none): dg_merkle_chunks(depth) + 1 entries (device),
                           the first row of every 2^11-bucket chunk in the indexed store and,
