@@ -840,19 +840,13 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
     }
     __syncthreads();
     DSTAMP(4);
-    // merge each differing bucket's keys (one lane per bucket): count, scan, write
-    u32 c = 0;
-    for (int pass = 0; pass < 2; pass++) {
-      u32 o = 0;
-      if (pass == 1) {
-        DSTAMP(5);
-        u32 t2;
-        o = block_excl_scan<DB>(c, s_wave, &t2);
-        if (tid == 0) {
-          p.cnt[tile] = t2;
-          if (t2) atomicAdd((unsigned long long*)&p.bsum[tile / DB], (unsigned long long)t2);
-        }
-      }
+    // merge each differing bucket's keys (one lane per bucket) ONCE: a lane keeps its
+    // first KR differing keys in registers, the block scan gives the offsets, and only a
+    // lane with more keys than that merges its buckets a second time to write them all
+    // (the merge used to run twice for every lane: count, then write)
+    constexpr u32 KR = 4;
+    u64 kr0 = 0, kr1 = 0, kr2 = 0, kr3 = 0;
+    auto merge = [&](bool write, u32 o) {
       u32 k2 = 0;
       for (u32 d = tid; d < ND; d += DB) {
         const u32 na = s_dn[d] >> 16;
@@ -865,12 +859,36 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
           for (; ia < ie && s_k[ia] == k; ia++) ha += s_h[ia];
           for (; jb < je && s_k[jb] == k; jb++) hb += s_h[jb];
           if (!(pa && pb) || ha != hb) {
-            if (pass == 1) p.keys[base + o + k2] = k;
+            if (write) {
+              p.keys[base + o + k2] = k;
+            } else {
+              kr0 = k2 == 0 ? k : kr0;
+              kr1 = k2 == 1 ? k : kr1;
+              kr2 = k2 == 2 ? k : kr2;
+              kr3 = k2 == 3 ? k : kr3;
+            }
             k2++;
           }
         }
       }
-      c = k2;
+      return k2;
+    };
+    const u32 c = merge(false, 0);
+    DSTAMP(5);
+    u32 t2;
+    const u32 o = block_excl_scan<DB>(c, s_wave, &t2);
+    if (tid == 0) {
+      p.cnt[tile] = t2;
+      if (t2) atomicAdd((unsigned long long*)&p.bsum[tile / DB], (unsigned long long)t2);
+    }
+    if (c > KR) {
+      merge(true, o);
+    } else {
+      u64* dst = p.keys + base + o;
+      if (c > 0) dst[0] = kr0;
+      if (c > 1) dst[1] = kr1;
+      if (c > 2) dst[2] = kr2;
+      if (c > 3) dst[3] = kr3;
     }
     DSTAMP(6);
     return;

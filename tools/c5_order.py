@@ -1,7 +1,9 @@
 """Config-5 join launch time (HIP events, 20 back-to-back launches) with the engine
 created before (C5_ORDER=engine_first) or after (data_first) the stores: tools/prof_c5.py
 (data first) measured the stream kernel ~10 % slower than bench.py's config5_rate (engine
-first) on the same box and data.  Prints the columns' device addresses modulo 2 MB too."""
+first) on the same box and data.  Prints the columns' device addresses modulo 2 MB too.
+C5_WARM=n: n synchronous joins first (bench.py's _timed does 6); C5_DEL=1: the host
+arrays freed once uploaded (bench.py's `del a, b`)."""
 import os
 import sys
 
@@ -21,8 +23,13 @@ out = Store.empty(sa.n + sb.n, dev)
 octx = Context.empty(0, ca.n + cb.n, dev)
 if eng is None:
     eng = Engine(0)
+if os.environ.get("C5_DEL") == "1":
+    del a, b
 d_counts = torch.zeros(8, dtype=torch.int64, device=dev)
 launch = eng.prepare_join2(sa, ca, sb, cb, out, octx, d_counts)
+for _ in range(int(os.environ.get("C5_WARM", "0"))):
+    launch()
+    eng.sync()
 res = []
 for rep in range(3):
     launch()
@@ -36,5 +43,5 @@ for rep in range(3):
     res.append(e0.elapsed_time(e1) * 1e3 / 20)
 mods = {n: [(t.data_ptr() % (2 << 20)) >> 12 for t in (s.key, s.val, s.ts, s.node, s.cnt)]
         for n, s in (("a", sa), ("b", sb), ("out", out))}
-print(f"{order}: us per launch {' '.join(f'{x:.1f}' for x in res)}  addr%2MB (4K pages) {mods}", flush=True)
+print(f"{order} warm={os.environ.get('C5_WARM', '0')} del={os.environ.get('C5_DEL', '0')}: us per launch {' '.join(f'{x:.1f}' for x in res)}  addr%2MB (4K pages) {mods}", flush=True)
 eng.close()
