@@ -191,6 +191,9 @@ _SIGS = {
     "dg_merkle_diff": (C.c_int, [C.c_void_p, C.POINTER(dg_merkle), C.POINTER(dg_store),
                                  C.POINTER(dg_merkle), C.POINTER(dg_store), P64, C.c_uint64, P64,
                                  P64]),
+    "dg_merkle_diff_async": (C.c_int, [C.c_void_p, C.POINTER(dg_merkle), C.POINTER(dg_store),
+                                       C.POINTER(dg_merkle), C.POINTER(dg_store), P64, C.c_uint64,
+                                       P64]),
     "dg_merkle_prepare": (C.c_int, [C.c_void_p, C.POINTER(dg_merkle), C.c_uint32,
                                     C.POINTER(dg_merkle_cont)]),
     "dg_merkle_continue": (C.c_int, [C.c_void_p, C.POINTER(dg_merkle), C.POINTER(dg_store),

@@ -1512,6 +1512,24 @@ int dg_merkle_diff(dg_engine* e, const dg_merkle* a, const dg_store* sa, const d
   return DG_OK;
 }
 
+int dg_merkle_diff_async(dg_engine* e, const dg_merkle* a, const dg_store* sa, const dg_merkle* b,
+                         const dg_store* sb, uint64_t* out_keys, uint64_t cap, uint64_t* d_total) {
+  if (!e) return fail(DG_E_INVAL, "null engine");
+  TRY(check_merkle(a, "dg_merkle_diff_async a"));
+  TRY(check_merkle(b, "dg_merkle_diff_async b"));
+  TRY(same_tree_shape(a, b, "dg_merkle_diff_async"));
+  TRY(check_store(sa, "dg_merkle_diff_async sa"));
+  TRY(check_store(sb, "dg_merkle_diff_async sb"));
+  if (!d_total) return fail(DG_E_INVAL, "dg_merkle_diff_async: null d_total");
+  if (cap && !out_keys) return fail(DG_E_INVAL, "dg_merkle_diff_async: null out_keys");
+  TRY(set_device(e));
+  TRY(settle(e));  // (a logged join that aborted is replayed before its output is read)
+  TRY(ensure_tmp(e, diff_scratch_words(a->depth, sa->n, sb->n) * sizeof(u64)));
+  HIP_TRY(launch_merkle_diff(merkle_of(a), rows_of(sa), merkle_of(b), rows_of(sb), out_keys, cap,
+                             (u64*)e->tmp, d_total, e->stream));
+  return DG_OK;
+}
+
 int dg_merkle_prepare(dg_engine* e, const dg_merkle* t, uint32_t levels, dg_merkle_cont* out) {
   if (!e) return fail(DG_E_INVAL, "null engine");
   TRY(check_merkle(t, "dg_merkle_prepare"));

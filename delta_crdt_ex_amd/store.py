@@ -660,6 +660,21 @@ class Engine:
         keys = out[: n.value]
         return (keys, int(tot.value)) if with_total else keys
 
+    def prepare_merkle_diff(self, a: MerkleTree, b: MerkleTree, out: torch.Tensor, cap: int,
+                            d_total: torch.Tensor):
+        """Pre-marshal dg_merkle_diff_async for repeated launches (benchmark loops, a
+        replica's anti-entropy timer): returns a zero-argument callable that enqueues the
+        diff; the first min(total, cap) keys land in `out`, the total in d_total[0]."""
+        ta, tb, sa, sb = a.abi(), b.abi(), a.store.abi(), b.store.abi()
+        refs = [C.byref(x) for x in (ta, sa, tb, sb)]
+        op, dp, f, h = _ptr(out, _abi.P64), _ptr(d_total, _abi.P64), self.lib.dg_merkle_diff_async, self.h
+
+        def launch():
+            check(f(h, refs[0], refs[1], refs[2], refs[3], op, int(cap), dp))
+
+        launch._keep = (a, b, out, d_total, ta, tb, sa, sb)
+        return launch
+
     def merkle_prepare(self, tree: MerkleTree, levels: int = 8) -> MerkleCont:
         """MerkleMap.prepare_partial_diff(mm, levels) (causal_crdt.ex:255)."""
         self._order()

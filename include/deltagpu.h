@@ -375,6 +375,13 @@ int dg_merkle_diff(dg_engine* e, const dg_merkle* a, const dg_store* sa, const d
                    const dg_store* sb, uint64_t* out_keys, uint64_t cap, uint64_t* n_out,
                    uint64_t* n_total);
 
+/* Same, asynchronous on the engine stream (the loop a replica's anti-entropy timer runs,
+ * or several shard diffs in flight): the total goes to d_total[0] (device) and the first
+ * min(total, cap) keys to out_keys once the stream reaches them.  Pending asynchronous
+ * joins are settled first, as by every call that reads a store. */
+int dg_merkle_diff_async(dg_engine* e, const dg_merkle* a, const dg_store* sa, const dg_merkle* b,
+                         const dg_store* sb, uint64_t* out_keys, uint64_t cap, uint64_t* d_total);
+
 /* MerkleMap.prepare_partial_diff(mm, levels) (causal_crdt.ex:255): a node-form
  * continuation of the tree's level min(levels, depth), every node of it.  Synchronous. */
 int dg_merkle_prepare(dg_engine* e, const dg_merkle* t, uint32_t levels, dg_merkle_cont* out);

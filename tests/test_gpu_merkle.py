@@ -126,6 +126,44 @@ def test_truncated_diff_is_the_prefix(engine, cap):
     assert np.array_equal(u64(got), full[:cap])
 
 
+def test_async_diff_equals_the_synchronous_one(engine):
+    """dg_merkle_diff_async: back-to-back launches into one output, the total on the
+    device, several caps and depths (small subtrees included), and after an asynchronous
+    join that is still pending (the call settles it first)."""
+    a, b = W.merkle_pair(n_keys=30000, diff_frac=0.05, seed=4)
+    sa, ca = up(a)
+    sb, cb = up(b)
+    full = R.store_diff(a["rows"], b["rows"])
+    for depth, cap in ((3, 10**6), (12, 7), (14, 10**6), (14, 0)):
+        ta, tb = engine.merkle_build(sa, depth), engine.merkle_build(sb, depth)
+        out = torch.zeros(max(cap, 1), dtype=torch.int64, device=DEV)
+        d_total = torch.zeros(1, dtype=torch.int64, device=DEV)
+        launch = engine.prepare_merkle_diff(ta, tb, out, cap, d_total)
+        for _ in range(3):
+            launch()
+        engine.sync()
+        n = min(len(full), cap)
+        assert int(d_total[0]) == len(full)
+        assert np.array_equal(u64(out[:n]), full[:n])
+    # a pending asynchronous join whose output the diff reads
+    j = Store.empty(sa.n + sb.n, DEV)
+    jc = Context.empty(0, ca.n + cb.n, DEV)
+    d_counts = torch.zeros(8, dtype=torch.int64, device=DEV)
+    engine.join2_async(sa, ca, sb, cb, j, jc, d_counts=d_counts)
+    engine.sync()
+    j.n = int(d_counts[0])
+    tj, tb = engine.merkle_build(j, 12), engine.merkle_build(sb, 12)
+    wj, _ = R.join2(a["rows"], a["ctx"], b["rows"], b["ctx"])
+    out = torch.zeros(len(full) + 1, dtype=torch.int64, device=DEV)
+    d_total = torch.zeros(1, dtype=torch.int64, device=DEV)
+    engine.join2_async(sa, ca, sb, cb, j, jc, d_counts=d_counts)  # pending
+    engine.prepare_merkle_diff(tj, tb, out, len(full) + 1, d_total)()
+    engine.sync()
+    want = R.store_diff(wj, b["rows"])
+    assert int(d_total[0]) == len(want)
+    assert np.array_equal(u64(out[: len(want)]), want)
+
+
 @pytest.mark.parametrize("levels,depth", [(8, 18), (3, 10), (1, 4), (8, 8)])
 def test_partial_diff_ping_pong(engine, levels, depth):
     """A.prepare -> B.continue -> A.continue -> ... ends with the differing keys, hop
