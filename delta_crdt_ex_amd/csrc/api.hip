@@ -44,6 +44,12 @@ struct dg_engine {
   // splice through `spl`)
   void* ubuf = nullptr;
   size_t ubuf_cap = 0;
+  // the full diff's per-group key sums: two buffers of diff_bsum_cap words, zero when
+  // allocated; a call adds into one and its write kernel zeroes the other, which the
+  // previous call used (no memset launch per diff)
+  u64* diff_bsum = nullptr;
+  u64 diff_bsum_cap = 0;
+  int diff_parity = 0;
   u32 epoch = 0;
   // small device counters + pinned host mirror.  d_counts[0..8) and ticket[0..16) are one
   // device allocation (ticket == (u32*)(d_counts + 8)), so a synchronous call brings its
@@ -162,6 +168,34 @@ int ensure_tmp(dg_engine* e, size_t bytes) {
     return fail(DG_E_NOMEM, "hipMalloc of %zu scratch bytes failed", cap);
   e->tmp_cap = cap;
   return DG_OK;
+}
+
+// the full diff's two group-sum buffers (see dg_engine::diff_bsum), grown on demand
+int ensure_diff_bsum(dg_engine* e, u64 groups) {
+  if (groups <= e->diff_bsum_cap) return DG_OK;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (e->diff_bsum) HIP_TRY(hipFree(e->diff_bsum));
+  e->diff_bsum = nullptr;
+  e->diff_bsum_cap = 0;
+  if (hipMalloc(&e->diff_bsum, 2 * groups * sizeof(u64)) != hipSuccess)
+    return fail(DG_E_NOMEM, "hipMalloc of %llu diff group sums failed", (unsigned long long)groups);
+  HIP_TRY(hipMemsetAsync(e->diff_bsum, 0, 2 * groups * sizeof(u64), e->stream));
+  e->diff_bsum_cap = groups;
+  return DG_OK;
+}
+
+Rows rows_of(const dg_store* s);
+MerkleT merkle_of(const dg_merkle* t);
+
+// one full diff enqueued: the group sums of this call and the ones its write kernel zeroes
+hipError_t enqueue_merkle_diff(dg_engine* e, const dg_merkle* a, const dg_store* sa, const dg_merkle* b,
+                               const dg_store* sb, uint64_t* out_keys, uint64_t cap, u64* d_total) {
+  const u64 g = e->diff_bsum_cap;
+  u64* use = e->diff_bsum + (e->diff_parity ? g : 0);
+  u64* zero = e->diff_bsum + (e->diff_parity ? 0 : g);
+  e->diff_parity ^= 1;
+  return launch_merkle_diff(merkle_of(a), rows_of(sa), merkle_of(b), rows_of(sb), out_keys, cap,
+                            (u64*)e->tmp, use, zero, d_total, e->stream);
 }
 
 // pinned host staging (kernel descriptors, digit histograms), grown on demand
@@ -704,6 +738,7 @@ int dg_engine_destroy(dg_engine* e) {
   if (e->fold) hipFree(e->fold);
   if (e->spl) hipFree(e->spl);
   if (e->ubuf) hipFree(e->ubuf);
+  if (e->diff_bsum) hipFree(e->diff_bsum);
   if (e->h_stage) hipHostFree(e->h_stage);
   if (e->own_stream && e->stream) hipStreamDestroy(e->stream);
   if (e->ev_in || e->ev_out) {  // a registered engine (creation got past the registry)
@@ -1503,8 +1538,8 @@ int dg_merkle_diff(dg_engine* e, const dg_merkle* a, const dg_store* sa, const d
   TRY(set_device(e));
   TRY(settle(e));
   TRY(ensure_tmp(e, diff_scratch_words(a->depth, sa->n, sb->n) * sizeof(u64)));
-  HIP_TRY(launch_merkle_diff(merkle_of(a), rows_of(sa), merkle_of(b), rows_of(sb), out_keys, cap,
-                             (u64*)e->tmp, e->d_counts, e->stream));
+  TRY(ensure_diff_bsum(e, diff_groups(a->depth)));
+  HIP_TRY(enqueue_merkle_diff(e, a, sa, b, sb, out_keys, cap, e->d_counts));
   TRY(read_counts(e, 1));
   const u64 total = e->h_counts[0];
   *n_out = std::min<u64>(total, cap);
@@ -1525,8 +1560,8 @@ int dg_merkle_diff_async(dg_engine* e, const dg_merkle* a, const dg_store* sa, c
   TRY(set_device(e));
   TRY(settle(e));  // (a logged join that aborted is replayed before its output is read)
   TRY(ensure_tmp(e, diff_scratch_words(a->depth, sa->n, sb->n) * sizeof(u64)));
-  HIP_TRY(launch_merkle_diff(merkle_of(a), rows_of(sa), merkle_of(b), rows_of(sb), out_keys, cap,
-                             (u64*)e->tmp, d_total, e->stream));
+  TRY(ensure_diff_bsum(e, diff_groups(a->depth)));
+  HIP_TRY(enqueue_merkle_diff(e, a, sa, b, sb, out_keys, cap, d_total));
   return DG_OK;
 }
 

@@ -300,12 +300,14 @@ inline u32 diff_sub(u32 depth) { return depth < DIFF_SUB ? depth : DIFF_SUB; }
 inline u64 diff_tiles(u32 depth) { return 1ull << (depth - diff_sub(depth)); }
 // subtree boundaries in both stores, per-subtree counts, then the differing keys staged
 // per subtree (at most one per row of either store), then the group sums
+inline u64 diff_groups(u32 depth) { return (diff_tiles(depth) + DIFF_BLOCK - 1) / DIFF_BLOCK; }  // of DIFF_BLOCK subtrees
 inline u64 diff_scratch_words(u32 depth, u64 na, u64 nb) {
-  return 2 * (diff_tiles(depth) + 1) + diff_tiles(depth) + na + nb + 1 + diff_tiles(depth) / 256 + 1;
+  return 2 * (diff_tiles(depth) + 1) + diff_tiles(depth) + na + nb + 1;
 }
 // differing keys, ascending; the first min(total, cap) written; *d_count = total.
 hipError_t launch_merkle_diff(const MerkleT& a, const Rows& sa, const MerkleT& b, const Rows& sb,
-                              u64* out_keys, u64 cap, u64* scratch, u64* d_count, hipStream_t st);
+                              u64* out_keys, u64 cap, u64* scratch, u64* bsum, u64* bsum_zero, u64* d_count,
+                              hipStream_t st);
 // partial diff.  scratch: 2 * ceil(n / 256) u64.
 inline u64 cont_tiles(u64 n) { return (n + 255) / 256; }
 hipError_t launch_cont_compare(const MerkleT& t, u32 L, const u64* pos, const u64* hash, u64 n,

@@ -547,7 +547,9 @@ struct DiffArgs {
   u64* bnd;   // ntiles + 1 boundaries x 2 stores: first row of each subtree in A, then in B
   u64* cnt;   // differing keys per subtree
   u64* keys;  // scratch: nA + nB keys
-  u64* bsum;  // per DB subtrees: the sum of their counts (zeroed before the count kernel)
+  u64* bsum;  // per DB subtrees: the sum of their counts (zero when the count kernel starts)
+  u64* bzero;  // the other parity's sums (the previous call's), zeroed by the write kernel
+  u64 ngroups;
   u64 ntiles;
   u32 sub;
   u64* d_count;
@@ -955,6 +957,8 @@ __global__ __launch_bounds__(WAVE) void merkle_diff_write_kernel(DiffArgs p) {
   // (subtree `tile`'s keys sit at bnd[tile] + bnd[ntiles + 1 + tile] in scratch)
   const int lane = threadIdx.x;
   const u64 tile = blockIdx.x, grp = tile / DB;
+  if (tile == 0)  // the previous call's group sums: zero for the next call
+    for (u64 x = lane; x < p.ngroups; x += WAVE) p.bzero[x] = 0;
   const u64 n = p.cnt[tile];
   const bool last = tile + 1 == p.ntiles;
   if (n == 0 && !last) return;  // uniform
@@ -1116,7 +1120,8 @@ hipError_t launch_merkle_update(const MerkleT& m, const Rows& olds, const Rows& 
 }
 
 hipError_t launch_merkle_diff(const MerkleT& a, const Rows& sa, const MerkleT& b, const Rows& sb,
-                              u64* out_keys, u64 cap, u64* scratch, u64* d_count, hipStream_t st) {
+                              u64* out_keys, u64 cap, u64* scratch, u64* bsum, u64* bsum_zero, u64* d_count,
+                              hipStream_t st) {
   DiffArgs p;
   p.ta = mt_of(a);
   p.tb = mt_of(b);
@@ -1129,10 +1134,10 @@ hipError_t launch_merkle_diff(const MerkleT& a, const Rows& sa, const MerkleT& b
   p.bnd = scratch;
   p.cnt = scratch + 2 * (p.ntiles + 1);
   p.keys = p.cnt + p.ntiles;
-  p.bsum = p.keys + sa.n + sb.n + 1;
+  p.bsum = bsum;  // zero: the write kernel of the call before zeroed it
+  p.bzero = bsum_zero;
+  p.ngroups = diff_groups(a.depth);
   p.d_count = d_count;
-  hipError_t e = hipMemsetAsync(p.bsum, 0, grid_of(p.ntiles, DB) * sizeof(u64), st);
-  if (e != hipSuccess) return e;
   // (the subtree bounds are searched inside the count kernel)
   hipLaunchKernelGGL(merkle_diff_count_kernel, dim3((unsigned)p.ntiles), dim3(DB), 0, st, p);
   hipLaunchKernelGGL(merkle_diff_write_kernel, dim3((unsigned)p.ntiles), dim3(WAVE), 0, st, p);
