@@ -341,7 +341,8 @@ def resident_delta(eng, torch, sa, ca, cb, ta, tb, b, reps=7):
     causal_crdt.ex:383-404), at wall time on the config-4 shard: H2D of the delta's rows
     and keyset from pinned host memory, dg_join_delta (the keyed join applied in place --
     every differing key keeps its one row -- its changed keys and the MerkleMap update),
-    and D2H of the changed keys and their rows (dg_take_keys) for the on_diffs callback.
+    and D2H of the changed keys and their rows (returned by dg_join_delta_rows) for the
+    on_diffs callback.
     The state is restored from a pristine copy before each rep (outside the clock)."""
     from delta_crdt_ex_amd import workloads as W
     from delta_crdt_ex_amd.store import Context, Store
@@ -390,10 +391,11 @@ def resident_delta(eng, torch, sa, ca, cb, ta, tb, b, reps=7):
         dbuf.copy_(msg, non_blocking=True)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        ch, sw = eng.join_delta(st, sc, dst, cb, kd, spare, tt, changed=changed)
+        # dg_join_delta_rows: the changed keys' joined rows come back from the join's own
+        # edit of the keyset (no dg_take_keys search of the 12.5M-row state afterwards)
+        ch, sw = eng.join_delta(st, sc, dst, cb, kd, spare, tt, changed=changed, rows=rst)
         t2 = time.perf_counter()
-        rows = eng.take_keys(st, ch, out=rst)
-        nr, nch = rows.n, int(ch.numel())
+        nr, nch = rst.n, int(ch.numel())
         rhost.copy_(cbuf, non_blocking=True)  # rows and changed keys: one D2H copy
         torch.cuda.synchronize()
         t3 = time.perf_counter()
@@ -410,8 +412,9 @@ def resident_delta(eng, torch, sa, ca, cb, ta, tb, b, reps=7):
             "deltas_per_s": 1e6 / med["total"],
             "note": "synchronous calls; the delta travels as one pinned message (one H2D copy) "
                     "and the changed keys with their rows as one D2H copy; median of reps; join_delta = "
-                    "dg_join_delta: the state's rows of the keyset taken, joined with the delta, "
-                    "written back in place (csrc/splice.hip), changed keys, MerkleMap update"}
+                    "dg_join_delta_rows: the state's rows of the keyset taken, joined with the delta, "
+                    "written back in place (csrc/splice.hip), changed keys, MerkleMap update, the "
+                    "changed keys' rows gathered from the join's edit"}
 
 
 def _timed(torch, fn, reps):

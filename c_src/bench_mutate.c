@@ -16,9 +16,10 @@
  * §3), and one op costs what a NIF's join_delta costs on a GPU-attached state:
  *   h2d   the delta (rows, dot-list context, keyset) as ONE packed copy into the
  *         state's scratch (no allocation per op)
- *   join  dg_join_delta: the keyed join in place or through the spare store, the changed
+ *   join  dg_join_delta_rows: the keyed join in place or through the spare store, the changed
  *         keys, the MerkleMap put/delete (the state's tree)
- *   d2h   the changed keys' rows (dg_take_keys) and the keys, back for on_diffs
+ *   d2h   the changed keys' rows (returned by dg_join_delta_rows) and the keys, back for
+ *         on_diffs
  * Also `batch`: the reference's trace workload (1000 x mutate(:add, ["key#{x}", "value"]),
  * :9-23) as ONE delta through one dg_join_delta -- how mutate_async batches amortize.
  *
@@ -284,19 +285,21 @@ static void gpu_apply(gpu* g, const uint64_t* key, const uint64_t* val, const in
   const double t1 = now_us();
   uint64_t n_changed = 0;
   int swapped = 0;
-  DG(dg_join_delta(g->e, &g->st, &g->ctx, &ds, &dc, d + o_keys, nk, &g->spare, &g->tree,
-                   g->changed, g->back_cap, &n_changed, &swapped));
+  /* the changed keys (written by the join) and their rows (dg_join_delta_rows: from the
+   * join's own edit) in ONE device block -- keys | key | val | ts | cnt | node, the row
+   * columns at stride S (64: a one-key op changes one key) -- and one copy of it home */
+  uint64_t S = 64;
+  uint64_t* b = g->d_back + g->back_cap;
+  dg_store tk = {b, b + S, (int64_t*)(b + 2 * S), (uint32_t*)(b + 4 * S), b + 3 * S, 0, S};
+  DG(dg_join_delta_rows(g->e, &g->st, &g->ctx, &ds, &dc, d + o_keys, nk, &g->spare, &g->tree,
+                        g->changed, g->back_cap, &n_changed, &swapped, &tk));
   const double t2 = now_us();
-  if (n_changed) {
-    /* the changed keys (written there by dg_join_delta) and their rows (dg_take_keys) in
-     * ONE device block -- keys | key | val | ts | cnt | node, the row columns at stride S
-     * (64 for a few keys, back_cap otherwise) -- and one copy of it home */
-    const uint64_t S = n_changed <= 16 ? 64 : g->back_cap;
-    uint64_t* b = g->d_back + g->back_cap;
-    dg_store tk = {b, b + S, (int64_t*)(b + 2 * S), (uint32_t*)(b + 4 * S), b + 3 * S, 0, S};
-    DG(dg_take_keys(g->e, &g->st, g->changed, n_changed, &tk));
-    DG(dg_copy_to_host(g->e, g->h_back, g->d_back, (g->back_cap + 5 * S) * 8));
+  if (tk.n > tk.cap) {  /* more rows than the small stride: take them again, wider */
+    S = g->back_cap;
+    dg_store wide = {b, b + S, (int64_t*)(b + 2 * S), (uint32_t*)(b + 4 * S), b + 3 * S, 0, S};
+    DG(dg_take_keys(g->e, &g->st, g->changed, n_changed, &wide));
   }
+  if (n_changed) DG(dg_copy_to_host(g->e, g->h_back, g->d_back, (g->back_cap + 5 * S) * 8));
   const double t3 = now_us();
   t[0] = t1 - t0;
   t[1] = t2 - t1;
@@ -329,15 +332,16 @@ static void gpu_mutate_batch(gpu* g, const uint64_t* key, const uint64_t* val, c
   int swapped = 0;
   DG(dg_mutate_batch(g->e, &g->st, &g->ctx, 0, m, (const uint8_t*)(d + 4 * m), d, d + m,
                      (const int64_t*)(d + 2 * m), d + 3 * m, m, &delta, &dots, g->mb_keys, m, &n_keys));
-  DG(dg_join_delta(g->e, &g->st, &g->ctx, &delta, &dots, g->mb_keys, n_keys, &g->spare, &g->tree,
-                   g->changed, g->back_cap, &n_changed, &swapped));
-  if (n_changed) {
-    uint64_t* b = g->d_back + g->back_cap;
-    const uint64_t S = g->back_cap;
-    dg_store tk = {b, b + S, (int64_t*)(b + 2 * S), (uint32_t*)(b + 4 * S), b + 3 * S, 0, S};
-    DG(dg_take_keys(g->e, &g->st, g->changed, n_changed, &tk));
-    DG(dg_copy_to_host(g->e, g->h_back, g->d_back, 6 * S * 8));
+  uint64_t* b = g->d_back + g->back_cap;
+  const uint64_t S = g->back_cap;
+  dg_store tk = {b, b + S, (int64_t*)(b + 2 * S), (uint32_t*)(b + 4 * S), b + 3 * S, 0, S};
+  DG(dg_join_delta_rows(g->e, &g->st, &g->ctx, &delta, &dots, g->mb_keys, n_keys, &g->spare,
+                        &g->tree, g->changed, g->back_cap, &n_changed, &swapped, &tk));
+  if (tk.n > tk.cap) {
+    fprintf(stderr, "return block too small\n");
+    exit(1);
   }
+  if (n_changed) DG(dg_copy_to_host(g->e, g->h_back, g->d_back, 6 * S * 8));
 }
 
 static void gpu_read(gpu* g) {

@@ -825,19 +825,33 @@ static ERL_NIF_TERM state_load(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
   return r;
 }
 
-/* The keys a dg_join_delta changed (in d->back[0, n_changed)) as [{key, value_map | nil}]
- * and the state's new context: their rows taken into the return block (grown and retaken
- * if a key holds more rows than the block's stride), the block copied home ONCE. */
+/* The rows half of the return block: key | val | ts | cnt | node columns at stride
+ * back_cap after the changed keys. */
+static dg_store back_rows(delta_buf* d) {
+  const uint64_t S = d->back_cap;
+  uint64_t* b = d->back + S;
+  dg_store tk = {b, b + S, (int64_t*)(b + 2 * S), (uint32_t*)(b + 4 * S), b + 3 * S, 0, S};
+  return tk;
+}
+
+/* The keys a dg_join_delta_rows changed (in d->back[0, n_changed)) as
+ * [{key, value_map | nil}] and the state's new context: their rows, which the join wrote
+ * into the return block (`taken` = their number; UINT64_MAX: not written, more than the
+ * block's stride holds -> grown and taken from the state), the block copied home ONCE. */
 static int changed_result(ErlNifEnv* env, engine_res* g, state_res* s, uint64_t n_changed,
-                          ERL_NIF_TERM* new_dots, ERL_NIF_TERM* changed_terms) {
+                          uint64_t taken, ERL_NIF_TERM* new_dots, ERL_NIF_TERM* changed_terms) {
   delta_buf* d = &s->d;
   ERL_NIF_TERM values = enif_make_new_map(env);
   int rc = DG_OK;
   for (int attempt = 0;; attempt++) {
     const uint64_t S = d->back_cap;
-    uint64_t* b = d->back + S;
-    dg_store tk = {b, b + S, (int64_t*)(b + 2 * S), (uint32_t*)(b + 4 * S), b + 3 * S, 0, S};
-    rc = dg_take_keys(g->e, &s->rows, d->back, n_changed, &tk);
+    dg_store tk = back_rows(d);
+    if (attempt == 0 && taken != UINT64_MAX) {
+      tk.n = taken;
+      rc = DG_OK;
+    } else {
+      rc = dg_take_keys(g->e, &s->rows, d->back, n_changed, &tk);
+    }
     if (rc == DG_E_CAPACITY && attempt == 0) {
       /* grow, keeping the changed keys: they pass through the host */
       uint64_t* keep = (uint64_t*)enif_alloc((n_changed ? n_changed : 1) * 8);
@@ -915,9 +929,14 @@ static ERL_NIF_TERM join_delta(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
   /* update_state_with_delta: the join (in place, or through the spare buffer: the structs
    * come back exchanged), the changed keys, the MerkleMap put/delete of them -- all or
    * nothing: on an error the state, its context and tree are as they were */
-  TRY(dg_join_delta(g->e, &s->rows, &s->ctx, &d->rows, &d->ctx, d->keys, n_keys, &s->spare,
-                    s->has_tree ? &s->tree : NULL, d->back, d->back_cap, &n_changed, &swapped));
-  TRY(changed_result(env, g, s, n_changed, &new_dots, &changed_terms));
+  {
+    dg_store tk = back_rows(d);
+    TRY(dg_join_delta_rows(g->e, &s->rows, &s->ctx, &d->rows, &d->ctx, d->keys, n_keys, &s->spare,
+                           s->has_tree ? &s->tree : NULL, d->back, d->back_cap, &n_changed,
+                           &swapped, &tk));
+    TRY(changed_result(env, g, s, n_changed, tk.n <= tk.cap ? tk.n : UINT64_MAX, &new_dots,
+                       &changed_terms));
+  }
 out:
   r = rc ? error_term(env, rc) : enif_make_tuple3(env, A_OK, new_dots, changed_terms);
   dgm_rows_free(&h);
@@ -1049,9 +1068,14 @@ static ERL_NIF_TERM mutate_batch_nif(ErlNifEnv* env, int argc, const ERL_NIF_TER
   TRY(room_for(g, s, d->rows.n, d->ctx.n));
   TRY(grow_back(g, d, n_keys ? n_keys : 1));
   if (s->has_tree) TRY(refresh_terms(g));
-  TRY(dg_join_delta(g->e, &s->rows, &s->ctx, &d->rows, &d->ctx, d->keys, n_keys, &s->spare,
-                    s->has_tree ? &s->tree : NULL, d->back, d->back_cap, &n_changed, &swapped));
-  TRY(changed_result(env, g, s, n_changed, &new_dots, &changed_terms));
+  {
+    dg_store tk = back_rows(d);
+    TRY(dg_join_delta_rows(g->e, &s->rows, &s->ctx, &d->rows, &d->ctx, d->keys, n_keys, &s->spare,
+                           s->has_tree ? &s->tree : NULL, d->back, d->back_cap, &n_changed,
+                           &swapped, &tk));
+    TRY(changed_result(env, g, s, n_changed, tk.n <= tk.cap ? tk.n : UINT64_MAX, &new_dots,
+                       &changed_terms));
+  }
 out:
   r = rc ? error_term(env, rc) : enif_make_tuple3(env, A_OK, new_dots, changed_terms);
   if (ops) enif_free(ops);

@@ -147,6 +147,10 @@ _SIGS = {
                                 C.POINTER(dg_store), C.POINTER(dg_context), P64, C.c_uint64,
                                 C.POINTER(dg_store), C.c_void_p, P64, C.c_uint64, P64,
                                 C.POINTER(C.c_int)]),
+    "dg_join_delta_rows": (C.c_int, [C.c_void_p, C.POINTER(dg_store), C.POINTER(dg_context),
+                                     C.POINTER(dg_store), C.POINTER(dg_context), P64, C.c_uint64,
+                                     C.POINTER(dg_store), C.c_void_p, P64, C.c_uint64, P64,
+                                     C.POINTER(C.c_int), C.POINTER(dg_store)]),
     "dg_take_keys": (C.c_int, [C.c_void_p, C.POINTER(dg_store), P64, C.c_uint64,
                                C.POINTER(dg_store)]),
     "dg_mutate_batch": (C.c_int, [C.c_void_p, C.POINTER(dg_store), C.POINTER(dg_context),

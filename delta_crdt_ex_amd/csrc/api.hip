@@ -891,10 +891,20 @@ int dg_join2_changes(dg_engine* e, const dg_store* a, const dg_context* ca, cons
   return DG_OK;
 }
 
-int dg_join_delta(dg_engine* e, dg_store* state, dg_context* state_ctx, const dg_store* delta,
-                  const dg_context* delta_ctx, const uint64_t* keys, uint64_t n_keys,
-                  dg_store* spare, dg_merkle* tree, uint64_t* changed, uint64_t cap,
-                  uint64_t* n_changed, int* swapped) {
+// dg_join_delta_rows' output: the changed keys' rows of `src`; more than rows->cap is
+// reported in rows->n, not as an error (the join before it is complete)
+static int take_changed_rows(dg_engine* e, const dg_store* src, const uint64_t* changed,
+                             uint64_t n_changed, dg_store* rows) {
+  const int rc = dg_take_keys(e, src, changed, n_changed, rows);
+  if (rc == DG_E_CAPACITY) return DG_OK;
+  return rc;
+}
+
+// dg_join_delta[_rows]: rows (optional) receives the changed keys' joined rows
+static int join_delta_impl(dg_engine* e, dg_store* state, dg_context* state_ctx, const dg_store* delta,
+                           const dg_context* delta_ctx, const uint64_t* keys, uint64_t n_keys,
+                           dg_store* spare, dg_merkle* tree, uint64_t* changed, uint64_t cap,
+                           uint64_t* n_changed, int* swapped, dg_store* rows) {
   if (!e) return fail(DG_E_INVAL, "null engine");
   if (!swapped || !n_changed || (cap && !changed) || !spare || !state || !state_ctx)
     return fail(DG_E_INVAL, "dg_join_delta: null argument");
@@ -944,6 +954,7 @@ int dg_join_delta(dg_engine* e, dg_store* state, dg_context* state_ctx, const dg
     state_ctx->kind = uc.kind;
     std::swap(*state, *spare);
     *swapped = 1;
+    if (rows) TRY(take_changed_rows(e, state, changed, *n_changed, rows));  // (the new state)
     return DG_OK;
   }
   TRY(splice_edit(e, &w, state_ctx, delta, delta_ctx, keys, n_keys, &w.uctx, true, changed, cap));
@@ -979,12 +990,12 @@ int dg_join_delta(dg_engine* e, dg_store* state, dg_context* state_ctx, const dg
                                  nullptr, 0, nullptr, nullptr, e->stream, guard));
     return DG_OK;
   };
+  dg_store ed = w.ed;  // the keyset's joined rows (scratch, key order)
+  ed.n = n_e;
   if (tree) {
     // MerkleMap.put/delete of the changed keys: every changed key is a keyset key, so its
     // old rows are among the taken rows and its new rows among the edit's (both small and
     // cache-resident: no search of the 12.5M-row state)
-    dg_store ed = w.ed;
-    ed.n = n_e;
     u64 dk = 0;
     TRY(tree_update(e, tree, &w.ak, &ed, changed, *n_changed, "dg_join_delta", false, copy, &dk));
     tree->n_keys += dk;
@@ -999,7 +1010,27 @@ int dg_join_delta(dg_engine* e, dg_store* state, dg_context* state_ctx, const dg
     std::swap(*state, *spare);
     *swapped = 1;
   }
+  // the changed keys' rows from the edit (a changed key is a keyset key: all of its
+  // joined rows are in the edit), not by a search of the state
+  if (rows) TRY(take_changed_rows(e, &ed, changed, *n_changed, rows));
   return DG_OK;
+}
+
+int dg_join_delta(dg_engine* e, dg_store* state, dg_context* state_ctx, const dg_store* delta,
+                  const dg_context* delta_ctx, const uint64_t* keys, uint64_t n_keys,
+                  dg_store* spare, dg_merkle* tree, uint64_t* changed, uint64_t cap,
+                  uint64_t* n_changed, int* swapped) {
+  return join_delta_impl(e, state, state_ctx, delta, delta_ctx, keys, n_keys, spare, tree, changed,
+                         cap, n_changed, swapped, nullptr);
+}
+
+int dg_join_delta_rows(dg_engine* e, dg_store* state, dg_context* state_ctx, const dg_store* delta,
+                       const dg_context* delta_ctx, const uint64_t* keys, uint64_t n_keys,
+                       dg_store* spare, dg_merkle* tree, uint64_t* changed, uint64_t cap,
+                       uint64_t* n_changed, int* swapped, dg_store* rows) {
+  if (!rows) return fail(DG_E_INVAL, "dg_join_delta_rows: null rows");
+  return join_delta_impl(e, state, state_ctx, delta, delta_ctx, keys, n_keys, spare, tree, changed,
+                         cap, n_changed, swapped, rows);
 }
 
 }  // extern "C"

@@ -599,13 +599,14 @@ class Engine:
 
     def join_delta(self, state: Store, state_ctx: Context, delta: Store, delta_ctx: Context,
                    keys: torch.Tensor, spare: Store, tree: MerkleTree | None = None,
-                   changed: torch.Tensor | None = None):
+                   changed: torch.Tensor | None = None, rows: Store | None = None):
         """CausalCrdt.update_state_with_delta on a device-resident state
         (causal_crdt.ex:383-404, dg_join_delta): `state` and `state_ctx` become the keyed
         join with the sync delta, `tree` (indexing `state`) is updated for the changed keys.
         In place when every joined key keeps its row count; otherwise the result lands in
         `spare` and the two Store objects exchange their columns (so `state` always holds
-        the joined rows).  Returns (changed keys, swapped)."""
+        the joined rows).  `rows` (optional): receives the changed keys' joined rows
+        (dg_join_delta_rows, what on_diffs reads).  Returns (changed keys, swapped)."""
         self._order()
         if changed is None:
             changed = torch.empty(max(int(keys.numel()), 1), dtype=_I64, device=self.device)
@@ -614,10 +615,15 @@ class Engine:
         kp, nk = self._keys(keys)
         n = C.c_uint64(0)
         sw = C.c_int(0)
-        check(self.lib.dg_join_delta(self.h, C.byref(ss), C.byref(sc), C.byref(sd), C.byref(cd),
-                                     kp, nk, C.byref(sp), C.byref(t) if t is not None else None,
-                                     _ptr(changed, _abi.P64), int(changed.numel()), C.byref(n),
-                                     C.byref(sw)))
+        args = (self.h, C.byref(ss), C.byref(sc), C.byref(sd), C.byref(cd), kp, nk, C.byref(sp),
+                C.byref(t) if t is not None else None, _ptr(changed, _abi.P64), int(changed.numel()),
+                C.byref(n), C.byref(sw))
+        if rows is None:
+            check(self.lib.dg_join_delta(*args))
+        else:
+            ro = rows.abi()
+            check(self.lib.dg_join_delta_rows(*args, C.byref(ro)))
+            rows.n = int(ro.n)
         if sw.value:
             for f in ("key", "val", "ts", "node", "cnt"):
                 a, b = getattr(state, f), getattr(spare, f)

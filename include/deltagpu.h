@@ -246,6 +246,19 @@ int dg_join_delta(dg_engine* e, dg_store* state, dg_context* state_ctx, const dg
                   dg_store* spare, dg_merkle* tree, uint64_t* changed, uint64_t cap,
                   uint64_t* n_changed, int* swapped);
 
+/* dg_join_delta plus the rows of the changed keys in the joined state -- what the caller
+ * hands to on_diffs and its reply (the changed keys' new value maps, causal_crdt.ex:344-352,
+ * the NIF's join_delta) -- into rows[0, rows->cap), rows->n = their number, in store
+ * order.  On the in-place and moved paths they are taken from the join's own edit of the
+ * keyset (small and cache-resident) instead of by a search of the whole state, as a
+ * dg_take_keys call after dg_join_delta would.  More rows than rows->cap is not an
+ * error (the join is complete): rows->n > rows->cap on return says the rows were not
+ * written; take them with dg_take_keys.  Synchronous. */
+int dg_join_delta_rows(dg_engine* e, dg_store* state, dg_context* state_ctx, const dg_store* delta,
+                       const dg_context* delta_ctx, const uint64_t* keys, uint64_t n_keys,
+                       dg_store* spare, dg_merkle* tree, uint64_t* changed, uint64_t cap,
+                       uint64_t* n_changed, int* swapped, dg_store* rows);
+
 /* Fold of join/3 over k stores (how CausalCrdt applies k deltas in a row,
  * causal_crdt.ex:86-89,383-384): out = join(...join(join(s0, s1), s2)..., s_{k-1})
  * over all keys.  A row survives iff for every input i it is present in s_i or its

@@ -40,11 +40,16 @@ def apply(engine, a, d, keys, depth=10, terms=None, with_tree=True):
     sd, cd = up(d)
     spare = Store.empty(st.n + sd.n, DEV)
     tree = engine.merkle_build(st, depth, MerkleTree.empty(depth, DEV, terms=terms)) if with_tree else None
-    changed, swapped = engine.join_delta(st, sc, sd, cd, kdev(keys), spare, tree)
+    # (dg_join_delta_rows: the changed keys' joined rows come back too, taken from the
+    # join's edit of the keyset on the in-place and moved paths)
+    rows = Store.empty(st.n + sd.n, DEV)
+    changed, swapped = engine.join_delta(st, sc, sd, cd, kdev(keys), spare, tree, rows=rows)
     wr, wc = R.join2(a["rows"], a["ctx"], d["rows"], d["ctx"], keys=keys)
     rows_eq(st, wr)
     ctx_eq(sc, wc)
-    assert np.array_equal(u64(changed), R.changed_keys(a["rows"], wr, keys))
+    wch = R.changed_keys(a["rows"], wr, keys)
+    assert np.array_equal(u64(changed), wch)
+    rows_eq(rows, tuple(c[np.isin(wr[0], wch)] for c in wr))
     if with_tree:
         fresh = engine.merkle_build(st, depth, MerkleTree.empty(depth, DEV, terms=terms))
         assert np.array_equal(tree.nodes.cpu().numpy(), fresh.nodes.cpu().numpy())
