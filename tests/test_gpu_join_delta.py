@@ -95,6 +95,28 @@ def test_not_a_sync_delta_takes_the_full_join(engine):
     apply(engine, a, d, keys, with_tree=False)
 
 
+def test_changed_rows_past_their_capacity(engine):
+    """dg_join_delta_rows with a rows buffer too small: the join is complete (state,
+    context, changed keys as with room), rows.n reports how many rows there are, and
+    dg_take_keys of the changed keys returns them."""
+    a, b = W.config4_shard(1, 8, keys_per_rank=40_000, diff_frac=0.02)
+    want = R.store_diff(a["rows"], b["rows"])
+    d = W.sync_delta(b, want)
+    st, sc = state_of(a, extra_ctx=8)
+    sd, cd = up(d)
+    spare = Store.empty(st.n + sd.n, DEV)
+    small = Store.empty(3, DEV)
+    changed, _ = engine.join_delta(st, sc, sd, cd, kdev(want), spare, None, rows=small)
+    wr, wc = R.join2(a["rows"], a["ctx"], d["rows"], d["ctx"], keys=want)
+    rows_eq(st, wr)
+    ctx_eq(sc, wc)
+    wch = R.changed_keys(a["rows"], wr, want)
+    assert np.array_equal(u64(changed), wch)
+    sel = np.isin(wr[0], wch)
+    assert small.n == int(sel.sum()) > small.cap
+    rows_eq(engine.take_keys(st, changed), tuple(c[sel] for c in wr))
+
+
 def test_applied_twice_changes_nothing(engine):
     a, b = W.config4_shard(0, 8, keys_per_rank=40_000, diff_frac=0.02)
     want = R.store_diff(a["rows"], b["rows"])
