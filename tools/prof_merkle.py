@@ -1,7 +1,8 @@
-"""The config-4 anti-entropy round at the bench's shard shape (rocprofv3 target): trees
-over node terms (dg_term_hashes, as bench.py builds them), builds, diffs, the sync delta
-(dg_take_keys), the keyed join with its changed keys (the splice), and the incremental
-tree update.  Usage: python tools/prof_merkle.py [keys_per_gpu]"""
+"""The config-4 anti-entropy round at the bench's shard shape (rocprofv3 target), as
+bench.py's config4_round runs it on the receiving replica: trees over node terms
+(dg_term_hashes), builds, the diff, the sync delta (dg_take_keys) and dg_join_delta_rows
+on A's device-resident state (the keyed join in place, its changed keys, the MerkleMap
+update, the changed keys' rows).  Usage: python tools/prof_merkle.py [keys_per_gpu]"""
 import os
 import sys
 
@@ -26,12 +27,23 @@ tb = eng.merkle_build(sb, depth, MerkleTree.empty(depth, dev, 3, 0, terms), 3, 0
 for _ in range(3):
     eng.merkle_build(sa, depth, ta, 3, 0)
     eng.merkle_build(sb, depth, tb, 3, 0)
+st = Store.empty(sa.n + sb.n, dev)
+spare = Store.empty(sa.n + sb.n, dev)
+sc = Context.empty(ca.kind, ca.n + cb.n, dev)
+rows = Store.empty(sa.n + sb.n, dev)
 for _ in range(5):
+    for f in ("key", "val", "ts", "node", "cnt"):  # A's pristine state (outside the round)
+        getattr(st, f)[: sa.n].copy_(getattr(sa, f)[: sa.n])
+    st.n = sa.n
+    sc.node[: ca.n].copy_(ca.node[: ca.n])
+    sc.cnt[: ca.n].copy_(ca.cnt[: ca.n])
+    sc.n, sc.kind = ca.n, ca.kind
+    t = ta.clone()
+    t.store = st
     torch.cuda.synchronize()
     keys = eng.merkle_diff(ta, tb)
     delta = eng.take_keys(sb, keys)
-    out, octx, changed = eng.join2_changes(sa, ca, delta, cb, keys=keys)
-    t = ta.clone()
-    eng.merkle_update(t, out, changed)
+    changed, swapped = eng.join_delta(st, sc, delta, cb, keys, spare, t, rows=rows)
 torch.cuda.synchronize()
-print("depth", depth, "diff keys", keys.numel(), "changed", changed.numel(), flush=True)
+print("depth", depth, "diff keys", keys.numel(), "changed", changed.numel(), "in place", not swapped,
+      flush=True)
