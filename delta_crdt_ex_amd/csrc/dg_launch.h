@@ -294,11 +294,8 @@ hipError_t launch_merkle_build(const Rows& s, const MerkleT& t, u64* d_keys, u32
 hipError_t launch_merkle_update(const MerkleT& t, const Rows& olds, const Rows& news, const u64* keys,
                                 u64 n_keys, u32* dirty, u64* d_keys, u32* arrive, u64* hand, i64* cdelta,
                                 u32* err, hipStream_t st);
-#ifndef DG_DIFF_WIDE  // (A/B: 1 = subtrees of 8192 buckets, 512-thread workgroups, 2 per CU)
-#define DG_DIFF_WIDE 0
-#endif
-constexpr int DIFF_BLOCK = DG_DIFF_WIDE ? 512 : 256;
-constexpr u32 DIFF_SUB = DG_DIFF_WIDE ? 13 : 12;  // levels a diff workgroup descends: subtrees of 4096 buckets
+constexpr int DIFF_BLOCK = 256;
+constexpr u32 DIFF_SUB = 12;  // levels a diff workgroup descends: subtrees of 4096 buckets
 inline u32 diff_sub(u32 depth) { return depth < DIFF_SUB ? depth : DIFF_SUB; }
 inline u64 diff_tiles(u32 depth) { return 1ull << (depth - diff_sub(depth)); }
 // subtree boundaries in both stores, per-subtree counts, then the differing keys staged

@@ -533,8 +533,8 @@ constexpr u32 OWN = XSUB / DB;        // buckets per thread
 #ifndef DG_DIFF_EXP
 #define DG_DIFF_EXP 0
 #endif
-constexpr u32 RCAP = DG_DIFF_WIDE ? 3328 : 1664;  // rows of the differing buckets staged in LDS
-constexpr u32 DCAP = DG_DIFF_WIDE ? 1024 : 512;   // differing buckets listed in LDS
+constexpr u32 RCAP = 1664;            // rows of the differing buckets staged in LDS
+constexpr u32 DCAP = 512;             // differing buckets listed in LDS
 constexpr u32 NHD = 128;              // node term hashes staged per tree (38.9 KB in all:
                                       // 4 workgroups per CU)
 static_assert(OWN == 16, "a thread owns 16 buckets: two 16-byte count loads per tree");
@@ -606,7 +606,7 @@ __device__ u64 g_df_stamps[4096 * 8];
   } while (0)
 #endif
 
-__global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) {  // (4 waves per SIMD: 128 VGPRs) all resident
+__global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) {  // 4 per CU: all resident
   __shared__ u32 s_wave[DB / WAVE + 1];
   __shared__ u32 s_da[DCAP], s_db[DCAP];  // a differing bucket's first row in A / B (from the subtree's)
   __shared__ u32 s_dp[DCAP + 1];          // its first staged row
