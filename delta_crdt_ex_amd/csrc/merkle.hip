@@ -172,6 +172,48 @@ __device__ void lds_upsweep(u64* nodes, u32 hi, u64 g0, u32 width, u64* s) {
   }
 }
 
+// The same for a full chunk (width == UPW == 4 * UPB) with ONE block barrier instead of
+// eleven: a thread takes its 4 leaves from LDS and makes levels 1 and 2 in registers, each
+// wave makes the next 6 levels with shuffles (at level 2 + k the lanes that are multiples
+// of 2^k combine their node with the one 2^(k-1) lanes up), the 8 wave roots meet in LDS
+// and wave 0 makes the last 3 levels.  Writes every level to `nodes` as lds_upsweep does
+// and leaves the chunk root in s[0].
+static_assert(UPW == 4 * UPB && UPB / WAVE == 8, "4 leaves per thread, 8 waves");
+__device__ void chunk_upsweep(u64* nodes, u32 hi, u64 g0, u64* s) {
+  const u32 tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
+  auto row = [&](u32 l) { return nodes + ((1ull << (hi - l)) - 1) + (g0 >> l); };
+  const u64 l0 = s[4 * tid], l1 = s[4 * tid + 1], l2 = s[4 * tid + 2], l3 = s[4 * tid + 3];
+  const u64 p0 = node_hash(l0, l1), p1 = node_hash(l2, l3);
+  row(1)[2 * tid] = p0;
+  row(1)[2 * tid + 1] = p1;
+  u64 v = node_hash(p0, p1);
+  row(2)[tid] = v;
+#pragma unroll
+  for (u32 k = 1; k <= 6; k++) {  // levels 3..8 inside the wave
+    const u64 o = __shfl_down(v, 1u << (k - 1), WAVE);
+    if ((lane & ((1u << k) - 1)) == 0) {
+      v = node_hash(v, o);
+      row(2 + k)[tid >> k] = v;
+    }
+  }
+  __syncthreads();  // every wave is done reading s (the leaves)
+  if (lane == 0) s[w] = v;  // level-8 node w
+  __syncthreads();
+  if (w == 0) {
+    u64 x = lane < 8 ? s[lane] : 0ull;
+#pragma unroll
+    for (u32 k = 1; k <= 3; k++) {  // levels 9..11
+      const u64 o = __shfl_down(x, 1u << (k - 1), WAVE);
+      if (lane < 8 && (lane & ((1u << k) - 1)) == 0) {
+        x = node_hash(x, o);
+        row(8 + k)[lane >> k] = x;
+      }
+    }
+    if (lane == 0) s[0] = x;
+  }
+  __syncthreads();
+}
+
 // ctr: the arrival counter, zero on entry and left zero (the last workgroup resets it: a
 // persistent engine word, no fill launch per build); scratch: per chunk its root and its
 // distinct-key count (u64 each, at hand[0, G) and hand[G, 2G)).
@@ -331,12 +373,18 @@ __global__ __launch_bounds__(UPB, 4) void merkle_chunk_kernel(Rows rows, MT t, c
       t.counts[g0 + x] = (uint16_t)(c > 0xFFFFu ? 0xFFFFu : c);
     }
     if (__ballot(over) && lane == 0) atomicOr(err, ERR_COUNT);
-    lds_upsweep(t.nodes, t.depth, g0, width, s);
+    if (width == UPW)  // (uniform)
+      chunk_upsweep(t.nodes, t.depth, g0, s);
+    else
+      lds_upsweep(t.nodes, t.depth, g0, width, s);
     chunk_root = s[0];
   } else if (dirty[g]) {
     for (u32 x = tid; x < width; x += UPB) s[x] = lvl[g0 + x];
     __syncthreads();
-    lds_upsweep(t.nodes, t.depth, g0, width, s);
+    if (width == UPW)  // (uniform)
+      chunk_upsweep(t.nodes, t.depth, g0, s);
+    else
+      lds_upsweep(t.nodes, t.depth, g0, width, s);
     chunk_root = s[0];
   } else if (tid == 0) {  // unchanged: its root as the previous kernels left it
     chunk_root = t.nodes[((1ull << (t.depth - L1)) - 1) + g];
