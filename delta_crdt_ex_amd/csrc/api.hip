@@ -188,6 +188,7 @@ Rows rows_of(const dg_store* s);
 MerkleT merkle_of(const dg_merkle* t);
 
 // one full diff enqueued: the group sums of this call and the ones its write kernel zeroes
+// (all g words: a call of another depth may have dirtied more groups than this one has)
 hipError_t enqueue_merkle_diff(dg_engine* e, const dg_merkle* a, const dg_store* sa, const dg_merkle* b,
                                const dg_store* sb, uint64_t* out_keys, uint64_t cap, u64* d_total) {
   const u64 g = e->diff_bsum_cap;
@@ -195,7 +196,7 @@ hipError_t enqueue_merkle_diff(dg_engine* e, const dg_merkle* a, const dg_store*
   u64* zero = e->diff_bsum + (e->diff_parity ? 0 : g);
   e->diff_parity ^= 1;
   return launch_merkle_diff(merkle_of(a), rows_of(sa), merkle_of(b), rows_of(sb), out_keys, cap,
-                            (u64*)e->tmp, use, zero, d_total, e->stream);
+                            (u64*)e->tmp, use, zero, g, d_total, e->stream);
 }
 
 // pinned host staging (kernel descriptors, digit histograms), grown on demand

@@ -306,8 +306,8 @@ inline u64 diff_scratch_words(u32 depth, u64 na, u64 nb) {
 }
 // differing keys, ascending; the first min(total, cap) written; *d_count = total.
 hipError_t launch_merkle_diff(const MerkleT& a, const Rows& sa, const MerkleT& b, const Rows& sb,
-                              u64* out_keys, u64 cap, u64* scratch, u64* bsum, u64* bsum_zero, u64* d_count,
-                              hipStream_t st);
+                              u64* out_keys, u64 cap, u64* scratch, u64* bsum, u64* bsum_zero, u64 nzero,
+                              u64* d_count, hipStream_t st);
 // partial diff.  scratch: 2 * ceil(n / 256) u64.
 inline u64 cont_tiles(u64 n) { return (n + 255) / 256; }
 hipError_t launch_cont_compare(const MerkleT& t, u32 L, const u64* pos, const u64* hash, u64 n,

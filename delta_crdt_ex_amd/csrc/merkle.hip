@@ -597,7 +597,7 @@ struct DiffArgs {
   u64* keys;  // scratch: nA + nB keys
   u64* bsum;  // per DB subtrees: the sum of their counts (zero when the count kernel starts)
   u64* bzero;  // the other parity's sums (the previous call's), zeroed by the write kernel
-  u64 ngroups;
+  u64 nzero;   // ... all of its words: a call of another depth may have used more of them
   u64 ntiles;
   u32 sub;
   u64* d_count;
@@ -1006,7 +1006,7 @@ __global__ __launch_bounds__(WAVE) void merkle_diff_write_kernel(DiffArgs p) {
   const int lane = threadIdx.x;
   const u64 tile = blockIdx.x, grp = tile / DB;
   if (tile == 0)  // the previous call's group sums: zero for the next call
-    for (u64 x = lane; x < p.ngroups; x += WAVE) p.bzero[x] = 0;
+    for (u64 x = lane; x < p.nzero; x += WAVE) p.bzero[x] = 0;
   const u64 n = p.cnt[tile];
   const bool last = tile + 1 == p.ntiles;
   if (n == 0 && !last) return;  // uniform
@@ -1168,8 +1168,8 @@ hipError_t launch_merkle_update(const MerkleT& m, const Rows& olds, const Rows& 
 }
 
 hipError_t launch_merkle_diff(const MerkleT& a, const Rows& sa, const MerkleT& b, const Rows& sb,
-                              u64* out_keys, u64 cap, u64* scratch, u64* bsum, u64* bsum_zero, u64* d_count,
-                              hipStream_t st) {
+                              u64* out_keys, u64 cap, u64* scratch, u64* bsum, u64* bsum_zero, u64 nzero,
+                              u64* d_count, hipStream_t st) {
   DiffArgs p;
   p.ta = mt_of(a);
   p.tb = mt_of(b);
@@ -1184,7 +1184,7 @@ hipError_t launch_merkle_diff(const MerkleT& a, const Rows& sa, const MerkleT& b
   p.keys = p.cnt + p.ntiles;
   p.bsum = bsum;  // zero: the write kernel of the call before zeroed it
   p.bzero = bsum_zero;
-  p.ngroups = diff_groups(a.depth);
+  p.nzero = nzero;
   p.d_count = d_count;
   // (the subtree bounds are searched inside the count kernel)
   hipLaunchKernelGGL(merkle_diff_count_kernel, dim3((unsigned)p.ntiles), dim3(DB), 0, st, p);

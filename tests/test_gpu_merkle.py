@@ -164,6 +164,21 @@ def test_async_diff_equals_the_synchronous_one(engine):
     assert np.array_equal(u64(out[: len(want)]), want)
 
 
+def test_diffs_of_different_depths_in_sequence(engine):
+    """The diff's per-group key sums live in two engine buffers that alternate by call; a
+    shallow diff between two deep ones must not leave the deep one's second group stale
+    (depth 21: 512 subtrees in 2 groups; depth 12: one)."""
+    a, b = W.merkle_pair(n_keys=200_000, diff_frac=0.01, seed=21)
+    sa, _ = up(a)
+    sb, _ = up(b)
+    full = R.store_diff(a["rows"], b["rows"])
+    deep = (engine.merkle_build(sa, 21), engine.merkle_build(sb, 21))
+    shallow = (engine.merkle_build(sa, 12), engine.merkle_build(sb, 12))
+    for trees in (deep, shallow, deep, deep, shallow, deep):
+        got, total = engine.merkle_diff(*trees, with_total=True)
+        assert total == len(full) and np.array_equal(u64(got), full)
+
+
 @pytest.mark.parametrize("levels,depth", [(8, 18), (3, 10), (1, 4), (8, 8)])
 def test_partial_diff_ping_pong(engine, levels, depth):
     """A.prepare -> B.continue -> A.continue -> ... ends with the differing keys, hop
