@@ -413,7 +413,10 @@ __global__ __launch_bounds__(UPB, 4) void merkle_chunk_kernel(Rows rows, MT t, c
       for (u32 x = tid; x < (1u << nlev); x += UPB)
         s[x] = first ? ld_sc1(hand + (c << nlev) + x) : src[(c << nlev) + x];
       __syncthreads();
-      lds_upsweep(t.nodes, hl, c << nlev, 1u << nlev, s);
+      if ((1u << nlev) == UPW)  // (uniform)
+        chunk_upsweep(t.nodes, hl, c << nlev, s);
+      else
+        lds_upsweep(t.nodes, hl, c << nlev, 1u << nlev, s);
     }
     hl -= nlev;
     first = false;
@@ -421,11 +424,23 @@ __global__ __launch_bounds__(UPB, 4) void merkle_chunk_kernel(Rows rows, MT t, c
   if (!BUILD && t.starts && cdelta) {
     // the update moved rows: chunk g's first row shifts by the row-count changes of the
     // chunks before it (an exclusive scan of cdelta, UPB chunks per round; the end by all)
+    // (CP consecutive entries per thread, their loads issued together: one round of
+    // UPB * CP = 4096 entries covers the 2048 chunks of a depth-22 tree)
+    constexpr int CP = 8;
     i64 carry = 0;
-    for (u64 c0 = 0; c0 <= G; c0 += UPB) {
-      const u64 x = c0 + tid;
-      const i64 v = x < G ? cdelta[x] : 0;
-      i64 incl = v;
+    for (u64 c0 = 0; c0 <= G; c0 += (u64)UPB * CP) {
+      const u64 x0 = c0 + (u64)tid * CP;
+      i64 v[CP], st0[CP];
+#pragma unroll
+      for (int q = 0; q < CP; q++) {
+        const u64 x = x0 + q;
+        v[q] = x < G ? cdelta[x] : 0;
+        st0[q] = x <= G ? (i64)t.starts[x] : 0;
+      }
+      i64 own = 0;
+#pragma unroll
+      for (int q = 0; q < CP; q++) own += v[q];
+      i64 incl = own;
 #pragma unroll
       for (int d = 1; d < WAVE; d <<= 1) {
         const i64 y = __shfl_up(incl, d, WAVE);
@@ -440,7 +455,13 @@ __global__ __launch_bounds__(UPB, 4) void merkle_chunk_kernel(Rows rows, MT t, c
         before += q < w ? y : 0;
         tot += y;
       }
-      if (x <= G) t.starts[x] = (u64)((i64)t.starts[x] + carry + before + incl - v);
+      i64 run = carry + before + incl - own;  // the changes of the chunks before x0
+#pragma unroll
+      for (int q = 0; q < CP; q++) {
+        const u64 x = x0 + q;
+        if (x <= G) t.starts[x] = (u64)(st0[q] + run);
+        run += v[q];
+      }
       carry += tot;
     }
   }
