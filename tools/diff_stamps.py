@@ -61,6 +61,23 @@ def main():
         print(f"{NAMES[k - 1]:32s} median {np.median(d):6.2f} us  p90 {np.percentile(d, 90):6.2f}  mean {d.mean():6.2f}")
     tot = us(f[:, 6] - f[:, 0])
     print(f"{'per-subtree total':32s} median {np.median(tot):6.2f} us  p90 {np.percentile(tot, 90):6.2f}")
+    where = buf.reshape(4096, 8)[:, 7]
+    if full.any() and where[full].any():  # a build that records CU and XCC (slot 7)
+        cu, xcc = (where & 0xFFFFFFFF).astype(np.int64), (where >> np.uint64(32)).astype(np.int64)
+        leaf = us(s[:, 2] - s[:, 1])
+        idx = np.flatnonzero(full)
+        print("leaf phase by XCC (median us):",
+              {int(x): round(float(np.median(leaf[idx][xcc[idx] == x])), 2) for x in np.unique(xcc[idx])})
+        rank = np.zeros(4096, np.int64)  # order of arrival of the subtrees sharing a CU
+        for key in np.unique(xcc[idx] * 65536 + cu[idx]):
+            m = idx[(xcc[idx] * 65536 + cu[idx]) == key]
+            rank[m[np.argsort(s[m, 0])]] = np.arange(len(m))
+        print("leaf phase by arrival rank on its CU (median, p90 us):",
+              {int(r): (round(float(np.median(leaf[idx][rank[idx] == r])), 2),
+                        round(float(np.percentile(leaf[idx][rank[idx] == r], 90)), 2))
+               for r in np.unique(rank[idx])})
+        print("per-subtree total by rank (median us):",
+              {int(r): round(float(np.median(tot[rank[idx] == r])), 2) for r in np.unique(rank[idx])})
     eng.close()
 
 
