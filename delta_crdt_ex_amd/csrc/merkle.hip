@@ -919,7 +919,10 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
     u64 kr0 = 0, kr1 = 0, kr2 = 0, kr3 = 0;
     auto merge = [&](bool write, u32 o) {
       u32 k2 = 0;
-      for (u32 d = tid; d < ND; d += DB) {
+      // (a lane's buckets are contiguous, so the lanes' outputs in lane order are in
+      // bucket order also when there are more differing buckets than lanes)
+      const u32 per = (ND + DB - 1) / DB, d1 = min(ND, (tid + 1) * per);
+      for (u32 d = tid * per; d < d1; d++) {
         const u32 na = s_dn[d] >> 16;
         u32 ia = s_dp[d], ie = ia + na, jb = ie, je = s_dp[d + 1];
         while (ia < ie || jb < je) {

@@ -126,6 +126,18 @@ def test_truncated_diff_is_the_prefix(engine, cap):
     assert np.array_equal(u64(got), full[:cap])
 
 
+@pytest.mark.parametrize("n_keys,depth", [(800, 12), (900, 12), (3000, 14)])
+def test_more_differing_buckets_than_lanes(engine, n_keys, depth):
+    """A subtree whose differing buckets (about 300-450) outnumber the count kernel's
+    lanes while their rows still fit the LDS stage: each lane merges several buckets, and
+    the keys must still come out in key order."""
+    a, b = W.merkle_pair(n_keys=n_keys, diff_frac=0.5, seed=9)
+    sa, _ = up(a)
+    sb, _ = up(b)
+    ta, tb = engine.merkle_build(sa, depth), engine.merkle_build(sb, depth)
+    assert np.array_equal(u64(engine.merkle_diff(ta, tb)), R.store_diff(a["rows"], b["rows"]))
+
+
 def test_async_diff_equals_the_synchronous_one(engine):
     """dg_merkle_diff_async: back-to-back launches into one output, the total on the
     device, several caps and depths (small subtrees included), and after an asynchronous
