@@ -13,15 +13,16 @@
  * one-key delta with a MapSet context (aw_lww_map.ex:99-146) from the replica's terms,
  * and update_state_with_delta (:383-404) joins it with keys = [key].  The delta is built
  * on the host here, as the Elixir side builds it from its own `value` map (INTEGRATION.md
- * §3), and one op costs what a NIF's join_delta costs on a GPU-attached state:
- *   h2d   the delta (rows, dot-list context, keyset) as ONE packed copy into the
- *         state's scratch (no allocation per op)
- *   join  dg_join_delta_rows: the keyed join in place or through the spare store, the changed
- *         keys, the MerkleMap put/delete (the state's tree)
- *   d2h   the changed keys' rows (returned by dg_join_delta_rows) and the keys, back for
- *         on_diffs
+ * §3), and each op goes through c_src/replica.c's dgr_join_delta -- the function the NIF's
+ * join_delta calls -- so one op costs what the NIF pays below the term layer: the delta
+ * packed into one page-locked message, the versioned in-place join (dg_join_delta_rows:
+ * the keyed join, the changed keys, the MerkleMap put/delete), and the changed keys'
+ * rows and the new context home with one wait.  `read` is dgr_read (the NIF's read/1),
+ * with its engine-owned output buffers.
  * Also `batch`: the reference's trace workload (1000 x mutate(:add, ["key#{x}", "value"]),
- * :9-23) as ONE delta through one dg_join_delta -- how mutate_async batches amortize.
+ * :9-23) as ONE host-built delta through dgr_join_delta, and the same through
+ * dgr_mutate_batch (the delta built on the device: the NIF's mutate_batch) -- how
+ * mutate_async batches amortize.
  *
  * Built twice from this file: bench_mutate (the GPU path, links libdeltagpu) and, with
  * -DDG_REF, bench_mutate_ref (the CPU restatement's keyed join per op, oracle/deltaref.c
@@ -35,6 +36,9 @@
 #include <time.h>
 
 #include "marshal.h"
+#ifndef DG_REF
+#include "replica.h"
+#endif
 
 #ifdef DG_REF
 int ref_join2(const dg_store* a, const dg_context* ca, const dg_store* b, const dg_context* cb,
@@ -200,155 +204,70 @@ static const char* OP_NAMES[N_OPS] = {"read", "add", "update", "remove"};
 
 #ifndef DG_REF
 /* ================================================================ the GPU path */
+/* Everything goes through c_src/replica.c, the code the NIF runs (deltagpu_nif.c's
+ * join_delta / mutate_batch / read): the delta packed into ONE page-locked message, the
+ * versioned in-place join with the MerkleMap update, the changed keys, their rows and the
+ * new context home with one wait, engine-owned buffers (no allocation per call). */
 typedef struct {
-  dg_engine* e;
-  dg_store st, spare;
-  dg_context ctx;
-  dg_merkle tree;
-  uint64_t* d_msg;    /* the packed delta: key | val | ts | cnt | dcnt | keyset | node | dnode */
-  uint64_t* h_msg;
-  uint64_t msg_words;
-  uint64_t *changed, *h_back;  /* the changed keys; host copy of keys + rows */
-  uint64_t* d_back;            /* rows + keys, packed for one copy home */
-  dg_store mb_rows;            /* dg_mutate_batch's delta, its dot list and touched keys */
-  dg_context mb_ctx;
-  uint64_t* mb_keys;
-  uint64_t back_cap;
-  uint64_t *rk, *rv, *h_rk;    /* read/1 output */
+  dgr_engine* g;
+  dgr_state* s;
+  uint64_t version;
 } gpu;
 
 static void gpu_upload(gpu* g, hrows* r) {
-  DG(dg_store_alloc(g->e, r->n + 16384, &g->st));
-  DG(dg_store_alloc(g->e, r->n + 16384, &g->spare));
+  DG(dgr_engine_open(0, &g->g));
   dg_store hs = hview(r);
-  DG(dg_store_upload(g->e, &hs, &g->st));
-  DG(dg_context_alloc(g->e, 4096, &g->ctx));  /* room for the union with a delta's dot list */
   uint32_t n0 = 0;
   uint64_t c0 = r->n;
   dg_context hc = {DG_CTX_VV, 0, &n0, &c0, 1, 1};
-  DG(dg_context_upload(g->e, &hc, &g->ctx));
-  g->ctx.kind = DG_CTX_VV;
-  /* the MerkleMap: ~3 keys per bucket (the bench's config-4 rule) */
+  DG(dgr_state_load(g->g, &hs, &hc, &g->s));
+  g->version = dgr_state_version(g->s);
+  /* the MerkleMap: ~3 keys per bucket (the bench's config-4 rule); rows hashed by id */
   uint32_t depth = 8;
   while (depth < 28 && (UINT64_C(3) << depth) < r->n) depth++;
-  memset(&g->tree, 0, sizeof g->tree);
-  g->tree.depth = depth;
-  DG(dg_buffer_alloc(g->e, ((UINT64_C(2) << depth) - 1) * 8, (void**)&g->tree.nodes));
-  DG(dg_buffer_alloc(g->e, ((UINT64_C(1) << depth) + 16) * 2, (void**)&g->tree.counts));
-  DG(dg_buffer_alloc(g->e, (dg_merkle_chunks(depth) + 1) * 8, (void**)&g->tree.starts));
-  DG(dg_merkle_build(g->e, &g->st, &g->tree));
-  g->msg_words = 8 * 2048;
-  DG(dg_buffer_alloc(g->e, g->msg_words * 8, (void**)&g->d_msg));
-  g->h_msg = calloc(g->msg_words, 8);
-  g->back_cap = 2048;
-  DG(dg_buffer_alloc(g->e, g->back_cap * 6 * 8, (void**)&g->d_back));
-  g->changed = g->d_back;  /* the changed keys open the block */
-  DG(dg_store_alloc(g->e, 2048, &g->mb_rows));
-  DG(dg_context_alloc(g->e, 8 * 2048, &g->mb_ctx));
-  g->mb_ctx.kind = DG_CTX_DOTS;
-  DG(dg_buffer_alloc(g->e, 2048 * 8, (void**)&g->mb_keys));
-  g->h_back = calloc(g->back_cap * 6, 8);
-  DG(dg_buffer_alloc(g->e, (r->n + 16384) * 8, (void**)&g->rk));
-  DG(dg_buffer_alloc(g->e, (r->n + 16384) * 8, (void**)&g->rv));
-  g->h_rk = calloc((r->n + 16384) * 2, 8);
+  DG(dgr_refresh_terms(g->g, NULL, 0, NULL, NULL, 0));
+  DG(dgr_merkle_build(g->s, g->version, depth));
 }
 
-/* one mutation: h2d, dg_join_delta, d2h of the changed keys' rows; phases in t[3] (us) */
+/* one delta as the NIF's join_delta applies it (host rows and dot list in, the changed
+ * keys' rows and the context out) */
 static void gpu_apply(gpu* g, const uint64_t* key, const uint64_t* val, const int64_t* ts,
                       const uint64_t* cnt, uint64_t n_rows, const uint32_t* dnode,
                       const uint64_t* dcnt, uint64_t nd, const uint64_t* keys, uint64_t nk,
                       double* t) {
+  static uint32_t* node = NULL;
+  static uint64_t node_cap = 0;
+  if (node_cap < n_rows + 1) {
+    free(node);
+    node_cap = 2 * n_rows + 16;
+    node = calloc(node_cap, 4);  /* every row of these deltas is node 0's */
+  }
+  dg_store ds = {(uint64_t*)key, (uint64_t*)val, (int64_t*)ts, node, (uint64_t*)cnt, n_rows, n_rows};
+  dg_context dc = {DG_CTX_DOTS, 0, (uint32_t*)dnode, (uint64_t*)dcnt, nd, nd};
+  dgr_changed c;
   const double t0 = now_us();
-  /* pack: 8-byte columns, then the u32 columns two to a word */
-  uint64_t* m = g->h_msg;
-  uint64_t o = 0;
-  const uint64_t o_key = o; memcpy(m + o, key, n_rows * 8); o += n_rows;
-  const uint64_t o_val = o; memcpy(m + o, val, n_rows * 8); o += n_rows;
-  const uint64_t o_ts = o; memcpy(m + o, ts, n_rows * 8); o += n_rows;
-  const uint64_t o_cnt = o; memcpy(m + o, cnt, n_rows * 8); o += n_rows;
-  const uint64_t o_dcnt = o; memcpy(m + o, dcnt, nd * 8); o += nd;
-  const uint64_t o_keys = o; memcpy(m + o, keys, nk * 8); o += nk;
-  const uint64_t o_node = o; memset(m + o, 0, (n_rows + 1) / 2 * 8);
-  o += (n_rows + 1) / 2;
-  const uint64_t o_dnode = o; o += (nd + 1) / 2;
-  (void)ts;  /* (every row of these deltas is node 0's: the node column stays zero) */
-  memcpy(m + o_dnode, dnode, nd * 4);
-  if (o > g->msg_words) {
-    fprintf(stderr, "delta too large\n");
-    exit(1);
-  }
-  DG(dg_copy_to_device(g->e, g->d_msg, m, o * 8));
-  uint64_t* d = g->d_msg;
-  dg_store ds = {d + o_key, d + o_val, (int64_t*)(d + o_ts), (uint32_t*)(d + o_node), d + o_cnt,
-                 n_rows, n_rows};
-  dg_context dc = {DG_CTX_DOTS, 0, (uint32_t*)(d + o_dnode), d + o_dcnt, nd, nd};
-  const double t1 = now_us();
-  uint64_t n_changed = 0;
-  int swapped = 0;
-  /* the changed keys (written by the join) and their rows (dg_join_delta_rows: from the
-   * join's own edit) in ONE device block -- keys | key | val | ts | cnt | node, the row
-   * columns at stride S (64: a one-key op changes one key) -- and one copy of it home */
-  uint64_t S = 64;
-  uint64_t* b = g->d_back + g->back_cap;
-  dg_store tk = {b, b + S, (int64_t*)(b + 2 * S), (uint32_t*)(b + 4 * S), b + 3 * S, 0, S};
-  DG(dg_join_delta_rows(g->e, &g->st, &g->ctx, &ds, &dc, d + o_keys, nk, &g->spare, &g->tree,
-                        g->changed, g->back_cap, &n_changed, &swapped, &tk));
-  const double t2 = now_us();
-  if (tk.n > tk.cap) {  /* more rows than the small stride: take them again, wider */
-    S = g->back_cap;
-    dg_store wide = {b, b + S, (int64_t*)(b + 2 * S), (uint32_t*)(b + 4 * S), b + 3 * S, 0, S};
-    DG(dg_take_keys(g->e, &g->st, g->changed, n_changed, &wide));
-  }
-  if (n_changed) DG(dg_copy_to_host(g->e, g->h_back, g->d_back, (g->back_cap + 5 * S) * 8));
-  const double t3 = now_us();
-  t[0] = t1 - t0;
-  t[1] = t2 - t1;
-  t[2] = t3 - t2;
+  DG(dgr_join_delta(g->s, g->version, &ds, &dc, keys, nk, &c));
+  g->version = c.version;
+  t[0] = 0;
+  t[1] = now_us() - t0;
+  t[2] = 0;
 }
 
-/* a batch of m adds (keys ascending) by node 0 built ON THE DEVICE (dg_mutate_batch: the
- * NIF's mutate_batch) and applied with dg_join_delta, the changed rows back: one op list
- * upload, the delta's dots from the state, the join, the return block */
+/* a batch of m adds by node 0 built ON THE DEVICE (the NIF's mutate_batch) */
 static void gpu_mutate_batch(gpu* g, const uint64_t* key, const uint64_t* val, const int64_t* ts,
                              uint64_t m) {
-  uint64_t* h = g->h_msg;
-  const uint64_t words = 4 * m + (m + 7) / 8 + 1;
-  if (words > g->msg_words) {
-    fprintf(stderr, "batch too large\n");
-    exit(1);
-  }
-  memcpy(h, key, m * 8);
-  memcpy(h + m, val, m * 8);
-  memcpy(h + 2 * m, ts, m * 8);
-  for (uint64_t i = 0; i < m; i++) h[3 * m + i] = i;  /* add_rank: every op an add */
-  uint8_t* kinds = (uint8_t*)(h + 4 * m);
+  static uint8_t* kinds = NULL;
+  if (!kinds) kinds = malloc(1 << 16);
   memset(kinds, 1, m);
-  DG(dg_copy_to_device(g->e, g->d_msg, h, words * 8));
-  uint64_t* d = g->d_msg;
-  dg_store delta = {g->mb_rows.key, g->mb_rows.val, g->mb_rows.ts, g->mb_rows.node, g->mb_rows.cnt, 0,
-                    g->mb_rows.cap};
-  dg_context dots = g->mb_ctx;
-  uint64_t n_keys = 0, n_changed = 0;
-  int swapped = 0;
-  DG(dg_mutate_batch(g->e, &g->st, &g->ctx, 0, m, (const uint8_t*)(d + 4 * m), d, d + m,
-                     (const int64_t*)(d + 2 * m), d + 3 * m, m, &delta, &dots, g->mb_keys, m, &n_keys));
-  uint64_t* b = g->d_back + g->back_cap;
-  const uint64_t S = g->back_cap;
-  dg_store tk = {b, b + S, (int64_t*)(b + 2 * S), (uint32_t*)(b + 4 * S), b + 3 * S, 0, S};
-  DG(dg_join_delta_rows(g->e, &g->st, &g->ctx, &delta, &dots, g->mb_keys, n_keys, &g->spare,
-                        &g->tree, g->changed, g->back_cap, &n_changed, &swapped, &tk));
-  if (tk.n > tk.cap) {
-    fprintf(stderr, "return block too small\n");
-    exit(1);
-  }
-  if (n_changed) DG(dg_copy_to_host(g->e, g->h_back, g->d_back, 6 * S * 8));
+  dgr_changed c;
+  DG(dgr_mutate_batch(g->s, g->version, 0, m, kinds, key, val, ts, &c));
+  g->version = c.version;
 }
 
 static void gpu_read(gpu* g) {
+  const uint64_t *k, *v;
   uint64_t n = 0;
-  DG(dg_read_lww(g->e, &g->st, NULL, 0, g->rk, g->rv, g->st.cap, &n));
-  DG(dg_copy_to_host(g->e, g->h_rk, g->rk, n * 8));
-  DG(dg_copy_to_host(g->e, g->h_rk + n, g->rv, n * 8));
+  DG(dgr_read(g->s, g->version, 1, NULL, 0, &k, &v, &n));
 }
 #else
 /* ================================================================ the CPU restatement */
@@ -404,7 +323,6 @@ int main(int argc, char** argv) {
 #ifndef DG_REF
   gpu g;
   memset(&g, 0, sizeof g);
-  DG(dg_engine_create(0, NULL, &g.e));
   gpu_upload(&g, &r);
 #define APPLY(...) gpu_apply(&g, __VA_ARGS__)
 #else
@@ -515,18 +433,13 @@ int main(int argc, char** argv) {
 #endif
   printf("{\"n_keys\": %lld, \"reps\": %d, \"path\": \"%s\", \"us\": {", (long long)n, reps,
 #ifndef DG_REF
-         "gpu"
+         "gpu (c_src/replica.c: the NIF's calls)"
 #else
          "cpu_restatement"
 #endif
   );
   for (int o = 0; o < N_OPS; o++) {
     printf("%s\"%s\": %.2f", o ? ", " : "", OP_NAMES[o], median(tot[o], reps));
-  }
-  printf("}, \"phases_us\": {");
-  for (int o = 1; o < N_OPS; o++) {
-    printf("%s\"%s\": {\"h2d\": %.2f, \"join_delta\": %.2f, \"d2h_changed\": %.2f}", o > 1 ? ", " : "",
-           OP_NAMES[o], median(ts[o][0], reps), median(ts[o][1], reps), median(ts[o][2], reps));
   }
   const double bmed = median(bt_us, n_batch);
   printf("}, \"batch_1000_adds_us\": %.2f, \"batch_us_per_op\": %.3f", bmed, bmed / nb);
@@ -536,7 +449,8 @@ int main(int argc, char** argv) {
   }
   printf("}\n");
 #ifndef DG_REF
-  dg_engine_destroy(g.e);
+  dgr_state_free(g.s);
+  dgr_engine_close(g.g);
 #endif
   return 0;
 }

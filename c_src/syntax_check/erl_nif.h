@@ -70,11 +70,13 @@ void enif_map_iterator_destroy(ErlNifEnv*, ErlNifMapIterator*);
 ERL_NIF_TERM enif_make_atom(ErlNifEnv*, const char*);
 ERL_NIF_TERM enif_make_badarg(ErlNifEnv*);
 ERL_NIF_TERM enif_make_binary(ErlNifEnv*, ErlNifBinary*);
+unsigned char* enif_make_new_binary(ErlNifEnv*, size_t, ERL_NIF_TERM*);
 ERL_NIF_TERM enif_make_copy(ErlNifEnv*, ERL_NIF_TERM);
 ERL_NIF_TERM enif_make_int(ErlNifEnv*, int);
 ERL_NIF_TERM enif_make_int64(ErlNifEnv*, ErlNifSInt64);
 ERL_NIF_TERM enif_make_uint64(ErlNifEnv*, ErlNifUInt64);
 ERL_NIF_TERM enif_make_list(ErlNifEnv*, unsigned, ...);
+ERL_NIF_TERM enif_make_list_from_array(ErlNifEnv*, const ERL_NIF_TERM*, unsigned);
 ERL_NIF_TERM enif_make_list_cell(ErlNifEnv*, ERL_NIF_TERM, ERL_NIF_TERM);
 ERL_NIF_TERM enif_make_new_map(ErlNifEnv*);
 int enif_make_map_put(ErlNifEnv*, ERL_NIF_TERM, ERL_NIF_TERM, ERL_NIF_TERM, ERL_NIF_TERM*);
@@ -83,6 +85,7 @@ ERL_NIF_TERM enif_make_resource(ErlNifEnv*, void*);
 ERL_NIF_TERM enif_make_string(ErlNifEnv*, const char*, ErlNifCharEncoding);
 ERL_NIF_TERM enif_make_tuple2(ErlNifEnv*, ERL_NIF_TERM, ERL_NIF_TERM);
 ERL_NIF_TERM enif_make_tuple3(ErlNifEnv*, ERL_NIF_TERM, ERL_NIF_TERM, ERL_NIF_TERM);
+ERL_NIF_TERM enif_make_tuple4(ErlNifEnv*, ERL_NIF_TERM, ERL_NIF_TERM, ERL_NIF_TERM, ERL_NIF_TERM);
 void* enif_alloc(size_t);
 void enif_free(void*);
 ErlNifEnv* enif_alloc_env(void);

@@ -183,6 +183,9 @@ _SIGS = {
     "dg_buffer_free": (C.c_int, [C.c_void_p, C.c_void_p]),
     "dg_copy_to_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
     "dg_copy_to_host": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
+    "dg_copy_async": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
+    "dg_host_alloc": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),
+    "dg_host_free": (C.c_int, [C.c_void_p, C.c_void_p]),
     "dg_sort_store": (C.c_int, [C.c_void_p, C.POINTER(dg_store), C.POINTER(dg_store)]),
     "dg_sort_context": (C.c_int, [C.c_void_p, C.POINTER(dg_context), C.POINTER(dg_context)]),
     "dg_remap_values": (C.c_int, [C.c_void_p, C.POINTER(dg_store), P64, P64, C.c_uint64]),

@@ -62,6 +62,7 @@ struct dg_engine {
   u64* d_pub = nullptr;  // its device address
   u64 pub_seq = 0;
   u32 h_ticket[16] = {};  // the ticket words as of the last synchronous call
+  u32 last_err_bits = 0;  // the error bits read_counts last failed on (0: it did not)
   // general scratch
   void* tmp = nullptr;
   size_t tmp_cap = 0;
@@ -285,15 +286,22 @@ int sync_words(dg_engine* e) {
   return DG_OK;
 }
 
-constexpr int MERKLE_ARRIVE = 6;  // ticket word: the Merkle kernels' arrival counter
+// ticket word: the Merkle kernels' arrival counter.  It is reset by the last workgroup of
+// every build / update launch, not per launch.  A launch either runs every workgroup to
+// that reset (the kernels never wait on another workgroup before arriving) or does not
+// start at all (a launch error); a kernel that faults leaves the device unusable anyway.
+// read_counts also zeroes it whenever a call reports error bits.
+constexpr int MERKLE_ARRIVE = 6;
 
 int read_counts(dg_engine* e, int n) {
   (void)n;
+  e->last_err_bits = 0;
   const int rc = sync_words(e);
   if (rc != DG_OK) return rc;
   u32 err = 0;
   memcpy(&err, (const char*)&e->h_counts[8] + sizeof(u32), sizeof(u32));
   if (err) {
+    e->last_err_bits = err;
     HIP_TRY(hipMemsetAsync(e->ticket, 0, 4 * sizeof(u32), e->stream));
     HIP_TRY(hipMemsetAsync(e->ticket + MERKLE_ARRIVE, 0, sizeof(u32), e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -893,12 +901,15 @@ int dg_join2_changes(dg_engine* e, const dg_store* a, const dg_context* ca, cons
 }
 
 // dg_join_delta_rows' output: the changed keys' rows of `src`; more than rows->cap is
-// reported in rows->n, not as an error (the join before it is complete)
+// reported in rows->n, not as an error (the join before it is complete).  It runs after
+// the join is committed, so any failure of the gather is reported the same way -- "rows
+// not written" (rows->n > rows->cap) -- and never as an error of a join that applied.
 static int take_changed_rows(dg_engine* e, const dg_store* src, const uint64_t* changed,
                              uint64_t n_changed, dg_store* rows) {
   const int rc = dg_take_keys(e, src, changed, n_changed, rows);
   if (rc == DG_E_CAPACITY) return DG_OK;
-  return rc;
+  if (rc != DG_OK) rows->n = rows->cap + 1;
+  return DG_OK;
 }
 
 // dg_join_delta[_rows]: rows (optional) receives the changed keys' joined rows
@@ -959,10 +970,12 @@ static int join_delta_impl(dg_engine* e, dg_store* state, dg_context* state_ctx,
     return DG_OK;
   }
   TRY(splice_edit(e, &w, state_ctx, delta, delta_ctx, keys, n_keys, &w.uctx, true, changed, cap));
-  if (read_counts(e, 6) != DG_OK) {
+  if (const int rc0 = read_counts(e, 6); rc0 != DG_OK) {
     // the join grid could not become resident (another process's persistent kernels) or
     // timed out: nothing of the state is written yet, so re-run the edit on a grid small
-    // enough to find room beside other work, as dg_join2_changes does
+    // enough to find room beside other work, as dg_join2_changes does.  Any other failure
+    // (a HIP error, a lost publish) is the call's error, its message kept.
+    if (!(e->last_err_bits & 3u)) return rc0;
     const int workers = e->join_workers;
     e->join_workers = RETRY_WORKERS;
     HIP_TRY(hipMemsetAsync(e->d_counts + 5, 0, sizeof(u64), e->stream));  // `moved`
@@ -1815,6 +1828,35 @@ int dg_copy_to_host(dg_engine* e, void* dst, const void* src, uint64_t bytes) {
   TRY(set_device(e));
   HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
+  return DG_OK;
+}
+
+int dg_copy_async(dg_engine* e, void* dst, const void* src, uint64_t bytes) {
+  if (!e || (bytes && (!dst || !src))) return fail(DG_E_INVAL, "dg_copy_async: null argument");
+  if (!bytes) return DG_OK;
+  TRY(set_device(e));
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, e->stream));
+  return DG_OK;
+}
+
+int dg_host_alloc(dg_engine* e, uint64_t bytes, void** p) {
+  if (!e || !p) return fail(DG_E_INVAL, "dg_host_alloc: null argument");
+  *p = nullptr;
+  TRY(set_device(e));
+  if (bytes == 0) return DG_OK;
+  if (hipHostMalloc(p, bytes, 0) != hipSuccess) {
+    *p = nullptr;
+    return fail(DG_E_NOMEM, "hipHostMalloc of %llu bytes failed", (unsigned long long)bytes);
+  }
+  return DG_OK;
+}
+
+int dg_host_free(dg_engine* e, void* p) {
+  if (!e) return fail(DG_E_INVAL, "null engine");
+  if (!p) return DG_OK;
+  TRY(set_device(e));
+  HIP_TRY(hipStreamSynchronize(e->stream));  // no copy of this engine still reads or writes it
+  HIP_TRY(hipHostFree(p));
   return DG_OK;
 }
 

@@ -721,7 +721,19 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
 #if DG_DIFF_EXP == 1  // diagnostic build only (timing, wrong keys): no bounds search
     const u64 x = r.n * tile / p.ntiles;
 #else
-    const u64 x = st ? st[(tile << sub) >> L1] : wave_bucket_start(p.ta, r.key, r.n, tile << sub);
+    // The chunk index describes the store the tree was built / updated against.  It is
+    // trusted only when its end is this store's row count and the start lies inside the
+    // store (wave-uniform: every lane reads the same two words); otherwise -- another store
+    // handed to the diff, rows changed without a dg_merkle_update, or a shard tree over a
+    // store that holds more shards -- the subtree's first row is searched, as without an
+    // index, so a stale index never reads past the store or yields wrong keys.
+    u64 x = 0;
+    bool use_st = st != nullptr;
+    if (use_st) {
+      x = st[(tile << sub) >> L1];
+      use_st = st[1ull << (depth - L1)] == r.n && x <= r.n;
+    }
+    if (!use_st) x = wave_bucket_start(p.ta, r.key, r.n, tile << sub);
 #endif
     if ((tid & (WAVE - 1)) == 0) {
       s_bnd[tid / WAVE] = x;

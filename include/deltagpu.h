@@ -191,6 +191,16 @@ int dg_buffer_alloc(dg_engine* e, uint64_t bytes, void** p);
 int dg_buffer_free(dg_engine* e, void* p);
 int dg_copy_to_device(dg_engine* e, void* dst, const void* src, uint64_t bytes);
 int dg_copy_to_host(dg_engine* e, void* dst, const void* src, uint64_t bytes);
+/* A copy in any direction ENQUEUED on the engine stream (no wait): it is ordered with the
+ * engine's kernels, so a synchronous call after it sees its data, and its destination is
+ * complete once any later synchronous call (or dg_engine_sync) returns.  Not replayed by
+ * dg_engine_sync.  The NIF packs a delta message into pinned memory and ships it with one
+ * such copy, and brings several result ranges home with one wait (c_src/replica.c). */
+int dg_copy_async(dg_engine* e, void* dst, const void* src, uint64_t bytes);
+/* Page-locked host memory (what dg_copy_async needs to overlap and what makes small copies
+ * cheap); dg_host_free waits for the engine stream first. */
+int dg_host_alloc(dg_engine* e, uint64_t bytes, void** p);
+int dg_host_free(dg_engine* e, void* p);
 
 /* Verify the sorted+unique precondition of a store (DG_E_ORDER if violated). */
 int dg_store_check(dg_engine* e, const dg_store* s);
@@ -253,7 +263,9 @@ int dg_join_delta(dg_engine* e, dg_store* state, dg_context* state_ctx, const dg
  * keyset (small and cache-resident) instead of by a search of the whole state, as a
  * dg_take_keys call after dg_join_delta would.  More rows than rows->cap is not an
  * error (the join is complete): rows->n > rows->cap on return says the rows were not
- * written; take them with dg_take_keys.  Synchronous. */
+ * written; take them with dg_take_keys.  The same holds for any failure of that gather,
+ * which runs after the join is committed: an error return always means the state, its
+ * context and tree are unchanged.  Synchronous. */
 int dg_join_delta_rows(dg_engine* e, dg_store* state, dg_context* state_ctx, const dg_store* delta,
                        const dg_context* delta_ctx, const uint64_t* keys, uint64_t n_keys,
                        dg_store* spare, dg_merkle* tree, uint64_t* changed, uint64_t cap,

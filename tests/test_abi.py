@@ -112,3 +112,40 @@ def test_null_arguments_are_rejected(lib):
     assert lib.dg_join2(None, C.byref(s), C.byref(x), C.byref(s), C.byref(x), None, 0,
                         C.byref(s), C.byref(x)) == _abi.DG_E_INVAL
     assert lib.dg_read_lww(None, C.byref(s), None, 0, None, None, 0, None) == _abi.DG_E_INVAL
+
+
+def test_replica_layer_exports_every_declared_function(lib):
+    """c_src/replica.h (the NIF's device half, bound by delta_crdt_ex_amd/nif.py): the
+    shared library exports every function the header declares, each with a ctypes
+    signature in the mirror, and dgr_changed matches gcc's layout."""
+    import re
+    from delta_crdt_ex_amd import nif
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "c_src")], check=True)
+    r = nif.load()
+    text = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "c_src", "replica.h")).read(), flags=re.S)
+    names = sorted(set(re.findall(r"\b(dgr_[a-z0-9_]+)\s*\(", text)))
+    assert len(names) >= 15
+    for name in names:
+        assert hasattr(r, name), name
+        assert name in nif._SIGS, f"ctypes signature missing for {name}"
+    src = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "replica.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(dgr_changed), offsetof(dgr_changed, version),
+         offsetof(dgr_changed, n_changed), offsetof(dgr_changed, keys), offsetof(dgr_changed, rows),
+         offsetof(dgr_changed, ctx));
+  return 0;
+}
+"""
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "l.c")
+        open(c, "w").write(src)
+        exe = os.path.join(d, "l")
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "c_src"), c, "-o", exe], check=True)
+        got = [int(x) for x in subprocess.run([exe], capture_output=True, text=True).stdout.split()]
+    D = nif.dgr_changed
+    assert got == [C.sizeof(D), D.version.offset, D.n_changed.offset, D.keys.offset, D.rows.offset,
+                   D.ctx.offset]
+    assert nif.DGR_E_STALE == int(re.search(r"DGR_E_STALE \((-?\d+)\)", text).group(1))
