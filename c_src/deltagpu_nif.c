@@ -8,37 +8,43 @@
  * from C with the same C-ABI calls this file makes (c_src/test_marshal.c).
  *
  * Resources
- *   engine   one dg_engine (one HIP stream) + the interning universe of this BEAM node
- *            + a mutex: every NIF below takes it (a dg_engine is not re-entrant, and
- *            several CausalCrdt processes call in from several dirty schedulers).
- *   state    a DEVICE-RESIDENT replica state: rows, context and, once built, its Merkle
- *            tree.  The Elixir struct keeps `dots` and `value` as real terms -- CausalCrdt
- *            reads them directly (causal_crdt.ex:118,259,331,346) -- and carries the
- *            state resource beside them, so a join ships only the delta to the device
- *            and brings back only the keys it changed.
+ *   engine   a dgr_engine (c_src/replica.h: one dg_engine, one HIP stream, engine-owned
+ *            buffers) + the interning universe of this BEAM node + a mutex: every NIF
+ *            below takes it (an engine is not re-entrant, and several CausalCrdt
+ *            processes call in from several dirty schedulers).
+ *   state    a DEVICE-RESIDENT replica state (a dgr_state: rows, context, spare buffer,
+ *            tree) at a VERSION.  The Elixir struct keeps `dots` and `value` as real terms
+ *            -- CausalCrdt reads them directly (causal_crdt.ex:118,259,331,346) -- and
+ *            carries {state, version, pending} beside them; the device answers only the
+ *            struct whose version it holds.
  *
- * NIFs (all dirty-CPU scheduled; errors are {:error, reason}, the Elixir side then
- * runs the reference code instead):
- *   engine_open(device)                       -> {:ok, engine}
- *   state_load(engine, dots, value)           -> {:ok, state}          (marshal once)
- *   join_delta(state, dots, value, keys)      -> {:ok, new_dots, changed}
+ * This file is the term layer only: everything on the device is c_src/replica.c, which
+ * the Python mirror of this NIF (delta_crdt_ex_amd/nif.py) and c_src/bench_mutate.c call
+ * too.
+ *
+ * NIFs (dirty-CPU scheduled but resolve_keys; errors are {:error, :stale} for an older
+ * struct and {:error, {code, message}} otherwise -- the Elixir side then uses the terms):
+ *   engine_open(device)                                -> {:ok, engine}
+ *   state_load(engine, dots, value)                    -> {:ok, state, version}
+ *   join_delta(state, version, dots, value, keys)      -> {:ok, version', new_dots, changed}
  *        join/3 (aw_lww_map.ex:153-158) of the resident state with a delta
  *        %{dots: dots, value: value} over `keys`, in place on the device
- *        (dg_join_delta: in place when every joined key keeps its row count);
- *        changed = [{key, value_map | nil}] for the keys whose raw
- *        value maps changed (causal_crdt.ex:344-352), so the caller updates its term
- *        map with Map.merge/Map.drop of those keys only; the Merkle tree, if built,
- *        gets put/delete + update_hashes of them (dg_merkle_update, :390-394).
- *   mutate_batch(state, node, ops)            -> {:ok, new_dots, changed}
+ *        (dg_join_delta_rows); changed = [{key, value_map | nil}] for the keys whose raw
+ *        value maps changed (causal_crdt.ex:344-352); the Merkle tree, if built, gets
+ *        put/delete + update_hashes of them (:390-394).
+ *   mutate_batch(state, version, node, ops)            -> {:ok, version', new_dots, changed}
  *        a batch of {:add, key, value, ts} / {:remove, key} ops by `node` as ONE delta
  *        (dg_mutate_batch, aw_lww_map.ex:99-146) applied like join_delta with the
- *        touched keys (the queued mutate_async calls of a GPU-attached replica)
- *   read(state, keys | :all)                  -> %{key => value}       (read/1,2, :211-224)
- *   take(state, keys)                         -> value map of those keys (Map.take, :118,331)
- *   merkle_build(state, depth)                -> :ok
- *   merkle_prepare(state, levels)             -> {:continue, cont}     (:255)
- *   merkle_continue(state, cont, levels, max) -> {:continue, cont} | {:ok, keys}  (:96-105)
- *   (a continuation is an opaque binary; `max` is max_sync_size, :98,105,206-214)
+ *        touched keys (the queued mutations of a GPU-attached replica)
+ *   read(state, version, keys | :all)                  -> {:ok, %{key => value}}  (:211-224)
+ *   take(state, version, keys)                         -> {:ok, value map}  (Map.take, :118,331)
+ *   merkle_build(state, version, depth)                -> :ok
+ *   merkle_prepare(state, version, levels)             -> {:continue, cont}     (:255)
+ *   merkle_continue(state, version, cont, levels, max) -> {:continue, cont} | {:ok, keys}
+ *        (:96-105; `max` is max_sync_size or :infinite, :98,105,206-214; a key this node
+ *        never interned comes back as {:"$dg_key", id})
+ *   resolve_keys(engine, keys)                         -> keys (placeholders -> terms)
+ *   (a continuation is an opaque binary)
  */
 #include <erl_nif.h>
 #include <stdlib.h>

@@ -410,3 +410,34 @@ def test_chunk_index_follows_the_rows(engine):
     ta2.starts = tb2.starts = None
     assert np.array_equal(u64(engine.merkle_diff(ta2, tb2)), with_index)
     assert np.array_equal(with_index, R.store_diff(out.to_numpy(), b["rows"]))
+
+
+def test_diff_against_a_store_the_index_does_not_describe(engine):
+    """a tree's chunk index describes the store it was built / updated against.
+    Handed another store -- here one whose row count changed without dg_merkle_update --
+    the diff must not trust it (it would read past the store or return wrong keys): it
+    searches the store instead, exactly as a tree without an index does."""
+    rng = np.random.default_rng(23)
+    a, b = W.random_pair(rng, 50_000, n_nodes=4, max_entries=3)
+    sa, ca = up(a)
+    sb, cb = up(b)
+    depth = 14
+    ta, tb = engine.merkle_build(sa, depth), engine.merkle_build(sb, depth)
+    for cut in (a["rows"][0].size // 2, 10):  # fewer rows than the index says
+        short = Store.from_numpy(*(c[:cut] for c in a["rows"]), device=DEV)
+        ta.store = short
+        got = u64(engine.merkle_diff(ta, tb))
+        ta.starts, kept = None, ta.starts
+        want = u64(engine.merkle_diff(ta, tb))
+        ta.starts = kept
+        assert np.array_equal(got, want)
+        assert np.all(got[1:] > got[:-1])
+    # more rows than the index says (a join's output under a tree of the old state)
+    out, _ = engine.join2(sa, ca, sb, cb)
+    assert out.n > sa.n
+    ta.store = out
+    got = u64(engine.merkle_diff(ta, tb))
+    ta.starts, kept = None, ta.starts
+    assert np.array_equal(got, u64(engine.merkle_diff(ta, tb)))
+    ta.starts, ta.store = kept, sa
+    assert np.array_equal(u64(engine.merkle_diff(ta, tb)), R.store_diff(a["rows"], b["rows"]))
