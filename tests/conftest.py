@@ -20,6 +20,8 @@ EARLY_CMDS = {
     "c_marshal": ([os.path.join(ROOT, "c_src", "_build", "test_marshal")], {"DG_REQUIRE_GPU": "1"}),
     "sharded2": ([sys.executable, "-u", os.path.join(ROOT, "tests", "sharded_round.py"), "--world", "2"],
                  {}),
+    "sharded4": ([sys.executable, "-u", os.path.join(ROOT, "tests", "sharded_round.py"), "--world", "4",
+                  "--keys-per-rank", "20000"], {}),
 }
 _EARLY: dict = {}
 

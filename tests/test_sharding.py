@@ -1,4 +1,4 @@
-"""Key-hash range sharding with world_size-2 torch.distributed/gloo
+"""Key-hash range sharding with world_size-2 and -4 torch.distributed/gloo
 on the CPU: per-shard joins reassemble the unsharded join exactly, the VV all-reduce
 yields the global context union, and Merkle shard roots localise the diff.  The
 per-shard compute here is the C oracle (the GPU box runs libdeltagpu per rank)."""
@@ -71,7 +71,7 @@ def _worker(rank, world, port, q):
             # its own half of the union, the all-reduce restores the whole
             import torch
             from delta_crdt_ex_amd.store import Context
-            half = (slice(None, None, 2) if rank == 0 else slice(1, None, 2))
+            half = slice(rank, None, world)
             hn, hc = ctx[1][half], ctx[2][half]
             c = Context(ctx[0], torch.from_numpy(hn.astype(np.int32)),
                         torch.from_numpy(np.ascontiguousarray(hc).view(np.int64)), len(hn))
@@ -107,11 +107,16 @@ def _worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(300)
-def test_two_rank_gloo_sharded_join_and_merkle():
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_sharded_join_and_merkle(world):
+    """world_size 2 and 4: the VV all-reduce (host arrays and device contexts), the shard
+    roots' all-gather and fold (== the unsharded root), and the diff restricted to the
+    differing shards (== the unsharded diff's slice) -- the sync round of
+    causal_crdt.ex:252-270 over key-hash shards."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in procs]
@@ -122,15 +127,16 @@ def test_two_rank_gloo_sharded_join_and_merkle():
 
 
 @pytest.mark.gpu
-def test_two_rank_sharded_round_through_libdeltagpu():
-    """tests/sharded_round.py: two processes on cuda:0, one key-hash shard each, run the
+def test_sharded_round_through_libdeltagpu():
+    """tests/sharded_round.py: two (and four) processes on cuda:0, one key-hash shard each, run the
     config-4 round through libdeltagpu (shard Merkle trees whose roots fold to the
     unsharded root, diff, take, keyed join, VV all-reduce, incremental Merkle update)
     against the C oracle's unsharded results.  Started at session start, before this
     process touches the GPU (conftest.EARLY_CMDS).  Unmeasured at 8 GPUs: the driver's
     SCALE run is the 8-GPU measurement."""
     from conftest import early_result
-    rc, out = early_result("sharded2")
-    assert rc == 0, out
-    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
-    assert len(lines) == 2 and all('"ok": true' in ln for ln in lines), out
+    for name, world in (("sharded2", 2), ("sharded4", 4)):
+        rc, out = early_result(name)
+        assert rc == 0, out
+        lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+        assert len(lines) == world and all('"ok": true' in ln for ln in lines), out
