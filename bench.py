@@ -710,6 +710,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--settle-ms", type=float, default=300.0,
+                    help="untimed joins for this long before the warm-up steps (clock ramp)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-merkle", action="store_true")
     ap.add_argument("--no-configs", action="store_true",
@@ -771,6 +773,16 @@ def main():
     n_in = len(a["rows"][0]) + len(b["rows"][0])
     n_in_all = [len(pr["a"]["rows"][0]) + len(pr["b"]["rows"][0]) for pr in pairs]
 
+    # settle: untimed joins of the same pairs for --settle-ms of wall time before the W
+    # warm-up steps, so that a short run (the driver's --steps 20 --warmup 5) times the
+    # GPU at its steady clocks rather than the ramp out of idle
+    t_settle = time.perf_counter()
+    n_settle = 0
+    while (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
+        for i in range(16):
+            launches[i % R]()
+        eng.sync()
+        n_settle += 16
     for i in range(args.warmup):
         launches[i % R]()
     eng.sync()
@@ -869,6 +881,8 @@ def main():
                 "avg_launch_us": avg_launch_s * 1e6,
                 "launch_timing": "HIP events on the engine stream around the timed region / steps",
                 "per_step_event_median_us": step_event_median_us,
+                "settle": {"ms": args.settle_ms, "joins": n_settle,
+                           "note": "untimed joins before the warm-up steps"},
             },
         }
     def aggregate(r, units_secs):

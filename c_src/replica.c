@@ -46,6 +46,8 @@ struct dgr_engine {
    * node u32 [5S, 6S) | context cnt [6S, 6S + C) | context node u32 [6S + C, 6S + 2C) */
   uint64_t *d_back, *h_back;
   uint64_t back_s, back_c;
+  /* dg_join_delta_home's result block (page-locked, DG_HOME_WORDS) */
+  uint64_t* h_home;
   /* read output: keys [0, cap) | values [cap, 2 cap) */
   uint64_t *d_rd, *h_rd;
   uint64_t rd_cap, h_rd_cap;
@@ -271,6 +273,7 @@ int dgr_engine_close(dgr_engine* g) {
   dg_buffer_free(e, g->mkeys);
   dg_buffer_free(e, g->d_back);
   dg_host_free(e, g->h_back);
+  dg_host_free(e, g->h_home);
   dg_buffer_free(e, g->d_rd);
   dg_host_free(e, g->h_rd);
   dg_store_free(e, &g->tk);
@@ -426,12 +429,48 @@ static int room_for(dgr_state* s, uint64_t rows, uint64_t dn) {
   return DG_OK;
 }
 
+/* A small delta (a local mutation, a small sync delta): dg_join_delta_home does the whole
+ * update_state_with_delta in one launch chain and writes the result into page-locked
+ * memory with ONE wait.  *done = 0: not small after all (nothing happened). */
+static int apply_small(dgr_state* s, const dg_store* drows, const dg_context* dctx, const uint64_t* dkeys,
+                       uint64_t n_keys, dgr_changed* out, int* done) {
+  dgr_engine* g = s->g;
+  *done = 0;
+  if (n_keys > 512 || drows->n > 512 || dctx->n > 1024 || s->ctx.kind != DG_CTX_VV) return DG_OK;
+  if (!g->h_home) TRY(dg_host_alloc(g->e, DG_HOME_WORDS * 8, (void**)&g->h_home));
+  int swapped = 0;
+  const int rc = dg_join_delta_home(g->e, &s->rows, &s->ctx, drows, dctx, dkeys, n_keys, &s->spare,
+                                    s->has_tree ? &s->tree : NULL, g->h_home, &swapped);
+  if (rc) {
+    s->version++;
+    return rc;
+  }
+  const uint64_t* h = g->h_home;
+  if (h[0] & DG_HOME_FALLBACK) return DG_OK;
+  s->version++;
+  *done = 1;
+  uint64_t* r = g->h_home + DG_HOME_ROWS;
+  const uint64_t S = DG_HOME_STRIDE;
+  out->version = s->version;
+  out->n_changed = h[1];
+  out->keys = h + DG_HOME_KEYS;
+  dg_store rows = {r, r + S, (int64_t*)(r + 2 * S), (uint32_t*)(r + 4 * S), r + 3 * S, h[2], S};
+  out->rows = rows;
+  dg_context c = {DG_CTX_VV, 0, (uint32_t*)(g->h_home + DG_HOME_CTX + DG_HOME_NODES),
+                  g->h_home + DG_HOME_CTX, h[3], DG_HOME_NODES};
+  out->ctx = c;
+  return DG_OK;
+}
+
 /* The join of a delta on the device (rows and context sorted, keys ascending unique) into
  * the state, and the result brought home with one wait. */
 static int apply_delta(dgr_state* s, const dg_store* drows, const dg_context* dctx, const uint64_t* dkeys,
                        uint64_t n_keys, dgr_changed* out) {
   dgr_engine* g = s->g;
   TRY(room_for(s, drows->n, dctx->n));
+  int done = 0;
+  TRY(apply_small(s, drows, dctx, dkeys, n_keys, out, &done));
+  if (done) return DG_OK;
   uint64_t S = umax(n_keys, 1);
   TRY(grow_back(g, S, s->ctx.n + dctx->n));
   S = g->back_s;
@@ -600,10 +639,16 @@ int dgr_read(dgr_state* s, uint64_t version, int all, const uint64_t* keys, uint
   *out_val = g->h_rd + half;
   if (s->rows.n == 0 || (!all && nk == 0)) return DG_OK;
   uint64_t n = 0;
-  TRY(dg_read_lww(g->e, &s->rows, all ? NULL : g->d_msg, nk, g->d_rd, g->d_rd + half, half, &n));
-  TRY(dg_copy_async(g->e, g->h_rd, g->d_rd, n * 8));
-  TRY(dg_copy_async(g->e, g->h_rd + half, g->d_rd + half, n * 8));
-  TRY(dg_engine_sync(g->e));
+  if (half <= 65536) {
+    /* a small read: the kernels write the page-locked output directly (it is mapped into
+     * the device's address space), so the read's own wait is the only one */
+    TRY(dg_read_lww(g->e, &s->rows, all ? NULL : g->d_msg, nk, g->h_rd, g->h_rd + half, half, &n));
+  } else {
+    TRY(dg_read_lww(g->e, &s->rows, all ? NULL : g->d_msg, nk, g->d_rd, g->d_rd + half, half, &n));
+    TRY(dg_copy_async(g->e, g->h_rd, g->d_rd, n * 8));
+    TRY(dg_copy_async(g->e, g->h_rd + half, g->d_rd + half, n * 8));
+    TRY(dg_engine_sync(g->e));
+  }
   *n_out = n;
   return DG_OK;
 }

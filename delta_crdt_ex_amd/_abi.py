@@ -42,6 +42,14 @@ DG_E_NOMEM = -4
 DG_E_ORDER = -5
 DG_E_CLAUSE = -6
 
+DG_HOME_FALLBACK = 1
+DG_HOME_KEYS = 8
+DG_HOME_STRIDE = 1536
+DG_HOME_ROWS = DG_HOME_KEYS + 512
+DG_HOME_NODES = 2048
+DG_HOME_CTX = DG_HOME_ROWS + 4 * DG_HOME_STRIDE + DG_HOME_STRIDE // 2
+DG_HOME_WORDS = DG_HOME_CTX + DG_HOME_NODES + DG_HOME_NODES // 2
+
 DG_CTX_VV = 0
 DG_CTX_DOTS = 1
 
@@ -147,6 +155,9 @@ _SIGS = {
                                 C.POINTER(dg_store), C.POINTER(dg_context), P64, C.c_uint64,
                                 C.POINTER(dg_store), C.c_void_p, P64, C.c_uint64, P64,
                                 C.POINTER(C.c_int)]),
+    "dg_join_delta_home": (C.c_int, [C.c_void_p, C.POINTER(dg_store), C.POINTER(dg_context),
+                                     C.POINTER(dg_store), C.POINTER(dg_context), P64, C.c_uint64,
+                                     C.POINTER(dg_store), C.c_void_p, C.c_void_p, C.POINTER(C.c_int)]),
     "dg_join_delta_rows": (C.c_int, [C.c_void_p, C.POINTER(dg_store), C.POINTER(dg_context),
                                      C.POINTER(dg_store), C.POINTER(dg_context), P64, C.c_uint64,
                                      C.POINTER(dg_store), C.c_void_p, P64, C.c_uint64, P64,

@@ -44,6 +44,13 @@ struct dg_engine {
   // splice through `spl`)
   void* ubuf = nullptr;
   size_t ubuf_cap = 0;
+  // dg_join_delta_home's scratch: the edit, the per-key index, the result block; and its
+  // tree-update scratch, whose dirty flags and chunk deltas stay zero between calls
+  void* sml = nullptr;
+  size_t sml_cap = 0;
+  void* tscr = nullptr;
+  size_t tscr_cap = 0;
+  u64 tscr_chunks = 0;  // the chunk capacity tscr is laid out for
   // the full diff's per-group key sums: two buffers of diff_bsum_cap words, zero when
   // allocated; a call adds into one and its write kernel zeroes the other, which the
   // previous call used (no memset launch per diff)
@@ -260,10 +267,14 @@ __global__ void publish_counts_kernel(const u64* d, u64* h, u64 seq) {
 // D2H copy and a stream synchronize (≈ 14 µs on top of a config-2 join), a one-wave kernel
 // publishes them into mapped host memory and the host polls its sequence word; past 20 ms
 // (a long call) the runtime's synchronize takes over, and it is what reports a fault.
-int sync_words(dg_engine* e) {
+// (small_res / small_home: dg_join_delta_home's result block goes home in the same kernel)
+int sync_words(dg_engine* e, const u64* small_res = nullptr, u64* small_home = nullptr) {
   const u64 seq = ++e->pub_seq;
-  hipLaunchKernelGGL(publish_counts_kernel, dim3(1), dim3(WAVE), 0, e->stream, e->d_counts,
-                     e->d_pub, seq);
+  if (small_home)
+    HIP_TRY(launch_small_home_publish(small_res, small_home, e->d_counts, e->d_pub, seq, e->stream));
+  else
+    hipLaunchKernelGGL(publish_counts_kernel, dim3(1), dim3(WAVE), 0, e->stream, e->d_counts,
+                       e->d_pub, seq);
   HIP_TRY(hipGetLastError());
   const volatile u64* flag = e->h_pub + 16;
   const auto t0 = std::chrono::steady_clock::now();
@@ -747,6 +758,8 @@ int dg_engine_destroy(dg_engine* e) {
   if (e->fold) hipFree(e->fold);
   if (e->spl) hipFree(e->spl);
   if (e->ubuf) hipFree(e->ubuf);
+  if (e->sml) hipFree(e->sml);
+  if (e->tscr) hipFree(e->tscr);
   if (e->diff_bsum) hipFree(e->diff_bsum);
   if (e->h_stage) hipHostFree(e->h_stage);
   if (e->own_stream && e->stream) hipStreamDestroy(e->stream);
@@ -1027,6 +1040,148 @@ static int join_delta_impl(dg_engine* e, dg_store* state, dg_context* state_ctx,
   // the changed keys' rows from the edit (a changed key is a keyset key: all of its
   // joined rows are in the edit), not by a search of the state
   if (rows) TRY(take_changed_rows(e, &ed, changed, *n_changed, rows));
+  return DG_OK;
+}
+
+// dg_join_delta_home: the fused small-delta join (small.hip) with ONE host wait.  States
+// of up to SMALL_COPY_TILES splice tiles get the moved-rows copy enqueued behind the join,
+// guarded by its `moved` word; a larger state whose rows moved copies after the wait.
+constexpr u64 SMALL_COPY_TILES = 64;
+static_assert(DIFF_MISMATCH == DG_DIFF_MISMATCH, "deltagpu.h and the diff kernels agree");
+static_assert(SMALL_O_KEYS == DG_HOME_KEYS &&SMALL_O_ROWS == DG_HOME_ROWS && SMALL_EDIT == DG_HOME_STRIDE &&
+                  SMALL_O_CTX == DG_HOME_CTX && SMALL_NODES == DG_HOME_NODES && SMALL_WORDS == DG_HOME_WORDS &&
+                  SMALL_FALLBACK == DG_HOME_FALLBACK,
+              "the result block is the header's home layout");
+
+int dg_join_delta_home(dg_engine* e, dg_store* state, dg_context* state_ctx, const dg_store* delta,
+                       const dg_context* delta_ctx, const uint64_t* keys, uint64_t n_keys,
+                       dg_store* spare, dg_merkle* tree, uint64_t* home, int* swapped) {
+  if (!e) return fail(DG_E_INVAL, "null engine");
+  if (!swapped || !spare || !state || !state_ctx || !home)
+    return fail(DG_E_INVAL, "dg_join_delta_home: null argument");
+  *swapped = 0;
+  home[0] = SMALL_FALLBACK;
+  TRY(check_store(state, "dg_join_delta_home state"));
+  TRY(check_store(delta, "dg_join_delta_home delta"));
+  TRY(check_ctx(state_ctx, "dg_join_delta_home state_ctx"));
+  TRY(check_ctx(delta_ctx, "dg_join_delta_home delta_ctx"));
+  if (tree) TRY(check_merkle(tree, "dg_join_delta_home tree"));
+  if (keys == nullptr && n_keys != 0) return fail(DG_E_INVAL, "dg_join_delta_home: keys NULL with n_keys>0");
+  const bool small = n_keys <= SMALL_KEYS && delta->n <= SMALL_DELTA && delta_ctx->n <= SMALL_DCTX &&
+                     state_ctx->kind == DG_CTX_VV && state_ctx->n <= SMALL_NODES &&
+                     spare->cap >= state->n + delta->n && state_ctx->cap >= 1 &&
+                     pair_aligned(state->key, state->val, state->ts, state->node, state->cnt) &&
+                     pair_aligned(spare->key, spare->val, spare->ts, spare->node, spare->cnt);
+  if (!small) return DG_OK;  // home[0] = SMALL_FALLBACK: the caller takes dg_join_delta_rows
+  TRY(set_device(e));
+  TRY(settle(e));
+  const u64 nk = n_keys, a_tiles = splice_tiles(state->n);
+  const bool copy_now = a_tiles <= SMALL_COPY_TILES;
+  // scratch: the edit | a_lo | a_off | end | shift | gap | tile_u0 | moved word | result
+  const size_t idx = ((nk + 1) * 8 + 255) / 256 * 256;
+  const size_t bytes = (SMALL_EDIT * 36 + 5 * 256) + 6 * idx + ((a_tiles + 2) * 8 + 255) / 256 * 256 + 256 +
+                       SMALL_WORDS * 8 + 256;
+  TRY(ensure_buf(e, &e->sml, &e->sml_cap, bytes));
+  char* q = (char*)e->sml;
+  dg_store ed = carve_store(q, SMALL_EDIT);
+  u64* a_lo = (u64*)q;
+  u64* a_off = (u64*)(q + idx);
+  u64* end = (u64*)(q + 2 * idx);
+  i64* shift = (i64*)(q + 3 * idx);
+  i64* gap = (i64*)(q + 4 * idx);
+  q += 6 * idx;
+  u64* tile_u0 = (u64*)q;
+  q += ((a_tiles + 2) * 8 + 255) / 256 * 256;
+  u32* moved_word = (u32*)q;
+  q += 256;
+  u64* res = (u64*)q;
+  SmallArgs p{};
+  p.a = rows_of(state);
+  p.aw = rows_out_of(state);
+  p.ca = ctx_of(state_ctx);
+  p.ca_node = state_ctx->node;
+  p.ca_cnt = state_ctx->cnt;
+  p.ca_cap = state_ctx->cap;
+  p.d = rows_of(delta);
+  p.cd = ctx_of(delta_ctx);
+  p.keys = keys;
+  p.nk = nk;
+  p.e = rows_out_of(&ed);
+  p.a_lo = a_lo;
+  p.a_off = a_off;
+  p.res = res;
+  p.has_tree = tree != nullptr;
+  u32* dirty = nullptr;
+  i64* cdelta = nullptr;
+  u64* hand = nullptr;
+  if (tree) {
+    // the tree update's scratch: dirty flags | per-chunk row-count changes | hand-off words,
+    // an engine buffer of its own whose first two parts stay zero between calls (the upsweep
+    // zeroes what it read), so no zeroing launch.  Their offsets are fixed by the chunk
+    // capacity the buffer was laid out for, never by this tree's depth: a deeper tree's
+    // hand-off words must not land where a shallower one expects zeros.
+    const u64 chunks = merkle_chunks(tree->depth);
+    if (chunks > e->tscr_chunks) {
+      const u64 cap = chunks < 64 ? 64 : chunks;
+      const size_t tb = (cap + 2 * cap + 4 * cap) * sizeof(u32);  // hand: merkle_ctr_words
+      TRY(ensure_buf(e, &e->tscr, &e->tscr_cap, tb));
+      HIP_TRY(hipMemsetAsync(e->tscr, 0, e->tscr_cap, e->stream));
+      e->tscr_chunks = cap;
+    }
+    const u64 cap = e->tscr_chunks;  // dirty: cap u32 (even) | cdelta: cap i64 | hand: 4 cap u32
+    dirty = (u32*)e->tscr;
+    cdelta = (i64*)(dirty + cap);
+    hand = (u64*)(cdelta + cap);
+    p.t = merkle_of(tree);
+    p.dirty = dirty;
+    p.cdelta = cdelta;
+  }
+  HIP_TRY(launch_small_delta(p, e->stream));
+  if (tree)  // MerkleMap.update_hashes: the dirty chunks and the levels above them
+    HIP_TRY(launch_merkle_upsweep(merkle_of(tree), rows_of(state), dirty, e->ticket + MERKLE_ARRIVE,
+                                  hand, cdelta, e->ticket + 3, e->stream));
+  SpliceArgs sp{};
+  sp.a = rows_of(state);
+  sp.keys = keys;
+  sp.nk = nk;
+  sp.a_lo = a_lo;
+  sp.a_off = a_off;
+  sp.end = end;
+  sp.shift = shift;
+  sp.gap = gap;
+  sp.tile_u0 = tile_u0;
+  sp.moved = moved_word;
+  sp.e = rows_of(&ed);
+  sp.e.n = SMALL_EDIT;  // a bound: the kernels read the count
+  sp.d_ne = res + 4;
+  sp.out = rows_out_of(spare);
+  sp.run_if = res + 6;  // the rows moved (0 also when the join fell back or failed)
+  if (copy_now) {
+    HIP_TRY(launch_splice_index(sp, e->stream));
+    HIP_TRY(launch_splice_copy(sp, false, e->stream));
+  }
+  TRY(sync_words(e, res, home));  // the one wait (the result block lands in `home` with it)
+  const u64 flags = home[0];
+  if (flags & SMALL_FALLBACK) return DG_OK;  // nothing written: the general path
+  if (flags & MERKLE_INPUT_ERR) {
+    if (flags & MERKLE_ERR_SHARD) return fail(DG_E_INVAL, "dg_join_delta_home: a key outside the tree's shard");
+    return fail(DG_E_CAPACITY, "dg_join_delta_home: a bucket would hold more than 65535 rows (use a deeper tree)");
+  }
+  const u64 n_e = home[4], n_ak = home[5];
+  if (home[6]) {  // rows moved: the state is in `spare` (copied behind the join, or now)
+    if (!copy_now) {
+      HIP_TRY(launch_splice_index(sp, e->stream));
+      HIP_TRY(launch_splice_copy(sp, false, e->stream));
+      TRY(read_counts(e, 0));
+    }
+    const u64 n = state->n - n_ak + n_e;
+    std::swap(*state, *spare);
+    state->n = n;
+    *swapped = 1;
+  }
+  state_ctx->n = home[3];
+  state_ctx->kind = DG_CTX_VV;
+  if (tree) tree->n_keys += home[7];
   return DG_OK;
 }
 
@@ -1587,6 +1742,12 @@ int dg_merkle_diff(dg_engine* e, const dg_merkle* a, const dg_store* sa, const d
   HIP_TRY(enqueue_merkle_diff(e, a, sa, b, sb, out_keys, cap, e->d_counts));
   TRY(read_counts(e, 1));
   const u64 total = e->h_counts[0];
+  if (total >= DIFF_MISMATCH) {
+    *n_out = 0;
+    if (n_total) *n_total = 0;
+    return fail(DG_E_INVAL, "dg_merkle_diff: a tree counts more rows than its store holds "
+                            "(the store is not the one the tree was built / updated against)");
+  }
   *n_out = std::min<u64>(total, cap);
   if (n_total) *n_total = total;
   return DG_OK;
@@ -1844,7 +2005,7 @@ int dg_host_alloc(dg_engine* e, uint64_t bytes, void** p) {
   *p = nullptr;
   TRY(set_device(e));
   if (bytes == 0) return DG_OK;
-  if (hipHostMalloc(p, bytes, 0) != hipSuccess) {
+  if (hipHostMalloc(p, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
     *p = nullptr;
     return fail(DG_E_NOMEM, "hipHostMalloc of %llu bytes failed", (unsigned long long)bytes);
   }

@@ -177,6 +177,9 @@ struct SpliceArgs {
   // (optional) an input-error word: when it has a MERKLE_INPUT_ERR bit set, E's rows are
   // not written (dg_join_delta's in-place copy runs after the tree update it depends on)
   const u32* guard;
+  // (optional) the index and copy kernels run only when *run_if != 0 (the fused small
+  // join enqueues the moved-rows copy before the host knows whether rows moved)
+  const u64* run_if;
 };
 // For every key of keys (ascending, n_keys): lo[u] = the first row of s whose key is >=
 // keys[u] and len[u] = its rows, found by streaming s's key column in tiles (each tile's
@@ -294,8 +297,54 @@ hipError_t launch_merkle_build(const Rows& s, const MerkleT& t, u64* d_keys, u32
 hipError_t launch_merkle_update(const MerkleT& t, const Rows& olds, const Rows& news, const u64* keys,
                                 u64 n_keys, u32* dirty, u64* d_keys, u32* arrive, u64* hand, i64* cdelta,
                                 u32* err, hipStream_t st);
+// the chunk kernel of an update alone: the dirty chunks re-reduced, the top levels, the
+// chunk index moved by cdelta (the fused small join set the bucket level, dirty, cdelta)
+hipError_t launch_merkle_upsweep(const MerkleT& t, const Rows& news, u32* dirty, u32* arrive, u64* hand,
+                                 i64* cdelta, u32* err, hipStream_t st);
+// ---- small.hip: dg_join_delta of a small delta, one launch (see the file header)
+constexpr u32 SMALL_KEYS = 512, SMALL_DELTA = 512, SMALL_DCTX = 1024, SMALL_NODES = 2048;
+constexpr u32 SMALL_TAKEN = 1024, SMALL_EDIT = 1536;
+struct SmallArgs {
+  Rows a;              // the state (read)
+  RowsOut aw;          // the same columns (the in-place write)
+  Ctx ca;              // the state's context (a VV)
+  u32* ca_node;        // ... written with the union
+  u64* ca_cnt;
+  u64 ca_cap;
+  Rows d;              // the delta, sorted
+  Ctx cd;              // its context, sorted
+  const u64* keys;     // ascending unique
+  u64 nk;
+  RowsOut e;           // scratch: the edit (SMALL_EDIT rows), the splice layout
+  u64* a_lo;           // scratch: nk, the keys' first state rows
+  u64* a_off;          // scratch: nk + 1, their offsets among the taken rows
+  MerkleT t;           // the tree (has_tree)
+  int has_tree;
+  u32* dirty;          // zero on entry
+  i64* cdelta;         // zero on entry (t.starts kept)
+  u64* res;            // result block (small_res_words())
+};
+// result block words: header [0] flags [1] changed keys [2] their rows [3] context entries
+// [4] edit rows [5] taken rows [6] moved [7] distinct-key change; then the changed keys
+// (SMALL_KEYS), their rows as key | val | ts | cnt (SMALL_EDIT each) and node (u32,
+// SMALL_EDIT / 2 words), the context's cnt (SMALL_NODES) and node (u32, SMALL_NODES / 2)
+constexpr u64 SMALL_HDR = 8;
+constexpr u64 SMALL_O_KEYS = SMALL_HDR, SMALL_O_ROWS = SMALL_O_KEYS + SMALL_KEYS;
+constexpr u64 SMALL_O_CTX = SMALL_O_ROWS + 4 * (u64)SMALL_EDIT + SMALL_EDIT / 2;
+constexpr u64 SMALL_WORDS = SMALL_O_CTX + SMALL_NODES + SMALL_NODES / 2;
+
+constexpr u32 SMALL_FALLBACK = 1u;  // flags: nothing written, the general path runs
+hipError_t launch_small_delta(const SmallArgs& p, hipStream_t st);
+// the used part of the result block into `home` (host memory the device can write), then
+// the engine's count block into the mapped publish words and the sequence number `seq`
+// (what sync_words' publish kernel does): the result is home when the host sees seq
+hipError_t launch_small_home_publish(const u64* res, u64* home, const u64* d_counts, u64* h_pub, u64 seq,
+                                     hipStream_t st);
 constexpr int DIFF_BLOCK = 256;
-constexpr u32 DIFF_SUB = 12;  // levels a diff workgroup descends: subtrees of 4096 buckets
+#ifndef DG_DIFF_SUB
+#define DG_DIFF_SUB 12
+#endif
+constexpr u32 DIFF_SUB = DG_DIFF_SUB;  // levels a diff workgroup descends: subtrees of 2^DIFF_SUB buckets
 inline u32 diff_sub(u32 depth) { return depth < DIFF_SUB ? depth : DIFF_SUB; }
 inline u64 diff_tiles(u32 depth) { return 1ull << (depth - diff_sub(depth)); }
 // subtree boundaries in both stores, per-subtree counts, then the differing keys staged
@@ -304,6 +353,10 @@ inline u64 diff_groups(u32 depth) { return (diff_tiles(depth) + DIFF_BLOCK - 1) 
 inline u64 diff_scratch_words(u32 depth, u64 na, u64 nb) {
   return 2 * (diff_tiles(depth) + 1) + diff_tiles(depth) + na + nb + 1;
 }
+// a subtree whose tree row counts overrun a store adds this to the total (no keys): at most
+// 2^18 subtrees (depth 30) keep the sum of markers below 2^63, and no total of real keys
+// reaches it (deltagpu.h DG_DIFF_MISMATCH)
+constexpr u64 DIFF_MISMATCH = 1ull << 44;
 // differing keys, ascending; the first min(total, cap) written; *d_count = total.
 hipError_t launch_merkle_diff(const MerkleT& a, const Rows& sa, const MerkleT& b, const Rows& sb,
                               u64* out_keys, u64 cap, u64* scratch, u64* bsum, u64* bsum_zero, u64 nzero,

@@ -747,7 +747,7 @@ __device__ __forceinline__ void commit_tile(const Staged& r, Buf& s) {
 // No look-back chain and no ticket: a stripe's counts were all published one merge
 // earlier, so step 4 rarely waits; its cost is one G-word read per iteration, issued
 // before the merge.  Spins stay bounded (scan.err bit 0 on timeout).
-constexpr int FUSE_IT = JB / WAVE / 2;  // fused splits: one wave per boundary, 2 per tile
+constexpr int FUSE_IT = 4;  // fused: tiles per workgroup whose splits the kernel searches itself
 // (stripe_sums' partials are double-buffered by iteration parity, which drops the barrier
 // a single buffer needs before its writes: measured neutral, config 5 356-360 vs 358-360 us
 // and config 2 34.5-35.4 vs 34.6-34.7 us, rocprofv3 on one box; kept, one barrier fewer)
@@ -944,19 +944,20 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       tile_geom(w, ga0, ga1, total, &gnat, &gnbt, &gb0);
       issue_tile(A, B, gnat, gnbt, ga0, gb0, r);
     }
-    // merge-path splits of this workgroup's (<= FUSE_IT) tiles, one wave per boundary
-    const int wv = tid / WAVE;
-    const u64 tk = w + (u64)(wv >> 1) * G;
-    if (tk < ntiles) {
-      const u64 d = min((tk + (wv & 1)) * (u64)JT, total);
+    // merge-path splits of this workgroup's (<= FUSE_IT) tiles: boundary q (tile q / 2,
+    // side q % 2) by wave q mod the block's waves
+    for (int q = tid / WAVE; q < 2 * FUSE_IT; q += JB / WAVE) {  // (wave-uniform)
+      const u64 tk = w + (u64)(q >> 1) * G;
+      if (tk >= ntiles) break;
+      const u64 d = min((tk + (q & 1)) * (u64)JT, total);
       // the proportional split is checked first with scalar loads (a counter the tile
       // loads in flight do not hold up); the search runs only where it is not exact
       const u64 g = split_guess(A.n, B.n, d);
       const u64 sp = guess_exact(A, B, d, g) ? g : mp_split(A, B, d);
-      if ((tid & (WAVE - 1)) == 0) s.spl[wv] = sp;
+      if ((tid & (WAVE - 1)) == 0) s.spl[q] = sp;
       if (KEYED) {
         const u64 kq = key_split(A, B, p.keys, p.n_keys, d, sp);
-        if ((tid & (WAVE - 1)) == 0) s.kspl[wv] = kq;
+        if ((tid & (WAVE - 1)) == 0) s.kspl[q] = kq;
       }
     }
   }

@@ -43,6 +43,7 @@
 //    differing buckets), which the peer merges with its own rows into keys.
 #include "dg_hash.h"
 #include "dg_launch.h"
+#include "dg_tree.h"
 
 namespace dg {
 
@@ -56,25 +57,6 @@ struct MT {
   TermH th;
   u64* starts;  // optional (nullptr): each chunk's first row, then the end (dg_merkle.starts)
 };
-
-// The value's and the node's terms in a row hash (dg_term_hashes): a canonical integer
-// value id [2^58, 2^63) and ids missing from the tables stand for themselves.
-__device__ __forceinline__ u64 th_val(const TermH& th, u64 v) {
-  if (!th.on || th.nv == 0 || (v >= (1ull << 58) && v < (1ull << 63))) return v;
-  u64 lo = 0, hi = th.nv;
-  while (lo < hi) {
-    const u64 mid = (lo + hi) >> 1;
-    if (th.vid[mid] < v)
-      lo = mid + 1;
-    else
-      hi = mid;
-  }
-  return (lo < th.nv && th.vid[lo] == v) ? th.vh[lo] : v;
-}
-
-__device__ __forceinline__ u64 th_node(const TermH& th, u32 n) {
-  return (th.on && (u64)n < th.nn) ? th.nh[n] : (u64)n;
-}
 
 __device__ __forceinline__ u64 bucket_of(const MT& t, u64 key) {
   return (key << t.sb) >> (64 - t.depth);
@@ -398,6 +380,9 @@ __global__ __launch_bounds__(UPB, 4) void merkle_chunk_kernel(Rows rows, MT t, c
     if (s_last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // all G arrived
   }
   __syncthreads();
+  // (an update's dirty flag read by every thread above: zero again for the next update,
+  // which the small-delta join relies on -- its scratch is not re-zeroed per call)
+  if (!BUILD && tid == 0) ((u32*)dirty)[g] = 0;
   if (!s_last) return;
   // ---- the last workgroup: levels depth - L1 .. 0, UPL levels per round; the first
   // round's inputs are the handed-off chunk roots (sc1 loads)
@@ -460,6 +445,7 @@ __global__ __launch_bounds__(UPB, 4) void merkle_chunk_kernel(Rows rows, MT t, c
       for (int q = 0; q < CP; q++) {
         const u64 x = x0 + q;
         if (x <= G) t.starts[x] = (u64)(st0[q] + run);
+        if (x < G && v[q]) ((i64*)cdelta)[x] = 0;  // read above: zero again for the next update
         run += v[q];
       }
       carry += tot;
@@ -602,11 +588,18 @@ constexpr u32 OWN = XSUB / DB;        // buckets per thread
 #ifndef DG_DIFF_EXP
 #define DG_DIFF_EXP 0
 #endif
-constexpr u32 RCAP = 1664;            // rows of the differing buckets staged in LDS
-constexpr u32 DCAP = 512;             // differing buckets listed in LDS
-constexpr u32 NHD = 128;              // node term hashes staged per tree (38.9 KB in all:
-                                      // 4 workgroups per CU)
-static_assert(OWN == 16, "a thread owns 16 buckets: two 16-byte count loads per tree");
+// rows of the differing buckets staged in LDS, differing buckets listed in LDS (the
+// subtree's share of a 1 %-differing config-4 shard is ~1000 rows in ~120 buckets at 4096
+// buckets, a quarter of that at 1024; a subtree beyond either merges over global memory)
+constexpr u32 RCAP = XSUB >= 4096 ? 1664 : 640;
+constexpr u32 DCAP = XSUB >= 4096 ? 512 : 160;
+constexpr u32 NHD = 128;              // node term hashes staged per tree
+#ifndef DG_DIFF_OCC
+#define DG_DIFF_OCC 4
+#endif
+constexpr int DIFF_OCC = DG_DIFF_OCC;  // count workgroups per CU the kernel is compiled for
+static_assert(OWN == 16 || OWN == 4, "a thread owns 16 or 4 buckets (32 or 8 bytes of counts per tree)");
+constexpr u32 CW = OWN / 2;           // count words (two u16 halves) per thread and tree
 
 struct DiffArgs {
   MT ta, tb;
@@ -630,20 +623,25 @@ struct DiffArgs {
 // deltagpu.h); mask_counts16 zeroes what the thread does not own, AFTER the round trip's
 // other loads are issued (any use of a loaded value -- a second load path for small
 // subtrees, a mask -- makes the compiler wait for it right there)
-__device__ __forceinline__ void load_counts16(const uint16_t* c, u32 first, u32 w[8]) {
-  const uint4* v = (const uint4*)(c + first);
-  const uint4 x = v[0], y = v[1];
-  w[0] = x.x, w[1] = x.y, w[2] = x.z, w[3] = x.w, w[4] = y.x, w[5] = y.y, w[6] = y.z, w[7] = y.w;
+__device__ __forceinline__ void load_counts16(const uint16_t* c, u32 first, u32 w[CW]) {
+  if constexpr (OWN == 16) {
+    const uint4* v = (const uint4*)(c + first);
+    const uint4 x = v[0], y = v[1];
+    w[0] = x.x, w[1] = x.y, w[2] = x.z, w[3] = x.w, w[4] = y.x, w[5] = y.y, w[6] = y.z, w[7] = y.w;
+  } else {
+    const uint2 x = *(const uint2*)(c + first);
+    w[0] = x.x, w[1] = x.y;
+  }
 }
-__device__ __forceinline__ void mask_counts16(u32 w[8], u32 nb, bool owns) {
+__device__ __forceinline__ void mask_counts16(u32 w[CW], u32 nb, bool owns) {
 #pragma unroll
-  for (u32 q = 0; q < 8; q++) {  // (nb < 16: a tree of fewer than 16 buckets, thread 0's)
+  for (u32 q = 0; q < CW; q++) {  // (nb < OWN: a tree of fewer buckets, thread 0's)
     const u32 keep = (2 * q + 1 < nb ? 0xFFFF0000u : 0u) | (2 * q < nb ? 0xFFFFu : 0u);
     w[q] &= owns ? keep : 0u;
   }
 }
 
-__device__ __forceinline__ u32 half16(const u32 w[8], u32 i) { return (w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu; }
+__device__ __forceinline__ u32 half16(const u32 w[CW], u32 i) { return (w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu; }
 
 // a buffer descriptor over [base, base + bytes) for a wave-uniform base (the halves go
 // through readfirstlane so the compiler can keep the descriptor in SGPRs; gfx950 flags)
@@ -675,7 +673,7 @@ __device__ u64 g_df_stamps[4096 * 8];
   } while (0)
 #endif
 
-__global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) {  // 4 per CU: all resident
+__global__ __launch_bounds__(DB, DIFF_OCC * DB / 256) void merkle_diff_count_kernel(DiffArgs p) {
   __shared__ u32 s_wave[DB / WAVE + 1];
   __shared__ u32 s_da[DCAP], s_db[DCAP];  // a differing bucket's first row in A / B (from the subtree's)
   __shared__ u32 s_dp[DCAP + 1];          // its first staged row
@@ -704,7 +702,7 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
   const u64 gi = sub >= 8 ? ((1ull << (depth - 8)) - 1) + (b0c >> 8) : root;
   const u64 qi = sub >= 4 ? ((1ull << (depth - 4)) - 1) + (b0c >> 4) : root;
   const u64 ga = p.ta.nodes[gi], gb = p.tb.nodes[gi], qa = p.ta.nodes[qi], qb = p.tb.nodes[qi];
-  u32 ca[8], cb[8];
+  u32 ca[CW], cb[CW];
   load_counts16(p.ta.counts + bucket0, owns ? (u32)tid * OWN : 0u, ca);
   load_counts16(p.tb.counts + bucket0, owns ? (u32)tid * OWN : 0u, cb);
   const u32 nna = nha_lds ? (u32)p.ta.th.nn : 0u, nnb = nhb_lds ? (u32)p.tb.th.nn : 0u;
@@ -751,11 +749,11 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
   u32 mine = 0;  // the owned buckets that differ (bit i: bucket 16 tid + i)
   const bool anc = owns && (sub < 8 || ga != gb) && (sub < 4 || qa != qb);
   if (nb >= (u32)(WAVE * OWN)) {
-    // the wave's 1024 buckets' nodes, loaded by the wave together: load i of a lane reads
-    // node 64 i + lane (owner lane 4 i + lane / 16, only under its differing ancestors),
-    // so each load instruction reads 512 contiguous bytes instead of one 8-B node from
-    // each of 64 lines (a lane's own 16 nodes); every load is issued before any compare,
-    // and the ballot of load i hands each of its four owner lanes its 16 bits
+    // the wave's 64 x OWN buckets' nodes, loaded by the wave together: load i of a lane
+    // reads node 64 i + lane (owner lane (64 i + lane) / OWN, only under its differing
+    // ancestors), so each load instruction reads 512 contiguous bytes instead of one 8-B
+    // node from each of 64 lines (a lane's own OWN nodes); every load is issued before any
+    // compare, and the ballot of load i hands each of its 64 / OWN owner lanes its OWN bits
     // (buffer loads: a lane that must not load passes an offset past the descriptor's
     // range, which the hardware answers with 0 and no memory access -- a conditional
     // global load would be a branch, and the compiler waits for each load at its join)
@@ -765,9 +763,10 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
     const __amdgpu_buffer_rsrc_t na = wave_rsrc(p.ta.nodes + lv, WAVE * OWN * 8);
     const __amdgpu_buffer_rsrc_t nbr = wave_rsrc(p.tb.nodes + lv, WAVE * OWN * 8);
     u64 x[OWN], y[OWN];
+    constexpr u32 OPL = WAVE / OWN;  // owner lanes per load
 #pragma unroll
     for (u32 i = 0; i < OWN; i++) {
-      const bool ld = (amask >> (4 * i + lane / 16)) & 1;
+      const bool ld = (amask >> (OPL * i + lane / OWN)) & 1;
       const int off = ld ? (int)((64 * i + lane) * 8) : 0x7ffffff0;
       x[i] = buf_load_u64(na, off);
       y[i] = buf_load_u64(nbr, off);
@@ -775,7 +774,7 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
 #pragma unroll
     for (u32 i = 0; i < OWN; i++) {
       const u64 bal = __ballot(x[i] != y[i]);
-      if ((u32)(lane >> 2) == i) mine = (u32)(bal >> (16 * (lane & 3))) & 0xFFFFu;
+      if ((u32)lane / OPL == i) mine = (u32)(bal >> (OWN * (lane % OPL))) & ((1u << OWN) - 1);
     }
   } else if (anc) {  // a subtree of fewer than 1024 buckets: a thread loads its own nodes
     const u64 lv = ((1ull << depth) - 1) + b0;
@@ -811,7 +810,7 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
   // the waves before its own (4 waves) -- four block scans took 12 barriers
   constexpr int NW = DB / WAVE;
   __shared__ u32 s_w4[4 * NW];
-  u32 offa, offb, slot0, d0, ND, R;
+  u32 offa, offb, slot0, d0, ND, R, TA, TB;
   {
     const u32 v[4] = {ta_, tb_, rd, (u32)__popc(mine)};
     u32 inc[4];
@@ -839,10 +838,22 @@ __global__ __launch_bounds__(DB, 4) void merkle_diff_count_kernel(DiffArgs p) { 
     d0 = below[3] + inc[3] - v[3];
     R = total[2];
     ND = total[3];
+    TA = total[0];
+    TB = total[1];
   }
   DSTAMP(2);
   const u64 a0 = s_bnd[0], c0 = s_bnd[1];  // (the barrier above came after the searches)
   const u64 base = a0 + c0;
+  if (a0 + TA > p.sa.n || c0 + TB > p.sb.n) {
+    // (uniform) the trees count more rows here than the stores hold from the subtree's first
+    // row: a store the tree does not describe.  No row is read past it and no key written;
+    // the marker reaches the total, which the host reports as an input error.
+    if (tid == 0) {
+      p.cnt[tile] = DIFF_MISMATCH;
+      atomicAdd((unsigned long long*)&p.bsum[tile / DB], (unsigned long long)DIFF_MISMATCH);
+    }
+    return;
+  }
   const bool lds = R <= RCAP && ND <= DCAP;  // uniform
   if (lds) {
     u32 d = d0, slot = slot0, ra = offa, rb = offb;
@@ -1052,7 +1063,7 @@ __global__ __launch_bounds__(WAVE) void merkle_diff_write_kernel(DiffArgs p) {
 #pragma unroll
   for (int d = WAVE / 2; d >= 1; d >>= 1) before += __shfl_xor(before, d, WAVE);
   if (last && lane == 0) *p.d_count = before + n;
-  if (n == 0 || before >= p.cap) return;
+  if (n == DIFF_MISMATCH || before >= p.cap) return;  // (no keys: the count kernel's marker)
   const u64 src = p.bnd[tile] + p.bnd[p.ntiles + 1 + tile];
   for (u64 x = lane; x < n && before + x < p.cap; x += WAVE) p.out[before + x] = p.keys[src + x];
 }
@@ -1200,6 +1211,15 @@ hipError_t launch_merkle_update(const MerkleT& m, const Rows& olds, const Rows& 
                        keys, n_keys, dirty, d_keys, err, cd);
   hipLaunchKernelGGL(merkle_chunk_kernel<false>, dim3((unsigned)G), dim3(UPB), 0, st, news, t, dirty,
                      arrive, hand, (u64*)nullptr, err, (const i64*)cd);
+  return hipGetLastError();
+}
+
+hipError_t launch_merkle_upsweep(const MerkleT& m, const Rows& news, u32* dirty, u32* arrive, u64* hand,
+                                 i64* cdelta, u32* err, hipStream_t st) {
+  const MT t = mt_of(m);
+  const u64 G = merkle_chunks(t.depth);
+  hipLaunchKernelGGL(merkle_chunk_kernel<false>, dim3((unsigned)G), dim3(UPB), 0, st, news, t, dirty,
+                     arrive, hand, (u64*)nullptr, err, (const i64*)(t.starts ? cdelta : nullptr));
   return hipGetLastError();
 }
 

@@ -130,6 +130,7 @@ __global__ __launch_bounds__(SB) void splice_check_kernel(const u64* bkey, u64 n
 // the first entry of every state tile whose first row falls in [end[u-1], end[u]) (so
 // the copy's tiles look their entry range up instead of searching for it)
 __global__ __launch_bounds__(SB) void splice_index_kernel(SpliceArgs p) {
+  if (p.run_if && *p.run_if == 0) return;  // (uniform) nothing moved: not needed
   const u64 u = (u64)blockIdx.x * SB + threadIdx.x;
   if (u > p.nk) return;
   const u64 ne = *p.d_ne;
@@ -223,6 +224,7 @@ __device__ __forceinline__ void store_tile(const RowsOut& o, const TileRows& x, 
 // E's rows: one thread per keyset entry u moves its key's rows [PE[u], PE[u + 1]) of E
 // (PE = shift + a_off) to j + gap[u] -- no search: the index kernel has placed them.
 __global__ __launch_bounds__(SB) void splice_erows_kernel(SpliceArgs p) {
+  if (p.run_if && *p.run_if == 0) return;  // (uniform) nothing moved: not needed
   const u64 u = (u64)blockIdx.x * SB + threadIdx.x;
   if (u >= p.nk) return;
   if (p.guard && (*p.guard & MERKLE_INPUT_ERR)) return;  // the tree update failed: no write
@@ -242,6 +244,7 @@ __global__ __launch_bounds__(SB) void splice_erows_kernel(SpliceArgs p) {
 // workgroup issues its rows' loads first: the index entries that place them are staged
 // while the loads are in flight.
 __global__ __launch_bounds__(SB) void splice_kernel(SpliceArgs p) {
+  if (p.run_if && *p.run_if == 0) return;  // (uniform) nothing moved: not needed
   __shared__ u64 s_end[SLC], s_lo[SLC];
   __shared__ i64 s_shift[SLC];
   TileRows x;

@@ -307,6 +307,9 @@ class Engine:
 
     def close(self):
         if getattr(self, "h", None):
+            if getattr(self, "_home", None) is not None:
+                self.lib.dg_host_free(self.h, self._home)
+                self._home = None
             self.lib.dg_engine_destroy(self.h)
             self.h = None
 
@@ -637,6 +640,51 @@ class Engine:
             tree.n_keys = int(t.n_keys) & ((1 << 64) - 1)
             tree.store = state
         return changed[: n.value], bool(sw.value)
+
+    def join_delta_home(self, state: Store, state_ctx: Context, delta: Store, delta_ctx: Context,
+                        keys: torch.Tensor, spare: Store, tree: MerkleTree | None = None):
+        """dg_join_delta_home: join_delta for a small delta in one launch chain with one
+        host wait, the result (changed keys, their rows, the new context) written into
+        page-locked host memory.  Returns None when the library declined (DG_HOME_FALLBACK:
+        nothing happened), else (changed keys, rows (key, val, ts, node, cnt), context
+        (node, cnt), swapped) as numpy arrays."""
+        self._order()
+        if getattr(self, "_home", None) is None:
+            p = C.c_void_p()
+            check(self.lib.dg_host_alloc(self.h, _abi.DG_HOME_WORDS * 8, C.byref(p)))
+            self._home = p
+        ss, sc, sd, cd, sp = state.abi(), state_ctx.abi(), delta.abi(), delta_ctx.abi(), spare.abi()
+        t = tree.abi() if tree is not None else None
+        kp, nk = self._keys(keys)
+        sw = C.c_int(0)
+        check(self.lib.dg_join_delta_home(self.h, C.byref(ss), C.byref(sc), C.byref(sd), C.byref(cd), kp,
+                                          nk, C.byref(sp), C.byref(t) if t is not None else None,
+                                          self._home, C.byref(sw)))
+        h = np.ctypeslib.as_array(C.cast(self._home, C.POINTER(C.c_uint64)), shape=(_abi.DG_HOME_WORDS,))
+        if int(h[0]) & _abi.DG_HOME_FALLBACK:
+            return None
+        nch, nr, nc = int(h[1]), int(h[2]), int(h[3])
+        S, R0 = _abi.DG_HOME_STRIDE, _abi.DG_HOME_ROWS
+        keys_out = h[_abi.DG_HOME_KEYS:_abi.DG_HOME_KEYS + nch].copy()
+        rows = (h[R0:R0 + nr].copy(), h[R0 + S:R0 + S + nr].copy(),
+                h[R0 + 2 * S:R0 + 2 * S + nr].copy().view(np.int64),
+                h[R0 + 4 * S:R0 + 5 * S].view(np.uint32)[:nr].copy(), h[R0 + 3 * S:R0 + 3 * S + nr].copy())
+        C0 = _abi.DG_HOME_CTX
+        ctx = (h[C0 + _abi.DG_HOME_NODES:C0 + 2 * _abi.DG_HOME_NODES].view(np.uint32)[:nc].copy(),
+               h[C0:C0 + nc].copy())
+        if sw.value:
+            for f in ("key", "val", "ts", "node", "cnt"):
+                a, b = getattr(state, f), getattr(spare, f)
+                setattr(state, f, b)
+                setattr(spare, f, a)
+            spare.n = 0
+        state.n = int(ss.n)
+        state_ctx.n = int(sc.n)
+        state_ctx.kind = int(sc.kind)
+        if tree is not None:
+            tree.n_keys = int(t.n_keys) & ((1 << 64) - 1)
+            tree.store = state
+        return keys_out, rows, ctx, bool(sw.value)
 
     def merkle_update(self, tree: MerkleTree, new: Store, keys: torch.Tensor) -> MerkleTree:
         """MerkleMap.put/delete of the changed `keys` + update_hashes: `tree` indexed

@@ -198,7 +198,9 @@ int dg_copy_to_host(dg_engine* e, void* dst, const void* src, uint64_t bytes);
  * such copy, and brings several result ranges home with one wait (c_src/replica.c). */
 int dg_copy_async(dg_engine* e, void* dst, const void* src, uint64_t bytes);
 /* Page-locked host memory (what dg_copy_async needs to overlap and what makes small copies
- * cheap); dg_host_free waits for the engine stream first. */
+ * cheap), mapped into the device's address space: an entry point's device OUTPUT pointers
+ * may point into it, and the kernels then write the result straight to the host (small
+ * outputs: no copy, no second wait).  dg_host_free waits for the engine stream first. */
 int dg_host_alloc(dg_engine* e, uint64_t bytes, void** p);
 int dg_host_free(dg_engine* e, void* p);
 
@@ -270,6 +272,33 @@ int dg_join_delta_rows(dg_engine* e, dg_store* state, dg_context* state_ctx, con
                        const dg_context* delta_ctx, const uint64_t* keys, uint64_t n_keys,
                        dg_store* spare, dg_merkle* tree, uint64_t* changed, uint64_t cap,
                        uint64_t* n_changed, int* swapped, dg_store* rows);
+
+/* dg_join_delta_rows for a SMALL delta in ONE launch chain with ONE host wait (the general
+ * path waits after each of its four steps): the keyed join, the changed keys, the MerkleMap
+ * put/delete + update_hashes, and the results written straight into `home`, host memory
+ * from dg_host_alloc of DG_HOME_WORDS words:
+ *   home[0] flags (0: done; DG_HOME_FALLBACK: nothing was done -- call dg_join_delta_rows)
+ *   home[1] changed keys   home[2] their rows   home[3] the state's context entries
+ *   home[DG_HOME_KEYS ...]  the changed keys, ascending
+ *   home[DG_HOME_ROWS ...]  their rows in store order: key | val | ts | cnt columns at stride
+ *                           DG_HOME_STRIDE, then node (uint32) at DG_HOME_ROWS + 4 stride
+ *   home[DG_HOME_CTX ...]   the new context: cnt (DG_HOME_NODES), then node (uint32)
+ * Small: keys <= 512, delta rows <= 512, delta context <= 1024 entries, a VV state context
+ * of <= 2048 entries, node ids < 2048, at most 1024 state rows under the keys, every
+ * delta key in `keys` (the sync and mutation shape) -- else DG_HOME_FALLBACK with the
+ * state, its context and the tree untouched.  Rows move (a key's row count changed) ->
+ * the joined state is in `spare` and the structs are exchanged (*swapped = 1), as
+ * dg_join_delta.  Synchronous. */
+#define DG_HOME_FALLBACK 1
+#define DG_HOME_KEYS 8
+#define DG_HOME_STRIDE 1536
+#define DG_HOME_ROWS (DG_HOME_KEYS + 512)
+#define DG_HOME_NODES 2048
+#define DG_HOME_CTX (DG_HOME_ROWS + 4 * DG_HOME_STRIDE + DG_HOME_STRIDE / 2)
+#define DG_HOME_WORDS (DG_HOME_CTX + DG_HOME_NODES + DG_HOME_NODES / 2)
+int dg_join_delta_home(dg_engine* e, dg_store* state, dg_context* state_ctx, const dg_store* delta,
+                       const dg_context* delta_ctx, const uint64_t* keys, uint64_t n_keys,
+                       dg_store* spare, dg_merkle* tree, uint64_t* home, int* swapped);
 
 /* Fold of join/3 over k stores (how CausalCrdt applies k deltas in a row,
  * causal_crdt.ex:86-89,383-384): out = join(...join(join(s0, s1), s2)..., s_{k-1})
@@ -395,7 +424,11 @@ int dg_merkle_update(dg_engine* e, dg_merkle* t, const dg_store* old_s, const dg
  * the rows of differing buckets are read (located by the trees' row counts).  The first
  * min(total, cap) keys are written to out_keys, *n_out = that number and *n_total = the
  * total: a total above cap is the reference's truncate(keys, max_sync_size)
- * (Enum.take, causal_crdt.ex:105,206-210), not an error.  Trees: same depth and shard. */
+ * (Enum.take, causal_crdt.ex:105,206-210), not an error.  Trees: same depth and shard.
+ * Each store must be the one its tree was built / updated against: where a tree counts
+ * more rows than its store holds, nothing is read past the store and DG_E_INVAL is
+ * returned (the async form's total is then >= DG_DIFF_MISMATCH). */
+#define DG_DIFF_MISMATCH (1ull << 44)
 int dg_merkle_diff(dg_engine* e, const dg_merkle* a, const dg_store* sa, const dg_merkle* b,
                    const dg_store* sb, uint64_t* out_keys, uint64_t cap, uint64_t* n_out,
                    uint64_t* n_total);

@@ -34,22 +34,34 @@ def up(rep):
     return Store.from_numpy(*rows, device=DEV), Context.from_numpy(ctx[0], ctx[1], ctx[2], DEV)
 
 
-def apply(engine, a, d, keys, depth=10, terms=None, with_tree=True):
+def apply(engine, a, d, keys, depth=10, terms=None, with_tree=True, home=False):
+    """home: through dg_join_delta_home (the fused small-delta path, one host wait), which
+    must take the delta (no DG_HOME_FALLBACK) and give what dg_join_delta_rows gives."""
     keys = np.unique(np.asarray(keys, np.uint64))
     st, sc = state_of(a, extra_ctx=len(d["ctx"][1]))
     sd, cd = up(d)
     spare = Store.empty(st.n + sd.n, DEV)
     tree = engine.merkle_build(st, depth, MerkleTree.empty(depth, DEV, terms=terms)) if with_tree else None
-    # (dg_join_delta_rows: the changed keys' joined rows come back too, taken from the
-    # join's edit of the keyset on the in-place and moved paths)
-    rows = Store.empty(st.n + sd.n, DEV)
-    changed, swapped = engine.join_delta(st, sc, sd, cd, kdev(keys), spare, tree, rows=rows)
     wr, wc = R.join2(a["rows"], a["ctx"], d["rows"], d["ctx"], keys=keys)
+    wch = R.changed_keys(a["rows"], wr, keys)
+    if home:
+        got = engine.join_delta_home(st, sc, sd, cd, kdev(keys), spare, tree)
+        assert got is not None, "the small path declined"
+        changed, hrows, hctx, swapped = got
+        assert np.array_equal(changed, wch)
+        want_rows = tuple(c[np.isin(wr[0], wch)] for c in wr)
+        for x, y in zip(hrows, want_rows):
+            assert np.array_equal(x, y)
+        assert np.array_equal(hctx[0], wc[1]) and np.array_equal(hctx[1], wc[2])
+    else:
+        # (dg_join_delta_rows: the changed keys' joined rows come back too, taken from the
+        # join's edit of the keyset on the in-place and moved paths)
+        rows = Store.empty(st.n + sd.n, DEV)
+        changed, swapped = engine.join_delta(st, sc, sd, cd, kdev(keys), spare, tree, rows=rows)
+        assert np.array_equal(u64(changed), wch)
+        rows_eq(rows, tuple(c[np.isin(wr[0], wch)] for c in wr))
     rows_eq(st, wr)
     ctx_eq(sc, wc)
-    wch = R.changed_keys(a["rows"], wr, keys)
-    assert np.array_equal(u64(changed), wch)
-    rows_eq(rows, tuple(c[np.isin(wr[0], wch)] for c in wr))
     if with_tree:
         fresh = engine.merkle_build(st, depth, MerkleTree.empty(depth, DEV, terms=terms))
         assert np.array_equal(tree.nodes.cpu().numpy(), fresh.nodes.cpu().numpy())
@@ -160,9 +172,10 @@ def _mutation_state(n_keys=20_000, seed=31):
     return a, rng
 
 
+@pytest.mark.parametrize("home", [False, True])
 @pytest.mark.parametrize("case", ["update", "new_key", "remove", "remove_absent", "nil_value",
                                   "same_value"])
-def test_one_key_mutation_delta(engine, case):
+def test_one_key_mutation_delta(engine, case, home):
     """A one-key add/remove delta with a dot-set context into a VV state: rows, context,
     changed keys and the tree against the C oracle and a fresh build.  `update` keeps the
     key's row count (in place when the key held one row), `new_key` and `remove` move rows
@@ -191,7 +204,7 @@ def test_one_key_mutation_delta(engine, case):
         ops = [("remove", int(keys[200]) + 1, 0, 0)]
     drows, dctx, dkeys = R.mutate_batch(a["rows"], a["ctx"], node, ops)
     d = {"rows": drows, "ctx": dctx}
-    st, sc, swapped, wr = apply(engine, a, d, dkeys, depth=12)
+    st, sc, swapped, wr = apply(engine, a, d, dkeys, depth=12, home=home)
     assert swapped == (case in ("new_key", "remove"))
     assert sc.kind == 0  # map ⊔ MapSet folds the dots into the VV (aw_lww_map.ex:45-52)
 
@@ -348,3 +361,89 @@ def test_join_delta_retries_an_aborted_grid(monkeypatch):
     assert len(c0) > 200_000 and np.array_equal(c0, c1) and t0 == t1
     for x, y in zip(r0, r1):
         assert np.array_equal(x, y)
+
+
+# ---------------------------------------------------------------- dg_join_delta_home
+# The fused small-delta path (csrc/small.hip): one launch chain, one host wait, the
+# result in page-locked memory -- what the NIF's join_delta / mutate_batch use for
+# mutations and small sync deltas (c_src/replica.c).
+
+@pytest.mark.parametrize("n_keys", [30_000, 300_000])
+def test_mutation_sequence_home(engine, n_keys):
+    """200 one-key mutations through dg_join_delta_home on one resident state + tree
+    (30k rows: the moved-rows copy is enqueued behind the join; 300k: after the wait),
+    against the oracle's fold, step by step."""
+    a, rng = _mutation_state(n_keys=n_keys, seed=33)
+    st, sc = state_of(a, extra_ctx=4)
+    spare = Store.empty(st.n + 300, DEV)
+    tree = engine.merkle_build(st, 14)
+    rows, ctx = a["rows"], a["ctx"]
+    node = int(ctx[1][1])
+    keys = np.unique(rows[0])
+    moved = 0
+    for i in range(200):
+        r = rng.random()
+        if r < 0.4:
+            op = ("add", int(rng.choice(keys)), int(rng.integers(1 << 40)), 10 ** 12 + i)
+        elif r < 0.7:
+            op = ("add", int(rng.integers(1 << 63)) | 1, int(rng.integers(1 << 40)), 10 ** 12 + i)
+        else:
+            op = ("remove", int(rng.choice(keys)), 0, 0)
+        drows, dctx, dkeys = R.mutate_batch(rows, ctx, node, [op])
+        sd, cd = up({"rows": drows, "ctx": dctx})
+        if spare.cap < st.n + sd.n:  # (after a swap the spare is the old state's buffer)
+            spare = Store.empty(st.n + sd.n + 64, DEV)
+        got = engine.join_delta_home(st, sc, sd, cd, kdev(dkeys), spare, tree)
+        assert got is not None
+        changed, hrows, hctx, swapped = got
+        moved += swapped
+        wr, wc = R.join2(rows, ctx, drows, dctx, keys=dkeys)
+        wch = R.changed_keys(rows, wr, dkeys)
+        assert np.array_equal(changed, wch)
+        for x, y in zip(hrows, tuple(c[np.isin(wr[0], wch)] for c in wr)):
+            assert np.array_equal(x, y)
+        assert np.array_equal(hctx[0], wc[1]) and np.array_equal(hctx[1], wc[2])
+        rows, ctx = wr, wc
+    assert moved > 20
+    rows_eq(st, rows)
+    ctx_eq(sc, ctx)
+    fresh = engine.merkle_build(st, 14)
+    assert np.array_equal(tree.nodes.cpu().numpy(), fresh.nodes.cpu().numpy())
+    assert np.array_equal(tree.bucket_counts(), fresh.bucket_counts())
+    assert np.array_equal(tree.starts.cpu().numpy(), fresh.starts.cpu().numpy())
+    assert tree.n_keys == fresh.n_keys
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_small_sync_deltas_home(engine, seed):
+    """Sync deltas of a few hundred keys: with moves (random replicas, VV or dot-set
+    contexts) and in place over node terms (config-4 shaped)."""
+    rng = np.random.default_rng(40 + seed)
+    a, b = W.random_pair(rng, 20_000, n_nodes=5, ts_range=1 << 10, dense_ctx=bool(seed))
+    kb = np.unique(np.concatenate([a["rows"][0], b["rows"][0]]))
+    keys = np.sort(rng.choice(kb, 120, replace=False))  # (<= 512 delta rows)
+    d = W.sync_delta(b, keys)
+    assert len(d["rows"][0]) <= 512
+    apply(engine, a, d, keys, home=True)
+    a, b = W.config4_shard(seed, 8, keys_per_rank=30_000, diff_frac=0.01)
+    want = R.store_diff(a["rows"], b["rows"])
+    assert 0 < len(want) <= 512
+    terms = TermHashes(*a["nodes"].universe.term_tables(), DEV)
+    _, _, swapped, _ = apply(engine, a, W.sync_delta(b, want), want, depth=13, terms=terms, home=True)
+    assert not swapped
+
+
+def test_home_declines_and_leaves_the_state(engine):
+    """A delta with a key outside the keyset (the right-biased carry: the general path),
+    or more keys than the small path takes: DG_HOME_FALLBACK, nothing touched."""
+    rng = np.random.default_rng(5)
+    a, b = W.random_pair(rng, 8_000, n_nodes=3)
+    kb = np.unique(b["rows"][0])
+    st, sc = state_of(a, extra_ctx=8)
+    tree = engine.merkle_build(st, 11)
+    snap = _snapshot(st, sc, tree)
+    for keys, dkeys in ((kb[:20], kb[:22]), (kb[:600], kb[:600])):
+        sd, cd = up(W.sync_delta(b, dkeys))
+        spare = Store.empty(st.n + sd.n, DEV)
+        assert engine.join_delta_home(st, sc, sd, cd, kdev(keys), spare, tree) is None
+        _assert_unchanged(st, sc, tree, snap)

@@ -416,7 +416,9 @@ def test_diff_against_a_store_the_index_does_not_describe(engine):
     """a tree's chunk index describes the store it was built / updated against.
     Handed another store -- here one whose row count changed without dg_merkle_update --
     the diff must not trust it (it would read past the store or return wrong keys): it
-    searches the store instead, exactly as a tree without an index does."""
+    searches the store instead, exactly as a tree without an index does.  Where the tree
+    counts more rows than the store holds, nothing is read past the store and the diff is
+    an input error (DG_DIFF_MISMATCH), with or without the index."""
     rng = np.random.default_rng(23)
     a, b = W.random_pair(rng, 50_000, n_nodes=4, max_entries=3)
     sa, ca = up(a)
@@ -426,18 +428,30 @@ def test_diff_against_a_store_the_index_does_not_describe(engine):
     for cut in (a["rows"][0].size // 2, 10):  # fewer rows than the index says
         short = Store.from_numpy(*(c[:cut] for c in a["rows"]), device=DEV)
         ta.store = short
-        got = u64(engine.merkle_diff(ta, tb))
+        with pytest.raises(DeltaGpuError, match="more rows than its store"):
+            engine.merkle_diff(ta, tb)
         ta.starts, kept = None, ta.starts
-        want = u64(engine.merkle_diff(ta, tb))
+        with pytest.raises(DeltaGpuError, match="more rows than its store"):
+            engine.merkle_diff(ta, tb)
         ta.starts = kept
-        assert np.array_equal(got, want)
-        assert np.all(got[1:] > got[:-1])
-    # more rows than the index says (a join's output under a tree of the old state)
+    # the engine is usable after the error: the matching pair diffs as the oracle says
+    ta.store = sa
+    assert np.array_equal(u64(engine.merkle_diff(ta, tb)), R.store_diff(a["rows"], b["rows"]))
+    # a join's output under a tree of the old state (here it holds fewer rows: the join drops
+    # the dots the other context covers); with and without the index the diff agrees
     out, _ = engine.join2(sa, ca, sb, cb)
-    assert out.n > sa.n
+    assert out.n != sa.n
     ta.store = out
-    got = u64(engine.merkle_diff(ta, tb))
+
+    def outcome():  # the keys, or the input error where a subtree overruns the store
+        try:
+            return u64(engine.merkle_diff(ta, tb)).tolist()
+        except DeltaGpuError as ex:
+            assert "more rows than its store" in str(ex)
+            return "mismatch"
+
+    got = outcome()
     ta.starts, kept = None, ta.starts
-    assert np.array_equal(got, u64(engine.merkle_diff(ta, tb)))
+    assert got == outcome()
     ta.starts, ta.store = kept, sa
     assert np.array_equal(u64(engine.merkle_diff(ta, tb)), R.store_diff(a["rows"], b["rows"]))
