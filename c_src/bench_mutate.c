@@ -27,13 +27,16 @@
  * Built twice from this file: bench_mutate (the GPU path, links libdeltagpu) and, with
  * -DDG_REF, bench_mutate_ref (the CPU restatement's keyed join per op, oracle/deltaref.c
  * ref_join2 on host rows -- bench.py's cpu_baseline leg only).  Prints one JSON line.
- *     bench_mutate N_KEYS [REPS]
+ *     bench_mutate N_KEYS [REPS [ops]]   ("ops": the single-op sections only)
  */
 #define _POSIX_C_SOURCE 200809L
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#ifndef DG_REF
+#include <dlfcn.h>
+#endif
 
 #include "marshal.h"
 #ifndef DG_REF
@@ -315,6 +318,7 @@ static void cpu_apply(cpu* c, const uint64_t* key, const uint64_t* val, const in
 int main(int argc, char** argv) {
   const int64_t n = argc > 1 ? atoll(argv[1]) : 1000;
   const int reps = argc > 2 ? atoi(argv[2]) : 200;
+  const int ops_only = argc > 3 && !strcmp(argv[3], "ops");  /* no batch sections (profiling) */
   hrows r;
   hrows_init(&r, (uint64_t)n + 16384);
   setup_rows(&r, n);
@@ -351,6 +355,15 @@ int main(int argc, char** argv) {
   } while (0)
 
   double scratch[3];
+#ifndef DG_REF
+  /* a DG_SMALL_STAMPS library build (tools/small_stamps.sh): the small join's phase stamps
+   * after every timed op, their medians printed per op (diagnostic; perturbs the timing) */
+  typedef int (*stamps_fn)(unsigned long long*, size_t);
+  stamps_fn stamps = (stamps_fn)dlsym(dlopen(NULL, RTLD_NOW), "dg_debug_small_stamps");
+  double* sph[N_OPS][16];
+  for (int o = 0; o < N_OPS; o++)
+    for (int k = 0; k < 16; k++) sph[o][k] = calloc((size_t)reps, sizeof(double));
+#endif
   for (int it = -5; it < reps; it++) {
     for (int o = 0; o < N_OPS; o++) {
       /* before_each: add [10, 10], remove ["key4"] */
@@ -377,6 +390,15 @@ int main(int argc, char** argv) {
       if (it >= 0) {
         tot[o][it] = el;
         for (int p = 0; p < 3; p++) ts[o][p][it] = t3[p];
+#ifndef DG_REF
+        if (stamps && o != OP_READ) {
+          unsigned long long st[16];
+          memset(st, 0, sizeof st);
+          stamps(st, 16);
+          for (int k = 1; k < 16; k++) /* phase k: from the previous nonzero stamp, us */
+            sph[o][k][it] = (st[k] && st[0] && st[k] >= st[0]) ? (double)(st[k] - st[0]) * 0.01 : -1.0;
+        }
+#endif
       }
     }
   }
@@ -388,7 +410,7 @@ int main(int argc, char** argv) {
   uint32_t* bn = calloc(nb, 4);
   double bt_us[16];
   int n_batch = 0;
-  for (int rep = 0; rep < 6; rep++) {
+  for (int rep = 0; rep < (ops_only ? 0 : 6); rep++) {
     for (int i = 0; i < nb; i++) {
       char s[32];
       snprintf(s, sizeof s, "key%d_%d", i, rep);
@@ -413,7 +435,7 @@ int main(int argc, char** argv) {
   int n_dmb = 0;
 #ifndef DG_REF
   /* the same workload with the delta built on the device (the NIF's mutate_batch) */
-  for (int rep = 0; rep < 6; rep++) {
+  for (int rep = 0; rep < (ops_only ? 0 : 6); rep++) {
     for (int i = 0; i < nb; i++) {
       char s[32];
       snprintf(s, sizeof s, "mkey%d_%d", i, rep);
@@ -449,6 +471,15 @@ int main(int argc, char** argv) {
   }
   printf("}\n");
 #ifndef DG_REF
+  if (stamps)
+    for (int o = 1; o < N_OPS; o++) {
+      printf("stamps %-6s (us from kernel start):", OP_NAMES[o]);
+      for (int k = 1; k < 16; k++) {
+        const double m = median(sph[o][k], reps);
+        if (m >= 0) printf(" %d:%.2f", k, m);
+      }
+      printf("\n");
+    }
   dgr_state_free(g.s);
   dgr_engine_close(g.g);
 #endif

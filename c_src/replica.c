@@ -207,6 +207,23 @@ static int ctx_sorted(const dg_context* c) {
   return 1;
 }
 
+/* the host (page-locked, mapped) side of a device view into the message buffer: the small
+ * join reads a small delta straight from there, with no copy launch */
+static void* on_host(const dgr_engine* g, const void* d) {
+  return (char*)g->h_msg + ((const char*)d - (const char*)g->d_msg);
+}
+
+static dg_store host_rows(const dgr_engine* g, const dg_store* d) {
+  dg_store v = {(uint64_t*)on_host(g, d->key), (uint64_t*)on_host(g, d->val), (int64_t*)on_host(g, d->ts),
+                (uint32_t*)on_host(g, d->node), (uint64_t*)on_host(g, d->cnt), d->n, d->cap};
+  return v;
+}
+
+static dg_context host_ctx(const dgr_engine* g, const dg_context* d) {
+  dg_context v = {d->kind, 0, (uint32_t*)on_host(g, d->node), (uint64_t*)on_host(g, d->cnt), d->n, d->cap};
+  return v;
+}
+
 static uint64_t rows_words(uint64_t n) { return 4 * even(n) + even((n + 1) / 2); }
 static uint64_t ctx_words(uint64_t n) { return even(n) + even((n + 1) / 2); }
 
@@ -432,11 +449,15 @@ static int room_for(dgr_state* s, uint64_t rows, uint64_t dn) {
 /* A small delta (a local mutation, a small sync delta): dg_join_delta_home does the whole
  * update_state_with_delta in one launch chain and writes the result into page-locked
  * memory with ONE wait.  *done = 0: not small after all (nothing happened). */
+static int small_fits(const dgr_state* s, const dg_store* drows, const dg_context* dctx, uint64_t n_keys) {
+  return n_keys <= 512 && drows->n <= 512 && dctx->n <= 1024 && s->ctx.kind == DG_CTX_VV;
+}
+
 static int apply_small(dgr_state* s, const dg_store* drows, const dg_context* dctx, const uint64_t* dkeys,
                        uint64_t n_keys, dgr_changed* out, int* done) {
   dgr_engine* g = s->g;
   *done = 0;
-  if (n_keys > 512 || drows->n > 512 || dctx->n > 1024 || s->ctx.kind != DG_CTX_VV) return DG_OK;
+  if (!small_fits(s, drows, dctx, n_keys)) return DG_OK;
   if (!g->h_home) TRY(dg_host_alloc(g->e, DG_HOME_WORDS * 8, (void**)&g->h_home));
   int swapped = 0;
   const int rc = dg_join_delta_home(g->e, &s->rows, &s->ctx, drows, dctx, dkeys, n_keys, &s->spare,
@@ -463,14 +484,16 @@ static int apply_small(dgr_state* s, const dg_store* drows, const dg_context* dc
 }
 
 /* The join of a delta on the device (rows and context sorted, keys ascending unique) into
- * the state, and the result brought home with one wait. */
+ * the state, and the result brought home with one wait.  try_small: the small join first. */
 static int apply_delta(dgr_state* s, const dg_store* drows, const dg_context* dctx, const uint64_t* dkeys,
-                       uint64_t n_keys, dgr_changed* out) {
+                       uint64_t n_keys, dgr_changed* out, int try_small) {
   dgr_engine* g = s->g;
   TRY(room_for(s, drows->n, dctx->n));
-  int done = 0;
-  TRY(apply_small(s, drows, dctx, dkeys, n_keys, out, &done));
-  if (done) return DG_OK;
+  if (try_small) {
+    int done = 0;
+    TRY(apply_small(s, drows, dctx, dkeys, n_keys, out, &done));
+    if (done) return DG_OK;
+  }
   uint64_t S = umax(n_keys, 1);
   TRY(grow_back(g, S, s->ctx.n + dctx->n));
   S = g->back_s;
@@ -532,6 +555,18 @@ int dgr_join_delta(dgr_state* s, uint64_t version, const dg_store* delta, const 
   o = pack_ctx(g, o, delta_ctx, &cv);
   const uint64_t nk = sort_unique(keys, n_keys, g->h_msg + o);
   const uint64_t* dk = g->d_msg + o;
+  if (rows_sorted(delta) && ctx_sorted(delta_ctx) && small_fits(s, delta, delta_ctx, nk)) {
+    /* a mutation or a small sync delta: the small join reads the message where the host
+     * packed it (mapped memory) -- no copy launch; declined, the general path copies it */
+    const dg_store hr = host_rows(g, &rv);
+    const dg_context hc = host_ctx(g, &cv);
+    TRY(room_for(s, delta->n, delta_ctx->n));
+    int done = 0;
+    TRY(apply_small(s, &hr, &hc, g->h_msg + o, nk, out, &done));
+    if (done) return DG_OK;
+    TRY(dg_copy_async(g->e, g->d_msg, g->h_msg, (o + nk) * 8));
+    return apply_delta(s, &rv, &cv, dk, nk, out, 0);
+  }
   TRY(dg_copy_async(g->e, g->d_msg, g->h_msg, (o + nk) * 8));
   const dg_store* dr = &rv;
   const dg_context* dc = &cv;
@@ -545,7 +580,7 @@ int dgr_join_delta(dgr_state* s, uint64_t version, const dg_store* delta, const 
     TRY(dg_sort_context(g->e, &cv, &g->dctx));
     dc = &g->dctx;
   }
-  return apply_delta(s, dr, dc, dk, nk, out);
+  return apply_delta(s, dr, dc, dk, nk, out, 1);
 }
 
 typedef struct {
@@ -616,7 +651,7 @@ int dgr_mutate_batch(dgr_state* s, uint64_t version, uint32_t node, uint64_t m, 
     TRY(rc);
     break;
   }
-  return apply_delta(s, &g->mrows, &g->mctx, g->mkeys, n_keys, out);
+  return apply_delta(s, &g->mrows, &g->mctx, g->mkeys, n_keys, out, 1);
 }
 
 int dgr_read(dgr_state* s, uint64_t version, int all, const uint64_t* keys, uint64_t n_keys,

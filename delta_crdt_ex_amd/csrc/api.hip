@@ -44,13 +44,9 @@ struct dg_engine {
   // splice through `spl`)
   void* ubuf = nullptr;
   size_t ubuf_cap = 0;
-  // dg_join_delta_home's scratch: the edit, the per-key index, the result block; and its
-  // tree-update scratch, whose dirty flags and chunk deltas stay zero between calls
+  // dg_join_delta_home's scratch: the edit, the per-key index, the result header
   void* sml = nullptr;
   size_t sml_cap = 0;
-  void* tscr = nullptr;
-  size_t tscr_cap = 0;
-  u64 tscr_chunks = 0;  // the chunk capacity tscr is laid out for
   // the full diff's per-group key sums: two buffers of diff_bsum_cap words, zero when
   // allocated; a call adds into one and its write kernel zeroes the other, which the
   // previous call used (no memset launch per diff)
@@ -267,15 +263,9 @@ __global__ void publish_counts_kernel(const u64* d, u64* h, u64 seq) {
 // D2H copy and a stream synchronize (≈ 14 µs on top of a config-2 join), a one-wave kernel
 // publishes them into mapped host memory and the host polls its sequence word; past 20 ms
 // (a long call) the runtime's synchronize takes over, and it is what reports a fault.
-// (small_res / small_home: dg_join_delta_home's result block goes home in the same kernel)
-int sync_words(dg_engine* e, const u64* small_res = nullptr, u64* small_home = nullptr) {
-  const u64 seq = ++e->pub_seq;
-  if (small_home)
-    HIP_TRY(launch_small_home_publish(small_res, small_home, e->d_counts, e->d_pub, seq, e->stream));
-  else
-    hipLaunchKernelGGL(publish_counts_kernel, dim3(1), dim3(WAVE), 0, e->stream, e->d_counts,
-                       e->d_pub, seq);
-  HIP_TRY(hipGetLastError());
+// wait_published: the host side alone, for a launch that publishes `seq` itself (the
+// small join's tail kernel).
+int wait_published(dg_engine* e, u64 seq) {
   const volatile u64* flag = e->h_pub + 16;
   const auto t0 = std::chrono::steady_clock::now();
   bool seen = false;
@@ -297,12 +287,20 @@ int sync_words(dg_engine* e, const u64* small_res = nullptr, u64* small_home = n
   return DG_OK;
 }
 
+int sync_words(dg_engine* e) {
+  const u64 seq = ++e->pub_seq;
+  hipLaunchKernelGGL(publish_counts_kernel, dim3(1), dim3(WAVE), 0, e->stream, e->d_counts, e->d_pub, seq);
+  HIP_TRY(hipGetLastError());
+  return wait_published(e, seq);
+}
+
 // ticket word: the Merkle kernels' arrival counter.  It is reset by the last workgroup of
 // every build / update launch, not per launch.  A launch either runs every workgroup to
 // that reset (the kernels never wait on another workgroup before arriving) or does not
 // start at all (a launch error); a kernel that faults leaves the device unusable anyway.
 // read_counts also zeroes it whenever a call reports error bits.
 constexpr int MERKLE_ARRIVE = 6;
+constexpr int TAIL_ARRIVE = 7;  // dg_join_delta_home's tail kernel: every workgroup arrives
 
 int read_counts(dg_engine* e, int n) {
   (void)n;
@@ -314,7 +312,7 @@ int read_counts(dg_engine* e, int n) {
   if (err) {
     e->last_err_bits = err;
     HIP_TRY(hipMemsetAsync(e->ticket, 0, 4 * sizeof(u32), e->stream));
-    HIP_TRY(hipMemsetAsync(e->ticket + MERKLE_ARRIVE, 0, sizeof(u32), e->stream));
+    HIP_TRY(hipMemsetAsync(e->ticket + MERKLE_ARRIVE, 0, 2 * sizeof(u32), e->stream));  // and TAIL_ARRIVE
     HIP_TRY(hipStreamSynchronize(e->stream));
     return fail(DG_E_DEVICE, "a kernel timed out or a join grid aborted (error bits 0x%x)", err);
   }
@@ -759,7 +757,6 @@ int dg_engine_destroy(dg_engine* e) {
   if (e->spl) hipFree(e->spl);
   if (e->ubuf) hipFree(e->ubuf);
   if (e->sml) hipFree(e->sml);
-  if (e->tscr) hipFree(e->tscr);
   if (e->diff_bsum) hipFree(e->diff_bsum);
   if (e->h_stage) hipHostFree(e->h_stage);
   if (e->own_stream && e->stream) hipStreamDestroy(e->stream);
@@ -1044,7 +1041,8 @@ static int join_delta_impl(dg_engine* e, dg_store* state, dg_context* state_ctx,
 }
 
 // dg_join_delta_home: the fused small-delta join (small.hip) with ONE host wait.  States
-// of up to SMALL_COPY_TILES splice tiles get the moved-rows copy enqueued behind the join,
+// of up to SMALL_COPY_TILES splice tiles get the moved-rows copy in the tail launch behind
+// the join (merkle.hip small_tail_kernel: with the tree's upsweep and the publish),
 // guarded by its `moved` word; a larger state whose rows moved copies after the wait.
 constexpr u64 SMALL_COPY_TILES = 64;
 static_assert(DIFF_MISMATCH == DG_DIFF_MISMATCH, "deltagpu.h and the diff kernels agree");
@@ -1111,35 +1109,33 @@ int dg_join_delta_home(dg_engine* e, dg_store* state, dg_context* state_ctx, con
   p.a_off = a_off;
   p.res = res;
   p.has_tree = tree != nullptr;
-  u32* dirty = nullptr;
-  i64* cdelta = nullptr;
-  u64* hand = nullptr;
-  if (tree) {
-    // the tree update's scratch: dirty flags | per-chunk row-count changes | hand-off words,
-    // an engine buffer of its own whose first two parts stay zero between calls (the upsweep
-    // zeroes what it read), so no zeroing launch.  Their offsets are fixed by the chunk
-    // capacity the buffer was laid out for, never by this tree's depth: a deeper tree's
-    // hand-off words must not land where a shallower one expects zeros.
-    const u64 chunks = merkle_chunks(tree->depth);
-    if (chunks > e->tscr_chunks) {
-      const u64 cap = chunks < 64 ? 64 : chunks;
-      const size_t tb = (cap + 2 * cap + 4 * cap) * sizeof(u32);  // hand: merkle_ctr_words
-      TRY(ensure_buf(e, &e->tscr, &e->tscr_cap, tb));
-      HIP_TRY(hipMemsetAsync(e->tscr, 0, e->tscr_cap, e->stream));
-      e->tscr_chunks = cap;
-    }
-    const u64 cap = e->tscr_chunks;  // dirty: cap u32 (even) | cdelta: cap i64 | hand: 4 cap u32
-    dirty = (u32*)e->tscr;
-    cdelta = (i64*)(dirty + cap);
-    hand = (u64*)(cdelta + cap);
-    p.t = merkle_of(tree);
-    p.dirty = dirty;
-    p.cdelta = cdelta;
-  }
+  if (tree) p.t = merkle_of(tree);  // MerkleMap.put/delete + update_hashes: in the join
+  p.splice_here = copy_now;
+  p.sp = rows_out_of(spare);
+  p.end = end;
+  p.shift = shift;
+  p.home = home;
+  p.d_counts = e->d_counts;
+  p.h_pub = e->d_pub;
+  p.seq = ++e->pub_seq;
   HIP_TRY(launch_small_delta(p, e->stream));
-  if (tree)  // MerkleMap.update_hashes: the dirty chunks and the levels above them
-    HIP_TRY(launch_merkle_upsweep(merkle_of(tree), rows_of(state), dirty, e->ticket + MERKLE_ARRIVE,
-                                  hand, cdelta, e->ticket + 3, e->stream));
+  if (copy_now) {  // the moved rows' copy into the spare (if they moved: else it returns)
+    SmallTailArgs ta{};
+    ta.a = rows_of(state);
+    ta.out = rows_out_of(spare);
+    ta.end = end;
+    ta.a_lo = a_lo;
+    ta.shift = shift;
+    ta.nk = nk;
+    ta.tiles = a_tiles;
+    ta.res = res;
+    ta.d_counts = e->d_counts;
+    ta.h_pub = e->d_pub;
+    ta.seq = p.seq;
+    ta.arrive_all = e->ticket + TAIL_ARRIVE;
+    HIP_TRY(launch_small_tail(ta, e->stream));
+  }
+  TRY(wait_published(e, p.seq));  // the one wait (the result block is in `home` by then)
   SpliceArgs sp{};
   sp.a = rows_of(state);
   sp.keys = keys;
@@ -1156,11 +1152,6 @@ int dg_join_delta_home(dg_engine* e, dg_store* state, dg_context* state_ctx, con
   sp.d_ne = res + 4;
   sp.out = rows_out_of(spare);
   sp.run_if = res + 6;  // the rows moved (0 also when the join fell back or failed)
-  if (copy_now) {
-    HIP_TRY(launch_splice_index(sp, e->stream));
-    HIP_TRY(launch_splice_copy(sp, false, e->stream));
-  }
-  TRY(sync_words(e, res, home));  // the one wait (the result block lands in `home` with it)
   const u64 flags = home[0];
   if (flags & SMALL_FALLBACK) return DG_OK;  // nothing written: the general path
   if (flags & MERKLE_INPUT_ERR) {

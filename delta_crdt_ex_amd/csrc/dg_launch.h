@@ -297,10 +297,6 @@ hipError_t launch_merkle_build(const Rows& s, const MerkleT& t, u64* d_keys, u32
 hipError_t launch_merkle_update(const MerkleT& t, const Rows& olds, const Rows& news, const u64* keys,
                                 u64 n_keys, u32* dirty, u64* d_keys, u32* arrive, u64* hand, i64* cdelta,
                                 u32* err, hipStream_t st);
-// the chunk kernel of an update alone: the dirty chunks re-reduced, the top levels, the
-// chunk index moved by cdelta (the fused small join set the bucket level, dirty, cdelta)
-hipError_t launch_merkle_upsweep(const MerkleT& t, const Rows& news, u32* dirty, u32* arrive, u64* hand,
-                                 i64* cdelta, u32* err, hipStream_t st);
 // ---- small.hip: dg_join_delta of a small delta, one launch (see the file header)
 constexpr u32 SMALL_KEYS = 512, SMALL_DELTA = 512, SMALL_DCTX = 1024, SMALL_NODES = 2048;
 constexpr u32 SMALL_TAKEN = 1024, SMALL_EDIT = 1536;
@@ -318,11 +314,19 @@ struct SmallArgs {
   RowsOut e;           // scratch: the edit (SMALL_EDIT rows), the splice layout
   u64* a_lo;           // scratch: nk, the keys' first state rows
   u64* a_off;          // scratch: nk + 1, their offsets among the taken rows
-  MerkleT t;           // the tree (has_tree)
+  MerkleT t;           // the tree (has_tree): nodes, counts and chunk index updated here
   int has_tree;
-  u32* dirty;          // zero on entry
-  i64* cdelta;         // zero on entry (t.starts kept)
-  u64* res;            // result block (small_res_words())
+  u64* res;            // the result block's header (device)
+  u64* home;           // the whole result block (host memory the device writes)
+  const u64* d_counts; // the engine's count block ...
+  u64* h_pub;          // ... published here with `seq` (dg_home.h) unless the tail kernel does
+  u64 seq;
+  // the moved-rows splice done by the tail kernel (splice_here): the edit's rows go
+  // straight to their places in `sp` and the per-key index (end, shift) is written here
+  int splice_here;
+  RowsOut sp;          // the spare store (the rows moved: the output)
+  u64* end;            // scratch: nk, each key's state rows' end
+  i64* shift;          // scratch: nk + 1, the shift of the gap before each key (and after all)
 };
 // result block words: header [0] flags [1] changed keys [2] their rows [3] context entries
 // [4] edit rows [5] taken rows [6] moved [7] distinct-key change; then the changed keys
@@ -335,11 +339,25 @@ constexpr u64 SMALL_WORDS = SMALL_O_CTX + SMALL_NODES + SMALL_NODES / 2;
 
 constexpr u32 SMALL_FALLBACK = 1u;  // flags: nothing written, the general path runs
 hipError_t launch_small_delta(const SmallArgs& p, hipStream_t st);
-// the used part of the result block into `home` (host memory the device can write), then
-// the engine's count block into the mapped publish words and the sequence number `seq`
-// (what sync_words' publish kernel does): the result is home when the host sees seq
-hipError_t launch_small_home_publish(const u64* res, u64* home, const u64* d_counts, u64* h_pub, u64 seq,
-                                     hipStream_t st);
+// small.hip: the moved rows' splice copy behind the small join, one launch: blocks
+// [0, tiles) copy the state's rows outside the keyset into the spare store (when the join
+// moved rows: res[6], res[0] == 0; the small join placed the edit's rows), and the last
+// workgroup to arrive publishes `seq` (dg_home.h) -- the small join does when no row moved.
+struct SmallTailArgs {
+  Rows a;              // the state (read)
+  RowsOut out;         // the spare store
+  const u64* end;      // per key (nk): its state rows' end
+  const u64* a_lo;     // per key: its first state row
+  const i64* shift;    // nk + 1
+  u64 nk, tiles;       // keys; splice tiles (SMALL_TILE rows each)
+  const u64* res;      // the small join's result header
+  const u64* d_counts;
+  u64* h_pub;
+  u64 seq;
+  u32* arrive_all;     // every block's arrival counter (zero, left zero)
+};
+constexpr u64 SMALL_TILE = 2048;  // rows per splice tile of the tail kernel
+hipError_t launch_small_tail(const SmallTailArgs& p, hipStream_t st);
 constexpr int DIFF_BLOCK = 256;
 #ifndef DG_DIFF_SUB
 #define DG_DIFF_SUB 12

@@ -199,10 +199,11 @@ __device__ void chunk_upsweep(u64* nodes, u32 hi, u64 g0, u64* s) {
 // ctr: the arrival counter, zero on entry and left zero (the last workgroup resets it: a
 // persistent engine word, no fill launch per build); scratch: per chunk its root and its
 // distinct-key count (u64 each, at hand[0, G) and hand[G, 2G)).
+// (the body of one workgroup g of G)
 template <bool BUILD, bool VEC = false>
-__global__ __launch_bounds__(UPB, 4) void merkle_chunk_kernel(Rows rows, MT t, const u32* dirty,
-                                                           u32* ctr, u64* hand, u64* d_keys,
-                                                           u32* err, const i64* cdelta) {
+__device__ __forceinline__ void chunk_block(Rows rows, MT t, const u32* dirty, u32* ctr, u64* hand,
+                                            u64* d_keys, u32* err, const i64* cdelta, const u64 g,
+                                            const u64 G) {
   __shared__ u64 s[UPW];
   __shared__ u32 s_c[BUILD ? UPW : 1];  // rows per bucket
   __shared__ u64 s_nh[BUILD ? NHL : 1]; // node term hashes
@@ -211,7 +212,7 @@ __global__ __launch_bounds__(UPB, 4) void merkle_chunk_kernel(Rows rows, MT t, c
   __shared__ u32 s_last;
   const u32 L1 = t.depth < (u32)UPL ? t.depth : (u32)UPL;
   const u32 width = 1u << L1;
-  const u64 g = blockIdx.x, g0 = g << L1, G = gridDim.x;
+  const u64 g0 = g << L1;
   const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
   u64* lvl = t.nodes + ((1ull << t.depth) - 1);
   u64 chunk_root = 0, chunk_keys = 0;
@@ -380,9 +381,6 @@ __global__ __launch_bounds__(UPB, 4) void merkle_chunk_kernel(Rows rows, MT t, c
     if (s_last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // all G arrived
   }
   __syncthreads();
-  // (an update's dirty flag read by every thread above: zero again for the next update,
-  // which the small-delta join relies on -- its scratch is not re-zeroed per call)
-  if (!BUILD && tid == 0) ((u32*)dirty)[g] = 0;
   if (!s_last) return;
   // ---- the last workgroup: levels depth - L1 .. 0, UPL levels per round; the first
   // round's inputs are the handed-off chunk roots (sc1 loads)
@@ -445,7 +443,6 @@ __global__ __launch_bounds__(UPB, 4) void merkle_chunk_kernel(Rows rows, MT t, c
       for (int q = 0; q < CP; q++) {
         const u64 x = x0 + q;
         if (x <= G) t.starts[x] = (u64)(st0[q] + run);
-        if (x < G && v[q]) ((i64*)cdelta)[x] = 0;  // read above: zero again for the next update
         run += v[q];
       }
       carry += tot;
@@ -465,6 +462,13 @@ __global__ __launch_bounds__(UPB, 4) void merkle_chunk_kernel(Rows rows, MT t, c
       *d_keys = tot;
     }
   }
+}
+
+template <bool BUILD, bool VEC = false>
+__global__ __launch_bounds__(UPB, 4) void merkle_chunk_kernel(Rows rows, MT t, const u32* dirty,
+                                                           u32* ctr, u64* hand, u64* d_keys,
+                                                           u32* err, const i64* cdelta) {
+  chunk_block<BUILD, VEC>(rows, t, dirty, ctr, hand, d_keys, err, cdelta, blockIdx.x, gridDim.x);
 }
 
 // ---------------------------------------------------------------- update
@@ -1211,15 +1215,6 @@ hipError_t launch_merkle_update(const MerkleT& m, const Rows& olds, const Rows& 
                        keys, n_keys, dirty, d_keys, err, cd);
   hipLaunchKernelGGL(merkle_chunk_kernel<false>, dim3((unsigned)G), dim3(UPB), 0, st, news, t, dirty,
                      arrive, hand, (u64*)nullptr, err, (const i64*)cd);
-  return hipGetLastError();
-}
-
-hipError_t launch_merkle_upsweep(const MerkleT& m, const Rows& news, u32* dirty, u32* arrive, u64* hand,
-                                 i64* cdelta, u32* err, hipStream_t st) {
-  const MT t = mt_of(m);
-  const u64 G = merkle_chunks(t.depth);
-  hipLaunchKernelGGL(merkle_chunk_kernel<false>, dim3((unsigned)G), dim3(UPB), 0, st, news, t, dirty,
-                     arrive, hand, (u64*)nullptr, err, (const i64*)(t.starts ? cdelta : nullptr));
   return hipGetLastError();
 }
 

@@ -22,17 +22,20 @@
 //   5. with a tree: per bucket (keys sorted => a bucket's keys adjacent) the leaf change
 //      Σ row_hash(new) - Σ row_hash(old) and the row-count change, checked (65535 rows
 //      per bucket, the tree's shard) BEFORE anything is written
-//   6. writes: the edit's rows in place when no key's row count changed (else the caller's
-//      guarded splice copy moves the state into its spare buffer, reading the edit and
-//      the per-key index from here), the union context, the bucket nodes, counts, dirty
-//      chunks and chunk-index deltas (the upsweep launch after this re-reduces the dirty
-//      chunks: MerkleMap.update_hashes), and the result block.
+//   6. writes: the edit's rows in place when no key's row count changed; else straight to
+//      their places in the spare store with the per-key splice index (end, shift) that the
+//      tail kernel's copy tiles search (merkle.hip small_tail_kernel: the state's other rows
+//      into the spare), or -- a state of more than SMALL_COPY_TILES tiles -- as the edit
+//      for the splice kernels after the wait; the union context, the bucket nodes, counts,
+//      dirty chunks and chunk-index deltas (the tail kernel re-reduces the dirty chunks:
+//      MerkleMap.update_hashes), and the result block.
 // Anything outside the limits sets SMALL_FALLBACK before any write: the caller then runs
 // the general path on the untouched state.
 //
 // Roofline: latency, not bandwidth -- a one-key op reads and writes a few hundred bytes;
 // what it saves is three host round trips.
 #include "dg_hash.h"
+#include "dg_home.h"
 #include "dg_launch.h"
 #include "dg_tree.h"
 
@@ -62,7 +65,10 @@ struct SmallLds {
       u32 n[SC];
     } dots;        // or its dot set, (node, cnt) ascending
   } cd;
+  u64 pb[SK], pv[2][SK];  // the changed buckets (ascending), their nodes per level (two halves)
+  int pp[SK + 1];         // their row-count changes' exclusive prefix
   u32 wave[NT / WAVE + 1];
+  u32 w4[4 * (NT / WAVE)];
   u32 flags, moved, nctx;
   int dkeys;
 };
@@ -85,6 +91,78 @@ __device__ __forceinline__ Row lds_d(const SmallLds& s, u32 i) {
   r.node = s.dn[i];
   r.cnt = s.dc[i];
   return r;
+}
+
+// Key k's first row in a[0, n) (ascending) and its run (at most SA + 1 counted), by the
+// lanes of one wave: key ids are uniform hashes, so the first round probes 64 rows around
+// the interpolated position (k / 2^64 of the way, 8 standard deviations wide); 64-ary
+// rounds narrow what is left to 64 rows (none at 10k rows, one at 10M), which one load
+// per lane settles, run included.  Two round trips at 10k rows where a thread's
+// interpolation search takes four or five.
+__device__ __forceinline__ void wave_find(const u64* a, u64 n, u64 k, u64& lo_out, u32& run_out) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  u64 lo = 0, hi = n;  // the first row >= k is in [lo, hi]
+  if (n > (u64)WAVE) {
+    const i64 g = (i64)__umul64hi(k, n);
+    const i64 st = (i64)(8.0 * 0.5 * __builtin_sqrt((double)n) / WAVE) + 1;
+    i64 qi = g + ((i64)lane - WAVE / 2) * st;
+    qi = qi < 0 ? 0 : (qi > (i64)n - 1 ? (i64)n - 1 : qi);
+    const u64 q = (u64)qi;
+    const int c = __popcll(__ballot(a[q] < k));  // a prefix of the lanes (q ascending)
+    const u64 qlo = __shfl(q, c > 0 ? c - 1 : 0, WAVE), qhi = __shfl(q, c < WAVE ? c : WAVE - 1, WAVE);
+    if (c > 0) lo = qlo + 1;
+    if (c < WAVE) hi = qhi;
+    while (hi - lo > (u64)WAVE) {
+      const u64 span = hi - lo;
+      const u64 p = lo + span * (u64)(lane + 1) / (WAVE + 1);
+      const int c2 = __popcll(__ballot(a[p] < k));
+      const u64 nlo = c2 ? lo + span * (u64)c2 / (WAVE + 1) + 1 : lo;
+      const u64 nhi = c2 < WAVE ? lo + span * (u64)(c2 + 1) / (WAVE + 1) : hi;
+      lo = nlo;
+      hi = nhi;
+    }
+  }
+  const u64 x = lo + (u64)lane;
+  const u64 v = x < n ? a[x] : 0ull;
+  const u64 first = lo + (u64)__popcll(__ballot(x < n && v < k));
+  const u64 eqm = __ballot(x < n && v == k);
+  u32 run = (u32)__popcll(eqm);
+  for (u64 e = lo + WAVE; (eqm >> (WAVE - 1)) & 1;) {  // the run goes on past the window
+    if (run > SA) break;
+    const u64 y = e + (u64)lane;
+    const u64 m = __ballot(y < n && a[y] == k);
+    run += (u32)__popcll(m);
+    if (!((m >> (WAVE - 1)) & 1)) break;
+    e += WAVE;
+  }
+  lo_out = first;
+  run_out = run;
+}
+
+// Four exclusive block scans with ONE barrier: the wave totals to LDS, every thread adds
+// up those of the waves before its own (ex: this thread's offsets, tot: the sums)
+__device__ __forceinline__ void block_scan4(const u32 (&v)[4], u32* sw, u32 (&ex)[4], u32 (&tot)[4]) {
+  constexpr int NW = NT / WAVE;
+  const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+  u32 inc[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) inc[j] = wave_incl_scan(v[j]);
+  if (lane == WAVE - 1)
+#pragma unroll
+    for (int j = 0; j < 4; j++) sw[j * NW + w] = inc[j];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    u32 below = 0, t = 0;
+#pragma unroll
+    for (int i = 0; i < NW; i++) {
+      const u32 x = sw[j * NW + i];
+      below += i < w ? x : 0u;
+      t += x;
+    }
+    ex[j] = below + inc[j] - v[j];
+    tot[j] = t;
+  }
 }
 
 // Dots.member?(delta context, dot)
@@ -172,7 +250,170 @@ __device__ __forceinline__ u32 merge_key(const SmallLds& s, u32 ia, u32 ie, u32 
   return ne;
 }
 
+// MerkleMap.update_hashes for the changed buckets only: their paths to the root.  The
+// changed buckets (head threads with a changed key, in key order = bucket order) are
+// compacted to pb / pv; at level l a node's new hash is made by the first entry below it
+// (its owner) from its children: a child that changed is its owner's value, one that did
+// not is read from the tree -- every such sibling of an entry's path is loaded up front (one
+// round trip), so the depth levels cost no memory waits.  At most 64 entries: one wave,
+// values in registers, owners found by ballots, no barrier; more: LDS and one barrier per
+// level.  Then the chunk index: every chunk after a changed one moves by the row-count
+// changes before it (dg_merkle.starts).
+#ifdef DG_SMALL_STAMPS
+// Diagnostic build only (DG_VARIANT=-DDG_SMALL_STAMPS): thread 0's phase timestamps
+// (s_memrealtime, 100 MHz) of the last small join, read with dg_debug_small_stamps
+__device__ u64 g_sm_stamps[16];
+#define SSTAMP(k)                                                            \
+  do {                                                                       \
+    if (threadIdx.x == 0) g_sm_stamps[k] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define SSTAMP(k) \
+  do {            \
+  } while (0)
+#endif
+constexpr int TMAXD = 28;  // the deepest tree (api.hip check_merkle)
+__device__ __forceinline__ void tree_paths(const SmallArgs& p, SmallLds& s, bool dirty, u64 v0, int drows,
+                                           bool moved) {
+  const int tid = threadIdx.x;
+  const MerkleT& t = p.t;
+  const u32 depth = t.depth;
+  u64* nodes = t.nodes;
+  __syncthreads();  // (s.wave)
+  u32 m, dtot;
+  const u32 i = block_excl_scan<NT>(dirty ? 1u : 0u, s.wave, &m);
+  __syncthreads();
+  const u32 pre = block_excl_scan<NT>(dirty ? (u32)drows : 0u, s.wave, &dtot);
+  if (dirty) {
+    s.pb[i] = bucket_of_t(t, s.key[tid]);
+    s.pv[0][i] = v0;
+    s.pp[i] = (int)pre;
+  }
+  if (tid == 0) s.pp[m] = (int)dtot;
+  __syncthreads();
+  SSTAMP(6);
+  if (m == 0) return;  // (uniform)
+  auto node_at = [&](u32 level, u64 n) { return nodes + ((1ull << level) - 1) + n; };
+  // the sibling of bucket b's ancestor l levels up (node 0 past the root): every lane
+  // loads every level unconditionally, so all the loads are in flight together (a load
+  // under a divergent condition is waited for where the condition ends)
+  auto sib_at = [&](u32 dep, u64 b, int l) -> u64 {
+    return (u32)l < dep ? ((1ull << (dep - l)) - 1) + ((b >> l) ^ 1ull) : 0ull;
+  };
+  if (m <= (u32)WAVE) {
+    if (tid < WAVE) {
+      const int lane = tid;
+      const bool valid = (u32)lane < m;
+      const u64 b = valid ? s.pb[lane] : 0ull;
+      u64 v = valid ? s.pv[0][lane] : 0ull;
+      u64 sib[TMAXD];
+#pragma unroll
+      for (int l = 0; l < TMAXD; l++) sib[l] = nodes[sib_at(depth, b, l)];
+#pragma unroll
+      for (int l = 0; l < TMAXD; l++) {
+        if ((u32)l < depth) {  // (uniform)
+          const u64 n = b >> l;
+          const u64 np = __shfl_up(n, 1, WAVE);
+          const bool owner = valid && (lane == 0 || np != n);
+          const u64 om = __ballot(owner);
+          const u64 above = lane < WAVE - 1 ? om & (~0ull << (lane + 1)) : 0ull;
+          const u64 below = om & ((1ull << lane) - 1ull);
+          const int j = above ? __ffsll((long long)above) - 1 : lane;  // the next owner
+          const int k = below ? 63 - __clzll((long long)below) : lane;  // the previous one
+          const u64 nj = __shfl(n, j, WAVE), vj = __shfl(v, j, WAVE), nkk = __shfl(n, k, WAVE);
+          if (owner) {
+            bool make = true;
+            u64 par = 0;
+            if (!(n & 1))  // a left child: its right sibling changed iff the next owner's node is it
+              par = node_hash(v, above && nj == n + 1 ? vj : sib[l]);
+            else if (below && nkk == n - 1)  // a right child whose left sibling's owner makes the parent
+              make = false;
+            else
+              par = node_hash(sib[l], v);
+            if (make) {
+              v = par;
+              *node_at(depth - l - 1, n >> 1) = par;
+            }
+          }
+        }
+      }
+    }
+  } else {
+    const bool valid = (u32)tid < m;
+    const u64 b = valid ? s.pb[tid] : 0ull;
+    u64 sib[TMAXD];
+#pragma unroll
+    for (int l = 0; l < TMAXD; l++) sib[l] = nodes[sib_at(depth, b, l)];
+#pragma unroll
+    for (int l = 0; l < TMAXD; l++) {
+      if ((u32)l < depth) {  // (uniform)
+        const int cur = l & 1;
+        const u64 n = b >> l;
+        if (valid && (tid == 0 || (s.pb[tid - 1] >> l) != n)) {  // the owner of node n
+          const u64 v = s.pv[cur][tid];
+          bool make = true;
+          u64 par = 0;
+          if (!(n & 1)) {  // the right sibling's owner, if it changed: the first entry past node n
+            u32 lo = (u32)tid + 1, hi = m;
+            while (lo < hi) {
+              const u32 mid = (lo + hi) >> 1;
+              if ((s.pb[mid] >> l) <= n)
+                lo = mid + 1;
+              else
+                hi = mid;
+            }
+            par = node_hash(v, lo < m && (s.pb[lo] >> l) == n + 1 ? s.pv[cur][lo] : sib[l]);
+          } else if (tid > 0 && (s.pb[tid - 1] >> l) == n - 1) {
+            make = false;
+          } else {
+            par = node_hash(sib[l], v);
+          }
+          if (make) {
+            s.pv[cur ^ 1][tid] = par;
+            *node_at(depth - l - 1, n >> 1) = par;
+          }
+        }
+        __syncthreads();
+      }
+    }
+  }
+  SSTAMP(7);
+  if (moved && t.starts) {  // (uniform) chunk x's first row moves by the changes of chunks < x
+    const u32 L1 = depth < MERKLE_UPL ? depth : MERKLE_UPL;
+    const u64 G = 1ull << (depth - L1);
+    const u64 x0 = (s.pb[0] >> L1) + 1;
+    constexpr int XB = 8;  // entries per thread and round, their loads issued together
+    for (u64 xb = x0 + (u64)tid * XB; xb <= G; xb += (u64)NT * XB) {
+      u64 st[XB];
+      int add[XB];
+#pragma unroll
+      for (int q = 0; q < XB; q++) {
+        const u64 x = xb + q;
+        add[q] = 0;
+        st[q] = 0;
+        if (x <= G) {
+          u32 lo = 0, hi = m;  // the entries of chunks before x
+          while (lo < hi) {
+            const u32 mid = (lo + hi) >> 1;
+            if ((s.pb[mid] >> L1) < x)
+              lo = mid + 1;
+            else
+              hi = mid;
+          }
+          add[q] = s.pp[lo];
+          if (add[q]) st[q] = t.starts[x];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < XB; q++)
+        if (add[q]) t.starts[xb + q] = st[q] + (u64)(i64)add[q];
+    }
+  }
+  SSTAMP(8);
+}
+
 __global__ __launch_bounds__(NT) void small_delta_kernel(SmallArgs p) {
+  SSTAMP(0);
   __shared__ SmallLds s;
   const int tid = threadIdx.x;
   const u32 nk = (u32)p.nk, nd = (u32)p.d.n, ncd = (u32)p.cd.n, ncs = (u32)p.ca.n;
@@ -188,25 +429,19 @@ __global__ __launch_bounds__(NT) void small_delta_kernel(SmallArgs p) {
     if (dvv) s.cd.tabD[x] = 0;
   }
   __syncthreads();
-  // ---- 1. the keys' state rows; the delta and the contexts staged
+  // ---- 1. the keys' state rows; the delta and the contexts staged.  The staging goes to
+  //      the threads from the top (each stream at its own offset) and the key searches to
+  //      the threads from the bottom, so a one-key op's loads are in flight together
   u32 fl = 0;
-  if ((u32)tid < nk) {
-    const u64 k = p.keys[tid];
-    const u64 lo = interp_lower_bound(p.a.key, 0, p.a.n, k);
-    u64 e = lo;
-    while (e < p.a.n && p.a.key[e] == k && e - lo <= SA) e++;
-    s.key[tid] = k;
-    s.alo[tid] = lo;
-    s.na[tid] = (u32)(e - lo);
-  }
-  for (u32 i = tid; i < nd; i += NT) {
+  auto from_top = [&](u32 o) { return (u32)((2 * NT - 1 - tid - o) % NT); };
+  for (u32 i = from_top(0); i < nd; i += NT) {
     s.dk[i] = p.d.key[i];
     s.dv[i] = p.d.val[i];
     s.dt[i] = p.d.ts[i];
     s.dn[i] = p.d.node[i];
     s.dc[i] = p.d.cnt[i];
   }
-  for (u32 i = tid; i < ncs; i += NT) {
+  for (u32 i = from_top(NT / 4); i < ncs; i += NT) {
     const u32 n = p.ca.node[i];
     const u64 c = p.ca.cnt[i];
     if (n >= SV || c == ~0ull)
@@ -214,7 +449,7 @@ __global__ __launch_bounds__(NT) void small_delta_kernel(SmallArgs p) {
     else
       s.tabS[n] = c + 1;
   }
-  for (u32 i = tid; i < ncd; i += NT) {
+  for (u32 i = from_top(NT / 2); i < ncd; i += NT) {
     const u32 n = p.cd.node[i];
     const u64 c = p.cd.cnt[i];
     if (n >= SV || c == ~0ull) fl |= SMALL_FALLBACK;
@@ -225,9 +460,52 @@ __global__ __launch_bounds__(NT) void small_delta_kernel(SmallArgs p) {
       s.cd.dots.c[i] = c;
     }
   }
+  // (has_tree) the key's bucket node and row count, loaded with the search
+  u64 t_old = 0;
+  u32 t_cnt = 0;
+  if ((u32)tid < nk && p.has_tree) {
+    const u64 b = bucket_of_t(p.t, p.keys[tid]);
+    t_old = p.t.nodes[((1ull << p.t.depth) - 1) + b];
+    t_cnt = p.t.counts[b];
+  }
+  if (nk <= (u32)(NT / WAVE)) {  // (uniform) a few keys: one wave searches each
+    const u32 u = (u32)tid / WAVE;
+    if (u < nk) {
+      const u64 k = p.keys[u];
+      u64 lo;
+      u32 run;
+      wave_find(p.a.key, p.a.n, k, lo, run);
+      if ((tid & (WAVE - 1)) == 0) {
+        s.key[u] = k;
+        s.alo[u] = lo;
+        s.na[u] = run;
+      }
+    }
+  } else if ((u32)tid < nk) {
+    const u64 k = p.keys[tid];
+    const u64 lo = interp_lower_bound(p.a.key, 0, p.a.n, k);
+    u64 e = lo;
+    for (;;) {  // the key's run, 4 rows per round trip
+      u64 kk[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) kk[q] = e + q < p.a.n ? p.a.key[e + q] : k + 1;
+      u32 c = 0;
+#pragma unroll
+      for (int q = 0; q < 4; q++) c += (c == (u32)q && kk[q] == k) ? 1u : 0u;
+      e += c;
+      if (c < 4 || e - lo > SA) break;
+    }
+    s.key[tid] = k;
+    s.alo[tid] = lo;
+    s.na[tid] = (u32)(e - lo);
+  }
   if (fl) atomicOr(&s.flags, fl);
   __syncthreads();
-  // ---- 2. the taken rows' offsets, the rows staged; delta keys inside the keyset
+  SSTAMP(1);
+  // ---- 2. the taken rows' offsets, the rows staged; delta keys inside the keyset.  And
+  //      Dots.union(state VV, delta context): per node the max, as counter + 1 (a dot set's
+  //      entries folded in by LDS atomics behind the scan's barriers)
+  for (u32 x = tid; x < SV; x += NT) s.tabU[x] = max(s.tabS[x], dvv ? s.cd.tabD[x] : 0ull);
   u32 tot;
   {
     const u32 v = (u32)tid < nk ? s.na[tid] : 0u;
@@ -239,6 +517,10 @@ __global__ __launch_bounds__(NT) void small_delta_kernel(SmallArgs p) {
   if (n_ak > SA) {  // (uniform)
     if (tid == 0) s.flags |= SMALL_FALLBACK;
   }
+  if (!dvv)
+    for (u32 i = tid; i < ncd; i += NT)
+      if (s.cd.dots.n[i] < SV)
+        atomicMax((unsigned long long*)&s.tabU[s.cd.dots.n[i]], (unsigned long long)(s.cd.dots.c[i] + 1));
   __syncthreads();
   if (!(s.flags & SMALL_FALLBACK)) {
     for (u32 q = tid; q < n_ak; q += NT) {
@@ -271,6 +553,7 @@ __global__ __launch_bounds__(NT) void small_delta_kernel(SmallArgs p) {
     }
   }
   __syncthreads();
+  SSTAMP(2);
   const bool fallback = s.flags & SMALL_FALLBACK;  // (uniform)
   // ---- 3. the join per key: kept rows, changed, distinct-key change
   u32 ne = 0, chg = 0, ja = 0, je = 0;
@@ -286,40 +569,31 @@ __global__ __launch_bounds__(NT) void small_delta_kernel(SmallArgs p) {
     const int dk = (int)(ne > 0) - (int)(s.na[tid] > 0);
     if (dk) atomicAdd(&s.dkeys, dk);
   }
-  // ---- 4. offsets: the edit's, the changed keys', their rows'
-  u32 n_e, n_chg, n_rows;
-  {
-    const u32 o = block_excl_scan<NT>(ne, s.wave, &n_e);
-    if ((u32)tid < nk) s.eoff[tid] = o;
-    if (tid == 0) s.eoff[nk] = n_e;
-    __syncthreads();
-    const u32 oc = block_excl_scan<NT>(chg, s.wave, &n_chg);
-    __syncthreads();
-    const u32 orr = block_excl_scan<NT>(chg ? ne : 0u, s.wave, &n_rows);
-    if ((u32)tid < nk) {
-      s.coff[tid] = oc;
-      s.roff[tid] = orr;
-    }
-  }
-  if (tid == 0 && n_e > SE) s.flags |= SMALL_FALLBACK;
-  // Dots.union(state VV, delta context): per node the max, as counter + 1
-  if (!fallback) {
-    for (u32 x = tid; x < SV; x += NT) s.tabU[x] = max(s.tabS[x], dvv ? s.cd.tabD[x] : 0ull);
-    __syncthreads();
-    if (!dvv)
-      for (u32 i = tid; i < ncd; i += NT) atomicMax((unsigned long long*)&s.tabU[s.cd.dots.n[i]],
-                                                   (unsigned long long)(s.cd.dots.c[i] + 1));
-  }
-  __syncthreads();
-  u32 nctx = 0, cpos = 0;
+  // ---- 4. offsets: the edit's, the changed keys', their rows', the union context's
+  //      entries -- four scans, one barrier
+  u32 n_e, n_chg, n_rows, nctx, cpos;
   {
     constexpr u32 PER = SV / NT;  // table entries per thread
     u32 own = 0;
 #pragma unroll
     for (u32 q = 0; q < PER; q++) own += s.tabU[tid * PER + q] != 0 ? 1u : 0u;
-    cpos = block_excl_scan<NT>(own, s.wave, &nctx);
+    const u32 v[4] = {ne, chg, chg ? ne : 0u, own};
+    u32 ex[4], tt[4];
+    block_scan4(v, s.w4, ex, tt);
+    n_e = tt[0];
+    n_chg = tt[1];
+    n_rows = tt[2];
+    nctx = tt[3];
+    cpos = ex[3];
+    if ((u32)tid < nk) {
+      s.eoff[tid] = ex[0];
+      s.coff[tid] = ex[1];
+      s.roff[tid] = ex[2];
+    }
+    if (tid == 0) s.eoff[nk] = n_e;
   }
-  if (tid == 0 && nctx > p.ca_cap) s.flags |= SMALL_FALLBACK;
+  if (tid == 0 && (n_e > SE || nctx > p.ca_cap)) atomicOr(&s.flags, SMALL_FALLBACK);
+  SSTAMP(3);
   // ---- 5. the tree: per bucket the leaf and row-count change, checked before any write
   // (leaf[u]: Σ row_hash of the key's new rows - of its old rows)
   if (!fallback && p.has_tree && (u32)tid < nk && chg) {
@@ -340,36 +614,57 @@ __global__ __launch_bounds__(NT) void small_delta_kernel(SmallArgs p) {
     if (head) {  // the bucket's keys: this one and the next ones in the same bucket
       i64 drows = 0;
       for (u32 u = tid; u < nk && bucket_of_t(t, s.key[u]) == b; u++) drows += (i64)s.ne[u] - (i64)s.na[u];
-      const i64 now = (i64)t.counts[b] + drows;
+      const i64 now = (i64)t_cnt + drows;
       if (now < 0 || now > 0xFFFF) atomicOr(&s.flags, MERKLE_ERR_COUNT);
     }
   }
   __syncthreads();
   const u32 flags = s.flags;
+  SSTAMP(4);
   u64* res = p.res;
+  // the result block goes straight into `home` (host memory); the header also into `res`
+  // (the tail kernel and the splice after the wait read it on the device)
+  u64* home = p.home;
+  // publish: the engine's count block and the sequence number, after every thread's home
+  // writes (dg_home.h); unless the rows moved and the tail kernel copies them (it does)
+  const bool moved = s.moved != 0;
   if (flags) {  // (uniform) nothing written: the caller takes the general path or reports
-    if (tid == 0) {
-      res[0] = flags;
-      for (int i = 1; i < (int)SMALL_HDR; i++) res[i] = 0;
+    if (tid < (int)SMALL_HDR) {
+      res[tid] = tid ? 0ull : (u64)flags;
+      home[tid] = tid ? 0ull : (u64)flags;
     }
+    publish_counts(p.d_counts, p.h_pub, p.seq);
     return;
   }
   // ---- 6. writes
-  const bool moved = s.moved != 0;
+  u64 t_new = 0;
+  int t_drows = 0;
+  bool t_dirty = false;  // a head thread whose bucket changed: t_new, its rows' change
   if ((u32)tid < nk) {
     const u32 e0 = s.eoff[tid], r0 = s.roff[tid];
     const u64 a0 = s.alo[tid];
+    // the splice's gap shift of this key's edit rows: E's row j goes to j + a_lo - a_off
+    const i64 gap = (i64)a0 - (i64)s.aoff[tid];
     u32 j = 0;
     bool c;
-    u64* rk = res + SMALL_O_ROWS;
+    u64* rk = home + SMALL_O_ROWS;
     const RowsOut rr{rk, rk + SE, (i64*)(rk + 2 * SE), (u32*)(rk + 4 * SE), rk + 3 * SE};
     merge_key(s, s.aoff[tid], s.aoff[tid + 1], ja, je, dvv, ncd, &c, [&](const Row& r) {
-      put_row(p.e, e0 + j, r);          // the edit (the moved path's splice reads it)
-      if (!moved) put_row(p.aw, a0 + j, r);  // in place: every key keeps its row count
-      if (chg) put_row(rr, r0 + j, r);   // the changed keys' rows, for the caller
+      if (!moved)
+        put_row(p.aw, a0 + j, r);  // in place: every key keeps its row count
+      else if (p.splice_here)
+        put_row(p.sp, (u64)((i64)(e0 + j) + gap), r);  // straight to its place in the spare
+      else
+        put_row(p.e, e0 + j, r);  // the edit, for the splice kernels after the wait
+      if (chg) put_row(rr, r0 + j, r);  // the changed keys' rows, for the caller
       j++;
     });
-    if (chg) res[SMALL_O_KEYS + s.coff[tid]] = s.key[tid];
+    if (moved && p.splice_here) {  // the index the tail kernel's splice tiles search
+      p.end[tid] = a0 + s.na[tid];
+      p.shift[tid] = (i64)e0 - (i64)s.aoff[tid];
+      if (tid == 0) p.shift[nk] = (i64)n_e - (i64)n_ak;
+    }
+    if (chg) home[SMALL_O_KEYS + s.coff[tid]] = s.key[tid];
     p.a_lo[tid] = a0;
     p.a_off[tid] = s.aoff[tid];
     if (tid == 0) p.a_off[nk] = n_ak;
@@ -377,7 +672,7 @@ __global__ __launch_bounds__(NT) void small_delta_kernel(SmallArgs p) {
       const MerkleT& t = p.t;
       const u64 k = s.key[tid], b = bucket_of_t(t, k);
       const bool head = tid == 0 || bucket_of_t(t, s.key[tid - 1]) != b;
-      if (head) {
+      if (head) {  // the bucket's keys: this one and the next ones in the same bucket
         u64 dh = 0;
         i64 drows = 0;
         bool any = false;
@@ -389,14 +684,12 @@ __global__ __launch_bounds__(NT) void small_delta_kernel(SmallArgs p) {
             any = true;
           }
         }
-        if (any) {
-          u64* lvl = t.nodes + ((1ull << t.depth) - 1);
-          lvl[b] += dh;
-          if (drows) t.counts[b] = (uint16_t)((i64)t.counts[b] + drows);
-          const u32 L1 = t.depth < MERKLE_UPL ? t.depth : MERKLE_UPL;
-          p.dirty[b >> L1] = 1u;
-          if (t.starts && drows)
-            atomicAdd((unsigned long long*)&p.cdelta[b >> L1], (unsigned long long)drows);
+        if (any) {  // MerkleMap.put/delete: the bucket's node and row count
+          t_dirty = true;
+          t_new = t_old + dh;
+          t_drows = (int)drows;
+          t.nodes[((1ull << t.depth) - 1) + b] = t_new;
+          if (drows) t.counts[b] = (uint16_t)((i64)t_cnt + drows);
         }
       }
     }
@@ -405,7 +698,7 @@ __global__ __launch_bounds__(NT) void small_delta_kernel(SmallArgs p) {
   {
     constexpr u32 PER = SV / NT;
     u32 o = cpos;
-    u64* rc = res + SMALL_O_CTX;
+    u64* rc = home + SMALL_O_CTX;
     u32* rn = (u32*)(rc + SV);
 #pragma unroll
     for (u32 q = 0; q < PER; q++) {
@@ -420,52 +713,121 @@ __global__ __launch_bounds__(NT) void small_delta_kernel(SmallArgs p) {
       }
     }
   }
-  if (tid == 0) {
-    res[0] = 0;
-    res[1] = n_chg;
-    res[2] = n_rows;
-    res[3] = nctx;
-    res[4] = n_e;
-    res[5] = n_ak;
-    res[6] = moved ? 1 : 0;
-    res[7] = (u64)(i64)s.dkeys;
+  if (tid < (int)SMALL_HDR) {
+    const u64 h[SMALL_HDR] = {0, n_chg, n_rows, nctx, n_e, n_ak, moved ? 1u : 0u, (u64)(i64)s.dkeys};
+    u64 v = 0;
+#pragma unroll
+    for (int i = 0; i < (int)SMALL_HDR; i++) v = i == tid ? h[i] : v;
+    res[tid] = v;
+    home[tid] = v;
+  }
+  SSTAMP(5);
+  if (p.has_tree) tree_paths(p, s, t_dirty, t_new, t_drows, moved);
+  SSTAMP(9);
+  if (!(moved && p.splice_here)) publish_counts(p.d_counts, p.h_pub, p.seq);
+  SSTAMP(10);
+}
+
+// ---------------------------------------------------------------- dg_join_delta_home's tail
+// (dg_launch.h SmallTailArgs) The moved rows' splice copy behind the small join, and the
+// publish by the last workgroup to finish.  A splice tile's rows: thread
+// t holds rows 2 (q NT + t) + h of the tile (q, h < 2), each column read as 16-byte pairs;
+// the per-key index (<= SMALL_KEYS entries, written by the small join) is staged in LDS
+// while the loads are in flight, and row i goes to i + shift[u*] with u* the first key
+// whose state rows end after i -- unless i is one of that key's rows (the edit's, placed
+// by the small join).
+static_assert(SMALL_TILE == 4 * NT, "4 rows per thread");
+__device__ __forceinline__ void small_tile_copy(const SmallTailArgs& p, u64 tile) {
+  __shared__ u64 s_end[SMALL_KEYS], s_lo[SMALL_KEYS];
+  __shared__ i64 s_sh[SMALL_KEYS + 1];
+  const u32 tid = threadIdx.x, nk = (u32)p.nk;
+  const u64 i0 = tile * SMALL_TILE, i1 = min<u64>(i0 + SMALL_TILE, p.a.n);
+  u64 key[4], val[4], cnt[4];
+  i64 ts[4];
+  u32 nd[4];
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const u64 i = i0 + 2 * ((u64)q * NT + tid);
+    if (i + 1 < i1) {  // i0 and i even: an aligned pair
+      const ulonglong2 k = *(const ulonglong2*)(p.a.key + i), v = *(const ulonglong2*)(p.a.val + i);
+      const longlong2 t2 = *(const longlong2*)(p.a.ts + i);
+      const ulonglong2 c = *(const ulonglong2*)(p.a.cnt + i);
+      const uint2 n = *(const uint2*)(p.a.node + i);
+      key[2 * q] = k.x, key[2 * q + 1] = k.y, val[2 * q] = v.x, val[2 * q + 1] = v.y;
+      ts[2 * q] = t2.x, ts[2 * q + 1] = t2.y, cnt[2 * q] = c.x, cnt[2 * q + 1] = c.y;
+      nd[2 * q] = n.x, nd[2 * q + 1] = n.y;
+    } else if (i < i1) {
+      key[2 * q] = p.a.key[i], val[2 * q] = p.a.val[i], ts[2 * q] = p.a.ts[i];
+      cnt[2 * q] = p.a.cnt[i], nd[2 * q] = p.a.node[i];
+    }
+  }
+  for (u32 x = tid; x < nk; x += NT) {
+    s_end[x] = p.end[x];
+    s_lo[x] = p.a_lo[x];
+  }
+  for (u32 x = tid; x <= nk; x += NT) s_sh[x] = p.shift[x];
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const u64 i = i0 + 2 * ((u64)(r >> 1) * NT + tid) + (r & 1);
+    if (i >= i1) continue;
+    u32 lo = 0, hi = nk;  // the first key whose rows end after row i
+    while (lo < hi) {
+      const u32 m = (lo + hi) >> 1;
+      if (s_end[m] > i)
+        hi = m;
+      else
+        lo = m + 1;
+    }
+    if (lo < nk && s_lo[lo] <= i) continue;  // a keyset key's row: the edit replaced it
+    const u64 o = (u64)((i64)i + s_sh[lo]);
+    p.out.key[o] = key[r];
+    p.out.val[o] = val[r];
+    p.out.ts[o] = ts[r];
+    p.out.node[o] = nd[r];
+    p.out.cnt[o] = cnt[r];
   }
 }
 
-// The used part of the result block into `home` (host memory): header, changed keys, their
-// rows (each column at its fixed stride), the context -- a few hundred bytes for one key --
-// then the engine's counts and the sequence number the host polls (api.hip sync_words).
-__global__ __launch_bounds__(256) void small_home_kernel(const u64* res, u64* home, const u64* d_counts,
-                                                         u64* h_pub, u64 seq) {
-  const u64 n_chg = res[1], n_rows = res[2], nctx = res[3];
-  const int tid = threadIdx.x;
-  if (tid < (int)SMALL_HDR) home[tid] = res[tid];
-  for (u64 i = tid; i < n_chg; i += 256) home[SMALL_O_KEYS + i] = res[SMALL_O_KEYS + i];
-  for (int c = 0; c < 4; c++)
-    for (u64 i = tid; i < n_rows; i += 256) home[SMALL_O_ROWS + c * SE + i] = res[SMALL_O_ROWS + c * SE + i];
-  const u32* rn = (const u32*)(res + SMALL_O_ROWS + 4 * SE);
-  u32* hn = (u32*)(home + SMALL_O_ROWS + 4 * SE);
-  for (u64 i = tid; i < n_rows; i += 256) hn[i] = rn[i];
-  for (u64 i = tid; i < nctx; i += 256) home[SMALL_O_CTX + i] = res[SMALL_O_CTX + i];
-  const u32* cn = (const u32*)(res + SMALL_O_CTX + SV);
-  u32* hc = (u32*)(home + SMALL_O_CTX + SV);
-  for (u64 i = tid; i < nctx; i += 256) hc[i] = cn[i];
-  if (tid < 16) h_pub[tid] = d_counts[tid];  // d_counts[0..8) and the ticket words
-  __threadfence_system();
+__global__ __launch_bounds__(NT) void small_tail_kernel(SmallTailArgs p) {
+  __shared__ u32 s_all;
+  if (blockIdx.x == 0) SSTAMP(12);
+  const bool moved = p.res[0] == 0 && p.res[6];  // (uniform) else the small join published
+  if (!moved) return;
+  small_tile_copy(p, blockIdx.x);
+  // every workgroup arrives once its part is done; the last one publishes
   __syncthreads();
-  if (tid == 0) __hip_atomic_store(h_pub + 16, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const u32 n = __hip_atomic_fetch_add(p.arrive_all, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_all = n == gridDim.x - 1;
+    if (s_all) __hip_atomic_store(p.arrive_all, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (s_all) {
+    __threadfence();
+    publish_counts(p.d_counts, p.h_pub, p.seq);
+  }
 }
 
 }  // namespace
+
+#ifdef DG_SMALL_STAMPS
+extern "C" int dg_debug_small_stamps(unsigned long long* host, size_t n) {
+  if (n > 16) n = 16;
+  if (hipDeviceSynchronize() != hipSuccess) return -3;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sm_stamps), n * 8) == hipSuccess ? 0 : -3;
+}
+#endif
 
 hipError_t launch_small_delta(const SmallArgs& p, hipStream_t st) {
   hipLaunchKernelGGL(small_delta_kernel, dim3(1), dim3(NT), 0, st, p);
   return hipGetLastError();
 }
 
-hipError_t launch_small_home_publish(const u64* res, u64* home, const u64* d_counts, u64* h_pub, u64 seq,
-                                     hipStream_t st) {
-  hipLaunchKernelGGL(small_home_kernel, dim3(1), dim3(256), 0, st, res, home, d_counts, h_pub, seq);
+
+hipError_t launch_small_tail(const SmallTailArgs& p, hipStream_t st) {
+  hipLaunchKernelGGL(small_tail_kernel, dim3((unsigned)(p.tiles ? p.tiles : 1)), dim3(NT), 0, st, p);
   return hipGetLastError();
 }
 

@@ -424,7 +424,9 @@ def test_small_sync_deltas_home(engine, seed):
     keys = np.sort(rng.choice(kb, 120, replace=False))  # (<= 512 delta rows)
     d = W.sync_delta(b, keys)
     assert len(d["rows"][0]) <= 512
-    apply(engine, a, d, keys, home=True)
+    # (depth 10: one chunk; 18: 128 chunks, every bucket path its own up to level ~7 and
+    # the chunk index moved past each changed chunk)
+    apply(engine, a, d, keys, depth=10 if seed == 0 else 18, home=True)
     a, b = W.config4_shard(seed, 8, keys_per_rank=30_000, diff_frac=0.01)
     want = R.store_diff(a["rows"], b["rows"])
     assert 0 < len(want) <= 512
