@@ -737,6 +737,28 @@ int dgr_merkle_build(dgr_state* s, uint64_t version, uint32_t depth) {
 }
 
 /* a device continuation -> bytes (u32 level | u64 n | u64 n_buckets | pos | hash | bucket) */
+#define CONT_SMALL_OUT 65536 /* entries of an outgoing continuation / keys kept in host memory */
+
+/* a continuation in host memory (the kernel wrote it there) framed as the message */
+static int frame_cont(dgr_engine* g, const dg_merkle_cont* co, const uint8_t** bin, uint64_t* len) {
+  const uint64_t bytes = 20 + 8 * (2 * co->n + co->n_buckets);
+  if (g->bin_cap < bytes) {
+    uint8_t* p = (uint8_t*)realloc(g->h_bin, bytes);
+    if (!p) return DG_E_NOMEM;
+    g->h_bin = p;
+    g->bin_cap = bytes;
+  }
+  memcpy(g->h_bin, &co->level, 4);
+  memcpy(g->h_bin + 4, &co->n, 8);
+  memcpy(g->h_bin + 12, &co->n_buckets, 8);
+  memcpy(g->h_bin + 20, co->pos, 8 * co->n);
+  memcpy(g->h_bin + 20 + 8 * co->n, co->hash, 8 * co->n);
+  if (co->n_buckets) memcpy(g->h_bin + 20 + 16 * co->n, co->bucket, 8 * co->n_buckets);
+  *bin = g->h_bin;
+  *len = bytes;
+  return DG_OK;
+}
+
 static int cont_to_bytes(dgr_engine* g, const dg_merkle_cont* c, const uint8_t** bin, uint64_t* len) {
   const uint64_t words = 2 * c->n + c->n_buckets;
   const uint64_t bytes = 20 + 8 * words;
@@ -766,10 +788,86 @@ int dgr_merkle_prepare(dgr_state* s, uint64_t version, uint32_t levels, const ui
   TRY(check_version(s, version));
   dgr_engine* g = s->g;
   const uint32_t L = levels < s->tree.depth ? levels : s->tree.depth;
-  TRY(grow_cont(g, &g->co, UINT64_C(1) << L, 1));
+  const uint64_t n = UINT64_C(1) << L;
+  if (n <= CONT_SMALL_OUT) { /* written by the kernel into page-locked memory: framed here */
+    TRY(grow_host(g, &g->h_cstage, &g->h_cstage_cap, 2 * n));
+    dg_merkle_cont co;
+    memset(&co, 0, sizeof co);
+    co.pos = g->h_cstage;
+    co.hash = g->h_cstage + n;
+    co.cap = n;
+    TRY(dg_merkle_prepare(g->e, &s->tree, levels, &co));
+    return frame_cont(g, &co, bin, len);
+  }
+  TRY(grow_cont(g, &g->co, n, 1));
   g->co.n = g->co.n_buckets = 0;
   TRY(dg_merkle_prepare(g->e, &s->tree, levels, &g->co));
   return cont_to_bytes(g, &g->co, bin, len);
+}
+
+/* One hop through dg_merkle_continue_home: the incoming continuation read where it was
+ * unpacked (mapped memory), the next one (truncated to max_sync) or the keys written by
+ * the kernel into page-locked memory, one launch and one wait.  *done = 0: over its
+ * limits (nothing happened; the general path runs). */
+static int continue_small(dgr_state* s, uint32_t level, uint64_t n, uint64_t nb, uint32_t levels,
+                          uint64_t max_sync, int* status, const uint8_t** out_bin, uint64_t* out_len,
+                          const uint64_t** keys, uint64_t* n_keys, int* done) {
+  dgr_engine* g = s->g;
+  *done = 0;
+  static int general = -1; /* DGR_CONT_GENERAL=1: always the general calls (A/B) */
+  if (general < 0) general = getenv("DGR_CONT_GENERAL") != NULL;
+  const uint32_t depth = s->tree.depth;
+  if (general || n > DG_CONT_HOME_ENTRIES || nb > DG_CONT_HOME_BUCKETS || level > depth + 1) return DG_OK;
+  dg_merkle_cont ci;
+  memset(&ci, 0, sizeof ci);
+  ci.level = level;
+  ci.pos = g->h_msg;
+  ci.hash = g->h_msg + n;
+  ci.bucket = g->h_msg + 2 * n;
+  ci.n = ci.cap = n;
+  ci.n_buckets = ci.cap_buckets = nb;
+  uint64_t C, CB = umax(umin(n, max_sync), 1);
+  if (level < depth) {
+    const uint32_t k = levels < depth - level ? levels : depth - level;
+    C = umin(n << k, max_sync);
+  } else {
+    C = umax(4 * umin(n, max_sync), 64);
+  }
+  C = umax(C, 1);
+  const uint64_t kcap = umax(umin(umin(max_sync, s->rows.n + n + 1), CONT_SMALL_OUT), 1);
+  TRY(grow_host(g, &g->h_ckeys, &g->h_ckeys_cap, kcap));
+  uint64_t nk = 0, ntot = 0;
+  dg_merkle_cont co;
+  for (int attempt = 0;; attempt++) {
+    if (C > CONT_SMALL_OUT) return DG_OK;
+    TRY(grow_host(g, &g->h_cstage, &g->h_cstage_cap, 2 * C + CB));
+    memset(&co, 0, sizeof co);
+    co.pos = g->h_cstage;
+    co.hash = g->h_cstage + C;
+    co.bucket = g->h_cstage + 2 * C;
+    co.cap = C;
+    co.cap_buckets = CB;
+    const int rc = dg_merkle_continue_home(g->e, &s->tree, &s->rows, &ci, levels, max_sync, &co, g->h_ckeys,
+                                           kcap, &nk, &ntot, status);
+    if (rc == DG_E_CAPACITY && attempt == 0) {
+      C = umax(co.n, C);
+      CB = umax(co.n_buckets, CB);
+      continue;
+    }
+    TRY(rc);
+    break;
+  }
+  if (*status == DG_CONT_DECLINED) return DG_OK;
+  if (*status == 0) {
+    if (ntot > nk && nk < max_sync) return DG_OK; /* more keys than kept here: the general path */
+    *keys = g->h_ckeys;
+    *n_keys = nk;
+    *done = 1;
+    return DG_OK;
+  }
+  TRY(frame_cont(g, &co, out_bin, out_len));
+  *done = 1;
+  return DG_OK;
 }
 
 int dgr_merkle_continue(dgr_state* s, uint64_t version, const uint8_t* bin, uint64_t len, uint32_t levels,
@@ -792,6 +890,10 @@ int dgr_merkle_continue(dgr_state* s, uint64_t version, const uint8_t* bin, uint
   /* the incoming continuation as ONE copy: pos | hash | bucket in the message buffer */
   TRY(grow_msg(g, 2 * n + nb + 1));
   if (2 * n + nb) memcpy(g->h_msg, bin + 20, (2 * n + nb) * 8);
+  int done = 0;
+  TRY(continue_small(s, level, n, nb, levels, max_sync, status, out_bin, out_len, keys, n_keys, &done));
+  if (done) return DG_OK;
+  *status = 0;
   TRY(dg_copy_async(g->e, g->d_msg, g->h_msg, (2 * n + nb) * 8));
   dg_merkle_cont ci;
   memset(&ci, 0, sizeof ci);

@@ -43,6 +43,9 @@ DG_E_ORDER = -5
 DG_E_CLAUSE = -6
 
 DG_HOME_FALLBACK = 1
+DG_CONT_DECLINED = 2
+DG_CONT_HOME_ENTRIES = 4096
+DG_CONT_HOME_BUCKETS = 512
 DG_HOME_KEYS = 8
 DG_HOME_STRIDE = 1536
 DG_HOME_ROWS = DG_HOME_KEYS + 512
@@ -218,6 +221,10 @@ _SIGS = {
                                      C.POINTER(dg_merkle_cont), C.c_uint32,
                                      C.POINTER(dg_merkle_cont), P64, C.c_uint64, P64, P64,
                                      C.POINTER(C.c_int)]),
+    "dg_merkle_continue_home": (C.c_int, [C.c_void_p, C.POINTER(dg_merkle), C.POINTER(dg_store),
+                                          C.POINTER(dg_merkle_cont), C.c_uint32, C.c_uint64,
+                                          C.POINTER(dg_merkle_cont), P64, C.c_uint64, P64, P64,
+                                          C.POINTER(C.c_int)]),
     "dg_merkle_truncate": (C.c_int, [C.c_void_p, C.POINTER(dg_merkle), C.POINTER(dg_merkle_cont),
                                      C.c_uint64]),
     "dg_merkle_fold_roots": (C.c_int, [P64, C.c_uint32, P64]),

@@ -300,6 +300,7 @@ int sync_words(dg_engine* e) {
 // start at all (a launch error); a kernel that faults leaves the device unusable anyway.
 // read_counts also zeroes it whenever a call reports error bits.
 constexpr int MERKLE_ARRIVE = 6;
+constexpr int CONT_HOME = 18;  // h_pub words [18, 24): dg_merkle_continue_home's result header
 constexpr int TAIL_ARRIVE = 7;  // dg_join_delta_home's tail kernel: every workgroup arrives
 
 int read_counts(dg_engine* e, int n) {
@@ -1046,6 +1047,8 @@ static int join_delta_impl(dg_engine* e, dg_store* state, dg_context* state_ctx,
 // guarded by its `moved` word; a larger state whose rows moved copies after the wait.
 constexpr u64 SMALL_COPY_TILES = 64;
 static_assert(DIFF_MISMATCH == DG_DIFF_MISMATCH, "deltagpu.h and the diff kernels agree");
+static_assert(CS_IN == DG_CONT_HOME_ENTRIES && CS_B == DG_CONT_HOME_BUCKETS && CONT_HOME + CS_HDR <= 24,
+              "deltagpu.h's limits; the header fits the publish block");
 static_assert(SMALL_O_KEYS == DG_HOME_KEYS &&SMALL_O_ROWS == DG_HOME_ROWS && SMALL_EDIT == DG_HOME_STRIDE &&
                   SMALL_O_CTX == DG_HOME_CTX && SMALL_NODES == DG_HOME_NODES && SMALL_WORDS == DG_HOME_WORDS &&
                   SMALL_FALLBACK == DG_HOME_FALLBACK,
@@ -1775,11 +1778,8 @@ int dg_merkle_prepare(dg_engine* e, const dg_merkle* t, uint32_t levels, dg_merk
     return fail(DG_E_CAPACITY, "dg_merkle_prepare: %llu entries needed", (unsigned long long)n);
   TRY(set_device(e));
   TRY(settle(e));
-  TRY(ensure_state(e, 2));
-  HIP_TRY(hipMemsetAsync(e->state, 0, sizeof(u64), e->stream));  // the root's position, 0
-  HIP_TRY(launch_cont_expand(merkle_of(t), 0, L, e->state, 1, out->pos, out->hash, e->stream));
-  HIP_TRY(hipStreamSynchronize(e->stream));
-  return DG_OK;
+  HIP_TRY(launch_cont_prepare(merkle_of(t), L, out->pos, out->hash, e->stream));
+  return sync_words(e);
 }
 
 int dg_merkle_continue(dg_engine* e, const dg_merkle* t, const dg_store* s, const dg_merkle_cont* in,
@@ -1847,6 +1847,78 @@ int dg_merkle_continue(dg_engine* e, const dg_merkle* t, const dg_store* s, cons
     return fail(DG_E_CAPACITY, "dg_merkle_continue: %llu leaf pairs needed", (unsigned long long)np);
   HIP_TRY(launch_leaves_write(m, rows_of(s), out->bucket, nd, e->state, out->pos, out->hash, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
+  *status = 1;
+  return DG_OK;
+}
+
+int dg_merkle_continue_home(dg_engine* e, const dg_merkle* t, const dg_store* s, const dg_merkle_cont* in,
+                            uint32_t levels, uint64_t max, dg_merkle_cont* out, uint64_t* keys, uint64_t cap,
+                            uint64_t* n_keys, uint64_t* n_total, int* status) {
+  if (!e) return fail(DG_E_INVAL, "null engine");
+  TRY(check_merkle(t, "dg_merkle_continue_home"));
+  TRY(check_store(s, "dg_merkle_continue_home"));
+  if (!in || !status || !n_keys || levels < 1 || (cap && !keys))
+    return fail(DG_E_INVAL, "dg_merkle_continue_home: bad arguments");
+  if (in->n && (!in->pos || !in->hash)) return fail(DG_E_INVAL, "dg_merkle_continue_home: null input");
+  const u32 depth = t->depth;
+  const bool leaf = in->level == depth + 1;
+  if (in->level > depth + 1) return fail(DG_E_INVAL, "dg_merkle_continue_home: level %u > depth %u", in->level, depth);
+  if (leaf && in->n_buckets && !in->bucket) return fail(DG_E_INVAL, "dg_merkle_continue_home: null buckets");
+  *n_keys = 0;
+  if (n_total) *n_total = 0;
+  *status = DG_CONT_DECLINED;
+  if (in->n > CS_IN || (leaf && in->n_buckets > CS_B)) return DG_OK;  // the general path
+  *status = 0;
+  if (leaf ? in->n_buckets == 0 : in->n == 0) return DG_OK;  // {:ok, []}
+  if (!leaf && !out) return fail(DG_E_INVAL, "dg_merkle_continue_home: null out");
+  TRY(set_device(e));
+  TRY(settle(e));
+  ContSmallArgs a{};
+  a.t = merkle_of(t);
+  a.s = rows_of(s);
+  a.level = in->level;
+  a.levels = levels;
+  a.max = max;
+  a.ipos = in->pos;
+  a.ihash = in->hash;
+  a.ibucket = leaf ? in->bucket : nullptr;
+  a.n = in->n;
+  a.nb = leaf ? in->n_buckets : 0;
+  if (out) {
+    a.opos = out->pos;
+    a.ohash = out->hash;
+    a.obucket = out->bucket;
+    a.ocap = out->pos && out->hash ? out->cap : 0;
+    a.ocap_b = out->bucket ? out->cap_buckets : 0;
+  }
+  a.keys = keys;
+  a.kcap = cap;
+  a.home = e->d_pub + CONT_HOME;
+  a.d_counts = e->d_counts;
+  a.h_pub = e->d_pub;
+  a.seq = ++e->pub_seq;
+  HIP_TRY(launch_cont_small(a, e->stream));
+  TRY(wait_published(e, a.seq));
+  u64 h[CS_HDR];
+  memcpy(h, (const void*)(e->h_pub + CONT_HOME), sizeof h);
+  if (h[0] == CS_BAD)
+    return fail(DG_E_INVAL, "dg_merkle_continue_home: a position or bucket outside the tree");
+  if (h[0] == CS_CAP) {
+    out->level = (u32)h[3];
+    out->n = h[4];
+    out->n_buckets = h[5];
+    *status = 0;
+    return fail(DG_E_CAPACITY, "dg_merkle_continue_home: %llu entries / %llu buckets needed",
+                (unsigned long long)h[4], (unsigned long long)h[5]);
+  }
+  if (h[0] == CS_OK) {
+    *n_keys = std::min<u64>(h[1], cap);
+    if (n_total) *n_total = h[1];
+    return DG_OK;
+  }
+  out->level = (u32)h[3];
+  out->n = h[1];
+  out->n_buckets = h[0] == CS_LEAF ? h[2] : 0;
   *status = 1;
   return DG_OK;
 }

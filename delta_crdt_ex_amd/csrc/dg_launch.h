@@ -379,6 +379,30 @@ constexpr u64 DIFF_MISMATCH = 1ull << 44;
 hipError_t launch_merkle_diff(const MerkleT& a, const Rows& sa, const MerkleT& b, const Rows& sb,
                               u64* out_keys, u64 cap, u64* scratch, u64* bsum, u64* bsum_zero, u64 nzero,
                               u64* d_count, hipStream_t st);
+// dg_merkle_continue_home's one-workgroup hop (merkle.hip cont_small_kernel): limits,
+// result kinds (home[0]) and arguments
+constexpr u32 CS_IN = 4096, CS_B = 512;  // entries / pairs in, buckets in (leaf form)
+constexpr u64 CS_OK = 0, CS_NODE = 1, CS_LEAF = 2, CS_CAP = 3, CS_BAD = 4;
+constexpr int CS_HDR = 6;
+struct ContSmallArgs {
+  MerkleT t;
+  Rows s;
+  u32 level, levels;
+  u64 max;                      // truncate_diff: node entries / leaf buckets kept
+  const u64 *ipos, *ihash, *ibucket;
+  u64 n, nb;                    // entries (pairs), buckets in
+  u64 *opos, *ohash, *obucket;  // the next continuation (host or device)
+  u64 ocap, ocap_b;
+  u64* keys;                    // {:ok, keys}: the first kcap
+  u64 kcap;
+  u64* home;                    // result header: kind, n | total, n_buckets, level, needed n, needed buckets
+  const u64* d_counts;
+  u64* h_pub;
+  u64 seq;
+};
+hipError_t launch_cont_small(const ContSmallArgs& a, hipStream_t st);
+// prepare_partial_diff: level L's positions and node hashes (2^L entries)
+hipError_t launch_cont_prepare(const MerkleT& t, u32 L, u64* opos, u64* ohash, hipStream_t st);
 // partial diff.  scratch: 2 * ceil(n / 256) u64.
 inline u64 cont_tiles(u64 n) { return (n + 255) / 256; }
 hipError_t launch_cont_compare(const MerkleT& t, u32 L, const u64* pos, const u64* hash, u64 n,

@@ -42,6 +42,7 @@
 //    reply is a leaf-form continuation (the sender's (key, leaf) pairs of the
 //    differing buckets), which the peer merges with its own rows into keys.
 #include "dg_hash.h"
+#include "dg_home.h"
 #include "dg_launch.h"
 #include "dg_tree.h"
 
@@ -1110,6 +1111,14 @@ __global__ __launch_bounds__(PB) void cont_expand_kernel(MT t, u32 L, u32 k, con
   ohash[j] = t.nodes[((1ull << (L + k)) - 1) + p];
 }
 
+// prepare_partial_diff: every node of level L, positions and hashes (host or device)
+__global__ __launch_bounds__(PB) void cont_prepare_kernel(MT t, u32 L, u64* opos, u64* ohash) {
+  const u64 j = (u64)blockIdx.x * PB + threadIdx.x;
+  if (j >> L) return;
+  opos[j] = j;
+  ohash[j] = t.nodes[((1ull << L) - 1) + j];
+}
+
 // Leaf form, built by the side that found differing buckets: per bucket its distinct
 // keys (count pass) and then (key, leaf) pairs at the bucket's offset (write pass).
 template <bool WRITE>
@@ -1172,6 +1181,323 @@ __global__ void pairs_before_kernel(MT t, const u64* keys, u64 n, const u64* buc
   if (threadIdx.x == 0) out[0] = bucket_start(t, keys, n, bucket[0]);
 }
 
+// ---------------------------------------------------------------- a small partial-diff hop
+// dg_merkle_continue_home: one hop of continue_partial_diff (+ truncate_diff to `max`) for
+// a continuation of at most CS_IN entries / CS_B buckets, by ONE workgroup, results written
+// straight into the caller's (host) arrays, one host wait -- the general path is three
+// to five launches, each waited for.  Same results as dg_merkle_continue followed by
+// dg_merkle_truncate(max), except that capacity is asked of the truncated output only.
+//   node form, level L < depth : compare, compact the differing positions (input order),
+//                                expand by k levels, only the first `max` children made
+//   node form, level == depth  : the first `max` differing buckets, their (key, leaf) pairs
+//                                from the store (a bucket's rows: an interpolation search
+//                                for its first key, the tree's row count for the rest)
+//   leaf form                  : per bucket, the store's rows merged with the peer's pairs
+//                                (staged in LDS): the differing keys, the first kcap written
+// The result header goes to home[0..8) and the sequence number is published (dg_home.h).
+constexpr int CSN = 512;  // threads (256 VGPRs: a bucket's 16 rows in registers)
+constexpr u32 CS_PER = CS_IN / CSN;
+static_assert(CS_IN % CSN == 0, "whole entries per thread");
+
+__device__ __forceinline__ u64 bucket_first_key(const MT& t, u64 b) {
+  return (t.sb ? (t.shard << (64 - t.sb)) : 0ull) + (b << (64 - t.sb - t.depth));
+}
+
+// the store rows of bucket b: [r, r + counts[b]) (the tree describes the store), clamped
+__device__ __forceinline__ void bucket_rows(const MT& t, const Rows& s, u64 b, u64& r, u64& re) {
+  r = interp_lower_bound(s.key, 0, s.n, bucket_first_key(t, b));
+  re = min<u64>(r + t.counts[b], s.n);
+}
+
+// A bucket's (key, leaf) pairs in registers: its rows (at most BR; the tree's row count)
+// loaded together -- one round trip after the search, two past BR / 2 rows -- hashed,
+// and the runs of equal keys summed (head bit i: row i starts a key, leaf[i] its sum).
+// big: more rows than that (the generic loops over global memory).
+constexpr int BR = 16;
+struct BucketPairs {
+  u64 key[BR], leaf[BR];
+  u32 head;
+  bool big;
+  u64 r, re;
+};
+
+__device__ __forceinline__ void bucket_pairs(const MT& t, const Rows& s, u64 b, BucketPairs& o) {
+  const u32 cnt = t.counts[b];
+  const u64 r = interp_lower_bound(s.key, 0, s.n, bucket_first_key(t, b));
+  const u64 re = min<u64>(r + cnt, s.n);
+  o.r = r;
+  o.re = re;
+  o.big = re - r > (u64)BR;
+  o.head = 0;
+  if (o.big || re == r) return;
+  const u32 m = (u32)(re - r);
+  u64 hs[BR];
+#pragma unroll
+  for (int half = 0; half < 2; half++) {
+    if (half == 1 && m <= (u32)(BR / 2)) {
+#pragma unroll
+      for (int i = BR / 2; i < BR; i++) {
+        o.key[i] = 0;
+        hs[i] = 0;
+      }
+      break;
+    }
+    u64 k[BR / 2], v[BR / 2], c[BR / 2];
+    i64 ts[BR / 2];
+    u32 nd[BR / 2];
+#pragma unroll
+    for (int q = 0; q < BR / 2; q++) {  // every load issued before any is used
+      const int i = half * (BR / 2) + q;
+      const u64 x = r + (u64)((u32)i < m ? i : m - 1);
+      k[q] = s.key[x];
+      v[q] = s.val[x];
+      ts[q] = s.ts[x];
+      nd[q] = s.node[x];
+      c[q] = s.cnt[x];
+    }
+#pragma unroll
+    for (int q = 0; q < BR / 2; q++) {
+      const int i = half * (BR / 2) + q;
+      o.key[i] = k[q];
+      hs[i] = row_hash(k[q], th_val(t.th, v[q]), ts[q], th_node(t.th, nd[q]), c[q]);
+    }
+  }
+  u64 acc = 0;
+#pragma unroll
+  for (int i = BR - 1; i >= 0; i--) {
+    const bool valid = (u32)i < m;
+    const bool cont = (u32)(i + 1) < m && o.key[i + 1 < BR ? i + 1 : i] == o.key[i];
+    acc = valid ? hs[i] + (cont ? acc : 0ull) : 0ull;
+    o.leaf[i] = acc;
+    if (valid && (i == 0 || o.key[i > 0 ? i - 1 : 0] != o.key[i])) o.head |= 1u << i;
+  }
+}
+
+// distinct keys of rows [r, re) / their (key, leaf) pairs at out[o..): over global memory
+__device__ __forceinline__ u32 distinct_keys(const Rows& s, u64 r, u64 re) {
+  u32 c = 0;
+  for (u64 x = r; x < re; x++) c += (x == r || s.key[x] != s.key[x - 1]) ? 1u : 0u;
+  return c;
+}
+
+__device__ __forceinline__ u32 pairs_global(const MT& t, const Rows& s, u64 r, u64 re, u64* opos, u64* ohash,
+                                            u64 o) {
+  u32 c = 0;
+  for (u64 x = r; x < re;) {
+    const u64 key = s.key[x];
+    u64 lf = 0;
+    for (; x < re && s.key[x] == key; x++) lf += rh(s, x, t.th);
+    opos[o + c] = key;
+    ohash[o + c] = lf;
+    c++;
+  }
+  return c;
+}
+
+// merge_bucket with the store side in registers: the keys on one side only or with
+// different leaves, ascending (WRITE: out[o..), below cap)
+template <bool WRITE>
+__device__ __forceinline__ u32 merge_regs(const BucketPairs& bp, const u64* pk, const u64* ph, u64 j, u64 je,
+                                          u64* out, u64 o, u64 cap) {
+  u32 c = 0;
+  auto emit = [&](u64 k) {
+    if (WRITE && o + c < cap) out[o + c] = k;
+    c++;
+  };
+#pragma unroll
+  for (int i = 0; i < BR; i++) {
+    if (!(bp.head >> i & 1u)) continue;
+    const u64 k = bp.key[i];
+    for (; j < je && pk[j] < k; j++) emit(pk[j]);
+    if (j < je && pk[j] == k) {
+      if (ph[j] != bp.leaf[i]) emit(k);
+      j++;
+    } else {
+      emit(k);
+    }
+  }
+  for (; j < je; j++) emit(pk[j]);
+  return c;
+}
+
+__global__ __launch_bounds__(CSN) void cont_small_kernel(ContSmallArgs a, MT t) {
+  __shared__ u64 s_dpos[CS_IN];
+  __shared__ u64 s_pk[CS_IN], s_ph[CS_IN];  // leaf form in: the peer's pairs; node form: bucket rows
+  __shared__ u32 s_wave[CSN / WAVE + 1];
+  __shared__ u32 s_bad;
+  const int tid = threadIdx.x;
+  const u32 depth = t.depth, L = a.level;
+  u64 h[CS_HDR] = {0, 0, 0, 0, 0, 0};  // the result header (every thread's copy is the same)
+  if (tid == 0) s_bad = 0;
+  __syncthreads();
+  if (L <= depth) {
+    // ---- node form: entries tid*PER .. +PER (consecutive: compaction keeps input order)
+    u64 pos[CS_PER];
+    u32 d = 0;
+    const u64 lim = 1ull << L;
+#pragma unroll
+    for (u32 q = 0; q < CS_PER; q++) {
+      const u64 i = (u64)tid * CS_PER + q;
+      const bool ok = i < a.n;
+      const u64 ic = ok ? i : 0;  // (n >= 1: the host handles an empty continuation)
+      pos[q] = a.ipos[ic];
+      const u64 hv = a.ihash[ic];
+      if (ok && pos[q] >= lim) atomicOr(&s_bad, 1u);
+      const u64 nv = t.nodes[(lim - 1) + (pos[q] < lim ? pos[q] : 0)];
+      d |= (ok && pos[q] < lim && nv != hv) ? 1u << q : 0u;
+    }
+    u32 nd;
+    const u32 o = block_excl_scan<CSN>((u32)__popc(d), s_wave, &nd);
+    {
+      u32 x = o;
+#pragma unroll
+      for (u32 q = 0; q < CS_PER; q++)
+        if (d >> q & 1u) s_dpos[x++] = pos[q];
+    }
+    __syncthreads();
+    if (s_bad) {
+      h[0] = CS_BAD;
+    } else if (nd == 0) {
+      h[0] = CS_OK;  // {:ok, []}
+    } else if (L < depth) {
+      const u32 k = min(a.levels, depth - L);
+      const u64 need = (u64)nd << k, m = min(need, a.max);
+      h[3] = L + k;
+      if (m > a.ocap) {
+        h[0] = CS_CAP;
+        h[4] = m;
+      } else {
+        const u64 mask = (1ull << k) - 1, base = (1ull << (L + k)) - 1;
+        for (u64 j = tid; j < m; j += CSN) {
+          const u64 p = (s_dpos[j >> k] << k) | (j & mask);
+          a.opos[j] = p;
+          a.ohash[j] = t.nodes[base + p];
+        }
+        h[0] = CS_NODE;
+        h[1] = m;
+      }
+    } else {
+      // the differing buckets -> leaf form, the first `max` of them: one bucket per thread,
+      // its pairs made in registers (the generic loops past CSN buckets)
+      const u64 nb = min<u64>(nd, a.max);
+      h[3] = depth + 1;
+      if (nb <= (u64)CSN) {
+        BucketPairs bp;
+        bp.big = false;
+        bp.head = 0;
+        bp.r = bp.re = 0;
+        u64 b = 0;
+        if ((u64)tid < nb) {
+          b = s_dpos[tid];
+          bucket_pairs(t, a.s, b, bp);
+        }
+        const u32 c = bp.big ? distinct_keys(a.s, bp.r, bp.re) : (u32)__popc(bp.head);
+        u32 np;
+        const u32 po = block_excl_scan<CSN>(c, s_wave, &np);
+        if (np > a.ocap || nb > a.ocap_b) {
+          h[0] = CS_CAP;
+          h[4] = np;
+          h[5] = nb;
+        } else {
+          if ((u64)tid < nb) {
+            a.obucket[tid] = b;
+            if (bp.big) {
+              pairs_global(t, a.s, bp.r, bp.re, a.opos, a.ohash, po);
+            } else {
+              u64 o2 = po;
+#pragma unroll
+              for (int i = 0; i < BR; i++)
+                if (bp.head >> i & 1u) {
+                  a.opos[o2] = bp.key[i];
+                  a.ohash[o2++] = bp.leaf[i];
+                }
+            }
+          }
+          h[0] = CS_LEAF;
+          h[1] = np;
+          h[2] = nb;
+        }
+      } else {
+        u32 c = 0;  // this thread's buckets' distinct keys
+        u64 r[CS_PER], re[CS_PER];
+#pragma unroll
+        for (u32 q = 0; q < CS_PER; q++) {
+          const u64 u = (u64)tid * CS_PER + q;
+          r[q] = re[q] = 0;
+          if (u < nb) bucket_rows(t, a.s, s_dpos[u], r[q], re[q]);
+          c += distinct_keys(a.s, r[q], re[q]);
+        }
+        u32 np;
+        const u32 po = block_excl_scan<CSN>(c, s_wave, &np);
+        if (np > a.ocap || nb > a.ocap_b) {
+          h[0] = CS_CAP;
+          h[4] = np;
+          h[5] = nb;
+        } else {
+          u64 o2 = po;
+#pragma unroll
+          for (u32 q = 0; q < CS_PER; q++) {
+            const u64 u = (u64)tid * CS_PER + q;
+            if (u < nb) a.obucket[u] = s_dpos[u];
+            o2 += pairs_global(t, a.s, r[q], re[q], a.opos, a.ohash, o2);
+          }
+          h[0] = CS_LEAF;
+          h[1] = np;
+          h[2] = nb;
+        }
+      }
+    }
+  } else {
+    // ---- leaf form received (<= CS_B = CSN buckets): the peer's pairs staged, then one
+    //      bucket per thread, its rows' (key, leaf) pairs in registers merged with them
+    static_assert(CS_B <= (u32)CSN, "one bucket per thread");
+    for (u64 i = tid; i < a.n; i += CSN) {
+      s_pk[i] = a.ipos[i];
+      s_ph[i] = a.ihash[i];
+    }
+    __syncthreads();
+    BucketPairs bp;
+    bp.big = false;
+    bp.head = 0;
+    bp.r = bp.re = 0;
+    u64 j = 0, je = 0;
+    u32 c = 0;
+    if ((u64)tid < a.nb) {
+      const u64 b = a.ibucket[tid];
+      if (b >> depth) {
+        atomicOr(&s_bad, 1u);
+      } else {
+        bucket_pairs(t, a.s, b, bp);
+        j = bucket_start(t, s_pk, a.n, b);
+        je = bucket_start(t, s_pk, a.n, b + 1);
+        c = bp.big ? merge_bucket<true, false>(a.s, t.th, bp.r, bp.re, a.s, t.th, s_pk, s_ph, j, je, nullptr, 0, 0)
+                   : merge_regs<false>(bp, s_pk, s_ph, j, je, nullptr, 0, 0);
+      }
+    }
+    u32 tot;
+    const u32 ko = block_excl_scan<CSN>(c, s_wave, &tot);
+    if (s_bad) {
+      h[0] = CS_BAD;
+    } else {
+      if (c) {
+        if (bp.big)
+          merge_bucket<true, true>(a.s, t.th, bp.r, bp.re, a.s, t.th, s_pk, s_ph, j, je, a.keys, ko, a.kcap);
+        else
+          merge_regs<true>(bp, s_pk, s_ph, j, je, a.keys, ko, a.kcap);
+      }
+      h[0] = CS_OK;
+      h[1] = tot;
+    }
+  }
+  if (tid < CS_HDR) {
+    u64 v = 0;
+#pragma unroll
+    for (int i = 0; i < CS_HDR; i++) v = i == tid ? h[i] : v;
+    a.home[tid] = v;
+  }
+  publish_counts(a.d_counts, a.h_pub, a.seq);
+}
+
 MT mt_of(const MerkleT& m) {
   MT t;
   t.depth = m.depth;
@@ -1215,6 +1541,16 @@ hipError_t launch_merkle_update(const MerkleT& m, const Rows& olds, const Rows& 
                        keys, n_keys, dirty, d_keys, err, cd);
   hipLaunchKernelGGL(merkle_chunk_kernel<false>, dim3((unsigned)G), dim3(UPB), 0, st, news, t, dirty,
                      arrive, hand, (u64*)nullptr, err, (const i64*)cd);
+  return hipGetLastError();
+}
+
+hipError_t launch_cont_prepare(const MerkleT& m, u32 L, u64* opos, u64* ohash, hipStream_t st) {
+  hipLaunchKernelGGL(cont_prepare_kernel, dim3(grid_of(1ull << L, PB)), dim3(PB), 0, st, mt_of(m), L, opos, ohash);
+  return hipGetLastError();
+}
+
+hipError_t launch_cont_small(const ContSmallArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(cont_small_kernel, dim3(1), dim3(CSN), 0, st, a, mt_of(a.t));
   return hipGetLastError();
 }
 

@@ -767,6 +767,41 @@ class Engine:
             return ("continue", out)
         return ("ok", keys[: nk.value], int(tot.value))
 
+    def merkle_continue_home(self, tree: MerkleTree, cont: MerkleCont, levels: int = 8,
+                             max_entries: int | None = None, cap: int | None = None):
+        """dg_merkle_continue_home: one hop (continue_partial_diff + truncate_diff to
+        max_entries; None: :infinite) in one launch with one host wait.  ("continue",
+        MerkleCont), ("ok", keys, total), or ("declined",) for a continuation over the
+        one-workgroup limits (then merkle_continue)."""
+        self._order()
+        s = tree.store
+        mx = (1 << 64) - 1 if max_entries is None else int(max_entries)
+        if cap is None:
+            cap = max(cont.n, 1) + s.n
+        keys = torch.empty(max(int(cap), 1), dtype=_I64, device=self.device)
+        cin = cont.abi()
+        t, ss = tree.abi(), s.abi()
+        out_cap, out_bcap = 4 * max(cont.n, 1), max(cont.n, 1)
+        if max_entries is not None:
+            out_cap = min(out_cap, max(int(max_entries), 1))
+        for _ in range(3):
+            out = MerkleCont.empty(out_cap, out_bcap, self.device)
+            co = out.abi()
+            nk, tot, st = C.c_uint64(), C.c_uint64(), C.c_int()
+            rc = self.lib.dg_merkle_continue_home(self.h, C.byref(t), C.byref(ss), C.byref(cin), levels,
+                                                  mx, C.byref(co), _ptr(keys, _abi.P64), int(cap),
+                                                  C.byref(nk), C.byref(tot), C.byref(st))
+            if rc != _abi.DG_E_CAPACITY:
+                break
+            out_cap, out_bcap = max(int(co.n), out_cap), max(int(co.n_buckets), out_bcap)
+        check(rc)
+        if st.value == _abi.DG_CONT_DECLINED:
+            return ("declined",)
+        if st.value == 1:
+            out._set(co)
+            return ("continue", out)
+        return ("ok", keys[: nk.value], int(tot.value))
+
     def merkle_truncate(self, tree: MerkleTree, cont: MerkleCont, max_entries: int) -> MerkleCont:
         """MerkleMap.truncate_diff(cont, max_sync_size) (causal_crdt.ex:98,212-214)."""
         c = cont.abi()

@@ -288,7 +288,9 @@ int dg_join_delta_rows(dg_engine* e, dg_store* state, dg_context* state_ctx, con
  * delta key in `keys` (the sync and mutation shape) -- else DG_HOME_FALLBACK with the
  * state, its context and the tree untouched.  Rows move (a key's row count changed) ->
  * the joined state is in `spare` and the structs are exchanged (*swapped = 1), as
- * dg_join_delta.  Synchronous. */
+ * dg_join_delta.  The delta, its context and `keys` may be device memory or host memory
+ * from dg_host_alloc (the kernel reads them over PCIe: no copy launch for a one-key op);
+ * they must stay unchanged until the call returns.  Synchronous. */
 #define DG_HOME_FALLBACK 1
 #define DG_HOME_KEYS 8
 #define DG_HOME_STRIDE 1536
@@ -441,7 +443,8 @@ int dg_merkle_diff_async(dg_engine* e, const dg_merkle* a, const dg_store* sa, c
                          const dg_store* sb, uint64_t* out_keys, uint64_t cap, uint64_t* d_total);
 
 /* MerkleMap.prepare_partial_diff(mm, levels) (causal_crdt.ex:255): a node-form
- * continuation of the tree's level min(levels, depth), every node of it.  Synchronous. */
+ * continuation of the tree's level min(levels, depth), every node of it.  `out`'s arrays
+ * may be device memory or host memory from dg_host_alloc.  Synchronous. */
 int dg_merkle_prepare(dg_engine* e, const dg_merkle* t, uint32_t levels, dg_merkle_cont* out);
 
 /* MerkleMap.continue_partial_diff(cont, mm, levels) (causal_crdt.ex:96) on the receiving
@@ -459,6 +462,22 @@ int dg_merkle_prepare(dg_engine* e, const dg_merkle* t, uint32_t levels, dg_merk
 int dg_merkle_continue(dg_engine* e, const dg_merkle* t, const dg_store* s, const dg_merkle_cont* in,
                        uint32_t levels, dg_merkle_cont* out, uint64_t* keys, uint64_t cap,
                        uint64_t* n_keys, uint64_t* n_total, int* status);
+
+/* One hop of dg_merkle_continue + dg_merkle_truncate(`max`) in ONE launch with ONE host
+ * wait, for a continuation of at most DG_CONT_HOME_ENTRIES entries (node form) or pairs and
+ * DG_CONT_HOME_BUCKETS buckets (leaf form): what a replica does per anti-entropy message.
+ * `in`, `out` and `keys` may be device memory or host memory from dg_host_alloc (the kernel
+ * reads and writes them over PCIe).  Results as the two calls give them, except that the
+ * capacity asked of `out` is the truncated output's (node form: min(children, max)
+ * entries; leaf form: the first min(buckets, max) buckets and their pairs).  A larger
+ * continuation: *status = DG_CONT_DECLINED and nothing done (use dg_merkle_continue).
+ * DG_E_INVAL for a position or bucket outside the tree (the general path does not check). */
+#define DG_CONT_DECLINED 2
+#define DG_CONT_HOME_ENTRIES 4096
+#define DG_CONT_HOME_BUCKETS 512
+int dg_merkle_continue_home(dg_engine* e, const dg_merkle* t, const dg_store* s, const dg_merkle_cont* in,
+                            uint32_t levels, uint64_t max, dg_merkle_cont* out, uint64_t* keys, uint64_t cap,
+                            uint64_t* n_keys, uint64_t* n_total, int* status);
 
 /* MerkleMap.truncate_diff(cont, max) (causal_crdt.ex:98,212-214): keep the first `max`
  * entries of a node-form continuation, or the pairs of the first `max` buckets of a

@@ -227,6 +227,57 @@ def test_partial_diff_ping_pong(engine, levels, depth):
     assert np.array_equal(rres[1], full)
 
 
+@pytest.mark.parametrize("levels,depth,max_sync", [(8, 18, 200), (3, 10, 7), (1, 4, None), (8, 8, 200),
+                                                    (8, 14, None), (4, 12, 1)])
+def test_continue_home_matches_the_general_hop(engine, levels, depth, max_sync):
+    """dg_merkle_continue_home (one launch, one host wait) against dg_merkle_continue +
+    dg_merkle_truncate on the same continuation, hop for hop on both sides: node form,
+    node -> leaf form, leaf form -> keys; the general calls where it declines."""
+    a, b = W.merkle_pair(n_keys=40000, diff_frac=0.005, seed=levels + depth)
+    sa, _ = up(a)
+    sb, _ = up(b)
+    ta, tb = engine.merkle_build(sa, depth), engine.merkle_build(sb, depth)
+    cont = engine.merkle_prepare(ta, levels)
+    side = [tb, ta]
+    hops = homed = 0
+    while True:
+        t = side[hops % 2]
+        want = engine.merkle_continue(t, cont, levels)
+        if want[0] == "continue" and max_sync is not None:
+            engine.merkle_truncate(t, want[1], max_sync)
+        got = engine.merkle_continue_home(t, cont, levels, max_sync)
+        hops += 1
+        if got[0] == "declined":
+            assert cont.n > 4096 or cont.n_buckets > 512
+            got = want
+        else:
+            homed += 1
+        assert got[0] == want[0]
+        if got[0] == "ok":
+            assert got[2] == want[2] and np.array_equal(u64(got[1]), u64(want[1]))
+            break
+        g, w = got[1], want[1]
+        assert (g.level, g.n, g.n_buckets) == (w.level, w.n, w.n_buckets)
+        assert np.array_equal(u64(g.pos[: g.n]), u64(w.pos[: w.n]))
+        assert np.array_equal(u64(g.hash[: g.n]), u64(w.hash[: w.n]))
+        assert np.array_equal(u64(g.bucket[: g.n_buckets]), u64(w.bucket[: w.n_buckets]))
+        cont = w
+    assert homed >= 1  # (depth 8: the leaf-form hop carries ~31k pairs, over the limit)
+
+
+def test_continue_home_rejects_positions_outside_the_tree(engine):
+    a, _ = W.merkle_pair(n_keys=2000, diff_frac=0.01, seed=3)
+    t = engine.merkle_build(up(a)[0], 10)
+    cont = engine.merkle_prepare(t, 4)
+    cont.pos[3] = 1 << 4  # level 4 holds positions 0..15
+    with pytest.raises(DeltaGpuError, match="outside the tree"):
+        engine.merkle_continue_home(t, cont, 4, 200)
+    # the engine is usable afterwards
+    cont = engine.merkle_prepare(t, 4)
+    res = engine.merkle_continue_home(t, cont, 4, 200)  # (its own tree: nothing differs)
+    assert res[0] == "ok" and res[2] == 0
+
+
 def test_partial_diff_equal_trees_and_truncation(engine):
     a, b = W.merkle_pair(n_keys=20000, diff_frac=0.02, seed=5)
     sa, _ = up(a)
@@ -325,15 +376,18 @@ def test_config4_shard_full_size(engine):
     assert np.array_equal(ta.bucket_counts(), fresh.bucket_counts())
 
 
+@pytest.mark.parametrize("home", [False, True])
 @pytest.mark.parametrize("max_sync_size", [200, None])
-def test_partial_diff_config4_shard(engine, max_sync_size):
+def test_partial_diff_config4_shard(engine, max_sync_size, home):
     """The partial-diff protocol at the scale and shape CausalCrdt runs it:
     a config-4 shard (12.5M keys, 1 % differing, depth 22), prepare_partial_diff(mm, 8) on
     the originator (causal_crdt.ex:255), then continue_partial_diff(cont, mm, 8) ping-pong
     between the replicas (:96), each {:continue, c} truncated to max_sync_size before it
     is sent (:98, default 200: delta_crdt.ex:32; None: :infinite), and the final keys
     truncated too (:105).  Every hop's continuation equals the C oracle's, hashes and
-    all; the keys are the first differing keys of the buckets the truncations kept."""
+    all; the keys are the first differing keys of the buckets the truncations kept.
+    home: each hop through dg_merkle_continue_home (continue + truncate, one launch, one
+    wait), the general calls where it declines (a continuation over its limits)."""
     a, b = W.config4_shard(3, 8, keys_per_rank=12_500_000, diff_frac=0.01)
     sa, _ = up(a)
     sb, _ = up(b)
@@ -346,9 +400,14 @@ def test_partial_diff_config4_shard(engine, max_sync_size):
     assert cont.n == rc[2].size == 256
     side = [(tb, rb, b["rows"]), (ta, ra, a["rows"])]
     hops, sizes = 0, []
+    homed = 0
     while True:
         t, r, rows = side[hops % 2]
-        res = engine.merkle_continue(t, cont, levels)
+        res = engine.merkle_continue_home(t, cont, levels, max_sync_size) if home else ("declined",)
+        truncated = res[0] != "declined"
+        homed += truncated
+        if not truncated:
+            res = engine.merkle_continue(t, cont, levels)
         rres = R.merkle_continue(r, rows, rc, levels)
         hops += 1
         assert res[0] == rres[0]
@@ -356,7 +415,8 @@ def test_partial_diff_config4_shard(engine, max_sync_size):
             break
         cont, rc = res[1], rres[1]
         if max_sync_size is not None:
-            engine.merkle_truncate(t, cont, max_sync_size)
+            if not truncated:
+                engine.merkle_truncate(t, cont, max_sync_size)
             rc = R.merkle_truncate(r, rc, max_sync_size)
         sizes.append((cont.n, cont.n_buckets))
         if rc[0] == "node":
@@ -367,6 +427,8 @@ def test_partial_diff_config4_shard(engine, max_sync_size):
         assert np.array_equal(u64(cont.pos[: cont.n]), rc[2])
         assert np.array_equal(u64(cont.hash[: cont.n]), rc[3])
     assert hops == 4  # level 8 -> 16 -> 22 -> leaf form -> keys
+    if home:  # (infinite: the first hop only -- 65,536 entries come back, over the limit)
+        assert homed == (4 if max_sync_size is not None else 1)
     keys = u64(res[1])
     assert np.array_equal(keys, rres[1])
     full = R.store_diff(a["rows"], b["rows"])
