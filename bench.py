@@ -681,11 +681,12 @@ def _run_json(cmd, timeout=300):
 def mutate_rate(sizes=(1000, 10_000), reps=300):
     """The reference's own benchmark shape (bench/basic_operations.exs:25-41): per-op
     latency of read / add / update / remove on replicas of 1k and 10k keys, each mutation
-    a one-key delta with a MapSet context joined into the GPU-resident state through
-    dg_join_delta (H2D of the delta, the join + changed keys + MerkleMap update, D2H of the
-    changed keys' rows), timed from C over the C-ABI (c_src/bench_mutate.c: no Python in
-    the loop -- what a NIF pays).  `batch_us_per_op`: the trace workload (1000 adds of new
-    keys, :9-23) as ONE delta through one dg_join_delta."""
+    a one-key delta with a MapSet context joined into the GPU-resident state through the
+    NIF's join_delta (c_src/replica.c: dg_join_delta_home -- the keyed join, changed keys,
+    MerkleMap path update and the results written into page-locked memory by one kernel, a
+    copy launch behind it when rows move, one host wait), timed from C (c_src/bench_mutate.c:
+    no Python in the loop -- what a NIF pays).  `batch_us_per_op`: the trace workload (1000
+    adds of new keys, :9-23) as ONE delta through the same call."""
     if not os.path.exists(MUTATE_EXE):
         raise RuntimeError(f"{MUTATE_EXE} is missing: built by __graft_entry__.build()")
     out = {"metric": "per-op latency of a local mutation on a GPU-resident replica "
@@ -693,6 +694,24 @@ def mutate_rate(sizes=(1000, 10_000), reps=300):
            "unit": "us"}
     for n in sizes:
         out[f"keys_{n}"] = _run_json([MUTATE_EXE, str(n), str(reps)])
+    return out
+
+
+HOP_EXE = os.path.join(ROOT, "c_src", "_build", "bench_hop")
+
+
+def hop_rate(n_keys=12_500_000, depth=22, reps=20):
+    """CausalCrdt's anti-entropy exchange (causal_crdt.ex:91-110,252-270) between two
+    config-4-shaped replicas (12.5M keys each, 1 % differing, depth 22, 8 levels per
+    message, max_sync_size 200) through the NIF's calls (c_src/replica.c:
+    dgr_merkle_prepare / dgr_merkle_continue -> dg_merkle_continue_home, one launch and
+    one wait per hop), each message copied between the calls as a send would; wall time
+    per hop, median (c_src/bench_hop.c)."""
+    if not os.path.exists(HOP_EXE):
+        raise RuntimeError(f"{HOP_EXE} is missing: built by __graft_entry__.build()")
+    out = _run_json([HOP_EXE, str(n_keys), str(depth), str(reps)], timeout=600)
+    out["metric"] = "per-message latency of the partial-diff exchange, microseconds, median"
+    out["unit"] = "us"
     return out
 
 
@@ -916,6 +935,7 @@ def main():
         if world == 1:
             secondaries["read_runs32"] = read_runs_rate(eng, torch, dev)
             secondaries["mutate"] = mutate_rate()
+            secondaries["anti_entropy_hops"] = hop_rate()
     if rank == 0:
         res.update(secondaries)
         if not args.no_cpu_baseline and world == 1:
