@@ -257,9 +257,17 @@ __device__ __forceinline__ u64 interp_lower_bound(const u64* k, u64 lo, u64 hi, 
     }
   }
   if (b - a <= 16) {  // the keys of (a, b): loaded together, counted
+    // (every load unconditional at a clamped index: a load under `a + j < b &&` was a
+    // branch, and each was waited for before the next went out -- 15 round trips)
+    // every load issued before any compare (the empty asm is a compiler barrier for memory
+    // operations: without it the scheduler waits for each load before issuing the next)
+    u64 v[15];
+#pragma unroll
+    for (u64 j = 1; j < 16; j++) v[j - 1] = k[a + j < b ? a + j : a];
+    asm volatile("" ::: "memory");
     u64 c = 0;
 #pragma unroll
-    for (u64 j = 1; j < 16; j++) c += (a + j < b && k[a + j] < x) ? 1 : 0;
+    for (u64 j = 1; j < 16; j++) c += ((a + j < b) & (v[j - 1] < x)) ? 1 : 0;
     return a + 1 + c;
   }
   u64 l2 = a + 1, h2 = b;

@@ -273,8 +273,15 @@ __device__ u64 g_sm_stamps[16];
   } while (0)
 #endif
 constexpr int TMAXD = 28;  // the deepest tree (api.hip check_merkle)
+
+// the sibling of bucket b's ancestor l levels up (node 0 past the root): every lane
+// loads every level unconditionally, so all the loads are in flight together (a load
+// under a divergent condition is waited for where the condition ends)
+__device__ __forceinline__ u64 sib_at(u32 dep, u64 b, int l) {
+  return (u32)l < dep ? ((1ull << (dep - l)) - 1) + ((b >> l) ^ 1ull) : 0ull;
+}
 __device__ __forceinline__ void tree_paths(const SmallArgs& p, SmallLds& s, bool dirty, u64 v0, int drows,
-                                           bool moved) {
+                                           bool moved, bool one_path, const u64 (&psib)[TMAXD]) {
   const int tid = threadIdx.x;
   const MerkleT& t = p.t;
   const u32 depth = t.depth;
@@ -294,13 +301,20 @@ __device__ __forceinline__ void tree_paths(const SmallArgs& p, SmallLds& s, bool
   SSTAMP(6);
   if (m == 0) return;  // (uniform)
   auto node_at = [&](u32 level, u64 n) { return nodes + ((1ull << level) - 1) + n; };
-  // the sibling of bucket b's ancestor l levels up (node 0 past the root): every lane
-  // loads every level unconditionally, so all the loads are in flight together (a load
-  // under a divergent condition is waited for where the condition ends)
-  auto sib_at = [&](u32 dep, u64 b, int l) -> u64 {
-    return (u32)l < dep ? ((1ull << (dep - l)) - 1) + ((b >> l) ^ 1ull) : 0ull;
-  };
-  if (m <= (u32)WAVE) {
+  if (one_path) {  // (one key: m == 1) thread 0 up the path, its siblings loaded in step 1
+    if (tid == 0) {
+      const u64 b = s.pb[0];
+      u64 v = s.pv[0][0];
+#pragma unroll
+      for (int l = 0; l < TMAXD; l++) {
+        if ((u32)l < depth) {
+          const u64 n = b >> l;
+          v = (n & 1) ? node_hash(psib[l], v) : node_hash(v, psib[l]);
+          *node_at(depth - l - 1, n >> 1) = v;
+        }
+      }
+    }
+  } else if (m <= (u32)WAVE) {
     if (tid < WAVE) {
       const int lane = tid;
       const bool valid = (u32)lane < m;
@@ -468,6 +482,15 @@ __global__ __launch_bounds__(NT) void small_delta_kernel(SmallArgs p) {
     t_old = p.t.nodes[((1ull << p.t.depth) - 1) + b];
     t_cnt = p.t.counts[b];
   }
+  // one key and a tree: its bucket path's siblings too (wave 0; tree_paths' one-path case)
+  const bool one_path = nk == 1 && p.has_tree;  // (uniform)
+  u64 psib[TMAXD];
+  if (one_path && tid < WAVE) {
+    const u64 b = bucket_of_t(p.t, p.keys[0]);
+#pragma unroll
+    for (int l = 0; l < TMAXD; l++) psib[l] = p.t.nodes[sib_at(p.t.depth, b, l)];
+  }
+  const u64 pubw = p.d_counts[tid & 15];  // the count block (publish_word): unchanged here
   if (nk <= (u32)(NT / WAVE)) {  // (uniform) a few keys: one wave searches each
     const u32 u = (u32)tid / WAVE;
     if (u < nk) {
@@ -488,7 +511,10 @@ __global__ __launch_bounds__(NT) void small_delta_kernel(SmallArgs p) {
     for (;;) {  // the key's run, 4 rows per round trip
       u64 kk[4];
 #pragma unroll
-      for (int q = 0; q < 4; q++) kk[q] = e + q < p.a.n ? p.a.key[e + q] : k + 1;
+      for (int q = 0; q < 4; q++) {  // (unconditional loads at clamped indices: issued together)
+        const u64 v = p.a.key[e + q < p.a.n ? e + q : lo];
+        kk[q] = e + q < p.a.n ? v : k + 1;
+      }
       u32 c = 0;
 #pragma unroll
       for (int q = 0; q < 4; q++) c += (c == (u32)q && kk[q] == k) ? 1u : 0u;
@@ -633,7 +659,7 @@ __global__ __launch_bounds__(NT) void small_delta_kernel(SmallArgs p) {
       res[tid] = tid ? 0ull : (u64)flags;
       home[tid] = tid ? 0ull : (u64)flags;
     }
-    publish_counts(p.d_counts, p.h_pub, p.seq);
+    publish_word(pubw, p.h_pub, p.seq);
     return;
   }
   // ---- 6. writes
@@ -722,9 +748,9 @@ __global__ __launch_bounds__(NT) void small_delta_kernel(SmallArgs p) {
     home[tid] = v;
   }
   SSTAMP(5);
-  if (p.has_tree) tree_paths(p, s, t_dirty, t_new, t_drows, moved);
+  if (p.has_tree) tree_paths(p, s, t_dirty, t_new, t_drows, moved, one_path, psib);
   SSTAMP(9);
-  if (!(moved && p.splice_here)) publish_counts(p.d_counts, p.h_pub, p.seq);
+  if (!(moved && p.splice_here)) publish_word(pubw, p.h_pub, p.seq);
   SSTAMP(10);
 }
 
