@@ -183,7 +183,10 @@ __device__ __forceinline__ void kfold_prep(const KFoldArgs& p) {
   for (int i0 = 0; i0 < k; i0 += 8) {
     u64 c[8];
 #pragma unroll
-    for (int q = 0; q < 8; q++) c[q] = i0 + q < k ? p.tabC[(u64)(i0 + q) * KNT + n] : 0ull;
+    for (int q = 0; q < 8; q++) c[q] = p.tabC[(u64)(i0 + q < k ? i0 + q : i0) * KNT + n];
+    asm volatile("" ::: "memory");  // (all eight issued before any is used)
+#pragma unroll
+    for (int q = 0; q < 8; q++) c[q] = i0 + q < k ? c[q] : 0ull;
 #pragma unroll
     for (int q = 0; q < 8; q++) {
       acc = max(acc, c[q]);
@@ -291,11 +294,21 @@ __global__ __launch_bounds__(FILL_BLOCK) void kfold_fill_kernel(KFoldArgs p) {
     const u64 j0 = n * i / P, jend = n * (i + 1) / P;
     for (u64 jb = j0; jb < jend; jb += (u64)FILL_PER * FILL_BLOCK) {
       u64 kc[FILL_PER], kp[FILL_PER];
+      // (every load unconditional at a clamped index and issued before any use -- the empty
+      // asm keeps the compiler from waiting for each before issuing the next)
 #pragma unroll
       for (int u = 0; u < FILL_PER; u++) {
         const u64 j = jb + (u64)u * FILL_BLOCK + threadIdx.x;
-        kc[u] = j < jend ? keys[j] : 0;
-        kp[u] = (lane == 0 && j > 0 && j < jend) ? keys[j - 1] : 0;  // lanes > 0: DPP
+        const u64 jc = j < jend ? j : j0;
+        kc[u] = keys[jc];
+        kp[u] = keys[jc > 0 ? jc - 1 : 0];  // (lane 0's previous key; lanes > 0: DPP)
+      }
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int u = 0; u < FILL_PER; u++) {
+        const u64 j = jb + (u64)u * FILL_BLOCK + threadIdx.x;
+        kc[u] = j < jend ? kc[u] : 0;
+        kp[u] = (lane == 0 && j > 0 && j < jend) ? kp[u] : 0;
       }
 #pragma unroll
       for (int u = 0; u < FILL_PER; u++) {
