@@ -607,6 +607,15 @@ def config5_rate(eng, torch, dev, rank=0, world=1, n_keys=12_500_000, reps=5, st
     ev1.record(eng.stream)
     eng.sync()
     tk = ev0.elapsed_time(ev1) * 1e-3 / steps
+    # the per-launch timeline of the same back-to-back loop: an event between every two
+    # launches (config 5 reproducible without a profiler in the process)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    evs[0].record(eng.stream)
+    for i in range(steps):
+        launch()
+        evs[i + 1].record(eng.stream)
+    eng.sync()
+    per_launch = [evs[i].elapsed_time(evs[i + 1]) * 1e3 for i in range(steps)]
     out.n = int(d_counts[0].item())
     octx.n = int(d_counts[1].item())
 
@@ -625,7 +634,11 @@ def config5_rate(eng, torch, dev, rank=0, world=1, n_keys=12_500_000, reps=5, st
                       "achieved": alg / tk / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                       "frac": alg / tk / 1e9 / HBM_PEAK_GBS,
                       "launch_timing": f"HIP events on the engine stream around {steps} "
-                                       "back-to-back dg_join2_async launches"},
+                                       "back-to-back dg_join2_async launches",
+                      "per_launch_us": [round(x, 2) for x in per_launch],
+                      "per_launch_median_us": sorted(per_launch)[len(per_launch) // 2],
+                      "per_launch_timing": "the same loop again with an event between every "
+                                           "two launches (no profiler in the process)"},
          "rows_in": n_in, "rows_out": out.n, "ms_per_read": tr * 1e3,
          "read_rows_per_s": out.n / tr, "read_keys_per_s": res["keys"] / tr,
          "read_keys": res["keys"], "read_alg_GBps": (36 * out.n + 16 * res["keys"]) / tr / 1e9,

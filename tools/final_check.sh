@@ -14,7 +14,7 @@ cp gpurun_out/join2_pmc.json profiles/join2_pmc.json
 grep hbm_bytes_per_launch $O/pmc_traffic.log
 timeout -k 10 900 python -u -m pytest tests -q --maxfail=10 --timeout 600 --timeout-method thread -m gpu > $O/pytest_gpu.log 2>&1 || { echo TESTS_FAILED; tail -3 $O/pytest_gpu.log; grep -E "^(FAILED|ERROR)" $O/pytest_gpu.log | head; exit 1; }
 tail -1 $O/pytest_gpu.log
-timeout -k 10 600 python -u bench.py > $O/bench.log 2>&1 || { echo BENCH_FAILED; tail -20 $O/bench.log; exit 1; }
+timeout -k 10 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.log 2>&1 || { echo BENCH_FAILED; tail -20 $O/bench.log; exit 1; }
 grep '^{"metric"' $O/bench.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); m=d['merkle']; print('headline', round(d['roofline']['frac'],4), d['roofline']['traffic'], 'c5', round(d['config5']['roofline']['frac'],4), 'c3', round(d['config3']['roofline']['frac'],4), 'build', round(m['roofline']['frac'],4), 'diff', round(m['diff_roofline']['frac'],4))"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c2 -o c2 -- python3 $R/bench.py --no-merkle --no-configs --no-cpu-baseline --steps 400 --warmup 50 > $O/c2.log 2>&1 || { echo PROF_C2_FAILED; tail -5 $O/c2.log; exit 1; }
