@@ -508,7 +508,7 @@ __global__ __launch_bounds__(NT) void small_delta_kernel(SmallArgs p) {
     const u64 k = p.keys[tid];
     const u64 lo = interp_lower_bound(p.a.key, 0, p.a.n, k);
     u64 e = lo;
-    for (;;) {  // the key's run, 4 rows per round trip
+    while (p.a.n > 0) {  // the key's run, 4 rows per round trip (an empty state: none)
       u64 kk[4];
 #pragma unroll
       for (int q = 0; q < 4; q++) {  // (unconditional loads at clamped indices: issued together)

@@ -449,3 +449,39 @@ def test_home_declines_and_leaves_the_state(engine):
         spare = Store.empty(st.n + sd.n, DEV)
         assert engine.join_delta_home(st, sc, sd, cd, kdev(keys), spare, tree) is None
         _assert_unchanged(st, sc, tree, snap)
+
+
+@pytest.mark.parametrize("with_tree", [False, True])
+def test_home_from_an_empty_state(engine, with_tree):
+    """A replica's first mutations (causal_crdt.ex:337-342 on a fresh AWLWWMap): the small
+    path from an empty state -- no state rows to search or move -- then more adds and a
+    remove, each against the oracle's fold (and a fresh tree)."""
+    rows = (np.zeros(0, np.uint64), np.zeros(0, np.uint64), np.zeros(0, np.int64),
+            np.zeros(0, np.uint32), np.zeros(0, np.uint64))
+    ctx = (R.VV, np.array([0], np.uint32), np.array([0], np.uint64))
+    st = Store.empty(64, DEV)
+    sc = Context.empty(R.VV, 8, DEV)
+    sc.node[0] = 0
+    sc.cnt[0] = 0
+    sc.n = 1
+    spare = Store.empty(64, DEV)
+    tree = engine.merkle_build(st, 6) if with_tree else None
+    ops = [("add", 5 << 58, 7, 100), ("add", 3 << 60, 8, 101), ("add", 5 << 58, 9, 102),
+           ("remove", 3 << 60, 0, 0), ("add", 1, 1, 103)]
+    for op in ops:
+        drows, dctx, dkeys = R.mutate_batch(rows, ctx, 0, [op])
+        sd, cd = up({"rows": drows, "ctx": dctx})
+        got = engine.join_delta_home(st, sc, sd, cd, kdev(dkeys), spare, tree)
+        assert got is not None
+        changed, hrows, hctx, swapped = got
+        if swapped:
+            spare = Store.empty(64, DEV)
+        wr, wc = R.join2(rows, ctx, drows, dctx, keys=dkeys)
+        assert np.array_equal(changed, R.changed_keys(rows, wr, dkeys))
+        rows, ctx = wr, wc
+        rows_eq(st, rows)
+        ctx_eq(sc, ctx)
+        if with_tree:
+            fresh = engine.merkle_build(st, 6)
+            assert np.array_equal(tree.nodes.cpu().numpy(), fresh.nodes.cpu().numpy())
+            assert np.array_equal(tree.bucket_counts(), fresh.bucket_counts())
