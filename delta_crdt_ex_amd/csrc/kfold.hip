@@ -501,6 +501,9 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
     s.rbeg[tid] = a;
   }
   bad = __syncthreads_or(bad);
+#ifdef DG_KFOLD_NO_STATE  // experiment build only: the delta-only half of the bucket work
+  nS = 0;                 // (what pass 1 of a two-pass fold would cost)
+#endif
   // the state row's loads go out now (they need only s0 and nS): they fly during the run
   // offsets' scan and the item loads, so staging costs one round trip, not two
   static_assert(CS <= KB && CU <= KB, "one state row and one item per thread");
