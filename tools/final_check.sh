@@ -19,6 +19,8 @@ grep '^{"metric"' $O/bench.log | python3 -c "import json,sys; d=json.loads(sys.s
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c2 -o c2 -- python3 $R/bench.py --no-merkle --no-configs --no-cpu-baseline --steps 400 --warmup 50 > $O/c2.log 2>&1 || { echo PROF_C2_FAILED; tail -5 $O/c2.log; exit 1; }
 python3 $R/tools/kernel_timeline.py $O/c2 0 | head -4
+python3 $R/tools/kernel_timeline.py $O/c2 400 join2_stream > $O/c2_timed_window.txt && cat $O/c2_timed_window.txt
+grep '^{"metric"' $O/c2.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('c2 under rocprofv3: bench events avg_launch_us', d['roofline']['avg_launch_us'])" >> $O/c2_timed_window.txt
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c5 -o c5 -- python3 $R/tools/bench_c5_line.py > $O/c5.log 2>&1 || { echo PROF_C5_FAILED; tail -5 $O/c5.log; exit 1; }
 python3 $R/tools/kernel_timeline.py $O/c5 0 | head -4
 grep '^{"metric"' $O/c5.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('c5 events avg_launch_us', d['roofline']['avg_launch_us'], 'frac', d['roofline']['frac'])"
