@@ -826,17 +826,24 @@ def main():
         dist.barrier()
     # HIP events on the engine stream bracket the timed region: the average launch
     # duration of the join (its kernels plus the gaps between back-to-back launches)
+    # (ev0 goes in behind the FIRST timed step: it fires when that join ends, so the events
+    # time steps 2..K back to back on the GPU and not the host's latency to submit step 1
+    # into an idle stream; the wall clock below times all K)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    if args.steps > 1:
+        launches[0]()
     ev0.record(stream)
-    for i in range(args.steps):
+    for i in range(1 if args.steps > 1 else 0, args.steps):
         launches[i % R]()
     ev1.record(stream)
+    host_submit_s = time.perf_counter() - t0
     eng.sync()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    avg_launch_s = ev0.elapsed_time(ev1) / 1e3 / args.steps
+    ev_steps = args.steps - 1 if args.steps > 1 else 1
+    avg_launch_s = ev0.elapsed_time(ev1) / 1e3 / ev_steps
     if world > 1:
         dist.barrier()
 
@@ -911,7 +918,9 @@ def main():
                           "and the events bracket both)",
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_launch_us": avg_launch_s * 1e6,
-                "launch_timing": "HIP events on the engine stream around the timed region / steps",
+                "launch_timing": "HIP events on the engine stream from the end of the timed "
+                                 "region's first step to the end of its last, / (steps - 1)",
+                "host_submit_us_per_step": host_submit_s / args.steps * 1e6,
                 "per_step_event_median_us": step_event_median_us,
                 "settle": {"ms": args.settle_ms, "joins": n_settle,
                            "note": "untimed joins before the warm-up steps"},
