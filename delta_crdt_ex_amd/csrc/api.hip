@@ -407,9 +407,9 @@ int join2_enqueue(dg_engine* e, const dg_store* a, const dg_context* ca, const d
   if (a->n + b->n && (!out->key || !out->val || !out->ts || !out->node || !out->cnt))
     return fail(DG_E_INVAL, "dg_join2: null output column");
   TRY(set_device(e));
-  TRY(ensure_state(e, 3 * join2_tiles(a->n, b->n) + 3));  // granules + tile + keyset splits
+  TRY(ensure_state(e, 3 * join2_tiles_cap(a->n, b->n) + 3));  // granules + tile + keyset splits
   const bool two_pass = (force_two_pass || e->join_mode == JOIN_TWO_PASS) && !chg;  // changes: single pass
-  if (!two_pass) TRY(ensure_counts(e, join2_tiles(a->n, b->n)));
+  if (!two_pass) TRY(ensure_counts(e, join2_tiles_cap(a->n, b->n)));
   const size_t ctx_bytes = (ctx_union_tmp_bytes(ca->n, cb->n) + 255) / 256 * 256;
   const size_t pass_bytes = two_pass ? (join2_pass_tmp_bytes(a->n, b->n) + 255) / 256 * 256 : 0;
   const size_t chg_bytes = chg ? join2_changes_tmp_bytes(a->n, b->n) : 0;

@@ -40,6 +40,9 @@ constexpr int JOIN_ITEMS = DG_JOIN_ITEMS;  // merged positions per thread
 constexpr int JOIN_TILE = JOIN_BLOCK * JOIN_ITEMS - 8;
 
 inline u64 join2_tiles(u64 na, u64 nb) { return (na + nb + JOIN_TILE - 1) / JOIN_TILE; }
+// tiles of a join after launch_join2 re-cuts them to fill its grid's stripes (fewer than
+// one more per workgroup): what the split and tile-count scratch is sized for
+inline u64 join2_tiles_cap(u64 na, u64 nb) { return join2_tiles(na, nb) + JOIN_MAX_GRID; }
 // join/3: a merge-path partition pass (its extra workgroup computes the context union,
 // d_counts[1] = its size), then one workgroup per tile that merges it, resolves its
 // output offset by decoupled look-back and writes its kept rows (d_counts[0] = output

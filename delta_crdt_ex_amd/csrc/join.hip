@@ -50,6 +50,7 @@ namespace {
 constexpr int JB = JOIN_BLOCK;
 constexpr int JI = JOIN_ITEMS;
 constexpr int JT = JOIN_TILE;
+static_assert(JT % 2 == 0, "even tiles (balance_tiles keeps them even)");
 constexpr int JS = JT + 5;  // LDS row slots: tile rows + one neighbour on each side per store
                             // (+1: the merge's look-ahead read past the last B slot)
 constexpr int VT = 64;      // VV table: node ids below this are looked up directly in LDS
@@ -265,6 +266,8 @@ struct JoinArgs {
   const u64* splits;  // merge-path split (a index) of every tile boundary (partition pass)
   u64* ksplits;       // keyed joins: first index of `keys` >= the key at every tile boundary
   u64 ntiles;
+  u64 jt;     // merged positions per tile, <= JT (launch_join2 spreads the tiles evenly
+              // over the grid's stripes)
   RowsOut out;
   Scan scan;  // look-back granules + tile tickets
   u64* d_count;
@@ -416,7 +419,7 @@ __device__ __forceinline__ u64 key_split(const Rows& A, const Rows& B, const u64
   return wave_lower_bound(keys, n_keys, min(ka, kb));
 }
 
-__global__ __launch_bounds__(PB) void join2_partition_kernel(Rows A, Rows B, u64 ntiles,
+__global__ __launch_bounds__(PB) void join2_partition_kernel(Rows A, Rows B, u64 ntiles, u64 jt,
                                                              u64* splits, CtxUnionArgs cu,
                                                              const u64* keys, u64 n_keys,
                                                              u64* ksplits) {
@@ -430,7 +433,7 @@ __global__ __launch_bounds__(PB) void join2_partition_kernel(Rows A, Rows B, u64
   }
   const u64 q = (u64)(blockIdx.x - 1) * (PB / WAVE) + (threadIdx.x >> 6);
   if (q > ntiles) return;
-  const u64 d = min(q * (u64)JT, A.n + B.n);
+  const u64 d = min(q * jt, A.n + B.n);
   const u64 s = mp_split(A, B, d);
   if ((threadIdx.x & (WAVE - 1)) == 0) splits[q] = s;
   if (keys) {
@@ -692,9 +695,9 @@ struct Staged {  // one thread's share of a staged tile, in registers
   bool ok[SLOTS];
 };
 
-__device__ __forceinline__ void tile_geom(u64 t, u64 a0, u64 a1, u64 total, int* nat, int* nbt,
-                                          u64* b0) {
-  const u64 d0 = t * JT, d1 = min(d0 + (u64)JT, total);
+__device__ __forceinline__ void tile_geom(u64 t, u64 jt, u64 a0, u64 a1, u64 total, int* nat,
+                                          int* nbt, u64* b0) {
+  const u64 d0 = t * jt, d1 = min(d0 + jt, total);
   *nat = (int)(a1 - a0);
   *nbt = (int)((d1 - a1) - (d0 - a0));
   *b0 = d0 - a0;
@@ -937,11 +940,11 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     // the exact search: replicas that hold the same keys (config 2) split exactly there,
     // so the tile streams in during the search (checked below; re-issued otherwise).
     {
-      ga0 = split_guess(A.n, B.n, w * (u64)JT);
-      ga1 = split_guess(A.n, B.n, min((w + 1) * (u64)JT, total));
+      ga0 = split_guess(A.n, B.n, w * p.jt);
+      ga1 = split_guess(A.n, B.n, min((w + 1) * p.jt, total));
       int gnat, gnbt;
       u64 gb0;
-      tile_geom(w, ga0, ga1, total, &gnat, &gnbt, &gb0);
+      tile_geom(w, p.jt, ga0, ga1, total, &gnat, &gnbt, &gb0);
       issue_tile(A, B, gnat, gnbt, ga0, gb0, r);
     }
     // merge-path splits of this workgroup's (<= FUSE_IT) tiles: boundary q (tile q / 2,
@@ -949,7 +952,7 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     for (int q = tid / WAVE; q < 2 * FUSE_IT; q += JB / WAVE) {  // (wave-uniform)
       const u64 tk = w + (u64)(q >> 1) * G;
       if (tk >= ntiles) break;
-      const u64 d = min((tk + (q & 1)) * (u64)JT, total);
+      const u64 d = min((tk + (q & 1)) * p.jt, total);
       // the proportional split is checked first with scalar loads (a counter the tile
       // loads in flight do not hold up); the search runs only where it is not exact
       const u64 g = split_guess(A.n, B.n, d);
@@ -993,7 +996,7 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   u64 a0 = split(t, 0, 0), a1 = split(t, 0, 1);
   int nat, nbt;
   u64 b0;
-  tile_geom(t, a0, a1, total, &nat, &nbt, &b0);
+  tile_geom(t, p.jt, a0, a1, total, &nat, &nbt, &b0);
   if (!LATE || a0 != ga0 || a1 != ga1) issue_tile(A, B, nat, nbt, a0, b0, r);  // (uniform)
   u64 kl = 0, km = 0, kk = 0;
   if (KEYED) {
@@ -1023,7 +1026,7 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     auto issue_next = [&]() {
       a0n = split(tn, k + 1, 0);
       a1n = split(tn, k + 1, 1);
-      tile_geom(tn, a0n, a1n, total, &natn, &nbtn, &b0n);
+      tile_geom(tn, p.jt, a0n, a1n, total, &natn, &nbtn, &b0n);
       issue_tile(A, B, natn, nbtn, a0n, b0n, r);
       if (KEYED) {
         kmn = kslice(tn, k + 1, &kln);
@@ -1315,7 +1318,7 @@ __global__ __launch_bounds__(JB) void join2_slot_kernel(JoinArgs p) {
   const u64 a0 = p.splits[t], a1 = p.splits[t + 1];
   int nat, nbt;
   u64 b0;
-  tile_geom(t, a0, a1, total, &nat, &nbt, &b0);
+  tile_geom(t, p.jt, a0, a1, total, &nat, &nbt, &b0);
   Staged r;
   issue_tile(p.a, p.b, nat, nbt, a0, b0, r);
   __syncthreads();  // zeroed tables visible
@@ -1459,6 +1462,27 @@ static CtxUnionArgs make_cu(const Ctx& a, const Ctx& b, u32* out_node, u64* out_
   return p;
 }
 
+// A stream grid of G workgroups runs ceil(ntiles / G) stripes, the last one partly
+// idle (config 2: 1969 tiles of 1016 positions on 512 workgroups, the fourth stripe 433
+// tiles).  The tiles are re-cut to jt = ceil(total / (stripes x G)) <= JT positions, so
+// every stripe is full and each of them carries less: ntiles grows by less than G
+// (join2_tiles_cap sizes the scratch).  Fused joins only (at most FUSE_IT stripes, so a
+// part-idle last stripe is a large share): config 2 34.3-35.0 against 36.4-38.6 us per
+// join (A/B, one box).  The long partitioned joins keep JT (config 5 measured 368-370
+// against 340-344 us re-cut, one stripe in 44 being part idle), and so do the
+// changed-keys joins, whose event scratch is laid out by join2_tiles.
+static void balance_tiles(JoinArgs& p, u64 G) {
+  const u64 total = p.a.n + p.b.n;
+  if (G == 0 || p.ntiles <= G) return;
+  const u64 k = (p.ntiles + G - 1) / G;
+  // (even, as JT is: two replicas of the same keys merge in pairs, so an even diagonal is
+  // split exactly by the proportional guess the fused kernel checks first -- odd tiles
+  // sent half the boundaries to the search: 42.4 against 35.1 us at config 2)
+  const u64 jt = std::min<u64>(((total + k * G - 1) / (k * G) + 1) & ~1ull, JT);
+  p.jt = jt;
+  p.ntiles = (total + jt - 1) / jt;
+}
+
 hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& cb,
                         const u64* keys, u64 n_keys, const RowsOut& out, u32* out_ctx_node,
                         u64* out_ctx_cnt, void* ctx_tmp, void* pass_tmp, int mode,
@@ -1472,9 +1496,14 @@ hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& 
   p.keys = keys;
   p.n_keys = n_keys;
   p.ntiles = join2_tiles(a.n, b.n);
-  u64* splits = scan.state + p.ntiles;  // look-back granules first, then the splits,
-  p.splits = splits;                    // then the keyset splits (keyed joins)
-  p.ksplits = splits + p.ntiles + 1;
+  p.jt = JT;
+  // scan.state: look-back granules first, then the splits, then the keyset splits (keyed
+  // joins); set again when the tiles are re-cut (balance below)
+  auto place_splits = [&]() {
+    p.splits = scan.state + p.ntiles;
+    p.ksplits = scan.state + 2 * p.ntiles + 1;
+  };
+  place_splits();
   const CtxUnionArgs cu = make_cu(ca, cb, out_ctx_node, out_ctx_cnt, d_counts + 1, ctx_tmp);
   p.out = out;
   p.scan = scan;
@@ -1529,13 +1558,15 @@ hipError_t launch_join2(const Rows& a, const Ctx& ca, const Rows& b, const Ctx& 
     const u64 gr = workers > 0 ? g + 1 : resident_grid((const void*)kern_late);
     const u64 gt = std::min<u64>(std::min<u64>(p.ntiles, gr - 1), (u64)CQ * JB);
     if (!no_fuse && gr >= 2 && p.ntiles <= (u64)FUSE_IT * gt) {
+      if (!chg_tmp) balance_tiles(p, gt);
+      place_splits();
       p.fused = 1;
       return launch_stream(kern_late, gt + 1, p, st);
     }
   }
   const u64 nb_part = (p.ntiles + 1 + (PB / WAVE) - 1) / (PB / WAVE);
   hipLaunchKernelGGL(join2_partition_kernel, dim3((unsigned)nb_part + 1), dim3(PB), 0, st, a, b,
-                     p.ntiles, splits, cu, keys, n_keys, p.ksplits);
+                     p.ntiles, p.jt, scan.state + p.ntiles, cu, keys, n_keys, p.ksplits);
   if (!stream) {
     char* t = (char*)pass_tmp;
     p.counts = (u32*)t;

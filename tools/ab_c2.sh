@@ -4,7 +4,7 @@ set -o pipefail
 R=$GRAFT_REPO_ROOT
 export DG_LIB_ANY_DIGEST=1
 mkdir -p $R/gpurun_out/abc2
-for round in 1 2; do
+for round in $(seq 1 ${ROUNDS:-2}); do
   for v in intree "$@"; do
     if [ $v = intree ]; then unset DG_LIB_PATH; else export DG_LIB_PATH=$R/delta_crdt_ex_amd/ab/$v; fi
     timeout -k 10 300 python -u $R/bench.py --no-cpu-baseline --no-merkle --no-configs --steps 20 --warmup 5 > $R/gpurun_out/abc2/$v.log 2>&1 || { echo FAIL $v; tail -5 $R/gpurun_out/abc2/$v.log; exit 1; }
