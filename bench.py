@@ -966,6 +966,8 @@ def main():
                 res["cpu_baseline"]["mutate"] = mutate_cpu_baseline()
         elif not args.no_cpu_baseline:
             res["cpu_baseline"] = None
+        import resource
+        res["host_peak_rss_gb"] = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20  # (KiB)
         print(json.dumps(res), flush=True)
     eng.close()
     if world > 1:
