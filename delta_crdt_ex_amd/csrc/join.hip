@@ -15,8 +15,9 @@
 //
 // Kernel shape (HBM-bound integer merge; no MFMA):
 //   1. join2_partition_kernel: one wave per tile boundary finds the merge-path split
-//      of diagonal q*JT.  Key ids are 64-bit hashes, so the key gap at the proportional
-//      split (one probe) lands within a few rows of the split and one 128-wide window
+//      of diagonal q*jt (jt = JT, or less: balance_tiles).  Key ids are 64-bit hashes,
+//      so the key gap at the proportional split (one probe) lands within a few rows of
+//      the split and one 128-wide window
 //      round finishes it (~5 cache lines per array instead of a 21-step search); any
 //      key distribution stays exact through a 128-ary fallback search.  One extra
 //      workgroup (the grid's first) computes the context union Dots.union(c1, c2) (:155).
@@ -408,7 +409,7 @@ __device__ __forceinline__ bool guess_exact(const Rows& A, const Rows& B, u64 d,
 }
 
 // Keyed joins: the first index of keys[0, n_keys) >= the key at merged position d (split
-// s), by the calling wave.  Tile t's keys lie in [key(t*JT), key((t+1)*JT)], so the
+// s), by the calling wave.  Tile t's keys lie in [key(t*jt), key((t+1)*jt)], so the
 // keyset entries they can match are [ksplit(t), ksplit(t+1)] (keys are unique).
 __device__ __forceinline__ u64 key_split(const Rows& A, const Rows& B, const u64* keys, u64 n_keys,
                                          u64 d, u64 s) {
