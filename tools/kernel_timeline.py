@@ -9,8 +9,11 @@ import csv
 import glob
 import os
 import re
+import signal
 import statistics
 import sys
+
+signal.signal(signal.SIGPIPE, signal.SIG_DFL)  # (piped into head: end quietly)
 
 d = sys.argv[1]
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 40
