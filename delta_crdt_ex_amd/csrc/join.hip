@@ -17,7 +17,7 @@
 //   1. join2_partition_kernel: one wave per tile boundary finds the merge-path split
 //      of diagonal q*jt (jt = JT, or less: balance_tiles).  Key ids are 64-bit hashes,
 //      so the key gap at the proportional split (one probe) lands within a few rows of
-//      the split and one 128-wide window
+//      the split and one 64-wide window
 //      round finishes it (~5 cache lines per array instead of a 21-step search); any
 //      key distribution stays exact through a 128-ary fallback search.  One extra
 //      workgroup (the grid's first) computes the context union Dots.union(c1, c2) (:155).
@@ -334,8 +334,8 @@ __device__ u64 mp_search(const Rows A, const Rows B, u64 d, u64 lo, u64 hi) {
 }
 
 // Merge-path split of diagonal d (= #A rows among the first d merged rows).
-// A window of 128 consecutive candidates is decided in ONE round trip (two per lane,
-// ballots), first around the proportional guess d * na / (na + nb): replicas that share
+// A window of 64 consecutive candidates is decided in ONE round trip (one per lane,
+// a ballot), first around the proportional guess d * na / (na + nb): replicas that share
 // most keys (config 2) split there exactly.  If the window does not bracket the split,
 // the key gap B.key[d-1-c] - A.key[c] at the window's middle c (in units of the 2^64
 // key space; the rows were just loaded, so this is a cache hit) converts to a row shift
@@ -362,19 +362,16 @@ __device__ u64 mp_split(const Rows A, const Rows B, u64 d) {
     i = (u64)ni;
   }
   for (int r = 0; r < 3; r++) {
-    u64 wlo = i > lo + PK / 2 ? i - PK / 2 : lo;
-    const u64 whi = min(wlo + (u64)PK, hi);
-    wlo = whi - PK > lo ? whi - PK : lo;
-    const u64 x0 = wlo + 2 * lane, x1 = x0 + 1;
-    const bool f0 = x0 < whi && !mp_pred(A, B, d, x0);
-    const bool f1 = x1 < whi && !mp_pred(A, B, d, x1);
-    const u64 m0 = __ballot(f0), m1 = __ballot(f1);
-    u64 kf = whi - wlo;  // first false candidate in the window (none: whi - wlo)
-    if (m0 | m1) {
-      const int l0 = m0 ? __ffsll((long long)m0) - 1 : 64;
-      const int l1 = m1 ? __ffsll((long long)m1) - 1 : 64;
-      kf = (l0 <= l1) ? 2 * l0 : 2 * l1 + 1;
-    }
+    // one candidate per lane: the gap-shifted guess is a median 11 rows off at config 5,
+    // so 64-wide windows bracket as well as 128-wide ones and read half the keys
+    // (partition 19.0 -> 16.9 us per config-5 join, rocprofv3 A/B)
+    constexpr u64 PW = WAVE;
+    u64 wlo = i > lo + PW / 2 ? i - PW / 2 : lo;
+    const u64 whi = min(wlo + PW, hi);
+    wlo = whi - PW > lo ? whi - PW : lo;
+    const u64 x0 = wlo + lane;
+    const u64 m0 = __ballot(x0 < whi && !mp_pred(A, B, d, x0));
+    const u64 kf = m0 ? (u64)(__ffsll((long long)m0) - 1) : whi - wlo;
     // bracketed iff the first false is not at the window's low edge (unless that edge is
     // lo) and some candidate is false (unless the window reaches hi)
     if ((kf > 0 || wlo == lo) && (kf < whi - wlo || whi == hi)) return wlo + kf;
