@@ -438,6 +438,18 @@ __device__ __forceinline__ Row drow(const KLds& s, u32 d) {
   return r;
 }
 
+// Delta row d / state row i equal to r, whose key is already known to be equal: the
+// other columns read one at a time, stopping at the first that differs (usually the value).
+// The key-mask walks compare this way (and skip an item's compare with itself): 707 ->
+// 691 us per config-3 fold (rocprofv3 A/B); the rank walks' order compares read lazily
+// measured 695 us, and stay eager.
+__device__ __forceinline__ bool drow_eq_k(const KLds& s, u32 d, const Row& r) {
+  return s.dval[d] == r.val && s.dts[d] == r.ts && s.dnode[d] == r.node && s.dcnt[d] == r.cnt;
+}
+__device__ __forceinline__ bool srow_eq_k(const KLds& s, u32 i, const Row& r) {
+  return s.sval[i] == r.val && s.sts[i] == r.ts && s.snode[i] == r.node && s.scnt[i] == r.cnt;
+}
+
 // sub-bucket of a key of bucket t: the next log2(NSUB) bits of its position in key space
 __device__ __forceinline__ u32 sub_of(u64 key, u64 T, u64 t) {
   return (u32)(__umul64hi(key, T * NSUB) - t * NSUB);
@@ -716,7 +728,7 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
       if (tg & (MARK | KIN)) cs.K |= 1ull << src;
       if (!(tg & MARK)) {
         cs.R |= 1ull << src;
-        if (row_eq(drow(s, tg & SLOT), r)) cs.M |= 1ull << src;
+        if (drow_eq_k(s, tg & SLOT, r)) cs.M |= 1ull << src;
       }
     }
     cs.node = r.node;
@@ -736,7 +748,7 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
       if (te & (MARK | KIN)) cu.K |= 1ull << se;
       if (!(te & MARK)) {
         cu.R |= 1ull << se;
-        if (row_eq(drow(s, te & SLOT), r)) {
+        if (e == (u32)tid || drow_eq_k(s, te & SLOT, r)) {  // (the item itself: no reads)
           cu.M |= 1ull << se;
           if (se < src) first = false;
         }
@@ -748,7 +760,7 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
     const u32 ie = s.y.e.sfirst[sb + 1];
     while (i < ie && s.skey[i] < r.key) i++;
     for (; first && i < ie && s.skey[i] == r.key; i++)
-      if (row_eq(srow(s, i), r)) first = false;
+      if (srow_eq_k(s, i, r)) first = false;
     du = first;
     cu.node = r.node;
     cu.cnt = r.cnt;
