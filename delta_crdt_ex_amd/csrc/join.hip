@@ -482,15 +482,20 @@ __device__ __forceinline__ bool key_in(const KeySlice& ks, u64 x) {
 
 // VV tables: tab_a[node] / tab_b[node] = the VV's counter for node ids < VT (coalesced
 // loads; the tables must have been zeroed behind a barrier).
-__device__ __forceinline__ void fill_vv_tables(const Ctx& ca, const Ctx& cb, u64* tab_a, u64* tab_b) {
+// Returns whether this thread met a node id >= VT (a VV entry outside the tables).
+__device__ __forceinline__ bool fill_vv_tables(const Ctx& ca, const Ctx& cb, u64* tab_a, u64* tab_b) {
+  bool far = false;
   for (u64 i = threadIdx.x; i < ca.n; i += JB) {
     const u32 nd = ca.node[i];
     if (nd < (u32)VT) tab_a[nd] = ca.cnt[i];
+    far |= nd >= (u32)VT;
   }
   for (u64 i = threadIdx.x; i < cb.n; i += JB) {
     const u32 nd = cb.node[i];
     if (nd < (u32)VT) tab_b[nd] = cb.cnt[i];
+    far |= nd >= (u32)VT;
   }
+  return far;
 }
 
 // ------------------------------------------------------------------- staging
@@ -554,7 +559,7 @@ constexpr int STOP = search_top(JT);
 // CHG: also set bit k of `ev` when item k changes its key's rows (diff/3 of
 // causal_crdt.ex:343-351 over `keys`): a dropped a row or a newly kept b row.
 // FAST: both contexts are version vectors (LDS counter tables); KEYED: a `keys` list.
-template <bool FAST, bool KEYED, bool CHG = false>
+template <bool FAST, bool KEYED, bool CHG = false, bool NOFB = false>
 __device__ __forceinline__ void merge_items(const Ctx& ca, const Ctx& cb, const u64* tab_a,
                                             const u64* tab_b, const KeySlice& ks,
                                             const u64 nb, const Buf& s, int nat, int nbt, u64 a0,
@@ -625,6 +630,8 @@ __device__ __forceinline__ void merge_items(const Ctx& ca, const Ctx& cb, const 
       bool cov;
       if (dn < (u32)VT) {
         cov = (takeA ? tab_b : tab_a)[dn] >= dc;
+      } else if (NOFB) {
+        cov = dc == 0;  // no VV has an entry >= VT: Map.get(vv, dn, 0) = 0
       } else {
         const u32* vn = takeA ? opaque_ptr(cb.node) : opaque_ptr(ca.node);
         const u64* vc = takeA ? opaque_ptr(cb.cnt) : opaque_ptr(ca.cnt);
@@ -1008,7 +1015,11 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   }
   __syncthreads();  // zeroed tables visible
   if (w < G) JSTAMP(w, 9);  // (stamps build: first tile's loads issued)
-  if (FAST) fill_vv_tables(p.ca, p.cb, s.tab[0], s.tab[1]);  // once per workgroup
+  bool vv_far = false;
+  if (FAST) {
+    vv_far = fill_vv_tables(p.ca, p.cb, s.tab[0], s.tab[1]);  // once per workgroup
+    if (LATE) vv_far = __syncthreads_or(vv_far);
+  }
   u64 base = 0;  // output offset of the first tile of the current stripe
   u32 np = 0;    // kept rows of this workgroup's tile of the previous stripe
   for (int k = 0;; k++) {
@@ -1043,8 +1054,17 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     u32 keep, ev = 0;
     unsigned short src[JI];
     const KeySlice ks{KEYED && km <= (u64)KS ? s.kslice[bi] : nullptr, p.keys + kl, km};
-    merge_items<FAST, KEYED, CHG>(p.ca, p.cb, s.tab[0], s.tab[1], ks, B.n, s.buf[bi], nat, nbt, a0,
-                                  b0, keep, src, &ev);
+    // (fused joins whose VVs have no entry beyond the LDS tables -- every real replica set:
+    // the merge without the global-memory coverage search, whose flat loads made each of
+    // the merge's LDS waits also wait for the stripe counts in flight; config 2 35.7-37.5
+    // against 36.3-39.6 us per join over three A/B sessions.  The partitioned kernel keeps
+    // one merge: its copy without the search measured slower, 375-377 vs 340-367 us)
+    if (LATE && FAST && !vv_far)
+      merge_items<FAST, KEYED, CHG, true>(p.ca, p.cb, s.tab[0], s.tab[1], ks, B.n, s.buf[bi], nat,
+                                          nbt, a0, b0, keep, src, &ev);
+    else
+      merge_items<FAST, KEYED, CHG>(p.ca, p.cb, s.tab[0], s.tab[1], ks, B.n, s.buf[bi], nat, nbt, a0,
+                                    b0, keep, src, &ev);
     JSTAMP(t, 3);
     u32 n;
     u32 pos = block_excl_scan1<JB>(__popc(keep), s.wave, &n);  // (barriers before s.wave's next use)
