@@ -96,9 +96,11 @@ __device__ __forceinline__ Row lds_d(const SmallLds& s, u32 i) {
 // Key k's first row in a[0, n) (ascending) and its run (at most SA + 1 counted), by the
 // lanes of one wave: key ids are uniform hashes, so the first round probes 64 rows around
 // the interpolated position (k / 2^64 of the way, 8 standard deviations wide); 64-ary
-// rounds narrow what is left to 64 rows (none at 10k rows, one at 10M), which one load
-// per lane settles, run included.  Two round trips at 10k rows where a thread's
-// interpolation search takes four or five.
+// rounds narrow [lo, hi] (hi INCLUSIVE: the first row >= k may be hi itself) to at most 64
+// candidates (none at 10k rows, one at 10M), which one load per lane settles, run
+// included: the window [lo, lo + 63] then holds hi, so a run starting at hi is seen (ADVICE
+// r5: narrowing only to hi - lo <= 64 left a run starting at hi = lo + 64 counted as 0).
+// Two round trips at 10k rows where a thread's interpolation search takes four or five.
 __device__ __forceinline__ void wave_find(const u64* a, u64 n, u64 k, u64& lo_out, u32& run_out) {
   const int lane = threadIdx.x & (WAVE - 1);
   u64 lo = 0, hi = n;  // the first row >= k is in [lo, hi]
@@ -112,7 +114,7 @@ __device__ __forceinline__ void wave_find(const u64* a, u64 n, u64 k, u64& lo_ou
     const u64 qlo = __shfl(q, c > 0 ? c - 1 : 0, WAVE), qhi = __shfl(q, c < WAVE ? c : WAVE - 1, WAVE);
     if (c > 0) lo = qlo + 1;
     if (c < WAVE) hi = qhi;
-    while (hi - lo > (u64)WAVE) {
+    while (hi - lo >= (u64)WAVE) {  // [lo, hi] has more than WAVE candidates
       const u64 span = hi - lo;
       const u64 p = lo + span * (u64)(lane + 1) / (WAVE + 1);
       const int c2 = __popcll(__ballot(a[p] < k));
@@ -165,9 +167,15 @@ __device__ __forceinline__ void block_scan4(const u32 (&v)[4], u32* sw, u32 (&ex
   }
 }
 
+// Map.get(vv, n, 0) >= c for a VV table of counter + 1 (0: absent, which covers cnt 0 as
+// the reference's Dots.member? does, aw_lww_map.ex:67-70, and the fused join, join.hip)
+__device__ __forceinline__ bool vv_tab_covers(const u64* tab, u32 n, u64 c) {
+  return n < SV ? max(tab[n], 1ull) > c : c == 0;
+}
+
 // Dots.member?(delta context, dot)
 __device__ __forceinline__ bool delta_covers(const SmallLds& s, bool dvv, u32 ncd, u32 n, u64 c) {
-  if (dvv) return n < SV && s.cd.tabD[n] > c;
+  if (dvv) return vv_tab_covers(s.cd.tabD, n, c);
   u32 lo = 0, hi = ncd;
   while (lo < hi) {
     const u32 m = (lo + hi) >> 1;
@@ -239,7 +247,7 @@ __device__ __forceinline__ u32 merge_key(const SmallLds& s, u32 ia, u32 ie, u32 
       }
     } else {  // the delta's only: kept unless the state's VV covers it
       const Row r = lds_d(s, ja++);
-      if (!(r.node < SV && s.tabS[r.node] > r.cnt)) {
+      if (!vv_tab_covers(s.tabS, r.node, r.cnt)) {
         emit(r);
         ne++;
         chg = true;
@@ -845,6 +853,34 @@ extern "C" int dg_debug_small_stamps(unsigned long long* host, size_t n) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sm_stamps), n * 8) == hipSuccess ? 0 : -3;
 }
 #endif
+
+// Test hook (tests/test_gpu_join_delta.py): wave_find of each query on device arrays, one
+// wave per query, on the null stream, synchronous
+__global__ __launch_bounds__(256) void wave_find_kernel(const u64* a, u64 n, const u64* q, u64 nq, u64* lo,
+                                                         u32* run) {
+  const u64 i = (u64)blockIdx.x * (256 / WAVE) + threadIdx.x / WAVE;
+  if (i >= nq) return;  // (uniform per wave)
+  u64 l;
+  u32 r;
+  wave_find(a, n, q[i], l, r);
+  if ((threadIdx.x & (WAVE - 1)) == 0) {
+    lo[i] = l;
+    run[i] = r;
+  }
+}
+
+}  // namespace dg
+
+extern "C" int dg_debug_wave_find(const unsigned long long* a, unsigned long long n, const unsigned long long* q,
+                                  unsigned long long nq, unsigned long long* lo, unsigned int* run) {
+  if (!nq) return 0;
+  hipLaunchKernelGGL(dg::wave_find_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, 0, (const dg::u64*)a,
+                     (dg::u64)n, (const dg::u64*)q, (dg::u64)nq, (dg::u64*)lo, (dg::u32*)run);
+  if (hipGetLastError() != hipSuccess) return -3;
+  return hipDeviceSynchronize() == hipSuccess ? 0 : -3;
+}
+
+namespace dg {
 
 hipError_t launch_small_delta(const SmallArgs& p, hipStream_t st) {
   hipLaunchKernelGGL(small_delta_kernel, dim3(1), dim3(NT), 0, st, p);

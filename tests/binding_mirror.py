@@ -96,9 +96,12 @@ def join_cpu(delta1, delta2, keys):
     return AW(r.dots, r.value)
 
 
-def read_cpu(state, keys="all"):
-    """The unchanged read/1,2 bodies (aw_lww_map.ex:211-224)."""
-    return T.read(T.AW(state.dots, state.value), None if keys == "all" else list(keys))
+def read_cpu(state, keys=None):
+    """The unchanged read/1,2 bodies (aw_lww_map.ex:211-224): keys None is read/1, a list
+    read/2, any other term the one key (`read(crdt, key)`, :222-224)."""
+    if keys is not None and not isinstance(keys, list):  # (is_list)
+        keys = [keys]
+    return T.read(T.AW(state.dots, state.value), None if keys is None else list(keys))
 
 
 def add(key, value, i, state, ts):
@@ -176,7 +179,11 @@ def apply_changed(state, gpu, dots, changed):
 
 
 def attach_gpu(state, min_dots=None, eng=None):
-    """CausalCrdt.init (:72) / read_from_storage: the device copy and its tree."""
+    """CausalCrdt.init (:72) / read_from_storage (:220-232): the device copy and its tree.
+    A handed-in struct's handle is never trusted -- a struct restored from storage may carry
+    one of a VM that has gone, or of another engine -- so the copy is rebuilt from the
+    struct's terms (which hold every queued mutation too)."""
+    state = detach(state)
     eng = eng or GPU.engine()
     if eng is None or len(state.value) < (GPU_MIN_DOTS if min_dots is None else min_dots):
         return state
@@ -194,11 +201,16 @@ def detach(state):
     return replace(state, gpu=None)
 
 
-def read(state, keys="all"):
+def read(state, keys=None):
+    """read/1 (keys None: the whole map -- the only way to the NIF's :all), read/2 of a
+    list, and read(crdt, key) of any other term (a Tg is a tuple: only lists are lists) as [key] (aw_lww_map.ex:218-224): a map
+    keyed by the atom :all reads its key :all, as the reference does."""
+    if keys is not None and not isinstance(keys, list):  # (is_list)
+        return read(state, [keys])
     g = state.gpu
-    if g is not None and not g[2] and (keys == "all" or len(keys) >= GPU_MIN_READ_KEYS):
+    if g is not None and not g[2] and (keys is None or len(keys) >= GPU_MIN_READ_KEYS):
         res, ver, _ = g
-        r = GPU.read(res, ver, keys if keys == "all" else list(keys))
+        r = GPU.read(res, ver, "all" if keys is None else list(keys))
         if r[0] == "ok":
             return r[1]
         # ("error", "stale"): an older struct -- its own terms answer
@@ -242,21 +254,63 @@ class Diff:
     originator: object
 
 
+class MemoryStorage:
+    """test/support/memory_storage.ex: write(name, state) / read(name) over a map."""
+
+    def __init__(self):
+        self.map = {}
+
+    def write(self, name, state):
+        self.map[name] = state
+
+    def read(self, name):
+        return self.map.get(name)
+
+
 class Replica:
     """CausalCrdt's state and the handlers on the data path (causal_crdt.ex:45-413):
     handle_operation, update_state_with_delta (diff/3, diffs_to_callback/3), read, and
-    the sync round (prepare, continue, send_diff / get_diff) run synchronously."""
+    the sync round (prepare, continue, send_diff / get_diff) run synchronously.
+
+    gpu_merkle: the device tree replaces MerkleMap; False: the device
+    does joins and reads only and the sync round is the CPU MerkleMap's (_sync_cpu)."""
 
     def __init__(self, node, clock, on_diffs=None, max_sync_size=200, gpu=True, min_dots=0,
-                 engine=None):
+                 engine=None, storage_module=None, name=None, gpu_merkle=True):
         self.engine = engine or GPU.engine()  # this replica's BEAM node's engine
+        self.gpu = gpu
+        self.min_dots = min_dots
+        self.gpu_merkle = gpu_merkle
         self.node_id = tg(node)
         self.clock = clock
         self.on_diffs = on_diffs
         self.max_sync_size = max_sync_size
+        self.storage_module = storage_module
+        self.name = name
+        self.sequence_number = 0
         st = compress_dots(new())  # init (:72)
-        self.crdt_state = attach_gpu(st, min_dots, self.engine) if gpu else st
+        self.crdt_state = self._attach(st)
         self.received = []
+        self.read_from_storage()  # handle_continue(:read_storage) (:78-80)
+
+    def _attach(self, st):
+        return attach_gpu(st, self.min_dots, self.engine) if self.gpu else detach(st)
+
+    def read_from_storage(self):  # :216-232, the restored struct re-attached (§3.3)
+        if self.storage_module is None:
+            return
+        stored = self.storage_module.read(self.name)
+        if stored is None:
+            return
+        node_id, seq, crdt_state, _merkle_map = stored
+        self.node_id, self.sequence_number = node_id, seq
+        self.crdt_state = self._attach(crdt_state)
+
+    def write_to_storage(self):  # :234-246: the struct detached (its terms hold the queue)
+        if self.storage_module is None:
+            return
+        self.storage_module.write(self.name, (self.node_id, self.sequence_number,
+                                              detach(self.crdt_state), None))
 
     # handle_operation (:337-342)
     def mutate(self, f, *args):
@@ -274,6 +328,7 @@ class Replica:
         diffs = diff(old, new_state, keys)
         self.crdt_state = new_state
         self.diffs_to_callback(old, new_state, [d[1] for d in diffs])
+        self.write_to_storage()
 
     def diffs_to_callback(self, old_state, new_state, keys):  # :359-381
         if not keys:
@@ -297,7 +352,7 @@ class Replica:
 
     # the sync round: sync_interval_or_state_to_all (:252-289) with one neighbour
     def sync_to(self, peer, trace=None):
-        if self.crdt_state.gpu is None:
+        if self.crdt_state.gpu is None or not self.gpu_merkle or not peer.gpu_merkle:
             return self._sync_cpu(peer)
         self.crdt_state, cont = merkle_prepare(self.crdt_state, LEVELS)
         d = Diff(cont, self.crdt_state.dots, self, peer, self)

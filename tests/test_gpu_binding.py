@@ -242,3 +242,86 @@ def test_two_nodes_keys_known_only_to_one_side():
     finally:
         e1.close()
         e2.close()
+
+
+# ---------------------------------------------------------------- storage and read(crdt, key)
+# causal_crdt.ex:216-250: the replica persists {node_id, seq, crdt_state, merkle_map} after
+# every delta and restores it at start; INTEGRATION §3.3 persists the struct detached and
+# re-attaches a restored one from its terms (never trusting a handle it carries).
+
+def _engine():
+    return B.nif.engine_open(0, wrap=tg, unwrap=B.untg)[1]
+
+
+def test_storage_backend_can_store_and_retrieve_state():  # causal_crdt_test.exs:80-85
+    store = B.MemoryStorage()
+    r = B.Replica(1, Clock(), storage_module=store, name="storage_test")
+    assert attached(r)
+    r.mutate("add", "Derek", "Kraan")
+    assert r.read() == {tg("Derek"): tg("Kraan")}
+    _node, _seq, persisted, _mm = store.read("storage_test")
+    assert persisted.gpu is None  # detached: no device handle, no queue
+    assert B.read_cpu(persisted) == {tg("Derek"): tg("Kraan")}
+
+
+@pytest.mark.parametrize("n_keys,min_dots", [(3, 0), (300, 0), (40, 100), (200, 100)])
+def test_storage_rehydrates_after_a_crash_on_a_new_engine(n_keys, min_dots):
+    """causal_crdt_test.exs:87-102 through GPU replicas: the VM goes (its engine and every
+    state resource with it), a NEW engine restores the replica from the snapshot -- on the
+    device at or above the attach threshold, on the BEAM below it -- even from a snapshot
+    that still carries the dead handle; then it mutates and syncs both ways with a live
+    replica (device trees with gpu_min_dots 0, the CPU MerkleMap otherwise)."""
+    store = B.MemoryStorage()
+    c = Clock()
+    gm = min_dots == 0
+    e1, e2 = _engine(), None
+    try:
+        r = B.Replica(1, c, storage_module=store, name="st", engine=e1, min_dots=min_dots, gpu_merkle=gm)
+        for i in range(n_keys):
+            r.mutate("add", f"k{i}", i)
+        r.mutate("remove", "k1")
+        if attached(r):  # a snapshot written before the patch: the struct with its handle
+            node, seq, persisted, mm = store.read("st")
+            assert persisted.gpu is None
+            store.write("st", (node, seq, B.replace(persisted, gpu=r.crdt_state.gpu), mm))
+        e1.close()  # the VM is gone: the handle's state is freed
+        e2 = _engine()
+        r2 = B.Replica(77, c, storage_module=store, name="st", engine=e2, min_dots=min_dots, gpu_merkle=gm)
+        assert r2.node_id == tg(1)
+        assert attached(r2) == (n_keys - 1 >= min_dots)
+        want = {tg(f"k{i}"): tg(i) for i in range(n_keys) if i != 1}
+        assert r2.read() == want
+        p = B.Replica(2, c, engine=e2, min_dots=min_dots, gpu_merkle=gm)
+        for j in range(5):
+            p.mutate("add", f"p{j}", -j)
+        p.mutate("add", "k0", "from-p")  # later clock: p's write wins (LWW)
+        r2.mutate("add", "k2", "again")
+        r2.sync_to(p)
+        p.sync_to(r2)
+        want.update({tg(f"p{j}"): tg(-j) for j in range(5)})
+        want[tg("k0")] = tg("from-p")
+        want[tg("k2")] = tg("again")
+        assert r2.read() == p.read() == want
+        assert attached(r2) == (n_keys - 1 >= min_dots)
+        # the restored replica keeps persisting: a third start sees the synced state
+        r3 = B.Replica(78, c, storage_module=store, name="st", engine=e2, min_dots=min_dots, gpu_merkle=gm)
+        assert r3.read() == want
+    finally:
+        e1.close()
+        if e2 is not None:
+            e2.close()
+
+
+def test_a_map_keyed_by_the_atom_all():
+    """read(crdt, key) reads the one key (aw_lww_map.ex:222-224), the atom :all included:
+    the dispatch reaches the NIF's whole-map read from read/1 only."""
+    from delta_crdt_ex_amd.terms import Atom
+    r = B.Replica(1, Clock())
+    r.mutate("add", Atom("all"), 1)
+    r.mutate("add", "x", 2)
+    r.crdt_state, _ = B.merkle_prepare(r.crdt_state, B.LEVELS)  # flushed: the device answers
+    s = r.crdt_state
+    a = tg(Atom("all"))
+    assert B.read(s, a) == B.read(s, [a]) == B.read_cpu(s, a) == {a: tg(1)}
+    assert B.read(s) == B.read_cpu(s) == {a: tg(1), tg("x"): tg(2)}
+    assert B.read(s, [tg("x")]) == {tg("x"): tg(2)}

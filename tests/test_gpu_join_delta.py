@@ -485,3 +485,125 @@ def test_home_from_an_empty_state(engine, with_tree):
             fresh = engine.merkle_build(st, 6)
             assert np.array_equal(tree.nodes.cpu().numpy(), fresh.nodes.cpu().numpy())
             assert np.array_equal(tree.bucket_counts(), fresh.bucket_counts())
+
+
+# ---------------------------------------------------------------- wave_find
+# The small path's per-key search (small.hip wave_find): its first row and run, against
+# np.searchsorted, at the sizes where the 64-ary narrowing ends on a window edge (every n in
+# [2^20, 1040^2) leaves hi - lo = 64 after the first round) and on shard-prefixed keys (the
+# interpolated probe misses: 64-ary rounds from the whole range).
+
+def _wave_find(a, q):
+    import ctypes as C
+    from delta_crdt_ex_amd import _abi
+    f = _abi.load().dg_debug_wave_find
+    f.restype = C.c_int
+    f.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
+    da, dq = kdev(a), kdev(q)
+    lo = torch.empty(len(q), dtype=torch.int64, device=DEV)
+    run = torch.empty(len(q), dtype=torch.int32, device=DEV)
+    torch.cuda.synchronize()
+    assert f(da.data_ptr(), len(a), dq.data_ptr(), len(q), lo.data_ptr(), run.data_ptr()) == 0
+    return u64(lo), run.cpu().numpy()
+
+
+def _keys_with_runs(rng, n, prefix_bits=0, prefix=0):
+    u = np.unique(rng.integers(0, 1 << 63, n, dtype=np.uint64) >> np.uint64(prefix_bits))
+    if prefix_bits:
+        u = u | np.uint64(prefix << (64 - prefix_bits))
+    reps = rng.choice([1, 1, 1, 2, 3], len(u))
+    a = np.repeat(u, reps)[:n]
+    return a, u
+
+
+@pytest.mark.parametrize("n", [0, 1, 63, 64, 65, 10_000, 1 << 20, (1 << 20) + 1, 1_060_000, 1040 ** 2 - 1,
+                               1040 ** 2, 3_000_000])
+@pytest.mark.parametrize("prefix_bits", [0, 3])
+def test_wave_find_matches_searchsorted(n, prefix_bits):
+    rng = np.random.default_rng(n + prefix_bits)
+    a, u = _keys_with_runs(rng, n, prefix_bits, 5)
+    assert len(a) == n
+    q = np.concatenate([np.unique(a), (np.unique(a) + np.uint64(1)) if n else a,
+                        np.array([0, (1 << 64) - 1, 5 << 61], np.uint64)])
+    lo, run = _wave_find(a, q)
+    want_lo = np.searchsorted(a, q, side="left")
+    want_run = np.searchsorted(a, q, side="right") - want_lo
+    bad = np.nonzero((lo != want_lo) | (run != want_run))[0]
+    assert len(bad) == 0, (n, prefix_bits, len(bad), q[bad[:4]], lo[bad[:4]], want_lo[bad[:4]], run[bad[:4]])
+
+
+def _unique_key_state(rng, n, prefix_bits=0, prefix=0):
+    """n rows, one per key (node 0..3 round robin), VV covering them all."""
+    keys = np.unique(rng.integers(0, 1 << 63, n + n // 50, dtype=np.uint64) >> np.uint64(prefix_bits))[:n]
+    if prefix_bits:
+        keys = keys | np.uint64(prefix << (64 - prefix_bits))
+    assert len(keys) == n
+    node = (np.arange(n) % 4).astype(np.uint32)
+    cnt = (np.arange(n) // 4 + 1).astype(np.uint64)
+    rows = (keys, rng.integers(0, 1 << 40, n).astype(np.uint64), np.full(n, 7, np.int64), node, cnt)
+    ctx = (R.VV, np.arange(4, dtype=np.uint32), np.full(4, (n + 3) // 4, np.uint64))
+    return {"rows": rows, "ctx": ctx}
+
+
+@pytest.mark.parametrize("n_rows,prefix_bits", [(1_060_000, 0), (1_060_000, 3)])
+def test_mutation_sequence_home_1m(engine, n_rows, prefix_bits):
+    """one-key mutations through dg_join_delta_home on a 1.06M-row state (where
+    wave_find's narrowing ends on the window edge) and on a shard-prefixed one, each step
+    against R.join2 (rows of changed keys and context) and the state at the end."""
+    rng = np.random.default_rng(n_rows + prefix_bits)
+    a = _unique_key_state(rng, n_rows, prefix_bits, 6)
+    st, sc = state_of(a, extra_ctx=4)
+    spare = Store.empty(st.n + 300, DEV)
+    tree = engine.merkle_build(st, 16, shard_bits=prefix_bits, shard=6 if prefix_bits else 0)
+    rows, ctx = a["rows"], a["ctx"]
+    keys = rows[0]
+    # every key whose first row sits on a probe edge is as likely as any: 300 ops over
+    # existing keys, plus new keys and removes
+    for i in range(300):
+        r = rng.random()
+        if r < 0.5:
+            op = ("add", int(rng.choice(keys)), int(rng.integers(1 << 40)), 10 ** 12 + i)
+        elif r < 0.65:
+            k = int(rng.integers(1 << 63) >> prefix_bits) | (6 << (64 - prefix_bits) if prefix_bits else 0)
+            op = ("add", k, int(rng.integers(1 << 40)), 10 ** 12 + i)
+        else:
+            op = ("remove", int(rng.choice(keys)), 0, 0)
+        drows, dctx, dkeys = R.mutate_batch(rows, ctx, 2, [op])
+        sd, cd = up({"rows": drows, "ctx": dctx})
+        if spare.cap < st.n + sd.n:
+            spare = Store.empty(st.n + sd.n + 64, DEV)
+        got = engine.join_delta_home(st, sc, sd, cd, kdev(dkeys), spare, tree)
+        assert got is not None
+        changed, hrows, hctx, _ = got
+        wr, wc = R.join2(rows, ctx, drows, dctx, keys=dkeys)
+        wch = R.changed_keys(rows, wr, dkeys)
+        assert np.array_equal(changed, wch), (i, op)
+        for x, y in zip(hrows, tuple(c[np.isin(wr[0], wch)] for c in wr)):
+            assert np.array_equal(x, y), (i, op)
+        rows, ctx = wr, wc
+    rows_eq(st, rows)
+    ctx_eq(sc, ctx)
+    fresh = engine.merkle_build(st, 16, shard_bits=prefix_bits, shard=6 if prefix_bits else 0)
+    assert np.array_equal(tree.nodes.cpu().numpy(), fresh.nodes.cpu().numpy())
+
+
+@pytest.mark.parametrize("home", [False, True])
+def test_counter_zero_dots(engine, home):
+    """a dot with counter 0 on a node absent from a VV is covered
+    (Map.get(vv, node, 0) >= 0, aw_lww_map.ex:67-70) on the small and the general path
+    alike: the delta's cnt-0 row is dropped, and a state row with cnt 0 on a node the
+    delta's VV lacks goes."""
+    rng = np.random.default_rng(77)
+    n = 2000
+    keys = np.unique(rng.integers(0, 1 << 63, n + 50, dtype=np.uint64))[:n]
+    node = np.zeros(n, np.uint32)
+    cnt = np.arange(1, n + 1, dtype=np.uint64)
+    node[10], cnt[10] = 3, 0  # (node 3 is in no VV)
+    a = {"rows": (keys, np.arange(n, dtype=np.uint64), np.full(n, 5, np.int64), node, cnt),
+         "ctx": (R.VV, np.array([0], np.uint32), np.array([n], np.uint64))}
+    dk = np.sort(np.array([keys[10], keys[20], keys[30]], np.uint64))
+    d = {"rows": (dk, np.array([7, 8, 9], np.uint64), np.full(3, 9, np.int64), np.full(3, 7, np.uint32),
+                  np.array([0, 0, 1], np.uint64)),
+         "ctx": (R.VV, np.array([7], np.uint32), np.array([1], np.uint64))}
+    st, sc, _, wr = apply(engine, a, d, dk, depth=8, home=home)
+    assert not (wr[3] == 3).any() and not ((wr[3] == 7) & (wr[4] == 0)).any() and ((wr[3] == 7) & (wr[4] == 1)).any()
