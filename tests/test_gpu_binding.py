@@ -286,12 +286,13 @@ def test_storage_rehydrates_after_a_crash_on_a_new_engine(n_keys, min_dots):
             store.write("st", (node, seq, B.replace(persisted, gpu=r.crdt_state.gpu), mm))
         e1.close()  # the VM is gone: the handle's state is freed
         e2 = _engine()
-        r2 = B.Replica(77, c, storage_module=store, name="st", engine=e2, min_dots=min_dots, gpu_merkle=gm)
+        r2 = B.Replica(77, c, storage_module=store, name="st", engine=e2, min_dots=min_dots, gpu_merkle=gm,
+                       max_sync_size="infinite")  # (one round moves every key: see the test above)
         assert r2.node_id == tg(1)
         assert attached(r2) == (n_keys - 1 >= min_dots)
         want = {tg(f"k{i}"): tg(i) for i in range(n_keys) if i != 1}
         assert r2.read() == want
-        p = B.Replica(2, c, engine=e2, min_dots=min_dots, gpu_merkle=gm)
+        p = B.Replica(2, c, engine=e2, min_dots=min_dots, gpu_merkle=gm, max_sync_size="infinite")
         for j in range(5):
             p.mutate("add", f"p{j}", -j)
         p.mutate("add", "k0", "from-p")  # later clock: p's write wins (LWW)
