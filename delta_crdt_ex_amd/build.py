@@ -25,7 +25,7 @@ _SUFFIX = ("_stamps" if STAMPS else "") + (("_" + VARIANT.replace("=", "").repla
 OBJ = os.path.join(HERE, "_build" + _SUFFIX)
 LIB = os.path.join(HERE, "ab", "libdeltagpu" + _SUFFIX + ".so") if _SUFFIX else os.path.join(HERE, "libdeltagpu.so")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
-SOURCES = ["join.hip", "kfold.hip", "take.hip", "splice.hip", "small.hip", "mutate.hip", "segred.hip", "merkle.hip", "remap.hip", "sort.hip", "api.hip"]
+SOURCES = ["join.hip", "kfold.hip", "take.hip", "splice.hip", "small.hip", "kdelta.hip", "mutate.hip", "segred.hip", "merkle.hip", "remap.hip", "sort.hip", "api.hip"]
 ARCH = os.environ.get("DG_OFFLOAD_ARCH", "gfx950")
 
 

@@ -47,6 +47,11 @@ struct dg_engine {
   // dg_join_delta_home's scratch: the edit, the per-key index, the result header
   void* sml = nullptr;
   size_t sml_cap = 0;
+  // dg_join_delta's one-wait path (kdelta.hip): per-key figures, the splice index, the
+  // union context (DG_KD=0: the splice path with its host waits, for A/B)
+  void* kdb = nullptr;
+  size_t kdb_cap = 0;
+  bool kd = true;
   // the full diff's per-group key sums: two buffers of diff_bsum_cap words, zero when
   // allocated; a call adds into one and its write kernel zeroes the other, which the
   // previous call used (no memset launch per diff)
@@ -688,6 +693,8 @@ int dg_engine_create(int device, void* hip_stream, dg_engine** out) {
     if (m && m[0] == '2') e->join_mode = JOIN_TWO_PASS;
     const char* sp = getenv("DG_SPLICE");
     if (sp && sp[0] == '0') e->splice = false;
+    const char* kd = getenv("DG_KD");
+    if (kd && kd[0] == '0') e->kd = false;
     const char* am = getenv("DG_APPLY_MODE");
     if (am && strcmp(am, "fold") == 0) e->apply_mode = 1;
     if (am && strcmp(am, "onepass") == 0) e->apply_mode = 2;
@@ -758,6 +765,7 @@ int dg_engine_destroy(dg_engine* e) {
   if (e->spl) hipFree(e->spl);
   if (e->ubuf) hipFree(e->ubuf);
   if (e->sml) hipFree(e->sml);
+  if (e->kdb) hipFree(e->kdb);
   if (e->diff_bsum) hipFree(e->diff_bsum);
   if (e->h_stage) hipHostFree(e->h_stage);
   if (e->own_stream && e->stream) hipStreamDestroy(e->stream);
@@ -923,6 +931,147 @@ static int take_changed_rows(dg_engine* e, const dg_store* src, const uint64_t* 
   return DG_OK;
 }
 
+// dg_join_delta's one-wait path (kdelta.hip): count + scan, the context union, the tree's
+// put/delete and re-reduction, the write (in place, or into `spare` with the moved rows'
+// copy behind it), then ONE publish and wait.  *done = false and nothing changed when the
+// delta has a row outside the keyset (the full join applies) or a key has more than KD_RUN
+// rows on a side (the splice applies); a tree input error is undone before it returns.
+static int kd_join_delta(dg_engine* e, dg_store* state, dg_context* state_ctx, const dg_store* delta,
+                         const dg_context* delta_ctx, const uint64_t* keys, uint64_t n_keys, dg_store* spare,
+                         dg_merkle* tree, uint64_t* changed, uint64_t cap, uint64_t* n_changed, int* swapped,
+                         dg_store* rows, bool* done) {
+  *done = false;
+  if (!e->kd || n_keys == 0 || state_ctx->kind != DG_CTX_VV || state->cap < state->n ||
+      !pair_aligned(state->key, state->val, state->ts, state->node, state->cnt) ||
+      !pair_aligned(spare->key, spare->val, spare->ts, spare->node, spare->cnt))
+    return DG_OK;
+  const u64 nk = n_keys, ntiles = (nk + KD_BLOCK - 1) / KD_BLOCK, a_tiles = splice_tiles(state->n);
+  const u64 uctx_cap = state_ctx->n + delta_ctx->n;
+  auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+  const size_t per_key = al(nk * 8), per_key1 = al((nk + 1) * 8), tiles_b = al(ntiles * KD_NV * 8);
+  const size_t uc_b = al(uctx_cap * 8) + al(uctx_cap * 4), cu_b = al(ctx_union_tmp_bytes(state_ctx->n, delta_ctx->n));
+  const size_t bytes = 7 * per_key + per_key1 + 2 * tiles_b + al((a_tiles + 2) * 8) + uc_b + cu_b;
+  TRY(ensure_buf(e, &e->kdb, &e->kdb_cap, bytes));
+  char* q = (char*)e->kdb;
+  auto take = [&](size_t b) {
+    char* r = q;
+    q += b;
+    return r;
+  };
+  KdArgs p{};
+  p.a = rows_of(state);
+  p.aw = rows_out_of(state);
+  p.ca = ctx_of(state_ctx);
+  p.ca_node = state_ctx->node;
+  p.ca_cnt = state_ctx->cnt;
+  p.ca_cap = state_ctx->cap;
+  p.d = rows_of(delta);
+  p.cd = ctx_of(delta_ctx);
+  p.keys = keys;
+  p.nk = nk;
+  p.a_lo = (u64*)take(per_key);
+  p.d_lo = (u64*)take(per_key);
+  p.runs = (u64*)take(per_key);
+  p.amask = (u64*)take(per_key);
+  p.dmask = (u64*)take(per_key);
+  p.dh = (u64*)take(per_key);
+  p.end = (u64*)take(per_key);
+  p.shift = (i64*)take(per_key1);
+  p.part = (u64*)take(tiles_b);
+  p.toff = (u64*)take(tiles_b);
+  p.tile_u0 = (u64*)take(al((a_tiles + 2) * 8));
+  u64* uc_cnt = (u64*)take(al(uctx_cap * 8));
+  u32* uc_node = (u32*)take(al(uctx_cap * 4));
+  void* cu_tmp = take(cu_b);
+  p.uc_node = uc_node;
+  p.uc_cnt = uc_cnt;
+  p.ntiles = ntiles;
+  p.changed = changed;
+  p.cap = cap;
+  p.has_rows = rows != nullptr;
+  if (rows) {
+    p.rows = rows_out_of(rows);
+    p.rows_cap = rows->cap;
+  }
+  p.sp = rows_out_of(spare);
+  p.a_tiles = a_tiles;
+  p.has_tree = tree != nullptr;
+  if (tree) p.t = merkle_of(tree);
+  p.d_counts = e->d_counts;
+  u32* err = e->ticket + 3;
+  p.err = err;
+  // the tree update's scratch (hand-off words | dirty flags | chunk row-count changes), as
+  // tree_update lays it out; dirty, cdelta and the error word zeroed in one launch
+  u32* dirty = nullptr;
+  u64* hand = nullptr;
+  i64* cdelta = nullptr;
+  u64 zw = 0;
+  if (tree) {
+    const u64 chunks = merkle_chunks(tree->depth), cw = merkle_ctr_words(tree->depth);
+    const u64 cpad = (chunks + 1) & ~1ull;
+    zw = cpad + 2 * chunks;
+    TRY(ensure_tmp(e, (cw + zw) * sizeof(u32)));
+    hand = (u64*)e->tmp;
+    dirty = (u32*)e->tmp + cw;
+    cdelta = (i64*)(dirty + cpad);
+  }
+  HIP_TRY(launch_splice_finish(nullptr, nullptr, 0, nullptr, nullptr, dirty, zw, nullptr, err, e->stream));
+  HIP_TRY(launch_kd_join(p, e->stream));
+  HIP_TRY(launch_ctx_union(ctx_of(state_ctx), ctx_of(delta_ctx), uc_node, uc_cnt, e->d_counts + 1, cu_tmp,
+                           e->stream));
+  if (tree)
+    HIP_TRY(launch_kd_tree(merkle_of(tree), keys, p.runs, p.dh, nk, e->d_counts + 4, 1, dirty,
+                           e->ticket + MERKLE_ARRIVE, hand, cdelta, err, e->stream));
+  HIP_TRY(launch_kd_write(p, e->stream));
+  SpliceArgs sp{};
+  sp.a = rows_of(state);
+  sp.keys = keys;
+  sp.nk = nk;
+  sp.a_lo = p.a_lo;
+  sp.end = p.end;
+  sp.shift = p.shift;
+  sp.tile_u0 = p.tile_u0;
+  sp.out = rows_out_of(spare);
+  sp.run_if = e->d_counts + 5;  // rows moved
+  sp.kguard = e->d_counts + 4;
+  HIP_TRY(launch_splice_move(sp, e->stream));
+  TRY(read_counts(e, 8));
+  const u64 g = e->h_counts[4];
+  if (g & (KD_BAD | KD_BIG)) return DG_OK;  // nothing written: another path applies
+  if (g & KD_CAP)
+    return fail(DG_E_CAPACITY, "dg_join_delta: %llu changed keys > cap %llu", (unsigned long long)e->h_counts[2],
+                (unsigned long long)cap);
+  if (e->h_ticket[3] & MERKLE_INPUT_ERR) {
+    // the tree update met an input error: no state row and no context entry was written
+    // (the write kernel saw the error word); the same update with the opposite sign
+    // restores every bucket node and count bit for bit
+    const int rc = input_error(e, "dg_join_delta");
+    const std::string msg = g_err;
+    HIP_TRY(launch_splice_finish(nullptr, nullptr, 0, nullptr, nullptr, dirty, zw, nullptr, nullptr, e->stream));
+    HIP_TRY(launch_kd_tree(merkle_of(tree), keys, p.runs, p.dh, nk, e->d_counts + 4, -1, dirty,
+                           e->ticket + MERKLE_ARRIVE, hand, cdelta, err, e->stream));
+    HIP_TRY(hipMemsetAsync(err, 0, sizeof(u32), e->stream));
+    TRY(read_counts(e, 0));
+    g_err = msg;
+    return rc;
+  }
+  const u64 n_e = e->h_counts[0], n_chg = e->h_counts[2], n_rows = e->h_counts[3];
+  const u64 n_ak = e->h_counts[6], dk = e->h_counts[7];
+  if (e->h_counts[5]) {  // rows moved: the state is in `spare`
+    const u64 n = state->n - n_ak + n_e;
+    std::swap(*state, *spare);
+    state->n = n;
+    *swapped = 1;
+  }
+  state_ctx->n = e->h_counts[1];
+  state_ctx->kind = DG_CTX_VV;
+  if (tree) tree->n_keys += dk;
+  *n_changed = n_chg;
+  if (rows) rows->n = n_rows;  // (more than rows->cap: not written, as the caller's contract says)
+  *done = true;
+  return DG_OK;
+}
+
 // dg_join_delta[_rows]: rows (optional) receives the changed keys' joined rows
 static int join_delta_impl(dg_engine* e, dg_store* state, dg_context* state_ctx, const dg_store* delta,
                            const dg_context* delta_ctx, const uint64_t* keys, uint64_t n_keys,
@@ -954,6 +1103,12 @@ static int join_delta_impl(dg_engine* e, dg_store* state, dg_context* state_ctx,
   const u64 uctx_cap = state_ctx->n + delta_ctx->n;
   const dg_context_kind out_kind =
       (state_ctx->kind == DG_CTX_DOTS && delta_ctx->kind == DG_CTX_DOTS) ? DG_CTX_DOTS : DG_CTX_VV;
+  {
+    bool done = false;
+    TRY(kd_join_delta(e, state, state_ctx, delta, delta_ctx, keys, n_keys, spare, tree, changed, cap,
+                      n_changed, swapped, rows, &done));
+    if (done) return DG_OK;
+  }
   Splice w;
   bool ok = false;
   const dg_store old_state = *state;

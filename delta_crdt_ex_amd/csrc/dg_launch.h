@@ -183,6 +183,9 @@ struct SpliceArgs {
   // (optional) the index and copy kernels run only when *run_if != 0 (the fused small
   // join enqueues the moved-rows copy before the host knows whether rows moved)
   const u64* run_if;
+  // (optional) the copy kernels run only when *kguard == 0 (dg_join_delta's one-wait path:
+  // its guard word says the index was not written)
+  const u64* kguard;
 };
 // For every key of keys (ascending, n_keys): lo[u] = the first row of s whose key is >=
 // keys[u] and len[u] = its rows, found by streaming s's key column in tiles (each tile's
@@ -205,6 +208,9 @@ hipError_t launch_splice_finish(const u32* un, const u64* uc, u64 nc, u32* on, u
                                 u64 n_dirty, u64* counts, u32* err_word, hipStream_t st,
                                 const u32* guard = nullptr);
 u64 splice_tiles(u64 n);  // state tiles of the copy (tile_u0 holds one more entry)
+constexpr u64 SPLICE_TILE = 2048;  // state rows per copy tile (splice.hip ST)
+// the copy of the untouched rows alone (splice_kernel; E's rows placed by the caller)
+hipError_t launch_splice_move(SpliceArgs p, hipStream_t st);
 
 // ---- mutate.hip (a batch of add/remove ops as one delta; see the file header)
 inline u64 mutate_tiles(u64 m) { return (m + 1023) / 1024; }
@@ -300,6 +306,58 @@ hipError_t launch_merkle_build(const Rows& s, const MerkleT& t, u64* d_keys, u32
 hipError_t launch_merkle_update(const MerkleT& t, const Rows& olds, const Rows& news, const u64* keys,
                                 u64 n_keys, u32* dirty, u64* d_keys, u32* arrive, u64* hand, i64* cdelta,
                                 u32* err, hipStream_t st);
+// the same from kdelta.hip's per-key figures (runs, dh; skipped when *guard != 0); sign -1
+// undoes sign +1 bit for bit
+hipError_t launch_kd_tree(const MerkleT& t, const u64* keys, const u64* runs, const u64* dh, u64 nk,
+                          const u64* guard, int sign, u32* dirty, u32* arrive, u64* hand, i64* cdelta,
+                          u32* err, hipStream_t st);
+// ---- kdelta.hip: dg_join_delta of a keyed delta of any size, one host wait (see the file header)
+constexpr int KD_BLOCK = 256;  // keys per workgroup
+constexpr u32 KD_RUN = 64;     // rows per key and side the per-key join takes (more: KD_BIG)
+constexpr int KD_NV = 7;       // per-workgroup figures: rows, kept rows, changed keys, their rows,
+                               // delta rows, distinct-key change, flags
+// guard bits (d_counts[4]): the delta has a row outside the keyset (the full join applies);
+// a key run over KD_RUN rows (the splice applies); more changed keys than `cap`
+constexpr u64 KD_BAD = 1, KD_BIG = 2, KD_CAP = 4;
+constexpr u64 KD_MOVED = 8;    // (flags only) a key's row count changed
+struct KdArgs {
+  Rows a;              // the state (read)
+  RowsOut aw;          // the same columns (the in-place write)
+  Ctx ca;              // its context (a VV)
+  u32* ca_node;        // ... written with the union (uc, d_counts[1] entries)
+  u64* ca_cnt;
+  u64 ca_cap;
+  const u32* uc_node;  // the union context (launch_ctx_union's output)
+  const u64* uc_cnt;
+  Rows d;              // the delta, sorted
+  Ctx cd;              // its context, sorted
+  const u64* keys;     // the keyset, ascending unique
+  u64 nk;
+  // per key (nk): first state row, first delta row, runs (na | nd << 16 | ne << 32 | chg << 48),
+  // kept-row masks, leaf change
+  u64 *a_lo, *d_lo, *runs, *amask, *dmask, *dh;
+  u64 *part, *toff;    // per workgroup KD_NV figures and their exclusive offsets
+  u64 ntiles;
+  u64* changed;        // changed keys (cap), device or mapped host memory
+  u64 cap;
+  RowsOut rows;        // their rows (rows_cap), when has_rows
+  u64 rows_cap;
+  int has_rows;
+  RowsOut sp;          // the spare store: the output when rows move
+  u64* end;            // the splice index (nk, nk + 1, a_tiles + 1)
+  i64* shift;
+  u64* tile_u0;
+  u64 a_tiles;
+  MerkleT t;           // the tree (has_tree): its term hashes for the leaf changes
+  int has_tree;
+  u64* d_counts;       // the count block (kd_scan_kernel)
+  const u32* err;      // the tree update's input-error word (state writes skipped when set)
+};
+// kd_count_kernel + kd_scan_kernel
+hipError_t launch_kd_join(const KdArgs& p, hipStream_t st);
+// kd_write_kernel
+hipError_t launch_kd_write(const KdArgs& p, hipStream_t st);
+
 // ---- small.hip: dg_join_delta of a small delta, one launch (see the file header)
 constexpr u32 SMALL_KEYS = 512, SMALL_DELTA = 512, SMALL_DCTX = 1024, SMALL_NODES = 2048;
 constexpr u32 SMALL_TAKEN = 1024, SMALL_EDIT = 1536;

@@ -1033,10 +1033,10 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     const u64 tn = t + G;
     u64 a0n = 0, a1n = 0, b0n = 0, kln = 0, kmn = 0;
     int natn = 0, nbtn = 0;
-    // the next tile's loads: issued before the merge on long joins (a whole merge to land
-    // in), after it on short fused ones (LATE; A/B: config 2 39 vs 42 us per join, config
-    // 5 0.39 vs 0.38 ms).  A run-time switch between the two placements was slower than
-    // either (43 us, 0.39 ms): the placement is a template parameter.
+    // the next tile's loads: issued before the merge, so they land while it runs.  (Until
+    // round 6 the fused kernel issued them after its merge, measured faster then, 39 vs 42 us;
+    // since the fused merge has no flat loads left (NOFB below) the early issue wins there
+    // too: config 2 34.1-35.2 against 36.1-37.2 us per join, A/B on one box, three rounds.)
     auto issue_next = [&]() {
       a0n = split(tn, k + 1, 0);
       a1n = split(tn, k + 1, 1);
@@ -1047,7 +1047,7 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         if (kmn <= (u64)KS && (u64)tid < kmn) kk = p.keys[kln + tid];
       }
     };
-    if (!LATE && tn < ntiles) issue_next();
+    if (tn < ntiles) issue_next();
     StripeCounts sc;  // stripe k-1's counts, in flight during the merge
     if (k > 0) stripe_load(cs, t - G - w, G, ntiles, epoch, sc);
     JSTAMP(t, 7);
@@ -1072,7 +1072,6 @@ __global__ __launch_bounds__(JB) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     for (int q = 0; q < JI; q++)
       if (keep & (1u << q)) s.comp[bi][pos++] = src[q];
     if (tid == 0) publish_count(cs, t, epoch, n);
-    if (LATE && tn < ntiles) issue_next();
     __syncthreads();
     if (CHG) {  // the tile's change events (keys, ascending, repeats allowed) -> chg_tmp,
                 // with the per-tile figures the changed-key kernels need (chg_sum/write)

@@ -1,0 +1,369 @@
+// kdelta.hip — update_state_with_delta for a keyed delta of ANY size with one host wait.
+//
+// CausalCrdt joins every sync delta and every batch of local mutations into the replica
+// with its keyset (reference causal_crdt.ex:383-394; aw_lww_map.ex:153-209).  When the
+// delta's keys all lie in the keyset, only the keyset's keys change, and each key's new
+// rows are join_dot_sets/4 (:196-209) of its state rows and its delta rows -- a handful of
+// rows per key.  So instead of a merge-path join of the taken rows (whose launch is sized
+// by counts the host must wait for), every keyset key is one thread:
+//
+//   kd_count_kernel   (one thread per key) its state run (an interpolation search of the
+//                     state: key ids are hashes) and delta run, the per-key join: which
+//                     state rows stay (s1 ∩ s2 ∪ s1 \ c2) and which delta rows come in
+//                     (s2 \ c1) -- kept as two bit masks -- whether the key changed (diff/3,
+//                     causal_crdt.ex:344-352) and its Merkle leaf change (Σ row_hash new -
+//                     Σ row_hash old); per workgroup the sums of rows, kept rows, changed
+//                     keys and their rows, delta rows seen
+//   kd_scan_kernel    (one workgroup) the workgroups' exclusive offsets and the totals; the
+//                     guard word: a delta row outside the keyset (the right-biased carry of
+//                     :185-188 applies: the caller runs the full join), a key run over
+//                     KD_RUN rows, more changed keys than the caller's capacity
+//   kd_tree_kernel    (merkle.hip, one thread per key) MerkleMap.put/delete of the changed
+//                     keys into the bucket level, then the dirty chunks re-reduced
+//   kd_write_kernel   (one thread per key) the key's new rows -- in place when no key's row
+//                     count changed, else straight to their final places in the spare store
+//                     -- the changed keys and their rows (device or page-locked host memory),
+//                     the splice index of the rows that move (splice.hip), and the union
+//                     context into the state's; every state write skipped when the tree
+//                     update reported an input error (all or nothing)
+//   splice_kernel     (splice.hip, only when rows moved) the untouched rows to the spare
+//
+// then the count block is published to mapped host memory and the host waits ONCE.
+//
+// Roofline: each key costs two searches (~6 dependent loads of the state, a few of the
+// delta) and reads its few rows twice (the second time from L2); a sync delta of 125k keys
+// into a 12.5M-row state reads ~10 MB.  Latency-bound by the search chains, not by bytes.
+#include "dg_hash.h"
+#include "dg_launch.h"
+#include "dg_tree.h"
+
+namespace dg {
+
+namespace {
+
+constexpr int KDB = KD_BLOCK;  // keys per workgroup, one per thread
+constexpr u32 KVT = 1024;      // VV tables in LDS cover node ids < KVT
+static_assert(KD_RUN <= 64, "a key's kept rows are a 64-bit mask per side");
+
+__device__ __forceinline__ u64 rhash(const MerkleT& t, const Row& r) {
+  return row_hash(r.key, th_val(t.th, r.val), r.ts, th_node(t.th, r.node), r.cnt);
+}
+
+// Map.get(vv, node, 0) >= cnt through the LDS table (node ids < KVT), else a search
+__device__ __forceinline__ bool vv_covers(const u64* tab, const Ctx& c, u32 n, u64 cnt) {
+  if (n < KVT) return tab[n] >= cnt;
+  return ctx_covers(c.node, c.cnt, c.n, 0, n, cnt);
+}
+
+// first row of key k in s (lower bound) and its run, at most KD_RUN + 1 counted (4 rows a
+// round trip, every load issued together at a clamped index)
+__device__ __forceinline__ void key_run(const u64* key, u64 n, u64 k, u64& lo, u32& run) {
+  lo = interp_lower_bound(key, 0, n, k);
+  u64 e = lo;
+  while (e < n) {
+    u64 kk[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const u64 v = key[e + q < n ? e + q : lo];
+      kk[q] = e + q < n ? v : k + 1;
+    }
+    u32 c = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) c += (c == (u32)q && kk[q] == k) ? 1u : 0u;
+    e += c;
+    if (c < 4 || e - lo > KD_RUN) break;
+  }
+  run = (u32)(e - lo);
+}
+
+// ---------------------------------------------------------------- count
+__global__ __launch_bounds__(KDB) void kd_count_kernel(KdArgs p) {
+  __shared__ u64 tabS[KVT], tabD[KVT];
+  __shared__ u64 red[KD_NV][KDB / WAVE];
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
+  const u64 u = (u64)blockIdx.x * KDB + tid;
+  const bool dvv = p.cd.kind == 0;
+  for (u32 x = tid; x < KVT; x += KDB) {
+    tabS[x] = 0;
+    tabD[x] = 0;
+  }
+  __syncthreads();
+  for (u64 i = tid; i < p.ca.n; i += KDB)
+    if (p.ca.node[i] < KVT) tabS[p.ca.node[i]] = p.ca.cnt[i];
+  if (dvv)
+    for (u64 i = tid; i < p.cd.n; i += KDB)
+      if (p.cd.node[i] < KVT) tabD[p.cd.node[i]] = p.cd.cnt[i];
+  u64 v[KD_NV] = {0, 0, 0, 0, 0, 0, 0};
+  u64 a_lo = 0, d_lo = 0, am = 0, dm = 0, dh = 0;
+  u32 na = 0, nd = 0, ne = 0;
+  bool chg = false, big = false;
+  if (u < p.nk) {
+    const u64 k = p.keys[u];
+    key_run(p.a.key, p.a.n, k, a_lo, na);
+    key_run(p.d.key, p.d.n, k, d_lo, nd);
+    big = na > KD_RUN || nd > KD_RUN;
+  }
+  __syncthreads();  // (the tables)
+  if (u < p.nk && !big) {
+    // join_dot_sets over the key's rows, both sides in tuple order
+    u32 i = 0, j = 0;
+    Row ra{}, rb{};
+    if (na) ra = load_row(p.a, a_lo);
+    if (nd) rb = load_row(p.d, d_lo);
+    while (i < na || j < nd) {
+      int c;  // -1: the state row first, 1: the delta row first, 0: the same row
+      if (i >= na) {
+        c = 1;
+      } else if (j >= nd) {
+        c = -1;
+      } else {
+        bool lt, eq;
+        row_cmp_bf(ra, rb, lt, eq);
+        c = eq ? 0 : (lt ? -1 : 1);
+      }
+      if (c <= 0) {
+        // the state's row: kept if the delta has it too, or the delta's context does not
+        // cover its dot (Dots.member?, :67-73)
+        const bool keep = c == 0 || !(dvv ? vv_covers(tabD, p.cd, ra.node, ra.cnt)
+                                          : ctx_covers(p.cd.node, p.cd.cnt, p.cd.n, 1, ra.node, ra.cnt));
+        if (keep) {
+          am |= 1ull << i;
+          ne++;
+        } else {
+          chg = true;
+          if (p.has_tree) dh -= rhash(p.t, ra);
+        }
+        if (c == 0 && ++j < nd) rb = load_row(p.d, d_lo + j);
+        if (++i < na) ra = load_row(p.a, a_lo + i);
+      } else {
+        // the delta's row only: kept unless the state's context covers it
+        if (!vv_covers(tabS, p.ca, rb.node, rb.cnt)) {
+          dm |= 1ull << j;
+          ne++;
+          chg = true;
+          if (p.has_tree) dh += rhash(p.t, rb);
+        }
+        if (++j < nd) rb = load_row(p.d, d_lo + j);
+      }
+    }
+    p.a_lo[u] = a_lo;
+    p.d_lo[u] = d_lo;
+    p.runs[u] = na | ((u64)nd << 16) | ((u64)ne << 32) | (chg ? 1ull << 48 : 0ull);
+    p.amask[u] = am;
+    p.dmask[u] = dm;
+    p.dh[u] = dh;
+  }
+  v[0] = na;
+  v[1] = ne;
+  v[2] = chg ? 1 : 0;
+  v[3] = chg ? ne : 0;
+  v[4] = nd;
+  v[5] = (u64)(i64)((int)(ne > 0) - (int)(na > 0));
+  v[6] = (big ? KD_BIG : 0u) | (ne != na ? KD_MOVED : 0u);
+#pragma unroll
+  for (int q = 0; q < KD_NV; q++) {
+    u64 x = v[q];
+    if (q < KD_NV - 1) {
+#pragma unroll
+      for (int d = WAVE / 2; d >= 1; d >>= 1) x += __shfl_xor(x, d, WAVE);
+    } else {
+      x = __ballot(x & KD_BIG) ? KD_BIG : 0;
+      x |= __ballot(v[q] & KD_MOVED) ? KD_MOVED : 0;
+    }
+    if (lane == 0) red[q][w] = x;
+  }
+  __syncthreads();
+  if (tid < KD_NV) {
+    u64 s = 0;
+#pragma unroll
+    for (int x = 0; x < KDB / WAVE; x++) s = tid < KD_NV - 1 ? s + red[tid][x] : (s | red[tid][x]);
+    p.part[blockIdx.x * KD_NV + tid] = s;
+  }
+}
+
+// ---------------------------------------------------------------- scan
+// the workgroups' exclusive offsets of the additive figures (toff), the totals and the guard
+// into the count block: [0] edit rows [2] changed keys [3] their rows [4] guard [5] moved
+// [6] state rows of the keyset [7] distinct-key change (d_counts[1]: the context union's)
+constexpr int KSB = 1024;
+__global__ __launch_bounds__(KSB) void kd_scan_kernel(KdArgs p) {
+  __shared__ u64 s_w[KSB / WAVE];
+  __shared__ u64 carry[KD_NV];
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
+  if (tid < KD_NV) carry[tid] = 0;
+  __syncthreads();
+  for (u64 t0 = 0; t0 < p.ntiles; t0 += KSB) {
+    const u64 t = t0 + tid;
+#pragma unroll 1
+    for (int q = 0; q < KD_NV; q++) {
+      const u64 x = t < p.ntiles ? p.part[t * KD_NV + q] : 0;
+      if (q == KD_NV - 1) {  // flags: OR
+        const u64 o = (__ballot(x & KD_BIG) ? KD_BIG : 0) | (__ballot(x & KD_MOVED) ? KD_MOVED : 0);
+        if (lane == 0) s_w[w] = o;
+        __syncthreads();
+        if (tid == 0)
+          for (int i = 0; i < KSB / WAVE; i++) carry[q] |= s_w[i];
+        __syncthreads();
+        continue;
+      }
+      u64 inc = x;  // inclusive wave scan (u64: totals may pass 2^32)
+#pragma unroll
+      for (int d = 1; d < WAVE; d <<= 1) {
+        const u64 y = __shfl_up(inc, d, WAVE);
+        if (lane >= d) inc += y;
+      }
+      if (lane == WAVE - 1) s_w[w] = inc;
+      __syncthreads();
+      u64 below = carry[q];
+      for (int i = 0; i < w; i++) below += s_w[i];
+      if (t < p.ntiles) p.toff[t * KD_NV + q] = below + inc - x;
+      __syncthreads();
+      if (tid == 0)
+        for (int i = 0; i < KSB / WAVE; i++) carry[q] += s_w[i];
+      __syncthreads();
+    }
+  }
+  if (tid == 0) {
+    const u64 n_ak = carry[0], n_e = carry[1], n_chg = carry[2], n_rows = carry[3], n_d = carry[4];
+    u64 g = carry[6] & KD_BIG;
+    if (n_d != p.d.n) g |= KD_BAD;      // a delta row whose key is outside the keyset
+    if (n_chg > p.cap) g |= KD_CAP;     // the caller's changed-key buffer is too small
+    p.d_counts[0] = n_e;
+    p.d_counts[2] = n_chg;
+    p.d_counts[3] = n_rows;
+    p.d_counts[4] = g;
+    p.d_counts[5] = (carry[6] & KD_MOVED) ? 1 : 0;
+    p.d_counts[6] = n_ak;
+    p.d_counts[7] = carry[5];
+  }
+}
+
+// ---------------------------------------------------------------- write
+__global__ __launch_bounds__(KDB) void kd_write_kernel(KdArgs p) {
+  __shared__ u64 s_w[4][KDB / WAVE];
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
+  const u64 u = (u64)blockIdx.x * KDB + tid;
+  const u64 guard = p.d_counts[4];
+  const bool tree_bad = p.err && (*p.err & MERKLE_INPUT_ERR);
+  if (guard) return;  // (uniform) nothing is written: the caller falls back or reports
+  const bool moved = p.d_counts[5] != 0;
+  if (blockIdx.x == 0 && !tree_bad) {  // the union context into the state's (Dots.union, :155)
+    const u64 nc = p.d_counts[1];
+    for (u64 i = tid; i < nc && i < p.ca_cap; i += KDB) {
+      p.ca_node[i] = p.uc_node[i];
+      p.ca_cnt[i] = p.uc_cnt[i];
+    }
+  }
+  u64 rn = 0;
+  u32 na = 0, nd = 0, ne = 0;
+  bool chg = false;
+  if (u < p.nk) {
+    rn = p.runs[u];
+    na = (u32)(rn & 0xFFFF);
+    nd = (u32)((rn >> 16) & 0xFFFF);
+    ne = (u32)((rn >> 32) & 0xFFFF);
+    chg = (rn >> 48) & 1;
+  }
+  // exclusive in-workgroup prefixes of (na, ne, chg, chg rows) + the workgroup's offsets
+  const u64 x[4] = {na, ne, chg ? 1u : 0u, chg ? ne : 0u};
+  u64 pre[4];
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    u64 inc = x[q];
+#pragma unroll
+    for (int d = 1; d < WAVE; d <<= 1) {
+      const u64 y = __shfl_up(inc, d, WAVE);
+      if (lane >= d) inc += y;
+    }
+    if (lane == WAVE - 1) s_w[q][w] = inc;
+    pre[q] = inc - x[q];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    u64 below = p.toff[blockIdx.x * KD_NV + q];
+    for (int i = 0; i < w; i++) below += s_w[q][i];
+    pre[q] += below;
+  }
+  if (u >= p.nk) return;
+  const u64 k = p.keys[u];
+  const u64 a_lo = p.a_lo[u], d_lo = p.d_lo[u], am = p.amask[u], dm = p.dmask[u];
+  const u64 a_off = pre[0], e_off = pre[1], c_off = pre[2], r_off = pre[3];
+  const u64 n_e = p.d_counts[0], n_ak = p.d_counts[6];
+  // the splice index (splice.hip): where this key's rows go and where the untouched rows
+  // before it move
+  const i64 gap = (i64)a_lo - (i64)a_off;
+  if (moved) {
+    p.end[u] = a_lo + na;
+    p.shift[u] = (i64)e_off - (i64)a_off;
+    const u64 end_lo = u > 0 ? p.a_lo[u - 1] + (p.runs[u - 1] & 0xFFFF) : 0ull;
+    const u64 end_hi = a_lo + na;
+    for (u64 t = (end_lo + SPLICE_TILE - 1) / SPLICE_TILE; t <= p.a_tiles && t * SPLICE_TILE < end_hi; t++)
+      p.tile_u0[t] = u;
+    if (u == p.nk - 1) {
+      p.shift[p.nk] = (i64)n_e - (i64)n_ak;
+      for (u64 t = (end_hi + SPLICE_TILE - 1) / SPLICE_TILE; t <= p.a_tiles; t++) p.tile_u0[t] = p.nk;
+    }
+  }
+  // the key's new rows in tuple order: the kept state rows and the new delta rows (disjoint)
+  const bool wr_state = !tree_bad;  // in place: only when the tree took the update
+  const bool wr_rows = chg && p.has_rows && r_off + ne <= p.rows_cap;
+  if (!(wr_state || moved) && !wr_rows && !chg) return;
+  u32 i = 0, j = 0, o = 0;
+  auto next_a = [&]() { while (i < na && !((am >> i) & 1)) i++; };
+  auto next_d = [&]() { while (j < nd && !((dm >> j) & 1)) j++; };
+  next_a();
+  next_d();
+  Row ra{}, rb{};
+  if (i < na) ra = load_row(p.a, a_lo + i);
+  if (j < nd) rb = load_row(p.d, d_lo + j);
+  while (i < na || j < nd) {
+    bool takeA;
+    if (i >= na) {
+      takeA = false;
+    } else if (j >= nd) {
+      takeA = true;
+    } else {
+      bool lt, eq;
+      row_cmp_bf(ra, rb, lt, eq);
+      takeA = lt;
+    }
+    const Row r = takeA ? ra : rb;
+    if (moved)
+      store_row(p.sp, (u64)((i64)(e_off + o) + gap), r);
+    else if (wr_state && chg)  // (unchanged keys keep their rows as they are)
+      store_row(p.aw, a_lo + o, r);
+    if (wr_rows) store_row(p.rows, r_off + o, r);
+    o++;
+    if (takeA) {
+      i++;
+      next_a();
+      if (i < na) ra = load_row(p.a, a_lo + i);
+    } else {
+      j++;
+      next_d();
+      if (j < nd) rb = load_row(p.d, d_lo + j);
+    }
+  }
+  if (chg && c_off < p.cap) p.changed[c_off] = k;
+}
+
+}  // namespace
+
+hipError_t launch_kd_join(const KdArgs& p0, hipStream_t st) {
+  KdArgs p = p0;
+  p.ntiles = (p.nk + KDB - 1) / KDB;
+  if (p.ntiles == 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(kd_count_kernel, dim3((unsigned)p.ntiles), dim3(KDB), 0, st, p);
+  hipLaunchKernelGGL(kd_scan_kernel, dim3(1), dim3(KSB), 0, st, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_kd_write(const KdArgs& p0, hipStream_t st) {
+  KdArgs p = p0;
+  p.ntiles = (p.nk + KDB - 1) / KDB;
+  hipLaunchKernelGGL(kd_write_kernel, dim3((unsigned)p.ntiles), dim3(KDB), 0, st, p);
+  return hipGetLastError();
+}
+
+}  // namespace dg

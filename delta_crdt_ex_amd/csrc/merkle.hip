@@ -537,6 +537,48 @@ __global__ __launch_bounds__(UB) void merkle_update_kernel(MT t, Rows olds, Rows
   if (__ballot(over) && (threadIdx.x & (WAVE - 1)) == 0) atomicOr(err, ERR_COUNT);
 }
 
+// The same put/delete from kdelta.hip's per-key figures: key u changed (runs bit 48) with
+// leaf change dh[u] and row-count change ne - na; sign -1 undoes sign +1.  The distinct-key
+// change is kd_scan_kernel's (d_counts[7]).
+__global__ __launch_bounds__(UB) void kd_tree_kernel(MT t, const u64* keys, const u64* runs, const u64* dh,
+                                                     u64 nk, const u64* guard, int sign, u32* dirty,
+                                                     u32* err, i64* cdelta) {
+  if (*guard) return;  // (uniform) the per-key figures are incomplete: nothing to apply
+  const u64 i = (u64)blockIdx.x * UB + threadIdx.x;
+  bool bad = false, over = false;
+  if (i < nk) {
+    const u64 rn = runs[i];
+    const int na = (int)(rn & 0xFFFF), ne = (int)((rn >> 32) & 0xFFFF);
+    const u64 d = sign > 0 ? dh[i] : (u64)0 - dh[i];
+    const int dr = sign > 0 ? ne - na : na - ne;
+    if (((rn >> 48) & 1) && (d != 0 || dr != 0)) {
+      const u64 x = keys[i];
+      if (t.sb && (x >> (64 - t.sb)) != t.shard) {
+        bad = true;
+      } else {
+        const u64 b = bucket_of(t, x);
+        u64* lvl = t.nodes + ((1ull << t.depth) - 1);
+        atomicAdd((unsigned long long*)&lvl[b], (unsigned long long)d);
+        if (dr) {  // the bucket's row count in its aligned 32-bit word (as merkle_update_kernel)
+          u32* wd = (u32*)t.counts + (b >> 1);
+          const u32 sh = 16u * (u32)(b & 1);
+          if (dr > 0) {
+            const u32 old = atomicAdd(wd, (u32)dr << sh);
+            over = ((old >> sh) & 0xFFFFu) + (u32)dr > 0xFFFFu;
+          } else {
+            atomicSub(wd, (u32)(-dr) << sh);
+          }
+        }
+        const u32 L1 = t.depth < (u32)UPL ? t.depth : (u32)UPL;
+        dirty[b >> L1] = 1u;
+        if (cdelta && dr) atomicAdd((unsigned long long*)&cdelta[b >> L1], (unsigned long long)(i64)dr);
+      }
+    }
+  }
+  if (__ballot(bad) && (threadIdx.x & (WAVE - 1)) == 0) atomicOr(err, ERR_SHARD);
+  if (__ballot(over) && (threadIdx.x & (WAVE - 1)) == 0) atomicOr(err, ERR_COUNT);
+}
+
 // ---------------------------------------------------------------- key-level merge
 // Merge keys[ia, ie) of store A (rows) with B, where B is either a store (rows) or a
 // list of (key, leaf) pairs; emit the keys present on one side only or with different
@@ -1577,6 +1619,21 @@ hipError_t launch_merkle_update(const MerkleT& m, const Rows& olds, const Rows& 
                        keys, n_keys, dirty, d_keys, err, cd);
   hipLaunchKernelGGL(merkle_chunk_kernel<false>, dim3((unsigned)G), dim3(UPB), 0, st, news, t, dirty,
                      arrive, hand, (u64*)nullptr, err, (const i64*)cd);
+  return hipGetLastError();
+}
+
+hipError_t launch_kd_tree(const MerkleT& m, const u64* keys, const u64* runs, const u64* dh, u64 nk,
+                          const u64* guard, int sign, u32* dirty, u32* arrive, u64* hand, i64* cdelta,
+                          u32* err, hipStream_t st) {
+  const MT t = mt_of(m);
+  const u64 G = merkle_chunks(t.depth);
+  i64* cd = t.starts ? cdelta : nullptr;
+  if (nk)
+    hipLaunchKernelGGL(kd_tree_kernel, dim3(grid_of(nk, UB)), dim3(UB), 0, st, t, keys, runs, dh, nk, guard,
+                       sign, dirty, err, cd);
+  Rows none{};
+  hipLaunchKernelGGL(merkle_chunk_kernel<false>, dim3((unsigned)G), dim3(UPB), 0, st, none, t, dirty, arrive,
+                     hand, (u64*)nullptr, err, (const i64*)cd);
   return hipGetLastError();
 }
 

@@ -243,8 +243,10 @@ __global__ __launch_bounds__(SB) void splice_erows_kernel(SpliceArgs p) {
 // One workgroup per ST state rows: every row outside the keyset to its place.  The
 // workgroup issues its rows' loads first: the index entries that place them are staged
 // while the loads are in flight.
+static_assert(ST == SPLICE_TILE, "dg_launch.h's copy tile");
 __global__ __launch_bounds__(SB) void splice_kernel(SpliceArgs p) {
   if (p.run_if && *p.run_if == 0) return;  // (uniform) nothing moved: not needed
+  if (p.kguard && *p.kguard) return;       // (uniform) the index was not written
   __shared__ u64 s_end[SLC], s_lo[SLC];
   __shared__ i64 s_shift[SLC];
   TileRows x;
@@ -323,6 +325,12 @@ hipError_t launch_splice_index(SpliceArgs p, hipStream_t st) {
   p.a_tiles = (p.a.n + ST - 1) / ST;
   hipLaunchKernelGGL(splice_index_kernel, dim3((unsigned)((p.nk + 1 + SB - 1) / SB)), dim3(SB), 0,
                      st, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_splice_move(SpliceArgs p, hipStream_t st) {
+  p.a_tiles = (p.a.n + ST - 1) / ST;
+  if (p.a_tiles) hipLaunchKernelGGL(splice_kernel, dim3((unsigned)p.a_tiles), dim3(SB), 0, st, p);
   return hipGetLastError();
 }
 
