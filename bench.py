@@ -215,10 +215,14 @@ def config4_round(eng, torch, dev, rank=0, world=1, keys_per_rank=12_500_000, st
         t1 = time.perf_counter()
         delta = eng.take_keys(sb, keys)
         t2 = time.perf_counter()
+        e2, e3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e2.record(eng.stream)
         changed, swapped = eng.join_delta(st, sc, delta, cb, keys, spare, tt)
+        e3.record(eng.stream)
         torch.cuda.synchronize()
         t3 = time.perf_counter()
         t.update(diff=t1 - t0, take=t2 - t1, join_delta=t3 - t2, total=t3 - t0,
+                 join_delta_ev=e2.elapsed_time(e3) * 1e-3,
                  diff_ev=e0.elapsed_time(e1) * 1e-3, keys=int(keys.numel()), total_keys=total,
                  rows=delta.n, changed=int(changed.numel()), in_place=not swapped)
         t["ok"] = tt.root() == eng.merkle_build(st, depth, None, sbits, rank if sbits else 0,
@@ -234,7 +238,7 @@ def config4_round(eng, torch, dev, rank=0, world=1, keys_per_rank=12_500_000, st
                        "causal_crdt.ex:91-110,252-270 with both replicas on this GPU (between "
                        "BEAM nodes each hop is one message); synchronous calls, wall time"}
     med = {k: float(np.median([r[k] for r in rounds]))
-           for k in ("diff", "take", "join_delta", "total", "diff_ev")}
+           for k in ("diff", "take", "join_delta", "total", "diff_ev", "join_delta_ev")}
     last = rounds[-1]
     acc = _diff_accounting(ta, tb)
     diff_alg = acc["bytes_no_keys"] + 8 * last["total_keys"]
@@ -263,7 +267,11 @@ def config4_round(eng, torch, dev, rank=0, world=1, keys_per_rank=12_500_000, st
                                            "sync_call_us: one synchronous dg_merkle_diff with "
                                            "its count publish and host wait, median of 5 "
                                            "rounds"},
-        "round_us": {k: v * 1e6 for k, v in med.items() if k != "diff_ev"},
+        "round_us": {k: v * 1e6 for k, v in med.items() if k not in ("diff_ev", "join_delta_ev")},
+        "join_delta_device_us": med["join_delta_ev"] * 1e6,
+        "join_delta_note": "round_us.join_delta: wall time of the Python call (ctypes, its one "
+                           "host wait, a torch synchronize); join_delta_device_us: HIP events on "
+                           "the engine stream around the same call (first kernel to last)",
         "round_keys": last["keys"], "round_total_keys": last["total_keys"],
         "round_delta_rows": last["rows"], "round_changed_keys": last["changed"],
         "update_equals_rebuild": all(r["ok"] for r in rounds),

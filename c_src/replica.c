@@ -494,50 +494,47 @@ static int apply_delta(dgr_state* s, const dg_store* drows, const dg_context* dc
     TRY(apply_small(s, drows, dctx, dkeys, n_keys, out, &done));
     if (done) return DG_OK;
   }
-  uint64_t S = umax(n_keys, 1);
+  /* the changed keys, their rows and the joined context straight into the page-locked
+   * block (dg_join_delta_out: the kernels write it, one wait); rows of the changed keys
+   * past the block (a key with several entries) are taken afterwards */
+  uint64_t S = umax(2 * n_keys + 64, 1);
   TRY(grow_back(g, S, s->ctx.n + dctx->n));
   S = g->back_s;
-  dg_store tk = back_rows(g->d_back, S);
+  uint64_t C = g->back_c;
+  uint64_t* hb = g->h_back;
+  dg_store tk = back_rows(hb, S);
+  dg_context co = {DG_CTX_VV, 0, (uint32_t*)(hb + 6 * S + C), hb + 6 * S, 0, C};
   uint64_t n_changed = 0;
   int swapped = 0;
-  const int rc = dg_join_delta_rows(g->e, &s->rows, &s->ctx, drows, dctx, dkeys, n_keys, &s->spare,
-                                    s->has_tree ? &s->tree : NULL, g->d_back, S, &n_changed, &swapped, &tk);
+  const int rc = dg_join_delta_out(g->e, &s->rows, &s->ctx, drows, dctx, dkeys, n_keys, &s->spare,
+                                   s->has_tree ? &s->tree : NULL, hb, S, &n_changed, &swapped, &tk, &co);
   s->version++; /* applied, or failed: either way no older struct reads the device again */
   TRY(rc);
-  if (tk.n > tk.cap) {
-    /* more rows than the block's stride: grow it (keeping the changed keys, parked in the
-     * message buffer) and take the rows from the joined state */
-    TRY(grow_msg(g, n_changed));
-    TRY(dg_copy_async(g->e, g->d_msg, g->d_back, n_changed * 8));
+  if (tk.n > tk.cap || co.n > co.cap) {
+    /* park the changed keys, grow the block, take the rows from the joined state and copy
+     * the context (the kernels write the page-locked block directly) */
+    TRY(grow_msg(g, n_changed + 1));
+    memcpy(g->h_msg, hb, n_changed * 8);
     TRY(grow_back(g, umax(tk.n, n_changed), s->ctx.n));
     S = g->back_s;
-    TRY(dg_copy_async(g->e, g->d_back, g->d_msg, n_changed * 8));
-    tk = back_rows(g->d_back, S);
-    TRY(dg_take_keys(g->e, &s->rows, g->d_back, n_changed, &tk));
+    C = g->back_c;
+    hb = g->h_back;
+    memcpy(hb, g->h_msg, n_changed * 8);
+    TRY(dg_copy_async(g->e, g->d_msg, g->h_msg, n_changed * 8));
+    tk = back_rows(hb, S);
+    TRY(dg_take_keys(g->e, &s->rows, g->d_msg, n_changed, &tk));
+    TRY(dg_copy_async(g->e, hb + 6 * S, s->ctx.cnt, s->ctx.n * 8));
+    TRY(dg_copy_async(g->e, hb + 6 * S + C, s->ctx.node, s->ctx.n * 4));
+    TRY(dg_engine_sync(g->e));
+    co.n = s->ctx.n;
+    co.kind = s->ctx.kind;
   }
-  const uint64_t C = g->back_c, nc = s->ctx.n, nr = tk.n;
-  uint64_t* db = g->d_back;
-  uint64_t* hb = g->h_back;
-  /* the context next to the rows, then home: the whole block in one copy when small,
-   * else the used ranges; one wait */
-  TRY(dg_copy_async(g->e, db + 6 * S, s->ctx.cnt, nc * 8));
-  TRY(dg_copy_async(g->e, db + 6 * S + C, s->ctx.node, nc * 4));
-  if (6 * S + 2 * C <= 65536) {
-    TRY(dg_copy_async(g->e, hb, db, (6 * S + 2 * C) * 8));
-  } else {
-    TRY(dg_copy_async(g->e, hb, db, n_changed * 8));
-    for (int c = 1; c <= 4; c++) TRY(dg_copy_async(g->e, hb + c * S, db + c * S, nr * 8));
-    TRY(dg_copy_async(g->e, hb + 5 * S, db + 5 * S, nr * 4));
-    TRY(dg_copy_async(g->e, hb + 6 * S, db + 6 * S, nc * 8));
-    TRY(dg_copy_async(g->e, hb + 6 * S + C, db + 6 * S + C, nc * 4));
-  }
-  TRY(dg_engine_sync(g->e));
   out->version = s->version;
   out->n_changed = n_changed;
   out->keys = hb;
   out->rows = back_rows(hb, S);
-  out->rows.n = nr;
-  dg_context c = {s->ctx.kind, 0, (uint32_t*)(hb + 6 * S + C), hb + 6 * S, nc, C};
+  out->rows.n = tk.n;
+  dg_context c = {co.kind, 0, (uint32_t*)(hb + 6 * S + C), hb + 6 * S, co.n, C};
   out->ctx = c;
   return DG_OK;
 }
@@ -644,7 +641,7 @@ int dgr_mutate_batch(dgr_state* s, uint64_t version, uint32_t node, uint64_t m, 
     TRY(grow_ctx(g, &g->mctx, attempt ? s->rows.n + n_adds + 1 : 8 * m + n_adds + 1));
     g->mctx.kind = DG_CTX_DOTS;
     g->mrows.n = 0;
-    rc = dg_mutate_batch(g->e, &s->rows, &s->ctx, node, m, (const uint8_t*)(d + 4 * m), d, d + m,
+    rc = dg_mutate_batch_async(g->e, &s->rows, &s->ctx, node, m, (const uint8_t*)(d + 4 * m), d, d + m,
                          (const int64_t*)(d + 2 * m), d + 3 * m, n_adds, &g->mrows, &g->mctx, g->mkeys,
                          g->mkeys_cap, &n_keys);
     if (rc == DG_E_CAPACITY && attempt == 0) continue;

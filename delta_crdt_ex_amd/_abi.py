@@ -165,12 +165,20 @@ _SIGS = {
                                      C.POINTER(dg_store), C.POINTER(dg_context), P64, C.c_uint64,
                                      C.POINTER(dg_store), C.c_void_p, P64, C.c_uint64, P64,
                                      C.POINTER(C.c_int), C.POINTER(dg_store)]),
+    "dg_join_delta_out": (C.c_int, [C.c_void_p, C.POINTER(dg_store), C.POINTER(dg_context),
+                                    C.POINTER(dg_store), C.POINTER(dg_context), P64, C.c_uint64,
+                                    C.POINTER(dg_store), C.c_void_p, P64, C.c_uint64, P64,
+                                    C.POINTER(C.c_int), C.POINTER(dg_store), C.POINTER(dg_context)]),
     "dg_take_keys": (C.c_int, [C.c_void_p, C.POINTER(dg_store), P64, C.c_uint64,
                                C.POINTER(dg_store)]),
     "dg_mutate_batch": (C.c_int, [C.c_void_p, C.POINTER(dg_store), C.POINTER(dg_context),
                                   C.c_uint32, C.c_uint64, C.c_void_p, P64, P64, PI64, P64,
                                   C.c_uint64, C.POINTER(dg_store), C.POINTER(dg_context), P64,
                                   C.c_uint64, P64]),
+    "dg_mutate_batch_async": (C.c_int, [C.c_void_p, C.POINTER(dg_store), C.POINTER(dg_context),
+                                        C.c_uint32, C.c_uint64, C.c_void_p, P64, P64, PI64, P64,
+                                        C.c_uint64, C.POINTER(dg_store), C.POINTER(dg_context), P64,
+                                        C.c_uint64, P64]),
     "dg_join2_async": (C.c_int, [C.c_void_p, C.POINTER(dg_store), C.POINTER(dg_context),
                                  C.POINTER(dg_store), C.POINTER(dg_context), P64, C.c_uint64,
                                  C.POINTER(dg_store), C.POINTER(dg_context), P64]),

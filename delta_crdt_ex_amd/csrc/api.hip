@@ -51,6 +51,8 @@ struct dg_engine {
   // union context (DG_KD=0: the splice path with its host waits, for A/B)
   void* kdb = nullptr;
   size_t kdb_cap = 0;
+  void* kdz = nullptr;  // its tree update's dirty flags and chunk row-count changes: zero
+  size_t kdz_cap = 0;   //   between calls (the re-reduction consumes them)
   bool kd = true;
   // the full diff's per-group key sums: two buffers of diff_bsum_cap words, zero when
   // allocated; a call adds into one and its write kernel zeroes the other, which the
@@ -307,12 +309,23 @@ int sync_words(dg_engine* e) {
 constexpr int MERKLE_ARRIVE = 6;
 constexpr int CONT_HOME = 18;  // h_pub words [18, 24): dg_merkle_continue_home's result header
 constexpr int TAIL_ARRIVE = 7;  // dg_join_delta_home's tail kernel: every workgroup arrives
+constexpr int KD_ARRIVE = 8;    // dg_join_delta's count kernel: the last workgroup scans
+constexpr int MUT_ARRIVE = 9;   // dg_mutate_batch's count kernel: the last tile scans
+constexpr int SPL_ARRIVE = 10;  // dg_join_delta's moved-rows copy: the last workgroup publishes
+constexpr int KD_ERR = 11;      // dg_join_delta's tree input-error word (zero between calls)
+
+int published_errors(dg_engine* e);
 
 int read_counts(dg_engine* e, int n) {
   (void)n;
-  e->last_err_bits = 0;
   const int rc = sync_words(e);
   if (rc != DG_OK) return rc;
+  return published_errors(e);
+}
+
+// the error bits of the count block just published (a look-back timeout, an aborted grid)
+int published_errors(dg_engine* e) {
+  e->last_err_bits = 0;
   u32 err = 0;
   memcpy(&err, (const char*)&e->h_counts[8] + sizeof(u32), sizeof(u32));
   if (err) {
@@ -766,6 +779,7 @@ int dg_engine_destroy(dg_engine* e) {
   if (e->ubuf) hipFree(e->ubuf);
   if (e->sml) hipFree(e->sml);
   if (e->kdb) hipFree(e->kdb);
+  if (e->kdz) hipFree(e->kdz);
   if (e->diff_bsum) hipFree(e->diff_bsum);
   if (e->h_stage) hipHostFree(e->h_stage);
   if (e->own_stream && e->stream) hipStreamDestroy(e->stream);
@@ -939,7 +953,7 @@ static int take_changed_rows(dg_engine* e, const dg_store* src, const uint64_t* 
 static int kd_join_delta(dg_engine* e, dg_store* state, dg_context* state_ctx, const dg_store* delta,
                          const dg_context* delta_ctx, const uint64_t* keys, uint64_t n_keys, dg_store* spare,
                          dg_merkle* tree, uint64_t* changed, uint64_t cap, uint64_t* n_changed, int* swapped,
-                         dg_store* rows, bool* done) {
+                         dg_store* rows, dg_context* ctx_out, bool* done) {
   *done = false;
   if (!e->kd || n_keys == 0 || state_ctx->kind != DG_CTX_VV || state->cap < state->n ||
       !pair_aligned(state->key, state->val, state->ts, state->node, state->cnt) ||
@@ -994,34 +1008,46 @@ static int kd_join_delta(dg_engine* e, dg_store* state, dg_context* state_ctx, c
     p.rows_cap = rows->cap;
   }
   p.sp = rows_out_of(spare);
+  if (ctx_out) {
+    p.co_node = ctx_out->node;
+    p.co_cnt = ctx_out->cnt;
+    p.co_cap = ctx_out->cap;
+  }
   p.a_tiles = a_tiles;
   p.has_tree = tree != nullptr;
   if (tree) p.t = merkle_of(tree);
   p.d_counts = e->d_counts;
-  u32* err = e->ticket + 3;
-  p.err = err;
-  // the tree update's scratch (hand-off words | dirty flags | chunk row-count changes), as
-  // tree_update lays it out; dirty, cdelta and the error word zeroed in one launch
+  p.arrive = e->ticket + KD_ARRIVE;
+  // the tree update's scratch: hand-off words (engine scratch), and the dirty flags and
+  // chunk row-count changes in a buffer of their own that stays zero between calls
   u32* dirty = nullptr;
   u64* hand = nullptr;
   i64* cdelta = nullptr;
   u64 zw = 0;
+  u32* err = e->ticket + KD_ERR;
+  p.err = err;
   if (tree) {
     const u64 chunks = merkle_chunks(tree->depth), cw = merkle_ctr_words(tree->depth);
     const u64 cpad = (chunks + 1) & ~1ull;
     zw = cpad + 2 * chunks;
-    TRY(ensure_tmp(e, (cw + zw) * sizeof(u32)));
+    TRY(ensure_tmp(e, cw * sizeof(u32)));
     hand = (u64*)e->tmp;
-    dirty = (u32*)e->tmp + cw;
+    if (zw * sizeof(u32) > e->kdz_cap) {
+      TRY(ensure_buf(e, &e->kdz, &e->kdz_cap, zw * sizeof(u32)));
+      HIP_TRY(hipMemsetAsync(e->kdz, 0, e->kdz_cap, e->stream));
+    }
+    dirty = (u32*)e->kdz;
     cdelta = (i64*)(dirty + cpad);
   }
-  HIP_TRY(launch_splice_finish(nullptr, nullptr, 0, nullptr, nullptr, dirty, zw, nullptr, err, e->stream));
+  p.dirty = dirty;
+  p.cdelta = cdelta;
+  p.cu_tmp = cu_tmp;
+  // four launches, one wait: the count (the per-key joins, the tree's put/delete, the scan
+  // and the context union by its last workgroup), the tree's re-reduction, the write, the
+  // moved rows' copy (its last workgroup publishes the count block)
   HIP_TRY(launch_kd_join(p, e->stream));
-  HIP_TRY(launch_ctx_union(ctx_of(state_ctx), ctx_of(delta_ctx), uc_node, uc_cnt, e->d_counts + 1, cu_tmp,
-                           e->stream));
   if (tree)
-    HIP_TRY(launch_kd_tree(merkle_of(tree), keys, p.runs, p.dh, nk, e->d_counts + 4, 1, dirty,
-                           e->ticket + MERKLE_ARRIVE, hand, cdelta, err, e->stream));
+    HIP_TRY(launch_merkle_rehash(merkle_of(tree), dirty, e->ticket + MERKLE_ARRIVE, hand, cdelta, err, e->stream));
   HIP_TRY(launch_kd_write(p, e->stream));
   SpliceArgs sp{};
   sp.a = rows_of(state);
@@ -1034,26 +1060,35 @@ static int kd_join_delta(dg_engine* e, dg_store* state, dg_context* state_ctx, c
   sp.out = rows_out_of(spare);
   sp.run_if = e->d_counts + 5;  // rows moved
   sp.kguard = e->d_counts + 4;
+  sp.h_pub = e->d_pub;
+  sp.pub_counts = e->d_counts;
+  sp.seq = ++e->pub_seq;
+  sp.arrive_all = e->ticket + SPL_ARRIVE;
   HIP_TRY(launch_splice_move(sp, e->stream));
-  TRY(read_counts(e, 8));
+  TRY(wait_published(e, sp.seq));
+  TRY(published_errors(e));
   const u64 g = e->h_counts[4];
-  if (g & (KD_BAD | KD_BIG)) return DG_OK;  // nothing written: another path applies
-  if (g & KD_CAP)
-    return fail(DG_E_CAPACITY, "dg_join_delta: %llu changed keys > cap %llu", (unsigned long long)e->h_counts[2],
-                (unsigned long long)cap);
-  if (e->h_ticket[3] & MERKLE_INPUT_ERR) {
-    // the tree update met an input error: no state row and no context entry was written
-    // (the write kernel saw the error word); the same update with the opposite sign
-    // restores every bucket node and count bit for bit
-    const int rc = input_error(e, "dg_join_delta");
+  const u32 tbits = e->h_ticket[KD_ERR];
+  if (g || (tbits & MERKLE_INPUT_ERR)) {
+    // nothing of the state or its context was written (the write kernel saw the guard or
+    // the error word), but the count kernel put the changes into the tree: the same update
+    // with the opposite sign restores every bucket node and count bit for bit
+    const int rc = (g & (KD_BAD | KD_BIG)) ? DG_OK
+                   : (g & KD_CAP) ? fail(DG_E_CAPACITY, "dg_join_delta: %llu changed keys > cap %llu",
+                                         (unsigned long long)e->h_counts[2], (unsigned long long)cap)
+                  : (tbits & MERKLE_ERR_SHARD) ? fail(DG_E_INVAL, "dg_join_delta: a key outside the tree's shard")
+                                  : fail(DG_E_CAPACITY, "dg_join_delta: a bucket holds more than 65535 rows "
+                                                        "(use a deeper tree)");
     const std::string msg = g_err;
-    HIP_TRY(launch_splice_finish(nullptr, nullptr, 0, nullptr, nullptr, dirty, zw, nullptr, nullptr, e->stream));
-    HIP_TRY(launch_kd_tree(merkle_of(tree), keys, p.runs, p.dh, nk, e->d_counts + 4, -1, dirty,
-                           e->ticket + MERKLE_ARRIVE, hand, cdelta, err, e->stream));
-    HIP_TRY(hipMemsetAsync(err, 0, sizeof(u32), e->stream));
-    TRY(read_counts(e, 0));
+    if (tree) {  // (dirty and cdelta are zero again: the re-reduction consumed them)
+      HIP_TRY(launch_kd_tree(merkle_of(tree), keys, p.runs, p.dh, nk, nullptr, -1, dirty,
+                             e->ticket + MERKLE_ARRIVE, hand, cdelta, err, e->stream));
+      HIP_TRY(hipMemsetAsync(err, 0, sizeof(u32), e->stream));  // (the undo's own bits too)
+      TRY(read_counts(e, 0));
+    }
     g_err = msg;
-    return rc;
+    return rc;  // (DG_OK with *done false: a delta row outside the keyset or a long key run --
+                // the full join or the splice applies)
   }
   const u64 n_e = e->h_counts[0], n_chg = e->h_counts[2], n_rows = e->h_counts[3];
   const u64 n_ak = e->h_counts[6], dk = e->h_counts[7];
@@ -1068,15 +1103,20 @@ static int kd_join_delta(dg_engine* e, dg_store* state, dg_context* state_ctx, c
   if (tree) tree->n_keys += dk;
   *n_changed = n_chg;
   if (rows) rows->n = n_rows;  // (more than rows->cap: not written, as the caller's contract says)
+  if (ctx_out) {
+    ctx_out->n = state_ctx->n;  // (more than ctx_out->cap: not written)
+    ctx_out->kind = DG_CTX_VV;
+  }
   *done = true;
   return DG_OK;
 }
 
 // dg_join_delta[_rows]: rows (optional) receives the changed keys' joined rows
-static int join_delta_impl(dg_engine* e, dg_store* state, dg_context* state_ctx, const dg_store* delta,
+// ctx_out (optional): a copy of the joined context
+static int join_delta_core(dg_engine* e, dg_store* state, dg_context* state_ctx, const dg_store* delta,
                            const dg_context* delta_ctx, const uint64_t* keys, uint64_t n_keys,
                            dg_store* spare, dg_merkle* tree, uint64_t* changed, uint64_t cap,
-                           uint64_t* n_changed, int* swapped, dg_store* rows) {
+                           uint64_t* n_changed, int* swapped, dg_store* rows, dg_context* ctx_out, bool* kd_done) {
   if (!e) return fail(DG_E_INVAL, "null engine");
   if (!swapped || !n_changed || (cap && !changed) || !spare || !state || !state_ctx)
     return fail(DG_E_INVAL, "dg_join_delta: null argument");
@@ -1106,7 +1146,8 @@ static int join_delta_impl(dg_engine* e, dg_store* state, dg_context* state_ctx,
   {
     bool done = false;
     TRY(kd_join_delta(e, state, state_ctx, delta, delta_ctx, keys, n_keys, spare, tree, changed, cap,
-                      n_changed, swapped, rows, &done));
+                      n_changed, swapped, rows, ctx_out, &done));
+    *kd_done = done;
     if (done) return DG_OK;
   }
   Splice w;
@@ -1334,6 +1375,25 @@ int dg_join_delta_home(dg_engine* e, dg_store* state, dg_context* state_ctx, con
   return DG_OK;
 }
 
+static int join_delta_impl(dg_engine* e, dg_store* state, dg_context* state_ctx, const dg_store* delta,
+                           const dg_context* delta_ctx, const uint64_t* keys, uint64_t n_keys,
+                           dg_store* spare, dg_merkle* tree, uint64_t* changed, uint64_t cap,
+                           uint64_t* n_changed, int* swapped, dg_store* rows, dg_context* ctx_out = nullptr) {
+  bool kd_done = false;
+  TRY(join_delta_core(e, state, state_ctx, delta, delta_ctx, keys, n_keys, spare, tree, changed, cap, n_changed,
+                      swapped, rows, ctx_out, &kd_done));
+  if (ctx_out && !kd_done) {  // (the other paths: the context copied after the join)
+    ctx_out->n = state_ctx->n;
+    ctx_out->kind = state_ctx->kind;
+    if (state_ctx->n <= ctx_out->cap && state_ctx->n) {
+      HIP_TRY(hipMemcpyAsync(ctx_out->node, state_ctx->node, state_ctx->n * 4, hipMemcpyDefault, e->stream));
+      HIP_TRY(hipMemcpyAsync(ctx_out->cnt, state_ctx->cnt, state_ctx->n * 8, hipMemcpyDefault, e->stream));
+      HIP_TRY(hipStreamSynchronize(e->stream));
+    }
+  }
+  return DG_OK;
+}
+
 int dg_join_delta(dg_engine* e, dg_store* state, dg_context* state_ctx, const dg_store* delta,
                   const dg_context* delta_ctx, const uint64_t* keys, uint64_t n_keys,
                   dg_store* spare, dg_merkle* tree, uint64_t* changed, uint64_t cap,
@@ -1349,6 +1409,15 @@ int dg_join_delta_rows(dg_engine* e, dg_store* state, dg_context* state_ctx, con
   if (!rows) return fail(DG_E_INVAL, "dg_join_delta_rows: null rows");
   return join_delta_impl(e, state, state_ctx, delta, delta_ctx, keys, n_keys, spare, tree, changed,
                          cap, n_changed, swapped, rows);
+}
+
+int dg_join_delta_out(dg_engine* e, dg_store* state, dg_context* state_ctx, const dg_store* delta,
+                      const dg_context* delta_ctx, const uint64_t* keys, uint64_t n_keys,
+                      dg_store* spare, dg_merkle* tree, uint64_t* changed, uint64_t cap,
+                      uint64_t* n_changed, int* swapped, dg_store* rows, dg_context* ctx_out) {
+  if (!rows || !ctx_out) return fail(DG_E_INVAL, "dg_join_delta_out: null rows or ctx_out");
+  return join_delta_impl(e, state, state_ctx, delta, delta_ctx, keys, n_keys, spare, tree, changed,
+                         cap, n_changed, swapped, rows, ctx_out);
 }
 
 }  // extern "C"
@@ -1651,11 +1720,11 @@ int dg_take_keys(dg_engine* e, const dg_store* s, const uint64_t* keys, uint64_t
   return DG_OK;
 }
 
-int dg_mutate_batch(dg_engine* e, const dg_store* state, const dg_context* ctx, uint32_t node,
-                    uint64_t m, const uint8_t* kind, const uint64_t* key, const uint64_t* val,
-                    const int64_t* ts, const uint64_t* add_rank, uint64_t n_adds, dg_store* delta,
-                    dg_context* delta_dots, uint64_t* keys_out, uint64_t keys_cap,
-                    uint64_t* n_keys_out) {
+static int mutate_batch_impl(dg_engine* e, const dg_store* state, const dg_context* ctx, uint32_t node,
+                             uint64_t m, const uint8_t* kind, const uint64_t* key, const uint64_t* val,
+                             const int64_t* ts, const uint64_t* add_rank, uint64_t n_adds, dg_store* delta,
+                             dg_context* delta_dots, uint64_t* keys_out, uint64_t keys_cap,
+                             uint64_t* n_keys_out, bool sync) {
   if (!e) return fail(DG_E_INVAL, "null engine");
   TRY(check_store(state, "dg_mutate_batch state"));
   TRY(check_ctx(ctx, "dg_mutate_batch ctx"));
@@ -1672,14 +1741,10 @@ int dg_mutate_batch(dg_engine* e, const dg_store* state, const dg_context* ctx, 
   HIP_TRY(hipMemsetAsync(e->ticket + 3, 0, sizeof(u32), e->stream));
   u32* err = e->ticket + 3;
   HIP_TRY(launch_mutate_count(rows_of(state), ctx_of(ctx), node, kind, key, val, ts, add_rank, m,
-                              e->state, e->d_counts, err, e->stream));
-  TRY(read_counts(e, 3));
+                              e->state, e->d_counts, err, e->ticket + MUT_ARRIVE, e->stream));
+  TRY(read_counts(e, 3));  // (the counts and the order flag, err = ticket[3], in one wait)
   const u64 n_keys = e->h_counts[0], n_rows = e->h_counts[1], n_sdots = e->h_counts[2];
-  u32 bad = 0;
-  HIP_TRY(hipMemcpyAsync(&e->h_counts[11], err, sizeof(u32), hipMemcpyDeviceToHost, e->stream));
-  HIP_TRY(hipStreamSynchronize(e->stream));
-  memcpy(&bad, &e->h_counts[11], sizeof(u32));
-  if (bad & 1u) return fail(DG_E_ORDER, "dg_mutate_batch: ops are not sorted by key");
+  if (e->h_ticket[3] & 1u) return fail(DG_E_ORDER, "dg_mutate_batch: ops are not sorted by key");
   const u64 n_dots = n_sdots + n_adds;
   if (keys_cap < n_keys || delta->cap < n_rows || delta_dots->cap < n_dots)
     return fail(DG_E_CAPACITY,
@@ -1702,12 +1767,30 @@ int dg_mutate_batch(dg_engine* e, const dg_store* state, const dg_context* ctx, 
                               e->state, keys_out, rows_out_of(delta), dnode, dcnt, err, e->stream));
   HIP_TRY(launch_mutate_dots(ctx_of(ctx), node, n_adds, n_sdots, dnode, dcnt, tnode, tcnt, sort_tmp,
                              sort_b, delta_dots->node, delta_dots->cnt, e->stream));
-  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (sync) HIP_TRY(hipStreamSynchronize(e->stream));
   delta->n = n_rows;
   delta_dots->n = n_dots;
   delta_dots->kind = DG_CTX_DOTS;
   *n_keys_out = n_keys;
   return DG_OK;
+}
+
+int dg_mutate_batch(dg_engine* e, const dg_store* state, const dg_context* ctx, uint32_t node,
+                    uint64_t m, const uint8_t* kind, const uint64_t* key, const uint64_t* val,
+                    const int64_t* ts, const uint64_t* add_rank, uint64_t n_adds, dg_store* delta,
+                    dg_context* delta_dots, uint64_t* keys_out, uint64_t keys_cap,
+                    uint64_t* n_keys_out) {
+  return mutate_batch_impl(e, state, ctx, node, m, kind, key, val, ts, add_rank, n_adds, delta, delta_dots,
+                           keys_out, keys_cap, n_keys_out, true);
+}
+
+int dg_mutate_batch_async(dg_engine* e, const dg_store* state, const dg_context* ctx, uint32_t node,
+                          uint64_t m, const uint8_t* kind, const uint64_t* key, const uint64_t* val,
+                          const int64_t* ts, const uint64_t* add_rank, uint64_t n_adds, dg_store* delta,
+                          dg_context* delta_dots, uint64_t* keys_out, uint64_t keys_cap,
+                          uint64_t* n_keys_out) {
+  return mutate_batch_impl(e, state, ctx, node, m, kind, key, val, ts, add_rank, n_adds, delta, delta_dots,
+                           keys_out, keys_cap, n_keys_out, false);
 }
 
 int dg_context_union(dg_engine* e, const dg_context* a, const dg_context* b, dg_context* out) {

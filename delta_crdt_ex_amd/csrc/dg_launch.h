@@ -186,6 +186,11 @@ struct SpliceArgs {
   // (optional) the copy kernels run only when *kguard == 0 (dg_join_delta's one-wait path:
   // its guard word says the index was not written)
   const u64* kguard;
+  // (optional, launch_splice_move) the publish of the count block by the last workgroup
+  u64* h_pub;
+  const u64* pub_counts;
+  u64 seq;
+  u32* arrive_all;
 };
 // For every key of keys (ascending, n_keys): lo[u] = the first row of s whose key is >=
 // keys[u] and len[u] = its rows, found by streaming s's key column in tiles (each tile's
@@ -209,16 +214,19 @@ hipError_t launch_splice_finish(const u32* un, const u64* uc, u64 nc, u32* on, u
                                 const u32* guard = nullptr);
 u64 splice_tiles(u64 n);  // state tiles of the copy (tile_u0 holds one more entry)
 constexpr u64 SPLICE_TILE = 2048;  // state rows per copy tile (splice.hip ST)
-// the copy of the untouched rows alone (splice_kernel; E's rows placed by the caller)
+// the copy of the untouched rows alone (splice_kernel; E's rows placed by the caller); with
+// p.h_pub the last workgroup publishes the count block (dg_home.h) when every one is done
 hipError_t launch_splice_move(SpliceArgs p, hipStream_t st);
 
 // ---- mutate.hip (a batch of add/remove ops as one delta; see the file header)
-inline u64 mutate_tiles(u64 m) { return (m + 1023) / 1024; }
-// count + scan: d_counts[0..2] = touched keys, delta rows, state dots; scratch: 6 *
-// mutate_tiles(m) u64; err bit 0: ops not sorted by key.
+inline u64 mutate_tiles(u64 m) { return (m + 255) / 256; }  // (mutate.hip MT)
+// count + scan (its last tile): d_counts[0..2] = touched keys, delta rows, state dots;
+// scratch: 6 * mutate_tiles(m) u64; err bit 0: ops not sorted by key; arrive: a counter,
+// zero on entry and left zero.
 hipError_t launch_mutate_count(const Rows& s, const Ctx& c, u32 node, const uint8_t* kind,
                                const u64* key, const u64* val, const i64* ts, const u64* rank,
-                               u64 m, u64* scratch, u64* d_counts, u32* err, hipStream_t st);
+                               u64 m, u64* scratch, u64* d_counts, u32* err, u32* arrive,
+                               hipStream_t st);
 // keys_out, rows_out and the state dots into dnode/dcnt[0, n_state_dots)
 hipError_t launch_mutate_write(const Rows& s, const Ctx& c, u32 node, const uint8_t* kind,
                                const u64* key, const u64* val, const i64* ts, const u64* rank,
@@ -306,8 +314,12 @@ hipError_t launch_merkle_build(const Rows& s, const MerkleT& t, u64* d_keys, u32
 hipError_t launch_merkle_update(const MerkleT& t, const Rows& olds, const Rows& news, const u64* keys,
                                 u64 n_keys, u32* dirty, u64* d_keys, u32* arrive, u64* hand, i64* cdelta,
                                 u32* err, hipStream_t st);
-// the same from kdelta.hip's per-key figures (runs, dh; skipped when *guard != 0); sign -1
-// undoes sign +1 bit for bit
+// the same from kdelta.hip's per-key figures (runs, dh; skipped when guard && *guard);
+// sign -1 undoes what kdelta.hip's count kernel applied, bit for bit, then the dirty chunks
+// are re-reduced
+// the dirty chunks of a tree re-reduced (after put/delete into its bucket level)
+hipError_t launch_merkle_rehash(const MerkleT& t, const u32* dirty, u32* arrive, u64* hand, const i64* cdelta,
+                                u32* err, hipStream_t st);
 hipError_t launch_kd_tree(const MerkleT& t, const u64* keys, const u64* runs, const u64* dh, u64 nk,
                           const u64* guard, int sign, u32* dirty, u32* arrive, u64* hand, i64* cdelta,
                           u32* err, hipStream_t st);
@@ -327,8 +339,9 @@ struct KdArgs {
   u32* ca_node;        // ... written with the union (uc, d_counts[1] entries)
   u64* ca_cnt;
   u64 ca_cap;
-  const u32* uc_node;  // the union context (launch_ctx_union's output)
-  const u64* uc_cnt;
+  u32* uc_node;        // the union context (the count kernel's last workgroup computes it)
+  u64* uc_cnt;
+  void* cu_tmp;        // its scratch (ctx_union_tmp_bytes)
   Rows d;              // the delta, sorted
   Ctx cd;              // its context, sorted
   const u64* keys;     // the keyset, ascending unique
@@ -343,17 +356,24 @@ struct KdArgs {
   RowsOut rows;        // their rows (rows_cap), when has_rows
   u64 rows_cap;
   int has_rows;
+  u32* co_node;        // (optional) a copy of the joined context (co_cap entries)
+  u64* co_cnt;
+  u64 co_cap;
   RowsOut sp;          // the spare store: the output when rows move
   u64* end;            // the splice index (nk, nk + 1, a_tiles + 1)
   i64* shift;
   u64* tile_u0;
   u64 a_tiles;
-  MerkleT t;           // the tree (has_tree): its term hashes for the leaf changes
+  MerkleT t;           // the tree (has_tree): put/delete by the count kernel
   int has_tree;
-  u64* d_counts;       // the count block (kd_scan_kernel)
-  const u32* err;      // the tree update's input-error word (state writes skipped when set)
+  u32* dirty;          // the tree update's dirty chunk flags and chunk row-count changes: zero
+  i64* cdelta;         //   on entry, left zero (the re-reduction consumes them)
+  u64* d_counts;       // the count block (the count kernel's last workgroup)
+  u32* arrive;         // the count kernel's arrival counter (zero, left zero)
+  u32* err;            // the tree update's input-error word, zero on entry (state writes
+                       //   skipped when set; the host zeroes it after reporting)
 };
-// kd_count_kernel + kd_scan_kernel
+// kd_count_kernel (its last workgroup scans)
 hipError_t launch_kd_join(const KdArgs& p, hipStream_t st);
 // kd_write_kernel
 hipError_t launch_kd_write(const KdArgs& p, hipStream_t st);

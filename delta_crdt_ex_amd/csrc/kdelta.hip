@@ -13,8 +13,8 @@
 //                     (s2 \ c1) -- kept as two bit masks -- whether the key changed (diff/3,
 //                     causal_crdt.ex:344-352) and its Merkle leaf change (Σ row_hash new -
 //                     Σ row_hash old); per workgroup the sums of rows, kept rows, changed
-//                     keys and their rows, delta rows seen
-//   kd_scan_kernel    (one workgroup) the workgroups' exclusive offsets and the totals; the
+//                     keys and their rows, delta rows seen; the last workgroup to finish
+//                     scans the workgroups' figures into exclusive offsets and totals, and the
 //                     guard word: a delta row outside the keyset (the right-biased carry of
 //                     :185-188 applies: the caller runs the full join), a key run over
 //                     KD_RUN rows, more changed keys than the caller's capacity
@@ -33,6 +33,7 @@
 // Roofline: each key costs two searches (~6 dependent loads of the state, a few of the
 // delta) and reads its few rows twice (the second time from L2); a sync delta of 125k keys
 // into a 12.5M-row state reads ~10 MB.  Latency-bound by the search chains, not by bytes.
+#include "dg_ctxu.h"
 #include "dg_hash.h"
 #include "dg_launch.h"
 #include "dg_tree.h"
@@ -76,13 +77,96 @@ __device__ __forceinline__ void key_run(const u64* key, u64 n, u64 k, u64& lo, u
   run = (u32)(e - lo);
 }
 
-// ---------------------------------------------------------------- count
+// agent-scope stores and loads for the hand-off to the last workgroup (written through to
+// the point of coherence: the workgroups run on all eight XCDs)
+__device__ __forceinline__ void st_ag(u64* p, u64 v) {
+  __hip_atomic_store((__attribute__((address_space(1))) u64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ u64 ld_ag(const u64* p) {
+  return __hip_atomic_load((__attribute__((address_space(1))) u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// MerkleMap.put/delete of the changed keys (the caller zeroed dirty and cdelta): key u's
+// leaf change d and row-count change dr.  The keys are ascending, so a wave's keys of one
+// bucket (and of one chunk) are adjacent lanes: segmented sums over the lanes leave ONE
+// atomic per bucket and per chunk.  merkle.hip's kd_tree_kernel applies the same with the
+// opposite sign to undo it.
+template <class T>
+__device__ __forceinline__ T seg_sum(T v, u64 seg, int lane) {
+#pragma unroll
+  for (int d = 1; d < WAVE; d <<= 1) {
+    const T y = __shfl_up(v, d, WAVE);
+    const u64 sy = __shfl_up(seg, d, WAVE);
+    if (lane >= d && sy == seg) v += y;  // (segments are contiguous runs of lanes)
+  }
+  return v;
+}
+__device__ __forceinline__ void tree_put(const KdArgs& p, bool valid, u64 x, bool chg, u64 d, int dr) {
+  const MerkleT& t = p.t;
+  const int lane = threadIdx.x & (WAVE - 1);
+  const u32 L1 = t.depth < MERKLE_UPL ? t.depth : MERKLE_UPL;
+  bool bad = false, over = false;
+  int act = 0;
+  const u64 b = valid ? (x << t.sb) >> (64 - t.depth) : ~0ull;
+  if (valid && chg && (d != 0 || dr != 0)) {
+    if (t.sb && (x >> (64 - t.sb)) != t.shard)
+      bad = true;  // (skipped both ways)
+    else
+      act = 1;
+  }
+  if (!act) {
+    d = 0;
+    dr = 0;
+  }
+  const u64 c = b == ~0ull ? ~0ull : b >> L1;
+  const u64 sd = seg_sum<u64>(d, b, lane);
+  const int sr = seg_sum<int>(dr, b, lane), sa = seg_sum<int>(act, b, lane);
+  const int cr = seg_sum<int>(dr, c, lane), ca = seg_sum<int>(act, c, lane);
+  const u64 nb = __shfl_down(b, 1, WAVE), nc = __shfl_down(c, 1, WAVE);
+  const bool last = lane == WAVE - 1;
+  if (b != ~0ull && (last || nb != b) && sa) {  // the bucket's last lane: its node and row count
+    u64* lvl = t.nodes + ((1ull << t.depth) - 1);
+    atomicAdd((unsigned long long*)&lvl[b], (unsigned long long)sd);
+    if (sr) {  // (its aligned 32-bit word of two u16 counts, as merkle_update_kernel)
+      u32* wd = (u32*)t.counts + (b >> 1);
+      const u32 sh = 16u * (u32)(b & 1);
+      if (sr > 0) {
+        const u32 old = atomicAdd(wd, (u32)sr << sh);
+        over = ((old >> sh) & 0xFFFFu) + (u32)sr > 0xFFFFu;
+      } else {
+        atomicSub(wd, (u32)(-sr) << sh);
+      }
+    }
+  }
+  if (c != ~0ull && (last || nc != c) && ca) {  // the chunk's last lane: dirty, its row-count change
+    p.dirty[c] = 1u;
+    if (t.starts && cr) atomicAdd((unsigned long long*)&p.cdelta[c], (unsigned long long)(i64)cr);
+  }
+  if (__ballot(bad) && lane == 0) atomicOr(p.err, MERKLE_ERR_SHARD);
+  if (__ballot(over) && lane == 0) atomicOr(p.err, MERKLE_ERR_COUNT);
+}
+
+// ---------------------------------------------------------------- count (+ scan)
+// The workgroup's keys are ascending, so their delta rows are one contiguous range: two
+// searches find its ends and its keys are staged in LDS (every key's delta run is found
+// there, not by a search of the delta in memory).  (Narrowing the state searches to the
+// workgroup's range the same way, by 64-ary wave searches, measured slower: 52 against
+// 45 us at config 4 -- their 256 scattered lines per bound outweigh what each key saves.)
+constexpr u32 KDL = 2048;  // delta keys staged per workgroup (more: searched in memory)
 __global__ __launch_bounds__(KDB) void kd_count_kernel(KdArgs p) {
   __shared__ u64 tabS[KVT], tabD[KVT];
+  __shared__ u64 s_dk[KDL];
+  __shared__ u64 s_rng[2];
   __shared__ u64 red[KD_NV][KDB / WAVE];
+  __shared__ u32 s_last;
   const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
   const u64 u = (u64)blockIdx.x * KDB + tid;
+  const u64 u0 = (u64)blockIdx.x * KDB, u1 = min<u64>(u0 + KDB, p.nk);
   const bool dvv = p.cd.kind == 0;
+  if (tid < 2) {  // the workgroup's delta range [lo, hi): its keys' rows (two searches)
+    const u64 x = tid ? p.keys[u1 - 1] + 1 : p.keys[u0];  // (key + 1: past the last key's run)
+    s_rng[tid] = tid && x == 0 ? p.d.n : interp_lower_bound(p.d.key, 0, p.d.n, x);  // (2^64 - 1)
+  }
   for (u32 x = tid; x < KVT; x += KDB) {
     tabS[x] = 0;
     tabD[x] = 0;
@@ -93,18 +177,43 @@ __global__ __launch_bounds__(KDB) void kd_count_kernel(KdArgs p) {
   if (dvv)
     for (u64 i = tid; i < p.cd.n; i += KDB)
       if (p.cd.node[i] < KVT) tabD[p.cd.node[i]] = p.cd.cnt[i];
+  const u64 dlo = s_rng[0], dhi = s_rng[1];
+  const bool dl = dhi - dlo <= KDL;  // (uniform)
+  if (dl)
+    for (u64 i = tid; i < dhi - dlo; i += KDB) s_dk[i] = p.d.key[dlo + i];
   u64 v[KD_NV] = {0, 0, 0, 0, 0, 0, 0};
   u64 a_lo = 0, d_lo = 0, am = 0, dm = 0, dh = 0;
   u32 na = 0, nd = 0, ne = 0;
   bool chg = false, big = false;
+  u64 k = 0;
   if (u < p.nk) {
-    const u64 k = p.keys[u];
-    key_run(p.a.key, p.a.n, k, a_lo, na);
-    key_run(p.d.key, p.d.n, k, d_lo, nd);
+    k = p.keys[u];
+    key_run(p.a.key, p.a.n, k, a_lo, na);  // the state: an interpolation search
+  }
+  __syncthreads();  // (the tables, the staged delta keys)
+  if (u < p.nk) {
+    if (dl) {  // the delta run from LDS
+      u32 lo = 0, hi = (u32)(dhi - dlo);
+      while (lo < hi) {
+        const u32 m = (lo + hi) >> 1;
+        if (s_dk[m] < k)
+          lo = m + 1;
+        else
+          hi = m;
+      }
+      u32 e = lo;
+      while (e < (u32)(dhi - dlo) && s_dk[e] == k && e - lo <= KD_RUN) e++;
+      d_lo = dlo + lo;
+      nd = e - lo;
+    } else {
+      key_run(p.d.key, p.d.n, k, d_lo, nd);
+    }
     big = na > KD_RUN || nd > KD_RUN;
   }
-  __syncthreads();  // (the tables)
-  if (u < p.nk && !big) {
+#ifndef DG_KD_EXP
+#define DG_KD_EXP 0  // experiment builds only: 1 no row hashes, 2 no per-key join (wrong results)
+#endif
+  if (u < p.nk && !big && DG_KD_EXP < 2) {
     // join_dot_sets over the key's rows, both sides in tuple order
     u32 i = 0, j = 0;
     Row ra{}, rb{};
@@ -131,7 +240,7 @@ __global__ __launch_bounds__(KDB) void kd_count_kernel(KdArgs p) {
           ne++;
         } else {
           chg = true;
-          if (p.has_tree) dh -= rhash(p.t, ra);
+          if (p.has_tree && DG_KD_EXP == 0) dh -= rhash(p.t, ra);
         }
         if (c == 0 && ++j < nd) rb = load_row(p.d, d_lo + j);
         if (++i < na) ra = load_row(p.a, a_lo + i);
@@ -141,18 +250,23 @@ __global__ __launch_bounds__(KDB) void kd_count_kernel(KdArgs p) {
           dm |= 1ull << j;
           ne++;
           chg = true;
-          if (p.has_tree) dh += rhash(p.t, rb);
+          if (p.has_tree && DG_KD_EXP == 0) dh += rhash(p.t, rb);
         }
         if (++j < nd) rb = load_row(p.d, d_lo + j);
       }
     }
     p.a_lo[u] = a_lo;
     p.d_lo[u] = d_lo;
-    p.runs[u] = na | ((u64)nd << 16) | ((u64)ne << 32) | (chg ? 1ull << 48 : 0ull);
     p.amask[u] = am;
     p.dmask[u] = dm;
-    p.dh[u] = dh;
   }
+  if (u < p.nk) {  // (a key over KD_RUN: no change recorded, so the undo skips it too)
+    p.runs[u] = big ? 0ull : (na | ((u64)nd << 16) | ((u64)ne << 32) | (chg ? 1ull << 48 : 0ull));
+    p.dh[u] = big ? 0ull : dh;
+  }
+  // the tree's put/delete right away (all or nothing: a guard or an input error found
+  // later makes the host undo it, merkle.hip kd_tree_kernel with the opposite sign)
+  if (p.has_tree) tree_put(p, u < p.nk && !big, k, chg, dh, (int)ne - (int)na);
   v[0] = na;
   v[1] = ne;
   v[2] = chg ? 1 : 0;
@@ -173,55 +287,58 @@ __global__ __launch_bounds__(KDB) void kd_count_kernel(KdArgs p) {
     if (lane == 0) red[q][w] = x;
   }
   __syncthreads();
+  // the workgroup's figures handed to the last workgroup, which scans them all
   if (tid < KD_NV) {
     u64 s = 0;
 #pragma unroll
     for (int x = 0; x < KDB / WAVE; x++) s = tid < KD_NV - 1 ? s + red[tid][x] : (s | red[tid][x]);
-    p.part[blockIdx.x * KD_NV + tid] = s;
+    st_ag(p.part + blockIdx.x * KD_NV + tid, s);
   }
-}
-
-// ---------------------------------------------------------------- scan
-// the workgroups' exclusive offsets of the additive figures (toff), the totals and the guard
-// into the count block: [0] edit rows [2] changed keys [3] their rows [4] guard [5] moved
-// [6] state rows of the keyset [7] distinct-key change (d_counts[1]: the context union's)
-constexpr int KSB = 1024;
-__global__ __launch_bounds__(KSB) void kd_scan_kernel(KdArgs p) {
-  __shared__ u64 s_w[KSB / WAVE];
-  __shared__ u64 carry[KD_NV];
-  const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
-  if (tid < KD_NV) carry[tid] = 0;
   __syncthreads();
-  for (u64 t0 = 0; t0 < p.ntiles; t0 += KSB) {
+  if (tid == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s_last = __hip_atomic_fetch_add(p.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    if (s_last) __hip_atomic_store(p.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // ---- the last workgroup: exclusive offsets of the additive figures (toff), the totals
+  // and the guard into the count block: [0] edit rows [2] changed keys [3] their rows
+  // [4] guard [5] moved [6] state rows of the keyset [7] distinct-key change (d_counts[1]:
+  // the context union's)
+  __shared__ u64 carry[KD_NV];
+  __shared__ u64 s_w[KD_NV][KDB / WAVE];
+  if (tid < KD_NV) carry[tid] = 0;
+  for (u64 t0 = 0; t0 < p.ntiles; t0 += KDB) {
     const u64 t = t0 + tid;
-#pragma unroll 1
-    for (int q = 0; q < KD_NV; q++) {
-      const u64 x = t < p.ntiles ? p.part[t * KD_NV + q] : 0;
-      if (q == KD_NV - 1) {  // flags: OR
-        const u64 o = (__ballot(x & KD_BIG) ? KD_BIG : 0) | (__ballot(x & KD_MOVED) ? KD_MOVED : 0);
-        if (lane == 0) s_w[w] = o;
-        __syncthreads();
-        if (tid == 0)
-          for (int i = 0; i < KSB / WAVE; i++) carry[q] |= s_w[i];
-        __syncthreads();
-        continue;
-      }
-      u64 inc = x;  // inclusive wave scan (u64: totals may pass 2^32)
+    u64 x[KD_NV], inc[KD_NV];
 #pragma unroll
-      for (int d = 1; d < WAVE; d <<= 1) {
-        const u64 y = __shfl_up(inc, d, WAVE);
-        if (lane >= d) inc += y;
+    for (int q = 0; q < KD_NV; q++) x[q] = t < p.ntiles ? ld_ag(p.part + t * KD_NV + q) : 0;
+#pragma unroll
+    for (int q = 0; q < KD_NV; q++) {
+      inc[q] = x[q];
+      if (q < KD_NV - 1) {
+#pragma unroll
+        for (int d = 1; d < WAVE; d <<= 1) {
+          const u64 y = __shfl_up(inc[q], d, WAVE);
+          if (lane >= d) inc[q] += y;
+        }
+      } else {
+        inc[q] = (__ballot(x[q] & KD_BIG) ? KD_BIG : 0) | (__ballot(x[q] & KD_MOVED) ? KD_MOVED : 0);
       }
-      if (lane == WAVE - 1) s_w[w] = inc;
-      __syncthreads();
-      u64 below = carry[q];
-      for (int i = 0; i < w; i++) below += s_w[i];
-      if (t < p.ntiles) p.toff[t * KD_NV + q] = below + inc - x;
-      __syncthreads();
-      if (tid == 0)
-        for (int i = 0; i < KSB / WAVE; i++) carry[q] += s_w[i];
-      __syncthreads();
+      if (lane == WAVE - 1) s_w[q][w] = inc[q];
     }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < KD_NV - 1; q++) {
+      u64 below = carry[q];
+      for (int i = 0; i < w; i++) below += s_w[q][i];
+      if (t < p.ntiles) p.toff[t * KD_NV + q] = below + inc[q] - x[q];
+    }
+    __syncthreads();
+    if (tid < KD_NV)
+      for (int i = 0; i < KDB / WAVE; i++) carry[tid] = tid < KD_NV - 1 ? carry[tid] + s_w[tid][i] : (carry[tid] | s_w[tid][i]);
+    __syncthreads();
   }
   if (tid == 0) {
     const u64 n_ak = carry[0], n_e = carry[1], n_chg = carry[2], n_rows = carry[3], n_d = carry[4];
@@ -236,6 +353,10 @@ __global__ __launch_bounds__(KSB) void kd_scan_kernel(KdArgs p) {
     p.d_counts[6] = n_ak;
     p.d_counts[7] = carry[5];
   }
+  // Dots.union(state context, delta context) (:155) into the union scratch; d_counts[1]
+  __shared__ u32 s_cw[KDB / WAVE + 1];
+  __syncthreads();
+  ctx_union_block<KDB>(make_cu(p.ca, p.cd, p.uc_node, p.uc_cnt, p.d_counts + 1, p.cu_tmp), s_cw);
 }
 
 // ---------------------------------------------------------------- write
@@ -248,10 +369,17 @@ __global__ __launch_bounds__(KDB) void kd_write_kernel(KdArgs p) {
   if (guard) return;  // (uniform) nothing is written: the caller falls back or reports
   const bool moved = p.d_counts[5] != 0;
   if (blockIdx.x == 0 && !tree_bad) {  // the union context into the state's (Dots.union, :155)
-    const u64 nc = p.d_counts[1];
+    const u64 nc = p.d_counts[1];       // (and the caller's copy, when it fits)
+    const bool co = p.co_node && nc <= p.co_cap;
     for (u64 i = tid; i < nc && i < p.ca_cap; i += KDB) {
-      p.ca_node[i] = p.uc_node[i];
-      p.ca_cnt[i] = p.uc_cnt[i];
+      const u32 n = p.uc_node[i];
+      const u64 c = p.uc_cnt[i];
+      p.ca_node[i] = n;
+      p.ca_cnt[i] = c;
+      if (co) {
+        p.co_node[i] = n;
+        p.co_cnt[i] = c;
+      }
     }
   }
   u64 rn = 0;
@@ -355,7 +483,6 @@ hipError_t launch_kd_join(const KdArgs& p0, hipStream_t st) {
   p.ntiles = (p.nk + KDB - 1) / KDB;
   if (p.ntiles == 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(kd_count_kernel, dim3((unsigned)p.ntiles), dim3(KDB), 0, st, p);
-  hipLaunchKernelGGL(kd_scan_kernel, dim3(1), dim3(KSB), 0, st, p);
   return hipGetLastError();
 }
 

@@ -374,6 +374,7 @@ __device__ __forceinline__ void chunk_block(Rows rows, MT t, const u32* dirty, u
     else
       lds_upsweep(t.nodes, t.depth, g0, width, s);
     chunk_root = s[0];
+    if (tid == 0) ((u32*)dirty)[g] = 0;  // consumed: the flags are zero again for the next update
   } else if (tid == 0) {  // unchanged: its root as the previous kernels left it
     chunk_root = t.nodes[((1ull << (t.depth - L1)) - 1) + g];
   }
@@ -425,6 +426,9 @@ __device__ __forceinline__ void chunk_block(Rows rows, MT t, const u32* dirty, u
         v[q] = x < G ? cdelta[x] : 0;
         st0[q] = x <= G ? (i64)t.starts[x] : 0;
       }
+#pragma unroll
+      for (int q = 0; q < CP; q++)  // consumed: zero again for the next update
+        if (x0 + q < G && v[q]) ((i64*)cdelta)[x0 + q] = 0;
       i64 own = 0;
 #pragma unroll
       for (int q = 0; q < CP; q++) own += v[q];
@@ -475,6 +479,7 @@ __global__ __launch_bounds__(UPB, 4) void merkle_chunk_kernel(Rows rows, MT t, c
                                                            u32* err, const i64* cdelta) {
   chunk_block<BUILD, VEC>(rows, t, dirty, ctr, hand, d_keys, err, cdelta, blockIdx.x, gridDim.x);
 }
+
 
 // ---------------------------------------------------------------- update
 constexpr int UB = 256;
@@ -539,44 +544,75 @@ __global__ __launch_bounds__(UB) void merkle_update_kernel(MT t, Rows olds, Rows
 
 // The same put/delete from kdelta.hip's per-key figures: key u changed (runs bit 48) with
 // leaf change dh[u] and row-count change ne - na; sign -1 undoes sign +1.  The distinct-key
-// change is kd_scan_kernel's (d_counts[7]).
+// change is the count kernel's (d_counts[7]).  The keys are ascending, so a wave's keys of
+// one bucket (and of one chunk) are adjacent lanes: segmented sums over the lanes leave ONE
+// atomic per bucket and per chunk (a small tree's few buckets took a thousand same-address
+// atomics per word from a batch of mutations: 16 us for 1000 keys).
+template <class T>
+__device__ __forceinline__ T seg_incl(T v, u64 seg, int lane) {
+#pragma unroll
+  for (int d = 1; d < WAVE; d <<= 1) {
+    const T y = __shfl_up(v, d, WAVE);
+    const u64 sy = __shfl_up(seg, d, WAVE);
+    if (lane >= d && sy == seg) v += y;  // (segments are contiguous runs of lanes)
+  }
+  return v;
+}
 __global__ __launch_bounds__(UB) void kd_tree_kernel(MT t, const u64* keys, const u64* runs, const u64* dh,
                                                      u64 nk, const u64* guard, int sign, u32* dirty,
                                                      u32* err, i64* cdelta) {
-  if (*guard) return;  // (uniform) the per-key figures are incomplete: nothing to apply
+  if (guard && *guard) return;  // (uniform) the per-key figures are incomplete: nothing to apply
   const u64 i = (u64)blockIdx.x * UB + threadIdx.x;
+  const int lane = threadIdx.x & (WAVE - 1);
+  const u32 L1 = t.depth < (u32)UPL ? t.depth : (u32)UPL;
   bool bad = false, over = false;
+  u64 b = ~0ull, d = 0;
+  int dr = 0, act = 0;
   if (i < nk) {
     const u64 rn = runs[i];
     const int na = (int)(rn & 0xFFFF), ne = (int)((rn >> 32) & 0xFFFF);
-    const u64 d = sign > 0 ? dh[i] : (u64)0 - dh[i];
-    const int dr = sign > 0 ? ne - na : na - ne;
-    if (((rn >> 48) & 1) && (d != 0 || dr != 0)) {
-      const u64 x = keys[i];
-      if (t.sb && (x >> (64 - t.sb)) != t.shard) {
-        bad = true;
-      } else {
-        const u64 b = bucket_of(t, x);
-        u64* lvl = t.nodes + ((1ull << t.depth) - 1);
-        atomicAdd((unsigned long long*)&lvl[b], (unsigned long long)d);
-        if (dr) {  // the bucket's row count in its aligned 32-bit word (as merkle_update_kernel)
-          u32* wd = (u32*)t.counts + (b >> 1);
-          const u32 sh = 16u * (u32)(b & 1);
-          if (dr > 0) {
-            const u32 old = atomicAdd(wd, (u32)dr << sh);
-            over = ((old >> sh) & 0xFFFFu) + (u32)dr > 0xFFFFu;
-          } else {
-            atomicSub(wd, (u32)(-dr) << sh);
-          }
+    const u64 x = keys[i];
+    b = bucket_of(t, x);
+    if (((rn >> 48) & 1)) {
+      const u64 dd = sign > 0 ? dh[i] : (u64)0 - dh[i];
+      const int r = sign > 0 ? ne - na : na - ne;
+      if (dd != 0 || r != 0) {
+        if (t.sb && (x >> (64 - t.sb)) != t.shard) {
+          bad = true;  // (skipped both ways)
+        } else {
+          d = dd;
+          dr = r;
+          act = 1;
         }
-        const u32 L1 = t.depth < (u32)UPL ? t.depth : (u32)UPL;
-        dirty[b >> L1] = 1u;
-        if (cdelta && dr) atomicAdd((unsigned long long*)&cdelta[b >> L1], (unsigned long long)(i64)dr);
       }
     }
   }
-  if (__ballot(bad) && (threadIdx.x & (WAVE - 1)) == 0) atomicOr(err, ERR_SHARD);
-  if (__ballot(over) && (threadIdx.x & (WAVE - 1)) == 0) atomicOr(err, ERR_COUNT);
+  const u64 c = b == ~0ull ? ~0ull : b >> L1;
+  const u64 sd = seg_incl<u64>(d, b, lane);
+  const int sr = seg_incl<int>(dr, b, lane), sa = seg_incl<int>(act, b, lane);
+  const int cr = seg_incl<int>(dr, c, lane), ca = seg_incl<int>(act, c, lane);
+  const u64 nb = __shfl_down(b, 1, WAVE), nc = __shfl_down(c, 1, WAVE);
+  const bool last = lane == WAVE - 1;
+  if (b != ~0ull && (last || nb != b) && sa) {  // the bucket's last lane: its node and row count
+    u64* lvl = t.nodes + ((1ull << t.depth) - 1);
+    atomicAdd((unsigned long long*)&lvl[b], (unsigned long long)sd);
+    if (sr) {  // the bucket's row count in its aligned 32-bit word (as merkle_update_kernel)
+      u32* wd = (u32*)t.counts + (b >> 1);
+      const u32 sh = 16u * (u32)(b & 1);
+      if (sr > 0) {
+        const u32 old = atomicAdd(wd, (u32)sr << sh);
+        over = ((old >> sh) & 0xFFFFu) + (u32)sr > 0xFFFFu;
+      } else {
+        atomicSub(wd, (u32)(-sr) << sh);
+      }
+    }
+  }
+  if (c != ~0ull && (last || nc != c) && ca) {  // the chunk's last lane: dirty, its row-count change
+    dirty[c] = 1u;
+    if (cdelta && cr) atomicAdd((unsigned long long*)&cdelta[c], (unsigned long long)(i64)cr);
+  }
+  if (__ballot(bad) && lane == 0) atomicOr(err, ERR_SHARD);
+  if (__ballot(over) && lane == 0) atomicOr(err, ERR_COUNT);
 }
 
 // ---------------------------------------------------------------- key-level merge
@@ -1634,6 +1670,16 @@ hipError_t launch_kd_tree(const MerkleT& m, const u64* keys, const u64* runs, co
   Rows none{};
   hipLaunchKernelGGL(merkle_chunk_kernel<false>, dim3((unsigned)G), dim3(UPB), 0, st, none, t, dirty, arrive,
                      hand, (u64*)nullptr, err, (const i64*)cd);
+  return hipGetLastError();
+}
+
+hipError_t launch_merkle_rehash(const MerkleT& m, const u32* dirty, u32* arrive, u64* hand, const i64* cdelta,
+                                u32* err, hipStream_t st) {
+  const MT t = mt_of(m);
+  const u64 G = merkle_chunks(t.depth);
+  Rows none{};
+  hipLaunchKernelGGL(merkle_chunk_kernel<false>, dim3((unsigned)G), dim3(UPB), 0, st, none, t, dirty, arrive,
+                     hand, (u64*)nullptr, err, t.starts ? cdelta : (const i64*)nullptr);
   return hipGetLastError();
 }
 

@@ -30,7 +30,7 @@ typedef uint8_t u8;
 
 namespace {
 
-constexpr int MB = 256, MI = 4, MT = MB * MI;
+constexpr int MB = 256, MI = 1, MT = MB * MI;  // (one op per thread: its state search is a chain)
 
 struct MutArgs {
   Rows s;
@@ -51,6 +51,7 @@ struct MutArgs {
   u64* dcnt;
   u64* d_counts;    // [0] keys, [1] rows, [2] state dots
   u32* err;         // bit 0: ops not sorted by key
+  u32* arrive;      // the count kernel's arrival counter (zero, left zero)
 };
 
 __device__ __forceinline__ u64 vv_of(const Ctx& c, u32 node) {
@@ -89,14 +90,7 @@ __device__ __forceinline__ Group group_at(const MutArgs& p, u64 i) {
   while (e < p.m && p.key[e] == key) e++;
   g.last = e - 1;
   g.add = p.kind[g.last] != 0;
-  u64 lo = 0, hi = p.s.n;  // the key's rows in the state
-  while (lo < hi) {
-    const u64 mid = (lo + hi) >> 1;
-    if (p.s.key[mid] < key)
-      lo = mid + 1;
-    else
-      hi = mid;
-  }
+  const u64 lo = interp_lower_bound(p.s.key, 0, p.s.n, key);  // the key's rows in the state
   u64 h = lo;
   while (h < p.s.n && p.s.key[h] == key) h++;
   g.lo = lo;
@@ -119,20 +113,40 @@ __global__ __launch_bounds__(MB) void mutate_count_kernel(MutArgs p) {
   block_excl_scan<MB>(nk, s_wave, &tk);
   block_excl_scan<MB>(nr, s_wave, &tr);
   block_excl_scan<MB>(nd, s_wave, &td);
+  // the tile's counts handed to the last tile, which scans them all (no scan launch): stored
+  // write-through (agent scope: the tiles run on every XCD), then one arrival
+  __shared__ u32 s_last;
   if (threadIdx.x == 0) {
-    p.cnt[t] = tk;
-    p.cnt[p.ntiles + t] = tr;
-    p.cnt[2 * p.ntiles + t] = td;
+    const u64 v[3] = {tk, tr, td};
+    for (int j = 0; j < 3; j++)
+      __hip_atomic_store((__attribute__((address_space(1))) u64*)(p.cnt + j * p.ntiles + t), v[j],
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s_last = __hip_atomic_fetch_add(p.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    if (s_last) __hip_atomic_store(p.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-}
-
-constexpr int MSB = 1024;
-__global__ __launch_bounds__(MSB) void mutate_scan_kernel(MutArgs p) {
-  __shared__ u32 s_wave[MSB / WAVE + 1];
+  __syncthreads();
+  if (!s_last) return;
   __shared__ u64 s_carry;
-  for (int j = 0; j < 3; j++)
-    scan_tile_counts<MSB>(p.cnt + j * p.ntiles, p.off + j * p.ntiles, p.ntiles, p.d_counts + j,
-                          s_wave, &s_carry);
+  for (int j = 0; j < 3; j++) {  // (the counts read agent-scope: other XCDs wrote them)
+    const u64* c = p.cnt + j * p.ntiles;
+    if (threadIdx.x == 0) s_carry = 0;
+    __syncthreads();
+    for (u64 c0 = 0; c0 < p.ntiles; c0 += MB) {
+      const u64 x = c0 + threadIdx.x;
+      const u32 v = x < p.ntiles ? (u32)__hip_atomic_load((__attribute__((address_space(1))) const u64*)(c + x),
+                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                 : 0u;
+      u32 tot;
+      const u32 o = block_excl_scan<MB>(v, s_wave, &tot);
+      if (x < p.ntiles) p.off[j * p.ntiles + x] = s_carry + o;
+      __syncthreads();
+      if (threadIdx.x == 0) s_carry += tot;
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) p.d_counts[j] = s_carry;
+    __syncthreads();
+  }
 }
 
 __global__ __launch_bounds__(MB) void mutate_write_kernel(MutArgs p) {
@@ -189,7 +203,7 @@ __global__ __launch_bounds__(256) void mutate_gen_kernel(MutArgs p, u64 n_adds, 
 
 static MutArgs make_mut(const Rows& s, const Ctx& c, u32 node, const u8* kind, const u64* key,
                         const u64* val, const i64* ts, const u64* rank, u64 m, u64* scratch,
-                        u64* d_counts, u32* err) {
+                        u64* d_counts, u32* err, u32* arrive = nullptr) {
   MutArgs p{};
   p.s = s;
   p.c = c;
@@ -205,16 +219,17 @@ static MutArgs make_mut(const Rows& s, const Ctx& c, u32 node, const u8* kind, c
   p.off = scratch + 3 * p.ntiles;
   p.d_counts = d_counts;
   p.err = err;
+  p.arrive = arrive;
   return p;
 }
 
 hipError_t launch_mutate_count(const Rows& s, const Ctx& c, u32 node, const u8* kind,
                                const u64* key, const u64* val, const i64* ts, const u64* rank,
-                               u64 m, u64* scratch, u64* d_counts, u32* err, hipStream_t st) {
-  MutArgs p = make_mut(s, c, node, kind, key, val, ts, rank, m, scratch, d_counts, err);
+                               u64 m, u64* scratch, u64* d_counts, u32* err, u32* arrive,
+                               hipStream_t st) {
+  MutArgs p = make_mut(s, c, node, kind, key, val, ts, rank, m, scratch, d_counts, err, arrive);
   if (m == 0) return hipMemsetAsync(d_counts, 0, 3 * sizeof(u64), st);
   hipLaunchKernelGGL(mutate_count_kernel, dim3((unsigned)p.ntiles), dim3(MB), 0, st, p);
-  hipLaunchKernelGGL(mutate_scan_kernel, dim3(1), dim3(MSB), 0, st, p);
   return hipGetLastError();
 }
 
@@ -251,6 +266,15 @@ hipError_t launch_mutate_dots(const Ctx& c, u32 node, u64 n_adds, u64 n_state_do
   p.dnode = dnode;
   p.dcnt = dcnt;
   const u64 n = n_state_dots + n_adds;
+  if (n_state_dots == 0) {  // the adds' dots alone are (node, C + 1 + r) ascending: no sort
+    if (n_adds) {
+      p.dnode = out_node;
+      p.dcnt = out_cnt;
+      const u64 g = std::min<u64>((n_adds + 255) / 256, 1024);
+      hipLaunchKernelGGL(mutate_gen_kernel, dim3((unsigned)g), dim3(256), 0, st, p, n_adds, (u64)0);
+    }
+    return hipGetLastError();
+  }
   if (n_adds) {
     const u64 g = std::min<u64>((n_adds + 255) / 256, 1024);
     hipLaunchKernelGGL(mutate_gen_kernel, dim3((unsigned)g), dim3(256), 0, st, p, n_adds,

@@ -26,6 +26,7 @@
 //
 // Roofline: the copy is 36 B read + 36 B written per untouched row, plus E's rows; the
 // index is O(|K| log |E|).  Nothing else touches the state.
+#include "dg_home.h"
 #include "dg_launch.h"
 
 namespace dg {
@@ -245,13 +246,16 @@ __global__ __launch_bounds__(SB) void splice_erows_kernel(SpliceArgs p) {
 // while the loads are in flight.
 static_assert(ST == SPLICE_TILE, "dg_launch.h's copy tile");
 __global__ __launch_bounds__(SB) void splice_kernel(SpliceArgs p) {
-  if (p.run_if && *p.run_if == 0) return;  // (uniform) nothing moved: not needed
-  if (p.kguard && *p.kguard) return;       // (uniform) the index was not written
   __shared__ u64 s_end[SLC], s_lo[SLC];
   __shared__ i64 s_shift[SLC];
+  __shared__ u32 s_all;
+  // (uniform) nothing moved, or the index was not written: no copy
+  const bool run = !(p.run_if && *p.run_if == 0) && !(p.kguard && *p.kguard);
+  // (a grid-stride loop over the tiles: launch_splice_move's grid is capped, so a launch
+  // whose rows did not move exits in a few us whatever the state's size)
+  for (u64 t = blockIdx.x; run && t < p.a_tiles; t += gridDim.x) {
   TileRows x;
   i64 to[SR];
-  const u64 t = blockIdx.x;
   const u64 i0 = t * ST;
   const u64 i1 = min<u64>(i0 + ST, p.a.n);
   // row i's first keyset entry whose state rows end after it: u*(i) = first u with
@@ -298,6 +302,26 @@ __global__ __launch_bounds__(SB) void splice_kernel(SpliceArgs p) {
     }
   }
   store_tile(p.out, x, to);
+  __syncthreads();  // (the next tile restages the index)
+  }
+  if (!p.h_pub) return;
+  if (!run) {  // (uniform) no workgroup copies: the first publishes right away
+    if (blockIdx.x == 0) publish_counts(p.pub_counts, p.h_pub, p.seq);
+    return;
+  }
+  // every workgroup arrives once its part is done; the last one publishes (dg_home.h)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const u32 n = __hip_atomic_fetch_add(p.arrive_all, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_all = n == gridDim.x - 1;
+    if (s_all) __hip_atomic_store(p.arrive_all, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (s_all) {
+    __threadfence();
+    publish_counts(p.pub_counts, p.h_pub, p.seq);
+  }
 }
 
 }  // namespace
@@ -330,7 +354,9 @@ hipError_t launch_splice_index(SpliceArgs p, hipStream_t st) {
 
 hipError_t launch_splice_move(SpliceArgs p, hipStream_t st) {
   p.a_tiles = (p.a.n + ST - 1) / ST;
-  if (p.a_tiles) hipLaunchKernelGGL(splice_kernel, dim3((unsigned)p.a_tiles), dim3(SB), 0, st, p);
+  u64 g = p.a_tiles < 512 ? p.a_tiles : 512;  // (a launch whose rows did not move: ~2 us)
+  if (p.h_pub && g == 0) g = 1;                // (the publish)
+  if (g) hipLaunchKernelGGL(splice_kernel, dim3((unsigned)g), dim3(SB), 0, st, p);
   return hipGetLastError();
 }
 

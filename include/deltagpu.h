@@ -273,6 +273,16 @@ int dg_join_delta_rows(dg_engine* e, dg_store* state, dg_context* state_ctx, con
                        dg_store* spare, dg_merkle* tree, uint64_t* changed, uint64_t cap,
                        uint64_t* n_changed, int* swapped, dg_store* rows);
 
+/* dg_join_delta_rows plus a copy of the joined context into ctx_out (ctx_out->n set; more
+ * than ctx_out->cap entries: not written).  `changed`, `rows` and ctx_out may be host memory
+ * from dg_host_alloc: a delta whose keys all lie in the keyset (a sync delta, a batch of
+ * mutations) is then joined, its tree updated and its results written there by the kernels,
+ * with ONE host wait (the NIF's join_delta and mutate_batch). */
+int dg_join_delta_out(dg_engine* e, dg_store* state, dg_context* state_ctx, const dg_store* delta,
+                      const dg_context* delta_ctx, const uint64_t* keys, uint64_t n_keys,
+                      dg_store* spare, dg_merkle* tree, uint64_t* changed, uint64_t cap,
+                      uint64_t* n_changed, int* swapped, dg_store* rows, dg_context* ctx_out);
+
 /* dg_join_delta_rows for a SMALL delta in ONE launch chain with ONE host wait (the general
  * path waits after each of its four steps): the keyed join, the changed keys, the MerkleMap
  * put/delete + update_hashes, and the results written straight into `home`, host memory
@@ -358,6 +368,16 @@ int dg_mutate_batch(dg_engine* e, const dg_store* state, const dg_context* ctx, 
                     const int64_t* ts, const uint64_t* add_rank, uint64_t n_adds, dg_store* delta,
                     dg_context* delta_dots, uint64_t* keys_out, uint64_t keys_cap,
                     uint64_t* n_keys_out);
+
+/* The same, asynchronous: the host values (delta->n, delta_dots->n, *n_keys_out) are set on
+ * return (one wait, for the counts), the outputs' device writes are enqueued on the engine
+ * stream -- later calls of this engine (dg_join_delta_rows with the delta) read them in
+ * order; any other reader calls dg_engine_sync first.  What the NIF's mutate_batch uses. */
+int dg_mutate_batch_async(dg_engine* e, const dg_store* state, const dg_context* ctx, uint32_t node,
+                          uint64_t m, const uint8_t* kind, const uint64_t* key, const uint64_t* val,
+                          const int64_t* ts, const uint64_t* add_rank, uint64_t n_adds, dg_store* delta,
+                          dg_context* delta_dots, uint64_t* keys_out, uint64_t keys_cap,
+                          uint64_t* n_keys_out);
 
 /* ---- causal-context algebra ----------------------------------------------- */
 /* Dots.union/2 (aw_lww_map.ex:39-52): VV ⊔ VV = per-node max; VV ⊔ DOTS folds the
