@@ -607,3 +607,87 @@ def test_counter_zero_dots(engine, home):
          "ctx": (R.VV, np.array([7], np.uint32), np.array([1], np.uint64))}
     st, sc, _, wr = apply(engine, a, d, dk, depth=8, home=home)
     assert not (wr[3] == 3).any() and not ((wr[3] == 7) & (wr[4] == 0)).any() and ((wr[3] == 7) & (wr[4] == 1)).any()
+
+
+# ---------------------------------------------------------------- the one-wait path (kdelta.hip)
+# dg_join_delta's per-key path for deltas of any size: its fallbacks leave nothing written,
+# and it equals the splice path (DG_KD=0) bit for bit.
+
+def _kd_engine(monkeypatch, on):
+    from delta_crdt_ex_amd.store import Engine
+    monkeypatch.setenv("DG_KD", "1" if on else "0")
+    return Engine(0)
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_kd_equals_the_splice_path(monkeypatch, seed):
+    """Sync deltas with moves and with dot-set contexts, through both paths on fresh
+    engines: the same state, context, changed keys, rows and tree."""
+    rng = np.random.default_rng(seed)
+    a, b = W.random_pair(rng, 30_000, n_nodes=6, ts_range=1 << 10, dense_ctx=bool(seed % 2))
+    kb = np.unique(np.concatenate([a["rows"][0], b["rows"][0]]))
+    keys = np.sort(rng.choice(kb, 4_000, replace=False))
+    d = W.sync_delta(b, keys)
+    out = []
+    for on in (True, False):
+        eng = _kd_engine(monkeypatch, on)
+        st, sc = state_of(a, extra_ctx=len(d["ctx"][1]))
+        sd, cd = up(d)
+        spare = Store.empty(st.n + sd.n, DEV)
+        rows = Store.empty(st.n + sd.n, DEV)
+        tree = eng.merkle_build(st, 12)
+        changed, swapped = eng.join_delta(st, sc, sd, cd, kdev(keys), spare, tree, rows=rows)
+        out.append(([c.copy() for c in st.to_numpy()], [c.copy() for c in sc.to_numpy()], u64(changed).copy(),
+                    [c.copy() for c in rows.to_numpy()], tree.nodes.cpu().numpy().copy(),
+                    tree.starts.cpu().numpy().copy(), tree.n_keys, swapped))
+        eng.close()
+    x, y = out
+    for p, q in zip(x[:2], y[:2]):
+        for c1, c2 in zip(p, q):
+            assert np.array_equal(c1, c2)
+    assert np.array_equal(x[2], y[2])
+    for c1, c2 in zip(x[3], y[3]):
+        assert np.array_equal(c1, c2)
+    assert np.array_equal(x[4], y[4]) and np.array_equal(x[5], y[5]) and x[6] == y[6] and x[7] == y[7]
+    wr, _ = R.join2(a["rows"], a["ctx"], d["rows"], d["ctx"], keys=keys)
+    assert all(np.array_equal(c1, c2) for c1, c2 in zip(x[0], wr))
+
+
+def test_kd_long_key_runs_fall_back(engine):
+    """A key with more rows than the per-key path takes (KD_RUN = 64): the call still
+    applies (the splice path), equal to the oracle, and the tree equals a fresh build."""
+    rng = np.random.default_rng(12)
+    n = 5000
+    keys = np.unique(rng.integers(0, 1 << 63, n + 10, dtype=np.uint64))[:n]
+    big = keys[100]
+    rk = np.concatenate([keys, np.full(79, big, np.uint64)])
+    node = np.zeros(len(rk), np.uint32)
+    cnt = np.arange(1, len(rk) + 1, dtype=np.uint64)
+    val = np.arange(len(rk), dtype=np.uint64)
+    order = np.lexsort((cnt, node, np.zeros(len(rk)), val, rk))
+    rows = (rk[order], val[order], np.full(len(rk), 3, np.int64), node[order], cnt[order])
+    a = {"rows": rows, "ctx": (R.VV, np.array([0], np.uint32), np.array([len(rk)], np.uint64))}
+    dk = np.sort(np.array([big, keys[7]], np.uint64))
+    d = {"rows": (dk, np.array([1, 2], np.uint64), np.full(2, 9, np.int64), np.full(2, 1, np.uint32),
+                  np.array([1, 2], np.uint64)),
+         "ctx": (R.VV, np.array([0, 1], np.uint32), np.array([len(rk), 2], np.uint64))}
+    apply(engine, a, d, dk, depth=9)
+
+
+def test_kd_changed_keys_past_their_capacity(engine):
+    """More changed keys than the caller's buffer: DG_E_CAPACITY, and the state, context and
+    tree are exactly what they were (the count kernel's tree update undone)."""
+    from delta_crdt_ex_amd._abi import CapacityError
+    a, b = W.config4_shard(2, 8, keys_per_rank=60_000, diff_frac=0.02)
+    want = R.store_diff(a["rows"], b["rows"])
+    d = W.sync_delta(b, want)
+    st, sc = state_of(a, extra_ctx=8)
+    sd, cd = up(d)
+    spare = Store.empty(st.n + sd.n, DEV)
+    tree = engine.merkle_build(st, 12)
+    snap = _snapshot(st, sc, tree)
+    small = torch.empty(5, dtype=torch.int64, device=DEV)
+    with pytest.raises(CapacityError):
+        engine.join_delta(st, sc, sd, cd, kdev(want), spare, tree, changed=small)
+    _assert_unchanged(st, sc, tree, snap)
+    apply(engine, a, d, want, depth=12)  # and the engine goes on
