@@ -126,6 +126,20 @@ def _diff_accounting(ta, tb):
             "bytes_no_keys": 16 * visited + 4 * dirty * (1 << sub) + 36 * rows}
 
 
+def _join_delta_roofline(last, t_dev):
+    """dg_join_delta's algorithmic bytes (§8(d)'s join bytes over the rows it touches: the
+    keyset's state rows read, the delta's rows read, the joined rows written, the keyset
+    read, and per changed key its bucket's leaf and row count read and written) over the
+    call's device time.  Latency-bound: a few searches and hashes per key, one wait."""
+    alg = 36 * (last["n_ak"] + last["rows"] + last["n_e"]) + 8 * last["keys"] + 20 * last["changed"]
+    return {"bound": "hbm (latency: per-key search chains)", "alg_bytes": alg,
+            "device_us": t_dev * 1e6, "achieved": alg / t_dev / 1e9, "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": alg / t_dev / 1e9 / HBM_PEAK_GBS,
+            "rows": {"state_rows_of_keyset": last["n_ak"], "delta_rows": last["rows"],
+                     "joined_rows_of_keyset": last["n_e"], "keys": last["keys"],
+                     "changed": last["changed"]}}
+
+
 def config4_round(eng, torch, dev, rank=0, world=1, keys_per_rank=12_500_000, steps=10,
                   max_sync_size=None, cdev=None):
     """BASELINE config 4 on this rank's key-hash shard (12.5M keys per GPU: 100M over 8):
@@ -227,6 +241,9 @@ def config4_round(eng, torch, dev, rank=0, world=1, keys_per_rank=12_500_000, st
                  rows=delta.n, changed=int(changed.numel()), in_place=not swapped)
         t["ok"] = tt.root() == eng.merkle_build(st, depth, None, sbits, rank if sbits else 0,
                                                 terms=terms).root()
+        # (outside the clock) the keyset's rows before and after: the join's row bytes
+        t["n_ak"] = int(torch.isin(sa.key[: sa.n], keys).sum())
+        t["n_e"] = int(torch.isin(st.key[: st.n], keys).sum())
         return t
 
     one_round()
@@ -269,6 +286,7 @@ def config4_round(eng, torch, dev, rank=0, world=1, keys_per_rank=12_500_000, st
                                            "rounds"},
         "round_us": {k: v * 1e6 for k, v in med.items() if k not in ("diff_ev", "join_delta_ev")},
         "join_delta_device_us": med["join_delta_ev"] * 1e6,
+        "join_delta_roofline": _join_delta_roofline(last, med["join_delta_ev"]),
         "join_delta_note": "round_us.join_delta: wall time of the Python call (ctypes, its one "
                            "host wait, a torch synchronize); join_delta_device_us: HIP events on "
                            "the engine stream around the same call (first kernel to last)",
@@ -584,7 +602,7 @@ def e2e_rate(eng, torch, pr, reps=20):
                     "median of reps"}
 
 
-def config5_rate(eng, torch, dev, rank=0, world=1, n_keys=12_500_000, reps=5, steps=20):
+def config5_rate(eng, torch, dev, rank=0, world=1, n_keys=12_500_000, reps=5, steps=20, settle_ms=0.0):
     """Config 5 at one GPU's share of 100M keys over 8 GPUs: full-state join of two
     remove-heavy replicas (50 % removes, 64 nodes, ts in [0,16): LWW ties everywhere),
     then read/1 of the result.  At N ranks each rank joins its key-hash shard of
@@ -605,6 +623,11 @@ def config5_rate(eng, torch, dev, rank=0, world=1, n_keys=12_500_000, reps=5, st
         launch()
         eng.sync()
 
+    t_settle = time.perf_counter()  # (optional) untimed joins first: the clocks up
+    while (time.perf_counter() - t_settle) * 1e3 < settle_ms:
+        for _ in range(8):
+            launch()
+        eng.sync()
     tj = _timed(torch, join, reps)
     # the kernels alone: `steps` launches back to back, HIP events on the engine stream
     launch()

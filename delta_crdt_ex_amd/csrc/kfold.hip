@@ -488,7 +488,7 @@ __global__ __launch_bounds__(KB) __attribute__((amdgpu_waves_per_eu(2 * KB / 256
   const int tid = threadIdx.x;
   const int k = p.k, nr = 2 * k;
   const u64 T = p.T;
-  if (tid == 0) {
+  if (tid == 0) {  // (the ticket: buckets in workgroup order measured the same, 692-697 us)
     const u32 t = atomicAdd(p.scan.ticket, 1u);
     if ((u64)t == T - 1) atomicExch(p.scan.ticket, 0u);
     s.bcast[0] = t;

@@ -13,6 +13,7 @@ import bench  # noqa: E402
 from delta_crdt_ex_amd.store import Engine  # noqa: E402
 
 eng = Engine(0)
-r, _ = bench.config5_rate(eng, torch, torch.device("cuda", 0))
+r, _ = bench.config5_rate(eng, torch, torch.device("cuda", 0),
+                          settle_ms=float(os.environ.get("C5_SETTLE_MS", "0")))
 print(json.dumps(r), flush=True)
 eng.close()
