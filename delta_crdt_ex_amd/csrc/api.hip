@@ -1042,13 +1042,11 @@ static int kd_join_delta(dg_engine* e, dg_store* state, dg_context* state_ctx, c
   p.dirty = dirty;
   p.cdelta = cdelta;
   p.cu_tmp = cu_tmp;
-  // four launches, one wait: the count (the per-key joins, the tree's put/delete, the scan
-  // and the context union by its last workgroup), the tree's re-reduction, the write, the
-  // moved rows' copy (its last workgroup publishes the count block)
+  // three launches, one wait: the count (the per-key joins, the tree's put/delete, the scan
+  // and the context union by its last workgroup), the write beside the tree's re-reduction,
+  // the moved rows' copy (its last workgroup publishes the count block)
   HIP_TRY(launch_kd_join(p, e->stream));
-  if (tree)
-    HIP_TRY(launch_merkle_rehash(merkle_of(tree), dirty, e->ticket + MERKLE_ARRIVE, hand, cdelta, err, e->stream));
-  HIP_TRY(launch_kd_write(p, e->stream));
+  HIP_TRY(launch_kd_finish(p, dirty, e->ticket + MERKLE_ARRIVE, hand, cdelta, e->stream));
   SpliceArgs sp{};
   sp.a = rows_of(state);
   sp.keys = keys;

@@ -317,9 +317,6 @@ hipError_t launch_merkle_update(const MerkleT& t, const Rows& olds, const Rows& 
 // the same from kdelta.hip's per-key figures (runs, dh; skipped when guard && *guard);
 // sign -1 undoes what kdelta.hip's count kernel applied, bit for bit, then the dirty chunks
 // are re-reduced
-// the dirty chunks of a tree re-reduced (after put/delete into its bucket level)
-hipError_t launch_merkle_rehash(const MerkleT& t, const u32* dirty, u32* arrive, u64* hand, const i64* cdelta,
-                                u32* err, hipStream_t st);
 hipError_t launch_kd_tree(const MerkleT& t, const u64* keys, const u64* runs, const u64* dh, u64 nk,
                           const u64* guard, int sign, u32* dirty, u32* arrive, u64* hand, i64* cdelta,
                           u32* err, hipStream_t st);
@@ -375,8 +372,9 @@ struct KdArgs {
 };
 // kd_count_kernel (its last workgroup scans)
 hipError_t launch_kd_join(const KdArgs& p, hipStream_t st);
-// kd_write_kernel
-hipError_t launch_kd_write(const KdArgs& p, hipStream_t st);
+// kd_finish_kernel (merkle.hip): the write (dg_kdw.h) and, with a tree, its dirty chunks' re-reduction in one launch
+hipError_t launch_kd_finish(const KdArgs& p, const u32* dirty, u32* arrive, u64* hand, const i64* cdelta,
+                            hipStream_t st);
 
 // ---- small.hip: dg_join_delta of a small delta, one launch (see the file header)
 constexpr u32 SMALL_KEYS = 512, SMALL_DELTA = 512, SMALL_DCTX = 1024, SMALL_NODES = 2048;

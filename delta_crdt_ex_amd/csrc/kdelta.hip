@@ -13,19 +13,22 @@
 //                     (s2 \ c1) -- kept as two bit masks -- whether the key changed (diff/3,
 //                     causal_crdt.ex:344-352) and its Merkle leaf change (Σ row_hash new -
 //                     Σ row_hash old); per workgroup the sums of rows, kept rows, changed
-//                     keys and their rows, delta rows seen; the last workgroup to finish
+//                     keys and their rows, delta rows seen (workgroup 0 of the launch:
+//                     the context union, Dots.union/2); the last key workgroup to finish
 //                     scans the workgroups' figures into exclusive offsets and totals, and the
 //                     guard word: a delta row outside the keyset (the right-biased carry of
 //                     :185-188 applies: the caller runs the full join), a key run over
 //                     KD_RUN rows, more changed keys than the caller's capacity
-//   kd_tree_kernel    (merkle.hip, one thread per key) MerkleMap.put/delete of the changed
-//                     keys into the bucket level, then the dirty chunks re-reduced
-//   kd_write_kernel   (one thread per key) the key's new rows -- in place when no key's row
-//                     count changed, else straight to their final places in the spare store
-//                     -- the changed keys and their rows (device or page-locked host memory),
+//                     (the tree's put/delete of the changed keys, tree_put below, is done
+//                     here too: segmented wave sums, one atomic per bucket and chunk)
+//   kd_finish_kernel  (merkle.hip + dg_kdw.h: one thread per key, and in the same launch
+//                     one workgroup per dirty chunk of the tree) the key's new rows -- in
+//                     place when no key's row count changed, else straight to their final
+//                     places in the spare store -- the changed keys and their rows (device or page-locked host memory),
 //                     the splice index of the rows that move (splice.hip), and the union
 //                     context into the state's; every state write skipped when the tree
-//                     update reported an input error (all or nothing)
+//                     update reported an input error (all or nothing); beside them the
+//                     dirty chunks re-reduced (update_hashes)
 //   splice_kernel     (splice.hip, only when rows moved) the untouched rows to the spare
 //
 // then the count block is published to mapped host memory and the host waits ONCE.
@@ -159,9 +162,18 @@ __global__ __launch_bounds__(KDB) void kd_count_kernel(KdArgs p) {
   __shared__ u64 s_rng[2];
   __shared__ u64 red[KD_NV][KDB / WAVE];
   __shared__ u32 s_last;
+  __shared__ u32 s_cw[KDB / WAVE + 1];
+  if (blockIdx.x == 0) {
+    // Dots.union(state context, delta context) (:155) into the union scratch and
+    // d_counts[1], by a workgroup of its own beside the keys' (it needs only the inputs; in
+    // the last workgroup's tail it added ~5 us to every call)
+    ctx_union_block<KDB>(make_cu(p.ca, p.cd, p.uc_node, p.uc_cnt, p.d_counts + 1, p.cu_tmp), s_cw);
+    return;
+  }
+  const u64 blk = blockIdx.x - 1;  // the keys' workgroups: 1 .. ntiles
   const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
-  const u64 u = (u64)blockIdx.x * KDB + tid;
-  const u64 u0 = (u64)blockIdx.x * KDB, u1 = min<u64>(u0 + KDB, p.nk);
+  const u64 u = blk * KDB + tid;
+  const u64 u0 = blk * KDB, u1 = min<u64>(u0 + KDB, p.nk);
   const bool dvv = p.cd.kind == 0;
   if (tid < 2) {  // the workgroup's delta range [lo, hi): its keys' rows (two searches)
     const u64 x = tid ? p.keys[u1 - 1] + 1 : p.keys[u0];  // (key + 1: past the last key's run)
@@ -292,12 +304,12 @@ __global__ __launch_bounds__(KDB) void kd_count_kernel(KdArgs p) {
     u64 s = 0;
 #pragma unroll
     for (int x = 0; x < KDB / WAVE; x++) s = tid < KD_NV - 1 ? s + red[tid][x] : (s | red[tid][x]);
-    st_ag(p.part + blockIdx.x * KD_NV + tid, s);
+    st_ag(p.part + blk * KD_NV + tid, s);
   }
   __syncthreads();
   if (tid == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    s_last = __hip_atomic_fetch_add(p.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    s_last = __hip_atomic_fetch_add(p.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p.ntiles - 1;
     if (s_last) __hip_atomic_store(p.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
@@ -353,127 +365,6 @@ __global__ __launch_bounds__(KDB) void kd_count_kernel(KdArgs p) {
     p.d_counts[6] = n_ak;
     p.d_counts[7] = carry[5];
   }
-  // Dots.union(state context, delta context) (:155) into the union scratch; d_counts[1]
-  __shared__ u32 s_cw[KDB / WAVE + 1];
-  __syncthreads();
-  ctx_union_block<KDB>(make_cu(p.ca, p.cd, p.uc_node, p.uc_cnt, p.d_counts + 1, p.cu_tmp), s_cw);
-}
-
-// ---------------------------------------------------------------- write
-__global__ __launch_bounds__(KDB) void kd_write_kernel(KdArgs p) {
-  __shared__ u64 s_w[4][KDB / WAVE];
-  const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
-  const u64 u = (u64)blockIdx.x * KDB + tid;
-  const u64 guard = p.d_counts[4];
-  const bool tree_bad = p.err && (*p.err & MERKLE_INPUT_ERR);
-  if (guard) return;  // (uniform) nothing is written: the caller falls back or reports
-  const bool moved = p.d_counts[5] != 0;
-  if (blockIdx.x == 0 && !tree_bad) {  // the union context into the state's (Dots.union, :155)
-    const u64 nc = p.d_counts[1];       // (and the caller's copy, when it fits)
-    const bool co = p.co_node && nc <= p.co_cap;
-    for (u64 i = tid; i < nc && i < p.ca_cap; i += KDB) {
-      const u32 n = p.uc_node[i];
-      const u64 c = p.uc_cnt[i];
-      p.ca_node[i] = n;
-      p.ca_cnt[i] = c;
-      if (co) {
-        p.co_node[i] = n;
-        p.co_cnt[i] = c;
-      }
-    }
-  }
-  u64 rn = 0;
-  u32 na = 0, nd = 0, ne = 0;
-  bool chg = false;
-  if (u < p.nk) {
-    rn = p.runs[u];
-    na = (u32)(rn & 0xFFFF);
-    nd = (u32)((rn >> 16) & 0xFFFF);
-    ne = (u32)((rn >> 32) & 0xFFFF);
-    chg = (rn >> 48) & 1;
-  }
-  // exclusive in-workgroup prefixes of (na, ne, chg, chg rows) + the workgroup's offsets
-  const u64 x[4] = {na, ne, chg ? 1u : 0u, chg ? ne : 0u};
-  u64 pre[4];
-#pragma unroll
-  for (int q = 0; q < 4; q++) {
-    u64 inc = x[q];
-#pragma unroll
-    for (int d = 1; d < WAVE; d <<= 1) {
-      const u64 y = __shfl_up(inc, d, WAVE);
-      if (lane >= d) inc += y;
-    }
-    if (lane == WAVE - 1) s_w[q][w] = inc;
-    pre[q] = inc - x[q];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int q = 0; q < 4; q++) {
-    u64 below = p.toff[blockIdx.x * KD_NV + q];
-    for (int i = 0; i < w; i++) below += s_w[q][i];
-    pre[q] += below;
-  }
-  if (u >= p.nk) return;
-  const u64 k = p.keys[u];
-  const u64 a_lo = p.a_lo[u], d_lo = p.d_lo[u], am = p.amask[u], dm = p.dmask[u];
-  const u64 a_off = pre[0], e_off = pre[1], c_off = pre[2], r_off = pre[3];
-  const u64 n_e = p.d_counts[0], n_ak = p.d_counts[6];
-  // the splice index (splice.hip): where this key's rows go and where the untouched rows
-  // before it move
-  const i64 gap = (i64)a_lo - (i64)a_off;
-  if (moved) {
-    p.end[u] = a_lo + na;
-    p.shift[u] = (i64)e_off - (i64)a_off;
-    const u64 end_lo = u > 0 ? p.a_lo[u - 1] + (p.runs[u - 1] & 0xFFFF) : 0ull;
-    const u64 end_hi = a_lo + na;
-    for (u64 t = (end_lo + SPLICE_TILE - 1) / SPLICE_TILE; t <= p.a_tiles && t * SPLICE_TILE < end_hi; t++)
-      p.tile_u0[t] = u;
-    if (u == p.nk - 1) {
-      p.shift[p.nk] = (i64)n_e - (i64)n_ak;
-      for (u64 t = (end_hi + SPLICE_TILE - 1) / SPLICE_TILE; t <= p.a_tiles; t++) p.tile_u0[t] = p.nk;
-    }
-  }
-  // the key's new rows in tuple order: the kept state rows and the new delta rows (disjoint)
-  const bool wr_state = !tree_bad;  // in place: only when the tree took the update
-  const bool wr_rows = chg && p.has_rows && r_off + ne <= p.rows_cap;
-  if (!(wr_state || moved) && !wr_rows && !chg) return;
-  u32 i = 0, j = 0, o = 0;
-  auto next_a = [&]() { while (i < na && !((am >> i) & 1)) i++; };
-  auto next_d = [&]() { while (j < nd && !((dm >> j) & 1)) j++; };
-  next_a();
-  next_d();
-  Row ra{}, rb{};
-  if (i < na) ra = load_row(p.a, a_lo + i);
-  if (j < nd) rb = load_row(p.d, d_lo + j);
-  while (i < na || j < nd) {
-    bool takeA;
-    if (i >= na) {
-      takeA = false;
-    } else if (j >= nd) {
-      takeA = true;
-    } else {
-      bool lt, eq;
-      row_cmp_bf(ra, rb, lt, eq);
-      takeA = lt;
-    }
-    const Row r = takeA ? ra : rb;
-    if (moved)
-      store_row(p.sp, (u64)((i64)(e_off + o) + gap), r);
-    else if (wr_state && chg)  // (unchanged keys keep their rows as they are)
-      store_row(p.aw, a_lo + o, r);
-    if (wr_rows) store_row(p.rows, r_off + o, r);
-    o++;
-    if (takeA) {
-      i++;
-      next_a();
-      if (i < na) ra = load_row(p.a, a_lo + i);
-    } else {
-      j++;
-      next_d();
-      if (j < nd) rb = load_row(p.d, d_lo + j);
-    }
-  }
-  if (chg && c_off < p.cap) p.changed[c_off] = k;
 }
 
 }  // namespace
@@ -482,14 +373,7 @@ hipError_t launch_kd_join(const KdArgs& p0, hipStream_t st) {
   KdArgs p = p0;
   p.ntiles = (p.nk + KDB - 1) / KDB;
   if (p.ntiles == 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(kd_count_kernel, dim3((unsigned)p.ntiles), dim3(KDB), 0, st, p);
-  return hipGetLastError();
-}
-
-hipError_t launch_kd_write(const KdArgs& p0, hipStream_t st) {
-  KdArgs p = p0;
-  p.ntiles = (p.nk + KDB - 1) / KDB;
-  hipLaunchKernelGGL(kd_write_kernel, dim3((unsigned)p.ntiles), dim3(KDB), 0, st, p);
+  hipLaunchKernelGGL(kd_count_kernel, dim3((unsigned)(p.ntiles + 1)), dim3(KDB), 0, st, p);  // (+ the union's)
   return hipGetLastError();
 }
 

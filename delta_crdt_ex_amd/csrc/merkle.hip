@@ -43,6 +43,7 @@
 //    differing buckets), which the peer merges with its own rows into keys.
 #include "dg_hash.h"
 #include "dg_home.h"
+#include "dg_kdw.h"
 #include "dg_launch.h"
 #include "dg_tree.h"
 
@@ -415,7 +416,7 @@ __device__ __forceinline__ void chunk_block(Rows rows, MT t, const u32* dirty, u
     // chunks before it (an exclusive scan of cdelta, UPB chunks per round; the end by all)
     // (CP consecutive entries per thread, their loads issued together: one round of
     // UPB * CP = 4096 entries covers the 2048 chunks of a depth-22 tree)
-    constexpr int CP = 8;
+    constexpr int CP = 4;
     i64 carry = 0;
     for (u64 c0 = 0; c0 <= G; c0 += (u64)UPB * CP) {
       const u64 x0 = c0 + (u64)tid * CP;
@@ -480,6 +481,21 @@ __global__ __launch_bounds__(UPB, 4) void merkle_chunk_kernel(Rows rows, MT t, c
   chunk_block<BUILD, VEC>(rows, t, dirty, ctr, hand, d_keys, err, cdelta, blockIdx.x, gridDim.x);
 }
 
+// dg_join_delta's write (dg_kdw.h, workgroups [0, nw): dispatched first, they start at once)
+// and the dirty chunks' re-reduction (the rest, one per chunk) in ONE launch: both read only
+// what kd_count_kernel wrote, so the write's ~15 us run under the re-reduction's instead of
+// after it.
+#ifndef DG_KDF_WAVES  // waves per SIMD the fused launch is compiled for: 6 = 73 VGPRs, three workgroups per CU, no spills (8: spills, 4: two per CU; 144-149 us vs 152 us per config-4 join_delta at 4 and 8, A/B)
+#define DG_KDF_WAVES 6
+#endif
+__global__ __launch_bounds__(UPB, DG_KDF_WAVES) void kd_finish_kernel(KdArgs p, u32 nw, MT t, const u32* dirty,
+                                                         u32* ctr, u64* hand, const i64* cdelta) {
+  if (blockIdx.x < nw) {
+    kd_write_block<UPB>(p, blockIdx.x);
+    return;
+  }
+  chunk_block<false>(Rows{}, t, dirty, ctr, hand, nullptr, nullptr, cdelta, blockIdx.x - nw, gridDim.x - nw);
+}
 
 // ---------------------------------------------------------------- update
 constexpr int UB = 256;
@@ -1673,13 +1689,16 @@ hipError_t launch_kd_tree(const MerkleT& m, const u64* keys, const u64* runs, co
   return hipGetLastError();
 }
 
-hipError_t launch_merkle_rehash(const MerkleT& m, const u32* dirty, u32* arrive, u64* hand, const i64* cdelta,
-                                u32* err, hipStream_t st) {
-  const MT t = mt_of(m);
-  const u64 G = merkle_chunks(t.depth);
-  Rows none{};
-  hipLaunchKernelGGL(merkle_chunk_kernel<false>, dim3((unsigned)G), dim3(UPB), 0, st, none, t, dirty, arrive,
-                     hand, (u64*)nullptr, err, t.starts ? cdelta : (const i64*)nullptr);
+hipError_t launch_kd_finish(const KdArgs& p0, const u32* dirty, u32* arrive, u64* hand, const i64* cdelta,
+                            hipStream_t st) {
+  KdArgs p = p0;
+  p.ntiles = (p.nk + KD_BLOCK - 1) / KD_BLOCK;
+  const u64 nw = (p.nk + UPB - 1) / UPB;
+  const MT t = p.has_tree ? mt_of(p.t) : MT{};
+  const u64 G = p.has_tree ? merkle_chunks(t.depth) : 0;
+  if (nw + G == 0) return hipSuccess;
+  hipLaunchKernelGGL(kd_finish_kernel, dim3((unsigned)(nw + G)), dim3(UPB), 0, st, p, (u32)nw, t, dirty, arrive,
+                     hand, t.starts ? cdelta : (const i64*)nullptr);
   return hipGetLastError();
 }
 
