@@ -222,19 +222,23 @@ def config4_round(eng, torch, dev, rank=0, world=1, keys_per_rank=12_500_000, st
         tt.store = st
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        t0 = time.perf_counter()
-        e0.record(eng.stream)
-        keys, total = eng.merkle_diff(ta, tb, cap=cap, with_total=True)
-        e1.record(eng.stream)
-        t1 = time.perf_counter()
-        delta = eng.take_keys(sb, keys)
-        t2 = time.perf_counter()
         e2, e3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e2.record(eng.stream)
-        changed, swapped = eng.join_delta(st, sc, delta, cb, keys, spare, tt)
-        e3.record(eng.stream)
+        # the calls run on the engine's own stream (as a caller that issues its work there:
+        # no cross-stream ordering per call); each is synchronous -- it returns once its
+        # results are on the host -- so the wall clock stops at its return
+        with torch.cuda.stream(eng.stream):
+            t0 = time.perf_counter()
+            e0.record(eng.stream)
+            keys, total = eng.merkle_diff(ta, tb, cap=cap, with_total=True)
+            e1.record(eng.stream)
+            t1 = time.perf_counter()
+            delta = eng.take_keys(sb, keys)
+            t2 = time.perf_counter()
+            e2.record(eng.stream)
+            changed, swapped = eng.join_delta(st, sc, delta, cb, keys, spare, tt)
+            t3 = time.perf_counter()
+            e3.record(eng.stream)
         torch.cuda.synchronize()
-        t3 = time.perf_counter()
         t.update(diff=t1 - t0, take=t2 - t1, join_delta=t3 - t2, total=t3 - t0,
                  join_delta_ev=e2.elapsed_time(e3) * 1e-3,
                  diff_ev=e0.elapsed_time(e1) * 1e-3, keys=int(keys.numel()), total_keys=total,
@@ -248,6 +252,41 @@ def config4_round(eng, torch, dev, rank=0, world=1, keys_per_rank=12_500_000, st
 
     one_round()
     rounds = [one_round() for _ in range(5)]
+
+    def c_abi_join_delta(reps=5):
+        """dg_join_delta as the NIF calls it: the C-ABI call alone (its arguments built
+        beforehand), from the round's state, delta and keys, A restored outside the clock."""
+        import ctypes as C
+        from delta_crdt_ex_amd import _abi
+        from delta_crdt_ex_amd.store import _ptr, check
+        keys = eng.merkle_diff(ta, tb, cap=cap)
+        delta = eng.take_keys(sb, keys)
+        chg = torch.empty(max(int(keys.numel()), 1), dtype=torch.int64, device=dev)
+        out = []
+        for _ in range(reps + 1):
+            for f in ("key", "val", "ts", "node", "cnt"):
+                getattr(st, f)[: sa.n].copy_(getattr(sa, f)[: sa.n])
+            st.n = sa.n
+            sc.node[: ca.n].copy_(ca.node[: ca.n])
+            sc.cnt[: ca.n].copy_(ca.cnt[: ca.n])
+            sc.n, sc.kind = ca.n, ca.kind
+            tt = ta.clone()
+            tt.store = st
+            ss, scc, sd, cd, sp, tr = st.abi(), sc.abi(), delta.abi(), cb.abi(), spare.abi(), tt.abi()
+            kp, nk = eng._keys(keys)
+            nn, sw = C.c_uint64(0), C.c_int(0)
+            args = (eng.h, C.byref(ss), C.byref(scc), C.byref(sd), C.byref(cd), kp, nk, C.byref(sp),
+                    C.byref(tr), _ptr(chg, _abi.P64), int(chg.numel()), C.byref(nn), C.byref(sw))
+            fn = eng.lib.dg_join_delta
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            rc = fn(*args)
+            out.append(time.perf_counter() - t0)
+            check(rc)
+            torch.cuda.synchronize()
+        return float(np.median(out[1:])) * 1e6
+
+    join_delta_c_us = c_abi_join_delta()
     resident = resident_delta(eng, torch, sa, ca, cb, ta, tb, b)
     partial = {"max_sync_size_200": partial_round(eng, torch, ta, tb, max_sync_size=200),
                "infinite": partial_round(eng, torch, ta, tb, max_sync_size=None, reps=3),
@@ -287,9 +326,13 @@ def config4_round(eng, torch, dev, rank=0, world=1, keys_per_rank=12_500_000, st
         "round_us": {k: v * 1e6 for k, v in med.items() if k not in ("diff_ev", "join_delta_ev")},
         "join_delta_device_us": med["join_delta_ev"] * 1e6,
         "join_delta_roofline": _join_delta_roofline(last, med["join_delta_ev"]),
-        "join_delta_note": "round_us.join_delta: wall time of the Python call (ctypes, its one "
-                           "host wait, a torch synchronize); join_delta_device_us: HIP events on "
-                           "the engine stream around the same call (first kernel to last)",
+        "join_delta_c_abi_us": join_delta_c_us,
+        "join_delta_note": "round_us.*: wall time of each synchronous Python call on the engine's "
+                           "stream, to its return (the results on the host: its one host wait "
+                           "included); join_delta_device_us: HIP events on the engine stream "
+                           "around the same call (the host's launch work included); "
+                           "join_delta_c_abi_us: the dg_join_delta C-ABI call alone, arguments "
+                           "built beforehand, as the NIF makes it (median of 5)",
         "round_keys": last["keys"], "round_total_keys": last["total_keys"],
         "round_delta_rows": last["rows"], "round_changed_keys": last["changed"],
         "update_equals_rebuild": all(r["ok"] for r in rounds),

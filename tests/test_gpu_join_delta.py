@@ -691,3 +691,4 @@ def test_kd_changed_keys_past_their_capacity(engine):
         engine.join_delta(st, sc, sd, cd, kdev(want), spare, tree, changed=small)
     _assert_unchanged(st, sc, tree, snap)
     apply(engine, a, d, want, depth=12)  # and the engine goes on
+
