@@ -198,6 +198,97 @@ __device__ void chunk_upsweep(u64* nodes, u32 hi, u64 g0, u64* s) {
   __syncthreads();
 }
 
+// The last workgroup of a chunk launch: levels depth - L1 .. 0, UPL levels per round (the
+// first round's inputs are the handed-off chunk roots, sc1 loads), the chunk index moved
+// by the chunks' row-count changes (cdelta, when given), and for a build the distinct-key
+// count.  s: the caller's UPW-node LDS stage.
+template <bool BUILD>
+__device__ __forceinline__ void chunk_tail(MT t, u64* hand, u64* d_keys, const i64* cdelta, const u64 G, u64* s) {
+  const u32 L1 = t.depth < (u32)UPL ? t.depth : (u32)UPL;
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
+  u32 hl = t.depth - L1;
+  bool first = true;
+  while (hl > 0) {
+    const u32 nlev = hl < (u32)UPL ? hl : (u32)UPL;
+    const u64 chunks = 1ull << (hl - nlev);
+    const u64* src = t.nodes + ((1ull << hl) - 1);
+    wait_vmem();  // this workgroup's own stores of level hl (depth > 2 * UPL) are complete
+    __syncthreads();
+    for (u64 c = 0; c < chunks; c++) {
+      for (u32 x = tid; x < (1u << nlev); x += UPB)
+        s[x] = first ? ld_sc1(hand + (c << nlev) + x) : src[(c << nlev) + x];
+      __syncthreads();
+      if ((1u << nlev) == UPW)  // (uniform)
+        chunk_upsweep(t.nodes, hl, c << nlev, s);
+      else
+        lds_upsweep(t.nodes, hl, c << nlev, 1u << nlev, s);
+    }
+    hl -= nlev;
+    first = false;
+  }
+  if (!BUILD && t.starts && cdelta) {
+    // the update moved rows: chunk g's first row shifts by the row-count changes of the
+    // chunks before it (an exclusive scan of cdelta, UPB chunks per round; the end by all)
+    // (CP consecutive entries per thread, their loads issued together: one round of
+    // UPB * CP = 4096 entries covers the 2048 chunks of a depth-22 tree)
+    constexpr int CP = 4;
+    i64 carry = 0;
+    for (u64 c0 = 0; c0 <= G; c0 += (u64)UPB * CP) {
+      const u64 x0 = c0 + (u64)tid * CP;
+      i64 v[CP], st0[CP];
+#pragma unroll
+      for (int q = 0; q < CP; q++) {
+        const u64 x = x0 + q;
+        v[q] = x < G ? cdelta[x] : 0;
+        st0[q] = x <= G ? (i64)t.starts[x] : 0;
+      }
+#pragma unroll
+      for (int q = 0; q < CP; q++)  // consumed: zero again for the next update
+        if (x0 + q < G && v[q]) ((i64*)cdelta)[x0 + q] = 0;
+      i64 own = 0;
+#pragma unroll
+      for (int q = 0; q < CP; q++) own += v[q];
+      i64 incl = own;
+#pragma unroll
+      for (int d = 1; d < WAVE; d <<= 1) {
+        const i64 y = __shfl_up(incl, d, WAVE);
+        if (lane >= d) incl += y;
+      }
+      __syncthreads();
+      if (lane == WAVE - 1) s[w] = (u64)incl;
+      __syncthreads();
+      i64 before = 0, tot = 0;
+      for (int q = 0; q < UPB / WAVE; q++) {
+        const i64 y = (i64)s[q];
+        before += q < w ? y : 0;
+        tot += y;
+      }
+      i64 run = carry + before + incl - own;  // the changes of the chunks before x0
+#pragma unroll
+      for (int q = 0; q < CP; q++) {
+        const u64 x = x0 + q;
+        if (x <= G) t.starts[x] = (u64)(st0[q] + run);
+        run += v[q];
+      }
+      carry += tot;
+    }
+  }
+  if (BUILD) {
+    u64 sum = 0;
+    for (u64 x = tid; x < G; x += UPB) sum += ld_sc1(hand + G + x);
+#pragma unroll
+    for (int d = WAVE / 2; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, WAVE);
+    __syncthreads();
+    if (lane == 0) s[w] = sum;
+    __syncthreads();
+    if (tid == 0) {
+      u64 tot = 0;
+      for (int q = 0; q < UPB / WAVE; q++) tot += s[q];
+      *d_keys = tot;
+    }
+  }
+}
+
 // ctr: the arrival counter, zero on entry and left zero (the last workgroup resets it: a
 // persistent engine word, no fill launch per build); scratch: per chunk its root and its
 // distinct-key count (u64 each, at hand[0, G) and hand[G, 2G)).
@@ -367,7 +458,7 @@ __device__ __forceinline__ void chunk_block(Rows rows, MT t, const u32* dirty, u
     else
       lds_upsweep(t.nodes, t.depth, g0, width, s);
     chunk_root = s[0];
-  } else if (dirty[g]) {
+  } else if (dirty && dirty[g]) {
     for (u32 x = tid; x < width; x += UPB) s[x] = lvl[g0 + x];
     __syncthreads();
     if (width == UPW)  // (uniform)
@@ -389,89 +480,7 @@ __device__ __forceinline__ void chunk_block(Rows rows, MT t, const u32* dirty, u
   }
   __syncthreads();
   if (!s_last) return;
-  // ---- the last workgroup: levels depth - L1 .. 0, UPL levels per round; the first
-  // round's inputs are the handed-off chunk roots (sc1 loads)
-  u32 hl = t.depth - L1;
-  bool first = true;
-  while (hl > 0) {
-    const u32 nlev = hl < (u32)UPL ? hl : (u32)UPL;
-    const u64 chunks = 1ull << (hl - nlev);
-    const u64* src = t.nodes + ((1ull << hl) - 1);
-    wait_vmem();  // this workgroup's own stores of level hl (depth > 2 * UPL) are complete
-    __syncthreads();
-    for (u64 c = 0; c < chunks; c++) {
-      for (u32 x = tid; x < (1u << nlev); x += UPB)
-        s[x] = first ? ld_sc1(hand + (c << nlev) + x) : src[(c << nlev) + x];
-      __syncthreads();
-      if ((1u << nlev) == UPW)  // (uniform)
-        chunk_upsweep(t.nodes, hl, c << nlev, s);
-      else
-        lds_upsweep(t.nodes, hl, c << nlev, 1u << nlev, s);
-    }
-    hl -= nlev;
-    first = false;
-  }
-  if (!BUILD && t.starts && cdelta) {
-    // the update moved rows: chunk g's first row shifts by the row-count changes of the
-    // chunks before it (an exclusive scan of cdelta, UPB chunks per round; the end by all)
-    // (CP consecutive entries per thread, their loads issued together: one round of
-    // UPB * CP = 4096 entries covers the 2048 chunks of a depth-22 tree)
-    constexpr int CP = 4;
-    i64 carry = 0;
-    for (u64 c0 = 0; c0 <= G; c0 += (u64)UPB * CP) {
-      const u64 x0 = c0 + (u64)tid * CP;
-      i64 v[CP], st0[CP];
-#pragma unroll
-      for (int q = 0; q < CP; q++) {
-        const u64 x = x0 + q;
-        v[q] = x < G ? cdelta[x] : 0;
-        st0[q] = x <= G ? (i64)t.starts[x] : 0;
-      }
-#pragma unroll
-      for (int q = 0; q < CP; q++)  // consumed: zero again for the next update
-        if (x0 + q < G && v[q]) ((i64*)cdelta)[x0 + q] = 0;
-      i64 own = 0;
-#pragma unroll
-      for (int q = 0; q < CP; q++) own += v[q];
-      i64 incl = own;
-#pragma unroll
-      for (int d = 1; d < WAVE; d <<= 1) {
-        const i64 y = __shfl_up(incl, d, WAVE);
-        if (lane >= d) incl += y;
-      }
-      __syncthreads();
-      if (lane == WAVE - 1) s[w] = (u64)incl;
-      __syncthreads();
-      i64 before = 0, tot = 0;
-      for (int q = 0; q < UPB / WAVE; q++) {
-        const i64 y = (i64)s[q];
-        before += q < w ? y : 0;
-        tot += y;
-      }
-      i64 run = carry + before + incl - own;  // the changes of the chunks before x0
-#pragma unroll
-      for (int q = 0; q < CP; q++) {
-        const u64 x = x0 + q;
-        if (x <= G) t.starts[x] = (u64)(st0[q] + run);
-        run += v[q];
-      }
-      carry += tot;
-    }
-  }
-  if (BUILD) {
-    u64 sum = 0;
-    for (u64 x = tid; x < G; x += UPB) sum += ld_sc1(hand + G + x);
-#pragma unroll
-    for (int d = WAVE / 2; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, WAVE);
-    __syncthreads();
-    if (lane == 0) s[w] = sum;
-    __syncthreads();
-    if (tid == 0) {
-      u64 tot = 0;
-      for (int q = 0; q < UPB / WAVE; q++) tot += s[q];
-      *d_keys = tot;
-    }
-  }
+  chunk_tail<BUILD>(t, hand, d_keys, cdelta, G, s);
 }
 
 template <bool BUILD, bool VEC = false>
@@ -479,6 +488,84 @@ __global__ __launch_bounds__(UPB, 4) void merkle_chunk_kernel(Rows rows, MT t, c
                                                            u32* ctr, u64* hand, u64* d_keys,
                                                            u32* err, const i64* cdelta) {
   chunk_block<BUILD, VEC>(rows, t, dirty, ctr, hand, d_keys, err, cdelta, blockIdx.x, gridDim.x);
+}
+
+// The update's re-reduction by NB persistent workgroups, chunks g = cb, cb + NB, ...: a
+// workgroup per chunk paid a dirty-flag load, a root load, a write-through hand-off and an
+// arrival for every chunk, and 2048 such workgroups took 32 us with nothing dirty (A/B).
+// Here a workgroup loads its chunks' flags and old roots in one round trip, re-reduces its
+// dirty chunks one after the other (the next chunk's leaves issued before the current
+// one's upsweep), hands every root off write-through and arrives once; the last one runs
+// chunk_tail.  The leaves are double-buffered in LDS.
+#ifndef DG_KDF_EXP
+#define DG_KDF_EXP 0  // A/B builds only: 3 = a workgroup per chunk (chunk_block)
+#endif
+constexpr u32 KCH = 16;  // chunks per workgroup at most (G <= KCH * NB)
+__device__ __forceinline__ void kd_chunks(MT t, u32* dirty, u32* ctr, u64* hand, const i64* cdelta, const u64 cb,
+                                          const u64 NB, const u64 G) {
+  __shared__ u64 s2[2][UPW];
+  __shared__ u32 s_fl[KCH];
+  __shared__ u64 s_rt[KCH];
+  __shared__ u32 s_last;
+  const u32 L1 = t.depth < (u32)UPL ? t.depth : (u32)UPL;
+  const u32 width = 1u << L1;
+  const int tid = threadIdx.x;
+  const u64* lvl = t.nodes + ((1ull << t.depth) - 1);
+  const u32 nc = (u32)((G - cb + NB - 1) / NB);  // this workgroup's chunks (<= KCH)
+  if ((u32)tid < nc) {
+    const u64 g = cb + (u64)tid * NB;
+    s_fl[tid] = dirty[g];
+    s_rt[tid] = t.nodes[((1ull << (t.depth - L1)) - 1) + g];
+  }
+  __syncthreads();
+  // leaves of the i-th dirty chunk from position j on, into buffer b (registers first)
+  auto next_dirty = [&](u32 j) {
+    while (j < nc && !s_fl[j]) j++;
+    return j;
+  };
+  u32 j = next_dirty(0);
+  u64 v[UPW / UPB];
+  if (j < nc)
+#pragma unroll
+    for (u32 q = 0; q < UPW / UPB; q++) {
+      const u32 x = tid + q * UPB;
+      v[q] = x < width ? lvl[((cb + (u64)j * NB) << L1) + x] : 0ull;
+    }
+  int b = 0;
+  for (u32 i = 0; i < nc; i++) {
+    const u64 g = cb + (u64)i * NB;
+    if (i != j) {  // clean: its root as the previous kernels left it
+      if (tid == 0) st_sc1(hand + g, s_rt[i]);
+      continue;
+    }
+#pragma unroll
+    for (u32 q = 0; q < UPW / UPB; q++) s2[b][tid + q * UPB] = v[q];
+    __syncthreads();
+    j = next_dirty(i + 1);  // the next dirty chunk's leaves in flight during this upsweep
+    if (j < nc)
+#pragma unroll
+      for (u32 q = 0; q < UPW / UPB; q++) {
+        const u32 x = tid + q * UPB;
+        v[q] = x < width ? lvl[((cb + (u64)j * NB) << L1) + x] : 0ull;
+      }
+    if (width == UPW)  // (uniform)
+      chunk_upsweep(t.nodes, t.depth, g << L1, s2[b]);
+    else
+      lds_upsweep(t.nodes, t.depth, g << L1, width, s2[b]);
+    if (tid == 0) {
+      st_sc1(hand + g, s2[b][0]);
+      dirty[g] = 0;  // consumed: the flags are zero again for the next update
+    }
+    b ^= 1;
+  }
+  if (tid == 0) {
+    wait_vmem();
+    s_last = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == NB - 1;
+    if (s_last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // all NB arrived
+  }
+  __syncthreads();
+  if (!s_last) return;
+  chunk_tail<false>(t, hand, nullptr, cdelta, G, s2[0]);
 }
 
 // dg_join_delta's write (dg_kdw.h, workgroups [0, nw): dispatched first, they start at once)
@@ -494,7 +581,15 @@ __global__ __launch_bounds__(UPB, DG_KDF_WAVES) void kd_finish_kernel(KdArgs p, 
     kd_write_block<UPB>(p, blockIdx.x);
     return;
   }
-  chunk_block<false>(Rows{}, t, dirty, ctr, hand, nullptr, nullptr, cdelta, blockIdx.x - nw, gridDim.x - nw);
+  // no key's row count changed (the count kernel's moved flag): every chunk's row-count
+  // change is zero, and the last workgroup skips the chunk index's scan
+  const i64* cd = p.d_counts[5] ? cdelta : nullptr;
+#if DG_KDF_EXP == 3  // (A/B: a workgroup per chunk)
+  chunk_block<false>(Rows{}, t, dirty, ctr, hand, nullptr, nullptr, cd, blockIdx.x - nw, gridDim.x - nw);
+#else
+  const u32 L1 = t.depth < (u32)UPL ? t.depth : (u32)UPL;
+  kd_chunks(t, (u32*)dirty, ctr, hand, cd, blockIdx.x - nw, gridDim.x - nw, 1ull << (t.depth - L1));
+#endif
 }
 
 // ---------------------------------------------------------------- update
@@ -1695,7 +1790,14 @@ hipError_t launch_kd_finish(const KdArgs& p0, const u32* dirty, u32* arrive, u64
   p.ntiles = (p.nk + KD_BLOCK - 1) / KD_BLOCK;
   const u64 nw = (p.nk + UPB - 1) / UPB;
   const MT t = p.has_tree ? mt_of(p.t) : MT{};
-  const u64 G = p.has_tree ? merkle_chunks(t.depth) : 0;
+  const u64 G0 = p.has_tree ? merkle_chunks(t.depth) : 0;
+#if DG_KDF_EXP == 3
+  const u64 G = G0;
+#else
+  // persistent chunk workgroups: at most 512 (three workgroups per CU beside the write's),
+  // at least G / KCH
+  const u64 G = G0 ? std::max<u64>(std::min<u64>(G0, 512), (G0 + KCH - 1) / KCH) : 0;
+#endif
   if (nw + G == 0) return hipSuccess;
   hipLaunchKernelGGL(kd_finish_kernel, dim3((unsigned)(nw + G)), dim3(UPB), 0, st, p, (u32)nw, t, dirty, arrive,
                      hand, t.starts ? cdelta : (const i64*)nullptr);
