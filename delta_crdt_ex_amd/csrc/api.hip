@@ -964,7 +964,7 @@ static int kd_join_delta(dg_engine* e, dg_store* state, dg_context* state_ctx, c
   auto al = [](size_t b) { return (b + 255) / 256 * 256; };
   const size_t per_key = al(nk * 8), per_key1 = al((nk + 1) * 8), tiles_b = al(ntiles * KD_NV * 8);
   const size_t uc_b = al(uctx_cap * 8) + al(uctx_cap * 4), cu_b = al(ctx_union_tmp_bytes(state_ctx->n, delta_ctx->n));
-  const size_t bytes = 7 * per_key + per_key1 + 2 * tiles_b + al((a_tiles + 2) * 8) + uc_b + cu_b;
+  const size_t bytes = 7 * per_key + per_key1 + tiles_b + al((a_tiles + 2) * 8) + uc_b + cu_b;
   TRY(ensure_buf(e, &e->kdb, &e->kdb_cap, bytes));
   char* q = (char*)e->kdb;
   auto take = [&](size_t b) {
@@ -992,7 +992,6 @@ static int kd_join_delta(dg_engine* e, dg_store* state, dg_context* state_ctx, c
   p.end = (u64*)take(per_key);
   p.shift = (i64*)take(per_key1);
   p.part = (u64*)take(tiles_b);
-  p.toff = (u64*)take(tiles_b);
   p.tile_u0 = (u64*)take(al((a_tiles + 2) * 8));
   u64* uc_cnt = (u64*)take(al(uctx_cap * 8));
   u32* uc_node = (u32*)take(al(uctx_cap * 4));

@@ -67,15 +67,34 @@ __device__ __forceinline__ void kd_write_block(const KdArgs& p, u64 blk) {
     if (lane == WAVE - 1) s_w[q][w] = inc;
     pre[q] = inc - x[q];
   }
-  const bool live = tile < p.ntiles;  // (whole waves)
-  u64 toff[4] = {0, 0, 0, 0};
-  if (live)
+  // the tiles' offsets: the figures of every earlier tile (kd_count_kernel's per-workgroup
+  // sums), added up here by the whole workgroup -- one round of loads -- instead of a scan
+  // by the count kernel's last workgroup
+  constexpr int TPW = NT / KD_BLOCK;  // count tiles per workgroup
+  const u64 t0 = blk * TPW;           // this workgroup's first tile
+  __shared__ u64 s_e[4][NT / WAVE], s_own[4][TPW];
+  u64 e[4] = {0, 0, 0, 0};
+  for (u64 t = tid; t < t0; t += NT) {
+    u64 y[4];
 #pragma unroll
-    for (int q = 0; q < 4; q++) toff[q] = p.toff[tile * KD_NV + q];
-  __syncthreads();
+    for (int q = 0; q < 4; q++) y[q] = p.part[t * KD_NV + q];
+#pragma unroll
+    for (int q = 0; q < 4; q++) e[q] += y[q];
+  }
+  if (tid < 4 * TPW && t0 + tid / 4 < p.ntiles) s_own[tid % 4][tid / 4] = p.part[(t0 + tid / 4) * KD_NV + tid % 4];
 #pragma unroll
   for (int q = 0; q < 4; q++) {
-    u64 below = toff[q];
+#pragma unroll
+    for (int d = WAVE / 2; d >= 1; d >>= 1) e[q] += __shfl_xor(e[q], d, WAVE);
+    if (lane == 0) s_e[q][w] = e[q];
+  }
+  __syncthreads();
+  const int ti = (int)(tile - t0);  // this thread's tile within the workgroup
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    u64 below = 0;
+    for (int i = 0; i < NT / WAVE; i++) below += s_e[q][i];
+    for (int i = 0; i < ti; i++) below += s_own[q][i];
     for (int i = w - w % WPT; i < w; i++) below += s_w[q][i];
     pre[q] += below;
   }

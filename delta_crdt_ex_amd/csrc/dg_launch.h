@@ -346,7 +346,7 @@ struct KdArgs {
   // per key (nk): first state row, first delta row, runs (na | nd << 16 | ne << 32 | chg << 48),
   // kept-row masks, leaf change
   u64 *a_lo, *d_lo, *runs, *amask, *dmask, *dh;
-  u64 *part, *toff;    // per workgroup KD_NV figures and their exclusive offsets
+  u64* part;           // per count workgroup its KD_NV figures (the write sums the earlier ones)
   u64 ntiles;
   u64* changed;        // changed keys (cap), device or mapped host memory
   u64 cap;

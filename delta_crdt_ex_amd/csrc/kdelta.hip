@@ -12,23 +12,23 @@
 //                     state rows stay (s1 ∩ s2 ∪ s1 \ c2) and which delta rows come in
 //                     (s2 \ c1) -- kept as two bit masks -- whether the key changed (diff/3,
 //                     causal_crdt.ex:344-352) and its Merkle leaf change (Σ row_hash new -
-//                     Σ row_hash old); per workgroup the sums of rows, kept rows, changed
-//                     keys and their rows, delta rows seen (workgroup 0 of the launch:
-//                     the context union, Dots.union/2); the last key workgroup to finish
-//                     scans the workgroups' figures into exclusive offsets and totals, and the
-//                     guard word: a delta row outside the keyset (the right-biased carry of
-//                     :185-188 applies: the caller runs the full join), a key run over
-//                     KD_RUN rows, more changed keys than the caller's capacity
-//                     (the tree's put/delete of the changed keys, tree_put below, is done
-//                     here too: segmented wave sums, one atomic per bucket and chunk)
-//   kd_finish_kernel  (merkle.hip + dg_kdw.h: one thread per key, and in the same launch
-//                     one workgroup per dirty chunk of the tree) the key's new rows -- in
-//                     place when no key's row count changed, else straight to their final
-//                     places in the spare store -- the changed keys and their rows (device or page-locked host memory),
-//                     the splice index of the rows that move (splice.hip), and the union
-//                     context into the state's; every state write skipped when the tree
-//                     update reported an input error (all or nothing); beside them the
-//                     dirty chunks re-reduced (update_hashes)
+//                     Σ row_hash old), put into the tree right away (segmented wave sums:
+//                     one atomic per bucket and chunk); per workgroup the sums of rows, kept
+//                     rows, changed keys and their rows, delta rows seen; the last key
+//                     workgroup to finish sums them into the totals and the guard word: a
+//                     delta row outside the keyset (the right-biased carry of :185-188
+//                     applies: the caller runs the full join), a key run over KD_RUN rows,
+//                     more changed keys than the caller's capacity.  Workgroup 0 of the
+//                     launch computes the context union (Dots.union/2).
+//   kd_finish_kernel  (merkle.hip + dg_kdw.h, one launch) one thread per key: its new rows --
+//                     in place when no key's row count changed, else straight to their
+//                     final places in the spare store -- the changed keys and their rows
+//                     (device or page-locked host memory), the splice index of the rows
+//                     that move (splice.hip), the union context into the state's; every
+//                     state write skipped when the tree update reported an input error (all
+//                     or nothing); each workgroup sums the earlier count workgroups'
+//                     figures for its offsets.  Beside them, persistent workgroups re-reduce
+//                     the dirty chunks of the tree (update_hashes).
 //   splice_kernel     (splice.hip, only when rows moved) the untouched rows to the spare
 //
 // then the count block is published to mapped host memory and the host waits ONCE.
@@ -314,42 +314,40 @@ __global__ __launch_bounds__(KDB) void kd_count_kernel(KdArgs p) {
   }
   __syncthreads();
   if (!s_last) return;
-  // ---- the last workgroup: exclusive offsets of the additive figures (toff), the totals
-  // and the guard into the count block: [0] edit rows [2] changed keys [3] their rows
-  // [4] guard [5] moved [6] state rows of the keyset [7] distinct-key change (d_counts[1]:
-  // the context union's)
+  // ---- the last workgroup: the totals and the guard into the count block: [0] edit rows
+  // [2] changed keys [3] their rows [4] guard [5] moved [6] state rows of the keyset [7]
+  // distinct-key change (d_counts[1]: the context union's).  (The per-workgroup offsets are
+  // summed by the write's workgroups themselves, dg_kdw.h: a scan here was ~3 more round
+  // trips on the call's critical path.)
   __shared__ u64 carry[KD_NV];
-  __shared__ u64 s_w[KD_NV][KDB / WAVE];
-  if (tid < KD_NV) carry[tid] = 0;
-  for (u64 t0 = 0; t0 < p.ntiles; t0 += KDB) {
-    const u64 t = t0 + tid;
-    u64 x[KD_NV], inc[KD_NV];
+  {
+    u64 x[KD_NV];
 #pragma unroll
-    for (int q = 0; q < KD_NV; q++) x[q] = t < p.ntiles ? ld_ag(p.part + t * KD_NV + q) : 0;
+    for (int q = 0; q < KD_NV; q++) x[q] = 0;
+    for (u64 t = tid; t < p.ntiles; t += KDB) {  // (every load of a round issued together)
+      u64 y[KD_NV];
+#pragma unroll
+      for (int q = 0; q < KD_NV; q++) y[q] = ld_ag(p.part + t * KD_NV + q);
+#pragma unroll
+      for (int q = 0; q < KD_NV; q++) x[q] = q < KD_NV - 1 ? x[q] + y[q] : (x[q] | y[q]);
+    }
 #pragma unroll
     for (int q = 0; q < KD_NV; q++) {
-      inc[q] = x[q];
       if (q < KD_NV - 1) {
 #pragma unroll
-        for (int d = 1; d < WAVE; d <<= 1) {
-          const u64 y = __shfl_up(inc[q], d, WAVE);
-          if (lane >= d) inc[q] += y;
-        }
+        for (int d = WAVE / 2; d >= 1; d >>= 1) x[q] += __shfl_xor(x[q], d, WAVE);
       } else {
-        inc[q] = (__ballot(x[q] & KD_BIG) ? KD_BIG : 0) | (__ballot(x[q] & KD_MOVED) ? KD_MOVED : 0);
+        x[q] = (__ballot(x[q] & KD_BIG) ? KD_BIG : 0) | (__ballot(x[q] & KD_MOVED) ? KD_MOVED : 0);
       }
-      if (lane == WAVE - 1) s_w[q][w] = inc[q];
+      if (lane == 0) red[q][w] = x[q];
     }
     __syncthreads();
+    if (tid < KD_NV) {
+      u64 c = 0;
 #pragma unroll
-    for (int q = 0; q < KD_NV - 1; q++) {
-      u64 below = carry[q];
-      for (int i = 0; i < w; i++) below += s_w[q][i];
-      if (t < p.ntiles) p.toff[t * KD_NV + q] = below + inc[q] - x[q];
+      for (int i = 0; i < KDB / WAVE; i++) c = tid < KD_NV - 1 ? c + red[tid][i] : (c | red[tid][i]);
+      carry[tid] = c;
     }
-    __syncthreads();
-    if (tid < KD_NV)
-      for (int i = 0; i < KDB / WAVE; i++) carry[tid] = tid < KD_NV - 1 ? carry[tid] + s_w[tid][i] : (carry[tid] | s_w[tid][i]);
     __syncthreads();
   }
   if (tid == 0) {
