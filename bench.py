@@ -287,6 +287,29 @@ def config4_round(eng, torch, dev, rank=0, world=1, keys_per_rank=12_500_000, st
         return float(np.median(out[1:])) * 1e6
 
     join_delta_c_us = c_abi_join_delta()
+
+    def c_abi_diff(reps=7):
+        """dg_merkle_diff as the NIF calls it: the synchronous C-ABI call alone (arguments and
+        the output buffer built beforehand), median of reps."""
+        import ctypes as C
+        from delta_crdt_ex_amd import _abi
+        from delta_crdt_ex_amd.store import _ptr, check
+        out_k = torch.empty(max(int(cap), 1), dtype=torch.int64, device=dev)
+        xa, xb, ya, yb = ta.abi(), tb.abi(), ta.store.abi(), tb.store.abi()
+        n_o, n_t = C.c_uint64(), C.c_uint64()
+        args = (eng.h, C.byref(xa), C.byref(ya), C.byref(xb), C.byref(yb), _ptr(out_k, _abi.P64), int(cap),
+                C.byref(n_o), C.byref(n_t))
+        fn = eng.lib.dg_merkle_diff
+        out = []
+        for _ in range(reps + 1):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            rc = fn(*args)
+            out.append(time.perf_counter() - t0)
+            check(rc)
+        return float(np.median(out[1:])) * 1e6
+
+    diff_c_us = c_abi_diff()
     resident = resident_delta(eng, torch, sa, ca, cb, ta, tb, b)
     partial = {"max_sync_size_200": partial_round(eng, torch, ta, tb, max_sync_size=200),
                "infinite": partial_round(eng, torch, ta, tb, max_sync_size=None, reps=3),
@@ -327,6 +350,10 @@ def config4_round(eng, torch, dev, rank=0, world=1, keys_per_rank=12_500_000, st
         "join_delta_device_us": med["join_delta_ev"] * 1e6,
         "join_delta_roofline": _join_delta_roofline(last, med["join_delta_ev"]),
         "join_delta_c_abi_us": join_delta_c_us,
+        "diff_c_abi_us": diff_c_us,
+        "diff_c_abi_note": "the synchronous dg_merkle_diff C-ABI call alone (count, write and "
+                           "publish kernels, one host wait; arguments built beforehand, as the "
+                           "NIF makes it), median of 7; round_us.diff is the Python call",
         "join_delta_note": "round_us.*: wall time of each synchronous Python call on the engine's "
                            "stream, to its return (the results on the host: its one host wait "
                            "included); join_delta_device_us: HIP events on the engine stream "

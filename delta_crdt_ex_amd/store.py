@@ -706,12 +706,18 @@ class Engine:
         if cap is None:
             cap = a.n_keys + b.n_keys
         cap = int(cap)
-        out = torch.empty(max(cap, 1), dtype=_I64, device=self.device)
+        # the kernels write into an engine-held buffer of `cap` keys (a fresh cap-sized
+        # tensor per call -- 200 MB at config 4 -- cost ~100 us of allocation); the caller
+        # gets its own copy of the n keys.  (The next engine call orders itself after the
+        # copy: _order.)
+        out = getattr(self, "_diff_out", None)
+        if out is None or out.numel() < max(cap, 1):
+            out = self._diff_out = torch.empty(max(cap, 1), dtype=_I64, device=self.device)
         n, tot = C.c_uint64(), C.c_uint64()
         ta, tb, sa, sb = a.abi(), b.abi(), a.store.abi(), b.store.abi()
         check(self.lib.dg_merkle_diff(self.h, C.byref(ta), C.byref(sa), C.byref(tb), C.byref(sb),
                                       _ptr(out, _abi.P64), cap, C.byref(n), C.byref(tot)))
-        keys = out[: n.value]
+        keys = out[: n.value].clone()
         return (keys, int(tot.value)) if with_total else keys
 
     def prepare_merkle_diff(self, a: MerkleTree, b: MerkleTree, out: torch.Tensor, cap: int,
