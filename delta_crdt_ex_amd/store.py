@@ -494,11 +494,23 @@ class Engine:
         """Map.take(value, keys) of a sync delta (causal_crdt.ex:324-335): the rows of `s`
         whose key is in `keys` (ascending unique device int64), in store order."""
         self._order()
-        if out is None:
-            out = Store.empty(max(s.n, 1), self.device)
-        so, ss = out.abi(), s.abi()
         kp, nk = self._keys(keys)
-        check(self.lib.dg_take_keys(self.h, C.byref(ss), kp, nk, C.byref(so)))
+        ss = s.abi()
+        if out is None:
+            # a sync delta holds a few rows per key: room for four (an output of the whole
+            # store's size -- 450 MB at config 4 -- cost more than the call); more rows than
+            # that: the call reports DG_E_CAPACITY and runs again into a store-sized output
+            out = Store.empty(min(max(s.n, 1), max(4 * int(nk), 256)), self.device)
+            so = out.abi()
+            rc = self.lib.dg_take_keys(self.h, C.byref(ss), kp, nk, C.byref(so))
+            if rc == _abi.DG_E_CAPACITY and out.cap < s.n:
+                out = Store.empty(max(s.n, 1), self.device)
+                so = out.abi()
+                rc = self.lib.dg_take_keys(self.h, C.byref(ss), kp, nk, C.byref(so))
+            check(rc)
+        else:
+            so = out.abi()
+            check(self.lib.dg_take_keys(self.h, C.byref(ss), kp, nk, C.byref(so)))
         out.n = int(so.n)
         return out
 

@@ -517,3 +517,22 @@ def test_diff_against_a_store_the_index_does_not_describe(engine):
     assert got == outcome()
     ta.starts, ta.store = kept, sa
     assert np.array_equal(u64(engine.merkle_diff(ta, tb)), R.store_diff(a["rows"], b["rows"]))
+
+
+@pytest.mark.parametrize("rows_per_key", [1, 9])
+def test_take_keys_output_sizing(engine, rows_per_key):
+    """Map.take(value, keys): the Python binding sizes the output for four rows per key and
+    runs again into a store-sized output when the keys hold more (DG_E_CAPACITY inside)."""
+    rng = np.random.default_rng(rows_per_key)
+    kk = np.unique(rng.integers(0, 1 << 63, 400, dtype=np.uint64))
+    key = np.repeat(kk, rows_per_key)
+    n = len(key)
+    rows = (key, np.arange(n, dtype=np.uint64), np.zeros(n, np.int64), np.zeros(n, np.uint32),
+            np.arange(1, n + 1, dtype=np.uint64))
+    s = Store.from_numpy(*rows, device=DEV)
+    want_keys = np.sort(rng.choice(kk, 100, replace=False))
+    got = engine.take_keys(s, torch.from_numpy(want_keys.view(np.int64)).to(DEV))
+    sel = np.isin(key, want_keys)
+    assert got.n == int(sel.sum())
+    for c_got, c_all in zip(got.to_numpy(), rows):
+        assert np.array_equal(c_got, c_all[sel])
