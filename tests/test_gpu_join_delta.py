@@ -692,3 +692,21 @@ def test_kd_changed_keys_past_their_capacity(engine):
     _assert_unchanged(st, sc, tree, snap)
     apply(engine, a, d, want, depth=12)  # and the engine goes on
 
+
+
+@pytest.mark.parametrize("depth,moves", [(24, False), (24, True), (11, True)])
+def test_kd_deep_and_one_chunk_trees(engine, depth, moves):
+    """The one-wait path's tree re-reduction by persistent workgroups: a depth-24 tree (8192
+    chunks: sixteen per workgroup) and a one-chunk tree, in place and with moved rows;
+    the tree equals a fresh build (apply checks nodes, counts, keys and the chunk index)."""
+    rng = np.random.default_rng(depth + moves)
+    if moves:
+        a, b = W.random_pair(rng, 60_000, n_nodes=5, ts_range=1 << 10)
+        kb = np.unique(np.concatenate([a["rows"][0], b["rows"][0]]))
+        keys = np.sort(rng.choice(kb, 3_000, replace=False))
+    else:
+        a, b = W.config4_shard(1, 8, keys_per_rank=200_000, diff_frac=0.02)
+        keys = R.store_diff(a["rows"], b["rows"])
+    assert len(keys) > 512  # (not the small path)
+    _, _, swapped, _ = apply(engine, a, W.sync_delta(b, keys), keys, depth=depth)
+    assert swapped == moves
