@@ -569,11 +569,11 @@ __device__ __forceinline__ void kd_chunks(MT t, u32* dirty, u32* ctr, u64* hand,
 }
 
 // dg_join_delta's write (dg_kdw.h, workgroups [0, nw): dispatched first, they start at once)
-// and the dirty chunks' re-reduction (the rest, one per chunk) in ONE launch: both read only
-// what kd_count_kernel wrote, so the write's ~15 us run under the re-reduction's instead of
-// after it.
-#ifndef DG_KDF_WAVES  // waves per SIMD the fused launch is compiled for: 6 = 73 VGPRs, three workgroups per CU, no spills (8: spills, 4: two per CU; 144-149 us vs 152 us per config-4 join_delta at 4 and 8, A/B)
-#define DG_KDF_WAVES 6
+// and the dirty chunks' re-reduction (the rest: kd_chunks' persistent workgroups) in ONE
+// launch: both read only what kd_count_kernel wrote, so the write's ~15 us run under the
+// re-reduction's instead of after it.
+#ifndef DG_KDF_WAVES  // waves per SIMD the launch is compiled for: 6 = 73 VGPRs, three
+#define DG_KDF_WAVES 6  // workgroups per CU, no spills (8 spills, 4 is two per CU: A/B slower)
 #endif
 __global__ __launch_bounds__(UPB, DG_KDF_WAVES) void kd_finish_kernel(KdArgs p, u32 nw, MT t, const u32* dirty,
                                                          u32* ctr, u64* hand, const i64* cdelta) {
