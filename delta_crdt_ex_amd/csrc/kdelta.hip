@@ -156,6 +156,21 @@ __device__ __forceinline__ void tree_put(const KdArgs& p, bool valid, u64 x, boo
 // workgroup's range the same way, by 64-ary wave searches, measured slower: 52 against
 // 45 us at config 4 -- their 256 scattered lines per bound outweigh what each key saves.)
 constexpr u32 KDL = 2048;  // delta keys staged per workgroup (more: searched in memory)
+#ifdef DG_STAMPS
+// Diagnostic build only (DG_STAMPS=1): per-workgroup timestamps (s_memrealtime, 100 MHz) of
+// the count kernel, read back with dg_debug_kd_stamps (tools/kd_stamps.py).  No barriers
+// added: thread `th` stamps slot k when it passes that point.
+__device__ u64 g_kd_stamps[4096 * 8];
+#define KDSTAMP(th, k)                                                        \
+  do {                                                                        \
+    if (threadIdx.x == (th) && blk < 4096)                                    \
+      g_kd_stamps[blk * 8 + (k)] = __builtin_amdgcn_s_memrealtime();          \
+  } while (0)
+#else
+#define KDSTAMP(th, k) \
+  do {                 \
+  } while (0)
+#endif
 __global__ __launch_bounds__(KDB) void kd_count_kernel(KdArgs p) {
   __shared__ u64 tabS[KVT], tabD[KVT];
   __shared__ u64 s_dk[KDL];
@@ -175,10 +190,12 @@ __global__ __launch_bounds__(KDB) void kd_count_kernel(KdArgs p) {
   const u64 u = blk * KDB + tid;
   const u64 u0 = blk * KDB, u1 = min<u64>(u0 + KDB, p.nk);
   const bool dvv = p.cd.kind == 0;
+  KDSTAMP(2, 0);
   if (tid < 2) {  // the workgroup's delta range [lo, hi): its keys' rows (two searches)
     const u64 x = tid ? p.keys[u1 - 1] + 1 : p.keys[u0];  // (key + 1: past the last key's run)
     s_rng[tid] = tid && x == 0 ? p.d.n : interp_lower_bound(p.d.key, 0, p.d.n, x);  // (2^64 - 1)
   }
+  KDSTAMP(0, 1);
   for (u32 x = tid; x < KVT; x += KDB) {
     tabS[x] = 0;
     tabD[x] = 0;
@@ -202,7 +219,9 @@ __global__ __launch_bounds__(KDB) void kd_count_kernel(KdArgs p) {
     k = p.keys[u];
     key_run(p.a.key, p.a.n, k, a_lo, na);  // the state: an interpolation search
   }
+  KDSTAMP(2, 2);
   __syncthreads();  // (the tables, the staged delta keys)
+  KDSTAMP(2, 3);
   if (u < p.nk) {
     if (dl) {  // the delta run from LDS
       u32 lo = 0, hi = (u32)(dhi - dlo);
@@ -272,6 +291,7 @@ __global__ __launch_bounds__(KDB) void kd_count_kernel(KdArgs p) {
     p.amask[u] = am;
     p.dmask[u] = dm;
   }
+  KDSTAMP(2, 4);
   if (u < p.nk) {  // (a key over KD_RUN: no change recorded, so the undo skips it too)
     p.runs[u] = big ? 0ull : (na | ((u64)nd << 16) | ((u64)ne << 32) | (chg ? 1ull << 48 : 0ull));
     p.dh[u] = big ? 0ull : dh;
@@ -279,6 +299,7 @@ __global__ __launch_bounds__(KDB) void kd_count_kernel(KdArgs p) {
   // the tree's put/delete right away (all or nothing: a guard or an input error found
   // later makes the host undo it, merkle.hip kd_tree_kernel with the opposite sign)
   if (p.has_tree) tree_put(p, u < p.nk && !big, k, chg, dh, (int)ne - (int)na);
+  KDSTAMP(2, 5);
   v[0] = na;
   v[1] = ne;
   v[2] = chg ? 1 : 0;
@@ -313,6 +334,7 @@ __global__ __launch_bounds__(KDB) void kd_count_kernel(KdArgs p) {
     if (s_last) __hip_atomic_store(p.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
+  KDSTAMP(0, 6);
   if (!s_last) return;
   // ---- the last workgroup: the totals and the guard into the count block: [0] edit rows
   // [2] changed keys [3] their rows [4] guard [5] moved [6] state rows of the keyset [7]
@@ -363,9 +385,17 @@ __global__ __launch_bounds__(KDB) void kd_count_kernel(KdArgs p) {
     p.d_counts[6] = n_ak;
     p.d_counts[7] = carry[5];
   }
+  KDSTAMP(0, 7);
 }
 
 }  // namespace
+
+#ifdef DG_STAMPS
+extern "C" int dg_debug_kd_stamps(unsigned long long* host, size_t n) {
+  if (n > 4096 * 8) n = 4096 * 8;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_kd_stamps), n * 8) == hipSuccess ? 0 : -3;
+}
+#endif
 
 hipError_t launch_kd_join(const KdArgs& p0, hipStream_t st) {
   KdArgs p = p0;
