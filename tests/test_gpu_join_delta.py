@@ -710,3 +710,98 @@ def test_kd_deep_and_one_chunk_trees(engine, depth, moves):
     assert len(keys) > 512  # (not the small path)
     _, _, swapped, _ = apply(engine, a, W.sync_delta(b, keys), keys, depth=depth)
     assert swapped == moves
+
+
+def _runs_state(rng, n, big, run):
+    """n keys with one row each, key `big` with `run` rows (distinct dots of node 0)."""
+    keys = np.unique(rng.integers(0, 1 << 63, n + 10, dtype=np.uint64))[:n]
+    rk = np.concatenate([keys, np.full(run - 1, keys[big], np.uint64)])
+    node = np.zeros(len(rk), np.uint32)
+    cnt = np.arange(1, len(rk) + 1, dtype=np.uint64)
+    val = np.arange(len(rk), dtype=np.uint64)
+    order = np.lexsort((cnt, node, np.zeros(len(rk)), val, rk))
+    rows = (rk[order], val[order], np.full(len(rk), 3, np.int64), node[order], cnt[order])
+    return keys, {"rows": rows, "ctx": (R.VV, np.array([0], np.uint32), np.array([len(rk)], np.uint64))}
+
+
+@pytest.mark.parametrize("run", [64, 65])
+def test_kd_key_run_at_the_limit(engine, run):
+    """A state key with exactly KD_RUN (64) rows stays on the per-key path; 65 rows fall
+    back (the splice path); both equal the oracle and a fresh tree, the delta replacing
+    every row of the key (a covering context) and adding one."""
+    rng = np.random.default_rng(run)
+    keys, a = _runs_state(rng, 3000, 100, run)
+    big = keys[100]
+    dk = np.sort(np.array([big, keys[5], keys[2000]], np.uint64))
+    d = {"rows": (dk, np.array([7, 8, 9], np.uint64), np.full(3, 9, np.int64), np.full(3, 1, np.uint32),
+                  np.array([1, 2, 3], np.uint64)),
+         "ctx": (R.VV, np.array([0, 1], np.uint32), np.array([len(a["rows"][0]), 3], np.uint64))}
+    _, _, swapped, _ = apply(engine, a, d, dk, depth=9)
+    assert swapped  # (the big key's run shrinks to one row)
+
+
+def test_kd_node_ids_past_the_lds_tables(engine):
+    """Contexts naming node ids >= 1024 (past the count kernel's LDS VV tables): coverage
+    through the searched context, on a delta of more than 512 keys."""
+    rng = np.random.default_rng(31)
+    n = 4000
+    keys = np.unique(rng.integers(0, 1 << 63, n + 10, dtype=np.uint64))[:n]
+    nodes = np.array([3, 1500, 70000], np.uint32)
+    node = nodes[rng.integers(0, 3, n)]
+    cnt = np.arange(1, n + 1, dtype=np.uint64)
+    a = {"rows": (keys, np.arange(n, dtype=np.uint64), np.full(n, 5, np.int64), node, cnt),
+         "ctx": (R.VV, nodes, np.array([n, n, n], np.uint64))}
+    sel = np.sort(rng.choice(n, 900, replace=False))
+    dk = keys[sel]
+    dnode = np.full(len(dk), 2000, np.uint32)
+    dcnt = np.arange(1, len(dk) + 1, dtype=np.uint64)
+    d = {"rows": (dk, np.arange(len(dk), dtype=np.uint64) + 10 ** 6, np.full(len(dk), 9, np.int64), dnode, dcnt),
+         # covers nodes 3 and 70000 up to half of the counters: those rows go, the others stay
+         "ctx": (R.VV, np.array([3, 2000, 70000], np.uint32), np.array([n // 2, len(dk), n // 2], np.uint64))}
+    apply(engine, a, d, dk, depth=10)
+
+
+def test_kd_removal_only_keys(engine):
+    """Keyset keys the delta has no rows for (a remove synced: its context covers the
+    state's dots), beside keys it updates -- more than 512 keys, rows move."""
+    rng = np.random.default_rng(32)
+    a, b = W.random_pair(rng, 20_000, n_nodes=4, ts_range=1 << 10)
+    kb = np.unique(b["rows"][0])
+    upd = np.sort(rng.choice(kb, 600, replace=False))
+    gone = np.setdiff1d(np.unique(a["rows"][0]), kb)[:400]  # keys B has none of
+    keys = np.union1d(upd, gone)
+    d = W.sync_delta(b, keys)  # (rows only for `upd`; B's context covers A's dots or not)
+    apply(engine, a, d, keys, depth=11)
+
+
+@pytest.mark.parametrize("moves", [False, True])
+def test_kd_sharded_tree(engine, moves):
+    """A shard tree (shard_bits 3) over one key-hash shard, through the per-key path with
+    and without moved rows: the tree (and its chunk index) equals a fresh shard build."""
+    from delta_crdt_ex_amd.store import MerkleTree
+    rng = np.random.default_rng(33 + moves)
+    if moves:
+        a, b = W.random_pair(rng, 80_000, n_nodes=5, ts_range=1 << 10)
+    else:
+        a, b = W.config4_shard(0, 1, keys_per_rank=400_000, diff_frac=0.02)
+    sh = lambda k: (np.asarray(k, np.uint64) >> np.uint64(61)) == 2  # noqa: E731  (shard 2 of 8)
+    cut = lambda rep: {**rep, "rows": tuple(c[sh(rep["rows"][0])] for c in rep["rows"])}  # noqa: E731
+    a, b = cut(a), cut(b)
+    kb = np.unique(np.concatenate([a["rows"][0], b["rows"][0]]))
+    keys = np.sort(rng.choice(kb, min(2000, len(kb)), replace=False)) if moves else R.store_diff(a["rows"], b["rows"])
+    assert len(keys) > 512
+    d = W.sync_delta(b, keys)
+    st, sc = state_of(a, extra_ctx=len(d["ctx"][1]))
+    sd, cd = up(d)
+    spare = Store.empty(st.n + sd.n, DEV)
+    tree = engine.merkle_build(st, 14, MerkleTree.empty(14, DEV, 3, 2), 3, 2)
+    changed, swapped = engine.join_delta(st, sc, sd, cd, kdev(keys), spare, tree)
+    wr, wc = R.join2(a["rows"], a["ctx"], d["rows"], d["ctx"], keys=keys)
+    rows_eq(st, wr)
+    ctx_eq(sc, wc)
+    assert np.array_equal(u64(changed), R.changed_keys(a["rows"], wr, keys))
+    fresh = engine.merkle_build(st, 14, MerkleTree.empty(14, DEV, 3, 2), 3, 2)
+    assert np.array_equal(tree.nodes.cpu().numpy(), fresh.nodes.cpu().numpy())
+    assert np.array_equal(tree.bucket_counts(), fresh.bucket_counts())
+    assert np.array_equal(tree.starts.cpu().numpy(), fresh.starts.cpu().numpy())
+    assert swapped == moves
