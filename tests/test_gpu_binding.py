@@ -326,3 +326,44 @@ def test_a_map_keyed_by_the_atom_all():
     assert B.read(s, a) == B.read(s, [a]) == B.read_cpu(s, a) == {a: tg(1)}
     assert B.read(s) == B.read_cpu(s) == {a: tg(1), tg("x"): tg(2)}
     assert B.read(s, [tg("x")]) == {tg("x"): tg(2)}
+
+
+def test_large_batches_and_sync_deltas_match_the_reference():
+    """Batches and sync deltas past the one-workgroup path's 512 keys (the NIF's
+    mutate_batch and join_delta then take dg_mutate_batch_async + dg_join_delta_out's
+    one-wait keyed path): 1,500 queued mutations flushed as one batch, and syncs moving
+    hundreds of keys both ways (max_sync_size :infinite), equal to the same history on CPU
+    replicas -- reads, raw states, on_diffs streams."""
+    import random
+    rnd = random.Random(7)
+    steps = []
+    for i in range(1500):
+        k = rnd.randrange(900)
+        if rnd.random() < 0.8:
+            steps.append(("add", 0, k, rnd.choice([i, str(i), None, (i, 1)])))
+        else:
+            steps.append(("remove", 0, k, None))
+    steps.append(("sync", 0, 0, None))
+    for i in range(700):
+        steps.append(("add", 1, 300 + i, -i))
+    steps.append(("sync", 1, 0, None))
+    steps.append(("sync", 0, 0, None))
+
+    def run(gpu):
+        c, r1, r2 = _pair(gpu, max_sync_size="infinite")
+        rs = (r1, r2)
+        for op, who, k, v in steps:
+            if op == "sync":
+                rs[who].sync_to(rs[1 - who])
+            else:
+                rs[who].mutate(op, k, *(() if op == "remove" else (v,)))
+        return rs
+
+    g, p = run(True), run(False)
+    for a, b in zip(g, p):
+        assert B.read(a.crdt_state) == B.read_cpu(b.crdt_state)
+        assert T.canon(T.AW(a.crdt_state.dots, a.crdt_state.value)) == \
+            T.canon(T.AW(b.crdt_state.dots, b.crdt_state.value))
+        assert [sorted(map(repr, x)) for x in a.received] == [sorted(map(repr, x)) for x in b.received]
+        assert a.crdt_state.gpu is not None
+    assert g[0].read() == g[1].read() and len(g[0].read()) > 512
