@@ -1043,7 +1043,6 @@ __global__ __launch_bounds__(DB, DIFF_OCC * DB / 256) void merkle_diff_count_ker
   }
   DSTAMP(2);
   const u64 a0 = s_bnd[0], c0 = s_bnd[1];  // (the barrier above came after the searches)
-  const u64 base = a0 + c0;
   if (a0 + TA > p.sa.n || c0 + TB > p.sb.n) {
     // (uniform) the trees count more rows here than the stores hold from the subtree's first
     // row: a store the tree does not describe.  No row is read past it and no key written;
@@ -1074,11 +1073,26 @@ __global__ __launch_bounds__(DB, DIFF_OCC * DB / 256) void merkle_diff_count_ker
     if (tid == 0) s_dp[ND] = R;
     __syncthreads();
     DSTAMP(3);
-    // hash the staged rows, all at once: row q belongs to the last differing bucket whose
-    // first staged row is <= q (a search of the LDS list), A's rows first.  A thread's rows
-    // go in batches of RB: every column load of the batch is issued before any row is
-    // hashed (one round trip per batch, not one per row), and the node term hashes come
-    // from LDS (staged above), not from a dependent global load
+    // one lane per differing bucket writes, for each of the bucket's staged rows, the row's
+    // place in its store into s_k (ROW_B: a row of B, ROW_FIRST: the first of its store's
+    // rows in the bucket); the hashing step below reads that one word per row and
+    // overwrites it with the row's key.  (Each row used to find its bucket by a binary
+    // search of the LDS list: ~9 dependent LDS reads per row before its loads went out.)
+    constexpr u64 ROW_B = 1ull << 63, ROW_FIRST = 1ull << 62;
+    for (u32 e = tid; e < ND; e += DB) {
+      const u32 sp = s_dp[e], xy = s_dn[e], x = xy >> 16, y = xy & 0xFFFFu;
+      const u64 fa = a0 + s_da[e], fb = c0 + s_db[e];
+      for (u32 r = 0; r < x; r++) s_k[sp + r] = (fa + r) | (r == 0 ? ROW_FIRST : 0ull);
+      for (u32 r = 0; r < y; r++) s_k[sp + x + r] = (fb + r) | ROW_B | (r == 0 ? ROW_FIRST : 0ull);
+    }
+    __syncthreads();
+    // hash the staged rows, all at once.  A thread's rows go in batches of RB: every column
+    // load of the batch is issued before any row is hashed (one round trip per batch, not
+    // one per row), and the node term hashes come from LDS (staged above), not from a
+    // dependent global load.  A lane past the staged rows loads row 0 of a non-empty store
+    // (its s_k entry may already hold another thread's key): no load sits under a
+    // divergent branch, so all of them go out before any wait.
+    const bool spare_b = p.sa.n == 0;
     constexpr int RB = 4;
     for (u32 u0 = 0; u0 < (RCAP + DB - 1) / DB; u0 += RB) {
       if (u0 * DB >= R) break;  // uniform
@@ -1089,23 +1103,14 @@ __global__ __launch_bounds__(DB, DIFF_OCC * DB / 256) void merkle_diff_count_ker
       bool side0[RB];
 #pragma unroll
       for (int j = 0; j < RB; j++) {
-        // (every lane loads: a lane past the staged rows reads the last one again, so
-        // no load sits under a divergent branch and all of them go out before any wait)
-        const u32 q = min((u0 + j) * DB + tid, R - 1);
+        const u32 q = (u0 + j) * DB + tid;
         {
-          u32 lo = 0, hi = ND;  // s_dp[lo] <= q < s_dp[hi]
-          while (hi - lo > 1) {
-            const u32 m = (lo + hi) >> 1;
-            if (s_dp[m] <= q)
-              lo = m;
-            else
-              hi = m;
-          }
-          const u32 r = q - s_dp[lo], na = s_dn[lo] >> 16;
-          fromb[j] = r >= na;
-          side0[j] = r == 0 || r == na;
+          const u64 e = s_k[min(q, R - 1)];
+          const bool in = q < R;
+          fromb[j] = in ? (e & ROW_B) != 0 : spare_b;
+          side0[j] = (e & ROW_FIRST) != 0;
           const Rows& S = fromb[j] ? p.sb : p.sa;
-          const u64 i = fromb[j] ? c0 + s_db[lo] + (r - na) : a0 + s_da[lo] + r;
+          const u64 i = in ? e & (ROW_FIRST - 1) : 0ull;
 #if DG_DIFF_EXP == 2  // diagnostic build only (timing, wrong keys): no row loads
           key[j] = i;
           val[j] = i ^ 5;
@@ -1187,7 +1192,7 @@ __global__ __launch_bounds__(DB, DIFF_OCC * DB / 256) void merkle_diff_count_ker
           }
           if (!(pa && pb) || ha != hb) {
             if (write) {
-              p.keys[base + o + k2] = k;
+              p.keys[s_bnd[0] + s_bnd[1] + o + k2] = k;
             } else {
               kr0 = k2 == 0 ? k : kr0;
               kr1 = k2 == 1 ? k : kr1;
@@ -1211,7 +1216,9 @@ __global__ __launch_bounds__(DB, DIFF_OCC * DB / 256) void merkle_diff_count_ker
     if (c > KR) {
       merge(true, o);
     } else {
-      u64* dst = p.keys + base + o;
+      // (the subtree's offset re-read from LDS: kept in registers through the kernel, it
+      // spilled to scratch, and its reload waited for every store in flight)
+      u64* dst = p.keys + (s_bnd[0] + s_bnd[1]) + o;
       if (c > 0) dst[0] = kr0;
       if (c > 1) dst[1] = kr1;
       if (c > 2) dst[2] = kr2;
@@ -1245,7 +1252,7 @@ __global__ __launch_bounds__(DB, DIFF_OCC * DB / 256) void merkle_diff_count_ker
                                            nullptr, nullptr, c0 + rb, c0 + rb + y, nullptr, 0, 0);
         else
           k2 += merge_bucket<false, true>(p.sa, p.ta.th, a0 + ra, a0 + ra + x, p.sb, p.tb.th,
-                                          nullptr, nullptr, c0 + rb, c0 + rb + y, p.keys + base,
+                                          nullptr, nullptr, c0 + rb, c0 + rb + y, p.keys + a0 + c0,
                                           o + k2, ~0ull);
       }
       ra += x;

@@ -15,7 +15,7 @@ PY
 done; done
 unset DG_LIB_PATH DG_LIB_ANY_DIGEST
 cd /tmp && export TMPDIR=/tmp
-for v in intree; do
+for v in base intree; do
   if [ $v = intree ]; then unset DG_LIB_PATH DG_LIB_ANY_DIGEST; else export DG_LIB_PATH=$R/delta_crdt_ex_amd/ab/libdeltagpu_$v.so DG_LIB_ANY_DIGEST=1; fi
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/t/mk_$v -o mk -- python3 $R/tools/prof_merkle.py > $R/gpurun_out/t/mk_$v.log 2>&1 || { echo MK_FAIL; tail -5 $R/gpurun_out/t/mk_$v.log; exit 1; }
   echo "== $v"; python3 $R/tools/kernel_timeline.py $R/gpurun_out/t/mk_$v 6 | tail -7
