@@ -340,6 +340,21 @@ def test_dense_diff(engine, depth, n_keys):
     assert np.array_equal(u64(engine.merkle_diff(ta, te)), np.unique(a["rows"][0]))
 
 
+@pytest.mark.parametrize("n_keys,depth", [(300, 8), (1500, 9), (1, 4)])
+def test_diff_against_an_empty_store_in_lds(engine, n_keys, depth):
+    """One store empty, few enough rows that the subtree's rows are staged in LDS: every
+    staged row comes from the other store, and the lanes past the staged rows load a row
+    of the non-empty store (both orders)."""
+    a, _ = W.merkle_pair(n_keys=n_keys, diff_frac=0.0, seed=n_keys)
+    sa, _ = up(a)
+    e = Store.empty(1, DEV)
+    ta, te = engine.merkle_build(sa, depth), engine.merkle_build(e, depth)
+    want = np.unique(a["rows"][0])
+    assert np.array_equal(u64(engine.merkle_diff(ta, te)), want)
+    assert np.array_equal(u64(engine.merkle_diff(te, ta)), want)
+    assert u64(engine.merkle_diff(te, te)).size == 0
+
+
 def test_bucket_over_65535_rows_is_refused(engine):
     k = np.zeros(70000, np.uint64)  # one key, 70,000 entries: one bucket
     rows = (k, np.arange(70000, dtype=np.uint64), np.zeros(70000, np.int64),
