@@ -259,10 +259,13 @@ class Universe:
         old = np.array([self._val_ids[i] for i in idx], dtype=np.uint64)
         new_ids = [rlo + (j + 1) * step for j in range(n)]
         new = np.array(new_ids, dtype=np.uint64)
+        # every old entry out before any new one goes in: a new id can equal an old id not
+        # yet moved (evenly spaced ids meet earlier midpoints), and moving them one by one
+        # then overwrote that value's term and lost the moved one
+        terms = [self._val_term.pop(self._val_ids[i]) for i in idx]
         for j, i in enumerate(idx):
-            t = self._val_term.pop(self._val_ids[i])
             self._val_ids[i] = new_ids[j]
-            self._val_term[new_ids[j]] = t
+            self._val_term[new_ids[j]] = terms[j]
             self._val_id[self._val_keys[i]] = new_ids[j]
         self.val_epoch += 1
         self.terms_version += 1

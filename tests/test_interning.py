@@ -113,6 +113,36 @@ def test_random_inserts_stay_ordered_across_relabels():
     assert all(U.value(v) == i for v, i in zip(ts, ids))
 
 
+def test_repeated_squeezes_keep_every_term():
+    """Values squeezed into one gap again and again force relabel after relabel; a new
+    evenly spaced id can equal an old id not yet moved (earlier midpoints), which the
+    relabel must not mistake for the moved value (it used to lose terms: KeyError or a
+    wrong term, found by the 1,500-op binding test)."""
+    for seed in range(12):
+        rng = random.Random(seed)
+        U = Universe()
+        vals = []
+        for _ in range(6):
+            a = rng.uniform(-1e6, 1e6)
+            b = a + rng.uniform(1, 1000)
+            seq = [a, b]
+            for _ in range(rng.randrange(60, 140)):
+                m = (a + b) / 2
+                seq.append(m)
+                if rng.random() < 0.5:
+                    a = m
+                else:
+                    b = m
+            seq += [rng.uniform(-1e6, 1e6) for _ in range(30)]
+            seq += ["s%d" % rng.randrange(10**6) for _ in range(20)]
+            for t in seq:
+                U.value(t)
+                vals.append(t)
+        assert all(U.value_term(U.value(t)) == t for t in vals)
+        ids, ts = U.value_ids()
+        assert ids == sorted(set(ids)) and ts == E.term_sorted(ts)
+
+
 def test_nodes_are_dense():
     U = Universe()
     assert [U.node(x) for x in (999_999_937, Atom("n"), 5, 999_999_937)] == [0, 1, 2, 0]
