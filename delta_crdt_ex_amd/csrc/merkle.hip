@@ -1284,25 +1284,52 @@ __global__ __launch_bounds__(DSB) void tile_scan_kernel(const u64* cnt, u64* off
 // group, no scan launch) plus the counts of the earlier tiles of its own group -- at
 // most 255 + ntiles / 256 words, loaded by the 64 lanes at once -- then the lanes copy
 // the tile's keys from scratch to the output below cap.  The last tile's wave writes
-// the total.
+// the total.  Two round trips: every word the offset and the copy's source need is
+// loaded at once (unconditional loads at clamped indices, the unused ones selected away),
+// then the keys, all before any store.  (Loads in loops and under branches made it a
+// chain of up to nine: count, group sums, the group's counts four times, bounds, keys
+// twice.)
 __global__ __launch_bounds__(WAVE) void merkle_diff_write_kernel(DiffArgs p) {
   // (subtree `tile`'s keys sit at bnd[tile] + bnd[ntiles + 1 + tile] in scratch)
   const int lane = threadIdx.x;
-  const u64 tile = blockIdx.x, grp = tile / DB;
+  const u64 tile = blockIdx.x, grp = tile / DB, g0 = grp * DB;
   if (tile == 0)  // the previous call's group sums: zero for the next call
     for (u64 x = lane; x < p.nzero; x += WAVE) p.bzero[x] = 0;
-  const u64 n = p.cnt[tile];
   const bool last = tile + 1 == p.ntiles;
-  if (n == 0 && !last) return;  // uniform
-  u64 before = 0;
-  for (u64 x = lane; x < grp; x += WAVE) before += p.bsum[x];
-  for (u64 x = grp * DB + lane; x < tile; x += WAVE) before += p.cnt[x];
+  constexpr int CQ = DB / WAVE;
+  const u64 n = p.cnt[tile];
+  const u64 sa = p.bnd[tile], sb = p.bnd[p.ntiles + 1 + tile];
+  u64 c[CQ];
+#pragma unroll
+  for (int q = 0; q < CQ; q++) {
+    const u64 x = g0 + (u64)lane + (u64)q * WAVE;
+    c[q] = p.cnt[x < tile ? x : tile];
+  }
+  const u64 b0 = p.bsum[(u64)lane < grp ? (u64)lane : 0ull];
+  u64 before = (u64)lane < grp ? b0 : 0ull;
+#pragma unroll
+  for (int q = 0; q < CQ; q++) before += g0 + (u64)lane + (u64)q * WAVE < tile ? c[q] : 0ull;
+  for (u64 x = lane + WAVE; x < grp; x += WAVE) before += p.bsum[x];  // (more than 64 groups)
 #pragma unroll
   for (int d = WAVE / 2; d >= 1; d >>= 1) before += __shfl_xor(before, d, WAVE);
   if (last && lane == 0) *p.d_count = before + n;
-  if (n == DIFF_MISMATCH || before >= p.cap) return;  // (no keys: the count kernel's marker)
-  const u64 src = p.bnd[tile] + p.bnd[p.ntiles + 1 + tile];
-  for (u64 x = lane; x < n && before + x < p.cap; x += WAVE) p.out[before + x] = p.keys[src + x];
+  // (no keys: an empty subtree, the count kernel's marker, a marker upstream, past cap)
+  if (n == 0 || n == DIFF_MISMATCH || before >= DIFF_MISMATCH || before >= p.cap) return;
+  const u64 src = sa + sb, m = n < p.cap - before ? n : p.cap - before;
+  constexpr int KQ = 4;
+  for (u64 x0 = 0; x0 < m; x0 += KQ * WAVE) {
+    u64 k[KQ];
+#pragma unroll
+    for (int q = 0; q < KQ; q++) {
+      const u64 x = x0 + (u64)q * WAVE + lane;
+      k[q] = p.keys[src + (x < m ? x : m - 1)];
+    }
+#pragma unroll
+    for (int q = 0; q < KQ; q++) {
+      const u64 x = x0 + (u64)q * WAVE + lane;
+      if (x < m) p.out[before + x] = k[q];
+    }
+  }
 }
 
 // ---------------------------------------------------------------- partial diff
