@@ -26,6 +26,9 @@ __global__ __launch_bounds__(TB) void take_keys_kernel(Rows s, const u64* keys, 
   __shared__ u32 s_off[TK + 1];
   __shared__ u32 s_wave[TB / WAVE + 1];
   __shared__ u64 s_b[2];
+  constexpr u32 MAPCAP = 4 * TK;  // output rows of a tile mapped to their key in LDS
+  __shared__ unsigned short s_map[MAPCAP];
+  static_assert(TK <= 65536, "key index in 16 bits");
   if (threadIdx.x == 0) {
     const u32 t = atomicAdd(scan.ticket, 1u);
     if ((u64)t == ntiles - 1) atomicExch(scan.ticket, 0u);
@@ -48,8 +51,22 @@ __global__ __launch_bounds__(TB) void take_keys_kernel(Rows s, const u64* keys, 
     } else if (i < nk) {
       const u64 key = keys[k0 + i];
       const u64 a = interp_lower_bound(s.key, 0, s.n, key);  // first row with key >= `key`
-      u64 e = a;  // a key's rows are few: walk them
-      while (e < s.n && s.key[e] == key) e++;
+      // a key's rows are few: walk them four a round trip, every load issued together at a
+      // clamped index (one dependent load per row was two round trips for a one-row key)
+      u64 e = a;
+      while (e < s.n) {
+        u64 kk[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const u64 v = s.key[e + j < s.n ? e + j : a];
+          kk[j] = e + j < s.n ? v : ~key;
+        }
+        u32 c = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) c += (c == (u32)j && kk[j] == key) ? 1u : 0u;
+        e += c;
+        if (c < 4) break;
+      }
       lo[q] = a;
       len[q] = (u32)(e - a);
     }
@@ -64,6 +81,10 @@ __global__ __launch_bounds__(TB) void take_keys_kernel(Rows s, const u64* keys, 
       s_lo[i] = lo[q];
       s_off[i] = off;
     }
+    // (each key's output rows point at it: one LDS read per output row below instead of
+    // a search of s_off, when the tile's rows fit the map)
+    if (total <= MAPCAP)
+      for (u32 r = 0; r < len[q]; r++) s_map[off + r] = (unsigned short)i;
     off += len[q];
   }
   if (threadIdx.x == 0) s_off[TK] = total;
@@ -92,14 +113,19 @@ __global__ __launch_bounds__(TB) void take_keys_kernel(Rows s, const u64* keys, 
       key_off[k0 + i] = base + s_off[i];
     }
   }
+  const bool mapped = total <= MAPCAP;  // (uniform)
   for (u32 o = threadIdx.x; o < total; o += TB) {
     u32 a = 0, b = TK;  // the key whose range holds o: last i with s_off[i] <= o
-    while (b - a > 1) {
-      const u32 m = (a + b) >> 1;
-      if (s_off[m] <= o)
-        a = m;
-      else
-        b = m;
+    if (mapped) {
+      a = s_map[o];
+    } else {
+      while (b - a > 1) {
+        const u32 m = (a + b) >> 1;
+        if (s_off[m] <= o)
+          a = m;
+        else
+          b = m;
+      }
     }
     const u64 r = s_lo[a] + (o - s_off[a]), g = base + o;
     if (g < cap) {

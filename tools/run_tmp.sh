@@ -1,7 +1,7 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT; cd $R
 mkdir -p gpurun_out/t
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_merkle.py tests/test_gpu_binding.py tests/test_gpu_join_delta.py -m gpu > gpurun_out/t/tests.log 2>&1 || { echo TEST_FAIL; tail -30 gpurun_out/t/tests.log; exit 1; }
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_merkle.py tests/test_gpu_binding.py tests/test_gpu_join_delta.py tests/test_gpu_configs.py tests/test_gpu_splice.py -m gpu > gpurun_out/t/tests.log 2>&1 || { echo TEST_FAIL; tail -30 gpurun_out/t/tests.log; exit 1; }
 tail -1 gpurun_out/t/tests.log
 for round in 1 2; do for v in base intree; do
   if [ $v = intree ]; then unset DG_LIB_PATH DG_LIB_ANY_DIGEST; else export DG_LIB_PATH=$R/delta_crdt_ex_amd/ab/libdeltagpu_$v.so DG_LIB_ANY_DIGEST=1; fi
