@@ -926,7 +926,7 @@ __global__ __launch_bounds__(DB, DIFF_OCC * DB / 256) void merkle_diff_count_ker
     // store that holds more shards -- the subtree's first row is searched, as without an
     // index, so a stale index never reads past the store or yields wrong keys.
     u64 x = 0;
-    bool use_st = st != nullptr;
+    bool use_st = st != nullptr && sub >= L1;  // (a subtree smaller than an index chunk: searched)
     if (use_st) {
       x = st[(tile << sub) >> L1];
       use_st = st[1ull << (depth - L1)] == r.n && x <= r.n;
