@@ -786,6 +786,15 @@ constexpr u32 OWN = XSUB / DB;        // buckets per thread
 #ifndef DG_DIFF_EXP
 #define DG_DIFF_EXP 0
 #endif
+// DG_DIFF_NT (A/B only): the staged rows' columns read with non-temporal loads (1: every
+// column, 2: all but the key).  Config-4 round (profiles/r6/ab_diff_take.txt): the count
+// kernel 65.7 -> 49.9 us, but the round's next calls read the same rows -- the take B's,
+// the keyed join A's -- and lose what the diff's cached loads left in L2 and the
+// last-level cache: take_keys 40 -> 54 us, kd_count 52 -> 60 us, the round no faster;
+// back to back 50.3 -> 52.0 us.  FETCH unchanged (114 MB).  Kept off.
+#ifndef DG_DIFF_NT
+#define DG_DIFF_NT 0
+#endif
 // rows of the differing buckets staged in LDS, differing buckets listed in LDS (the
 // subtree's share of a 1 %-differing config-4 shard is ~1000 rows in ~120 buckets at 4096
 // buckets, a quarter of that at 1024; a subtree beyond either merges over global memory)
@@ -1118,11 +1127,19 @@ __global__ __launch_bounds__(DB, DIFF_OCC * DB / 256) void merkle_diff_count_ker
           nd[j] = (u32)i & 3;
           cnt[j] = i;
 #else
+#if DG_DIFF_NT  // (A/B: non-temporal row loads, above)
+          key[j] = DG_DIFF_NT == 2 ? S.key[i] : __builtin_nontemporal_load(S.key + i);
+          val[j] = __builtin_nontemporal_load(S.val + i);
+          ts[j] = __builtin_nontemporal_load(S.ts + i);
+          nd[j] = __builtin_nontemporal_load(S.node + i);
+          cnt[j] = __builtin_nontemporal_load(S.cnt + i);
+#else
           key[j] = S.key[i];
           val[j] = S.val[i];
           ts[j] = S.ts[i];
           nd[j] = S.node[i];
           cnt[j] = S.cnt[i];
+#endif
 #endif
         }
       }

@@ -4,7 +4,7 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT; cd $R
 O=$R/gpurun_out/sub; mkdir -p $O
-VARS="intree DG_DIFF_SUB10 DG_DIFF_SUB10_DG_DIFF_OCC5 DG_DIFF_SUB10_DG_DIFF_OCC6"
+VARS="intree DG_DIFF_NT1 DG_DIFF_NT2"
 use() { if [ $1 = intree ]; then unset DG_LIB_PATH DG_LIB_ANY_DIGEST; else export DG_LIB_PATH=$R/delta_crdt_ex_amd/ab/libdeltagpu_$1.so DG_LIB_ANY_DIGEST=1; fi; }
 for v in $VARS; do use $v
   timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_merkle.py -m gpu > $O/t_$v.log 2>&1 || { echo TEST_FAIL $v; tail -20 $O/t_$v.log; exit 1; }
@@ -25,3 +25,14 @@ import sys,csv
 for r in csv.reader(sys.stdin): print('$v round count kernel avg %.1f min %.1f' % (float(r[3])/1e3, float(r[5])/1e3))"
 done
 find $O -name "*kernel_trace.csv" -delete
+# FETCH per dispatch of the count kernel in the config-4 round, per build
+for v in $VARS; do use $v
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_$v -o p -- python3 $R/tools/prof_merkle.py > $O/pmc_$v.log 2>&1 || { echo PMC_FAILED $v; tail -5 $O/pmc_$v.log; exit 1; }
+  python3 - "$O/pmc_$v" "$v" <<'PY'
+import csv, glob, os, sys
+v = [float(r["Counter_Value"]) for f in glob.glob(os.path.join(sys.argv[1], "**", "*counter_collection.csv"), recursive=True)
+     for r in csv.DictReader(open(f)) if "merkle_diff_count" in r["Kernel_Name"]]
+print(sys.argv[2], "count kernel FETCH_SIZE per dispatch kB %.1f (%d dispatches)" % (sum(v) / max(len(v), 1), len(v)))
+PY
+done
+find $O -name "*counter_collection.csv" -size +1M -delete
